@@ -1,0 +1,166 @@
+// Python bindings of the HIP kernel library (module `tensorflow_distributed_learning_amd._C`).
+//
+// Kernels launch on the caller's current HIP stream, so every entry point here is capturable
+// into a hipGraph by torch.cuda.graph (the engine captures whole train steps).
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPStream.h>
+
+#include <vector>
+
+#include "kernels/mnist_cnn.h"
+#include "kernels/ops.h"
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_cuda_f32(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be float32");
+}
+
+// Owns the scratch buffers and the argument block of one replica's fused MNIST step.
+class MnistStep {
+ public:
+  MnistStep(at::Tensor X, at::Tensor Y, at::Tensor idx_buf, at::Tensor W, at::Tensor G,
+            std::vector<int64_t> offsets, int64_t b, double scale, at::Tensor lr, at::Tensor metrics)
+      : X_(X), Y_(Y), idx_(idx_buf), W_(W), G_(G), lr_(lr), metrics_(metrics) {
+    check_cuda_f32(X, "X");
+    check_cuda_f32(W, "W");
+    check_cuda_f32(G, "G");
+    check_cuda_f32(lr, "lr");
+    check_cuda_f32(metrics, "metrics");
+    TORCH_CHECK(Y.is_cuda() && Y.scalar_type() == at::kInt, "Y must be int32 on GPU");
+    TORCH_CHECK(idx_buf.is_cuda() && idx_buf.scalar_type() == at::kInt, "idx must be int32 on GPU");
+    TORCH_CHECK(X.numel() % 784 == 0, "X must be [N,28,28,1]");
+    TORCH_CHECK(offsets.size() == 8, "8 variable offsets expected");
+    TORCH_CHECK(b >= 1 && b <= 256, "fused MNIST step supports 1 <= per-replica batch <= 256");
+    TORCH_CHECK(W.numel() == G.numel(), "slab size mismatch");
+    for (auto o : offsets) TORCH_CHECK(o % 4 == 0 && o >= 0 && o < W.numel(), "offsets must be 16B aligned");
+    auto f = W.options();
+    auto u8 = f.dtype(at::kByte);
+    P1_ = at::empty({b * 169 * 32}, f);
+    A1_ = at::empty({b * 169 * 32}, u8);
+    P2_ = at::empty({b * 1600}, f);
+    A2_ = at::empty({b * 1600}, u8);
+    H_ = at::empty({b * 128}, f);
+    dH_ = at::empty({b * 128}, f);
+    dC2_ = at::empty({b * 25 * 4 * 64}, f);
+    part2_ = at::zeros({tdl::kMnistConv2Splits * tdl::kMnistPart2Rows * 64}, f);
+    part1_ = at::zeros({(int64_t)tdl::mnist_nb7((int)b) * tdl::kMnistPart1Cols}, f);
+    a_ = tdl::MnistArgs{};
+    a_.X = X_.data_ptr<float>();
+    a_.Y = Y_.data_ptr<int>();
+    a_.idx = idx_.data_ptr<int>();
+    a_.W = W_.data_ptr<float>();
+    a_.G = G_.data_ptr<float>();
+    a_.ow1 = (int)offsets[0]; a_.ob1 = (int)offsets[1]; a_.ow2 = (int)offsets[2]; a_.ob2 = (int)offsets[3];
+    a_.ow3 = (int)offsets[4]; a_.ob3 = (int)offsets[5]; a_.ow4 = (int)offsets[6]; a_.ob4 = (int)offsets[7];
+    a_.P1 = P1_.data_ptr<float>();
+    a_.A1 = A1_.data_ptr<uint8_t>();
+    a_.P2 = P2_.data_ptr<float>();
+    a_.A2 = A2_.data_ptr<uint8_t>();
+    a_.H = H_.data_ptr<float>();
+    a_.dH = dH_.data_ptr<float>();
+    a_.dC2 = dC2_.data_ptr<float>();
+    a_.part2 = part2_.data_ptr<float>();
+    a_.part1 = part1_.data_ptr<float>();
+    a_.metrics = metrics_.data_ptr<float>();
+    a_.lr = lr_.data_ptr<float>();
+    a_.b = (int)b;
+    a_.scale = (float)scale;
+    a_.nslab = (int)W.numel();
+  }
+
+  void set_idx_offset(int64_t off) {
+    TORCH_CHECK(off >= 0 && off + a_.b <= idx_.numel(), "idx offset out of range");
+    a_.idx = idx_.data_ptr<int>() + off;
+  }
+
+  // Individual stages (tests / profiling): 1..7, 9.
+  void stage(int64_t k, bool apply_sgd) {
+    hipStream_t s = cur_stream();
+    switch (k) {
+      case 1: tdl::mnist_conv1_pool(a_, s); break;
+      case 2: tdl::mnist_conv2_pool(a_, s); break;
+      case 3: tdl::mnist_dense1(a_, s); break;
+      case 4: tdl::mnist_head(a_, s); break;
+      case 5: tdl::mnist_dense1_bwd(a_, s); break;
+      case 6: tdl::mnist_conv2_wgrad(a_, s); break;
+      case 7: tdl::mnist_conv2_dgrad(a_, s); break;
+      case 9: tdl::mnist_finalize(a_, apply_sgd, s); break;
+      default: TORCH_CHECK(false, "unknown stage");
+    }
+  }
+
+  // forward + loss + backward: leaves the complete gradient in G (after finalize).
+  void forward_backward(int64_t idx_off) {
+    set_idx_offset(idx_off);
+    hipStream_t s = cur_stream();
+    tdl::mnist_conv1_pool(a_, s);
+    tdl::mnist_conv2_pool(a_, s);
+    tdl::mnist_dense1(a_, s);
+    tdl::mnist_head(a_, s);
+    tdl::mnist_dense1_bwd(a_, s);
+    tdl::mnist_conv2_wgrad(a_, s);
+    tdl::mnist_conv2_dgrad(a_, s);
+  }
+
+  void finalize(bool apply_sgd) { tdl::mnist_finalize(a_, apply_sgd, cur_stream()); }
+
+  // forward only (evaluation): K1..K3 + logits via head is training-only, so eval uses K1-K3.
+  void forward_features(int64_t idx_off) {
+    set_idx_offset(idx_off);
+    hipStream_t s = cur_stream();
+    tdl::mnist_conv1_pool(a_, s);
+    tdl::mnist_conv2_pool(a_, s);
+    tdl::mnist_dense1(a_, s);
+  }
+
+  std::vector<at::Tensor> buffers() { return {P1_, A1_, P2_, A2_, H_, dH_, dC2_, part2_, part1_}; }
+
+ private:
+  at::Tensor X_, Y_, idx_, W_, G_, lr_, metrics_;
+  at::Tensor P1_, A1_, P2_, A2_, H_, dH_, dC2_, part2_, part1_;
+  tdl::MnistArgs a_;
+};
+
+void sgd(at::Tensor w, at::Tensor g, at::Tensor lr) {
+  check_cuda_f32(w, "w");
+  check_cuda_f32(g, "g");
+  check_cuda_f32(lr, "lr");
+  TORCH_CHECK(w.numel() == g.numel());
+  tdl::sgd_apply(w.data_ptr<float>(), g.data_ptr<float>(), lr.data_ptr<float>(), w.numel(), cur_stream());
+}
+
+void sgd_momentum(at::Tensor w, at::Tensor g, at::Tensor v, at::Tensor lr, double m, bool nesterov) {
+  check_cuda_f32(w, "w");
+  check_cuda_f32(g, "g");
+  check_cuda_f32(v, "v");
+  check_cuda_f32(lr, "lr");
+  TORCH_CHECK(w.numel() == g.numel() && v.numel() == w.numel());
+  tdl::sgd_momentum_apply(w.data_ptr<float>(), g.data_ptr<float>(), v.data_ptr<float>(), lr.data_ptr<float>(),
+                          (float)m, nesterov, w.numel(), cur_stream());
+}
+
+}  // namespace
+
+void register_ops(pybind11::module& m);
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "gfx950 HIP kernels of tensorflow_distributed_learning_amd";
+  pybind11::class_<MnistStep>(m, "MnistStep")
+      .def(pybind11::init<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, std::vector<int64_t>, int64_t,
+                          double, at::Tensor, at::Tensor>())
+      .def("set_idx_offset", &MnistStep::set_idx_offset)
+      .def("stage", &MnistStep::stage, pybind11::arg("k"), pybind11::arg("apply_sgd") = false)
+      .def("forward_backward", &MnistStep::forward_backward)
+      .def("forward_features", &MnistStep::forward_features)
+      .def("finalize", &MnistStep::finalize)
+      .def("buffers", &MnistStep::buffers);
+  m.def("sgd", &sgd);
+  m.def("sgd_momentum", &sgd_momentum);
+  register_ops(m);
+}

@@ -1,0 +1,41 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels of this framework.
+//
+// Everything here is written for 64-lane wavefronts and the f32-input MFMA
+// instructions of gfx950 (v_mfma_f32_16x16x4_f32: exact f32, one f32 A and one
+// f32 B value per lane, four f32 accumulators per lane).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tdl {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWave = 64;
+
+// D(16x16) += A(16x4) * B(4x16), f32 in / f32 accumulate.
+// Lane l supplies A[l & 15][l >> 4] and B[l >> 4][l & 15];
+// lane l receives D[(l >> 4) * 4 + r][l & 15] in acc[r].
+__device__ __forceinline__ f4 mfma16x16x4(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f4 zero4() { return f4{0.f, 0.f, 0.f, 0.f}; }
+
+__device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+__device__ __forceinline__ void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
+
+// Sum across the four 16-lane groups of a wave (lanes l, l^16, l^32, l^48).
+__device__ __forceinline__ float sum_lane_groups(float v) {
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+}  // namespace tdl

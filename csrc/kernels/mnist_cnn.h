@@ -1,0 +1,60 @@
+// Host-visible interface of the fused MNIST-CNN train step (see mnist_cnn.hip).
+//
+// Model (reference tf_dist_example.py:40-48):
+//   Conv2D(32,3,relu) -> MaxPool2 -> Conv2D(64,3,relu) -> MaxPool2 -> Flatten
+//   -> Dense(128,relu) -> Dense(10), NHWC, f32, TF weight layouts (HWIO / [in,out]).
+// Loss SparseCategoricalCrossentropy(from_logits) scaled 1/(b*R) (ex:50), SGD (ex:51),
+// SparseCategoricalAccuracy accumulated on device (ex:52).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tdl {
+
+struct MnistArgs {
+  // dataset (device resident) + per-step sample indices for this replica
+  const float* X;     // [N, 28, 28, 1]
+  const int* Y;       // [N]
+  const int* idx;     // [b] sample ids of this replica's slice of the global batch
+  // flat parameter / gradient slabs and per-variable offsets (floats)
+  float* W;
+  float* G;
+  int ow1, ob1, ow2, ob2, ow3, ob3, ow4, ob4;
+  // activations / saved state
+  float* P1;          // [b,13,13,32] pooled relu(conv1)
+  uint8_t* A1;        // [b,13,13,32] argmax (dy*2+dx) of each pool window
+  float* P2;          // [b,5,5,64] == [b,1600]
+  uint8_t* A2;        // [b,1600]
+  float* H;           // [b,128] relu(dense1)
+  float* dH;          // [b,128]
+  float* dC2;         // [b,25,4,64] grad of conv2 output, pool-window-major
+  float* part2;       // [4][304][64] split-K partials of conv2 wgrad (+ bias row 288)
+  float* part1;       // [nb7][320] per-block partials of conv1 wgrad (+ bias)
+  float* metrics;     // [0] loss sum, [1] correct, [2] count
+  const float* lr;    // device scalar learning rate
+  int b;              // per-replica batch
+  float scale;        // 1 / (b * R)
+  int nslab;          // slab length (floats)
+};
+
+constexpr int kMnistConv2Splits = 4;
+constexpr int kMnistPart2Rows = 304;
+constexpr int kMnistPart1Cols = 320;
+__host__ __device__ inline int mnist_nb7(int b) { return (b * 169 + 63) / 64; }
+
+void mnist_conv1_pool(const MnistArgs& a, hipStream_t s);
+void mnist_conv2_pool(const MnistArgs& a, hipStream_t s);
+void mnist_dense1(const MnistArgs& a, hipStream_t s);
+void mnist_head(const MnistArgs& a, hipStream_t s);
+void mnist_dense1_bwd(const MnistArgs& a, hipStream_t s);
+void mnist_conv2_wgrad(const MnistArgs& a, hipStream_t s);
+void mnist_conv2_dgrad(const MnistArgs& a, hipStream_t s);
+void mnist_finalize(const MnistArgs& a, bool apply_sgd, hipStream_t s);
+
+// Plain SGD over a flat slab: w -= lr * g  (lr read from device memory).
+void sgd_apply(float* w, const float* g, const float* lr, int64_t n, hipStream_t s);
+// Momentum SGD (Keras semantics): v = m*v - lr*g ; w += v  (nesterov: w += m*v - lr*g)
+void sgd_momentum_apply(float* w, const float* g, float* v, const float* lr, float momentum,
+                        bool nesterov, int64_t n, hipStream_t s);
+
+}  // namespace tdl

@@ -1,0 +1,17 @@
+// Host-visible interface of the generic (shape-agnostic) HIP ops.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tdl {
+
+// out[r, :] = src[idx[r], :] * scale   (row gather of a device-resident dataset; f32 rows)
+void gather_rows_f32(const float* src, const int* idx, float* out, int64_t rows, int64_t row_elems, float scale,
+                     hipStream_t s);
+// out[r, :] = float(src[idx[r], :]) * scale   (uint8 images -> f32, the reference's map(scale))
+void gather_rows_u8(const uint8_t* src, const int* idx, float* out, int64_t rows, int64_t row_elems, float scale,
+                    hipStream_t s);
+// out[r] = src[idx[r]]   (labels)
+void gather_i32(const int* src, const int* idx, int* out, int64_t rows, hipStream_t s);
+
+}  // namespace tdl

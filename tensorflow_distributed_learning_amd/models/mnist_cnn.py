@@ -1,0 +1,135 @@
+"""The reference's MNIST CNN (tf_dist_example.py:39-53) as a model family of this framework.
+
+* :func:`build_mnist_cnn`   – the Keras-style ``Sequential`` exactly as the reference builds it.
+* :data:`MNIST_CNN_VARIABLES` – TF variable names / layouts (HWIO conv kernels, [in,out] dense).
+* :func:`reference_logits`  – plain-PyTorch functional forward (NHWC semantics); the fp32/fp64
+  oracle for the fused HIP kernels.
+* :class:`FusedMnistTrainStep` – one replica's fused train step on the gfx950 kernels of
+  ``csrc/kernels/mnist_cnn.hip`` (8 launches: fwd + softmax-xent + bwd + finalize[/SGD]).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Sequence
+
+import torch
+import torch.nn.functional as F
+
+from ..engine.slab import SlabLayout
+
+MNIST_CNN_VARIABLES = [
+    ("conv2d/kernel:0", (3, 3, 1, 32)),
+    ("conv2d/bias:0", (32,)),
+    ("conv2d_1/kernel:0", (3, 3, 32, 64)),
+    ("conv2d_1/bias:0", (64,)),
+    ("dense/kernel:0", (1600, 128)),
+    ("dense/bias:0", (128,)),
+    ("dense_1/kernel:0", (128, 10)),
+    ("dense_1/bias:0", (10,)),
+]
+MNIST_NUM_PARAMS = 225_034
+
+
+def mnist_layout() -> SlabLayout:
+    return SlabLayout.from_shapes(MNIST_CNN_VARIABLES)
+
+
+def glorot_uniform(shape: Sequence[int], gen: torch.Generator) -> torch.Tensor:
+    """Keras glorot_uniform: limit = sqrt(6 / (fan_in + fan_out)); conv fans include the
+    receptive field (kh*kw*cin, kh*kw*cout)."""
+    if len(shape) == 2:
+        fan_in, fan_out = shape
+    else:
+        rf = int(math.prod(shape[:-2]))
+        fan_in, fan_out = shape[-2] * rf, shape[-1] * rf
+    lim = math.sqrt(6.0 / (fan_in + fan_out))
+    return (torch.rand(tuple(shape), generator=gen, dtype=torch.float32) * 2 - 1) * lim
+
+
+def init_mnist_params(seed: int = 0) -> List[torch.Tensor]:
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for name, shape in MNIST_CNN_VARIABLES:
+        out.append(glorot_uniform(shape, g) if name.endswith("kernel:0") else torch.zeros(shape))
+    return out
+
+
+def reference_logits(params: Sequence[torch.Tensor], x: torch.Tensor) -> torch.Tensor:
+    """Forward of the reference model in plain PyTorch.  x: [b,28,28,1] NHWC."""
+    w1, b1, w2, b2, w3, b3, w4, b4 = params
+    h = x.permute(0, 3, 1, 2)
+    h = F.relu(F.conv2d(h, w1.permute(3, 2, 0, 1), b1))
+    h = F.max_pool2d(h, 2)
+    h = F.relu(F.conv2d(h, w2.permute(3, 2, 0, 1), b2))
+    h = F.max_pool2d(h, 2)
+    h = h.permute(0, 2, 3, 1).reshape(h.shape[0], -1)  # Flatten in HWC order (Keras NHWC)
+    h = F.relu(h @ w3 + b3)
+    return h @ w4 + b4
+
+
+def reference_loss(params, x, y, num_replicas: int = 1):
+    """SparseCategoricalCrossentropy(from_logits=True) averaged over the GLOBAL batch
+    (per-replica sum / (b * R)), as tf.distribute + Keras compute it."""
+    logits = reference_logits(params, x)
+    ce = F.cross_entropy(logits, y.long(), reduction="none")
+    return ce.sum() / (x.shape[0] * num_replicas), logits, ce
+
+
+def build_mnist_cnn(keras_module=None):
+    """Build (not compile) the reference's Sequential model with this framework's Keras API."""
+    if keras_module is None:
+        from .. import keras as keras_module
+    L = keras_module.layers
+    return keras_module.Sequential(
+        [
+            L.Conv2D(32, 3, activation="relu", input_shape=(28, 28, 1)),
+            L.MaxPooling2D(),
+            L.Conv2D(64, 3, activation="relu"),
+            L.MaxPooling2D(),
+            L.Flatten(),
+            L.Dense(128, activation="relu"),
+            L.Dense(10),
+        ]
+    )
+
+
+class FusedMnistTrainStep:
+    """One replica's MNIST train step on the hand-written gfx950 kernels.
+
+    The dataset lives on the device (``X`` [N,28,28,1] f32, ``Y`` [N] int32); each step reads its
+    ``b`` sample ids from ``idx_buf`` at an offset, so a captured hipGraph replays over new data by
+    refreshing ``idx_buf`` only.  ``W``/``G`` are the flat parameter / gradient slabs in
+    :func:`mnist_layout` order.
+    """
+
+    def __init__(self, X: torch.Tensor, Y: torch.Tensor, idx_buf: torch.Tensor, W: torch.Tensor,
+                 G: torch.Tensor, layout: SlabLayout, per_replica_batch: int, num_replicas: int,
+                 lr: torch.Tensor, metrics: Optional[torch.Tensor] = None):
+        from .. import ops
+
+        C = ops.hip()
+        if [tuple(s.shape) for s in layout.specs] != [s for _, s in MNIST_CNN_VARIABLES]:
+            raise ValueError("layout does not match the MNIST CNN variables")
+        self.b = int(per_replica_batch)
+        self.R = int(num_replicas)
+        self.metrics = metrics if metrics is not None else torch.zeros(4, device=W.device)
+        self.lr = lr
+        self.X, self.Y, self.idx_buf, self.W, self.G = X, Y, idx_buf, W, G
+        self._impl = C.MnistStep(X, Y, idx_buf, W, G, [int(o) for o in layout.offsets], self.b,
+                                 1.0 / (self.b * self.R), lr, self.metrics)
+
+    def forward_backward(self, idx_offset: int) -> None:
+        self._impl.forward_backward(int(idx_offset))
+
+    def finalize(self, apply_sgd: bool) -> None:
+        self._impl.finalize(bool(apply_sgd))
+
+    def stage(self, k: int, apply_sgd: bool = False) -> None:
+        self._impl.stage(int(k), bool(apply_sgd))
+
+    def set_idx_offset(self, off: int) -> None:
+        self._impl.set_idx_offset(int(off))
+
+    def buffers(self) -> Dict[str, torch.Tensor]:
+        names = ["P1", "A1", "P2", "A2", "H", "dH", "dC2", "part2", "part1"]
+        return dict(zip(names, self._impl.buffers()))

@@ -1,0 +1,105 @@
+"""Numerics of the fused gfx950 MNIST-CNN train step vs a plain-PyTorch fp64 reference."""
+import pytest
+import torch
+
+from tensorflow_distributed_learning_amd.models import mnist_cnn as M
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(cuda, b, R=1, N=512, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    X = torch.rand(N, 28, 28, 1, generator=g)
+    Y = torch.randint(0, 10, (N,), generator=g, dtype=torch.int32)
+    params = M.init_mnist_params(seed)
+    # non-zero biases so bias paths are exercised
+    for i in (1, 3, 5, 7):
+        params[i] = (torch.rand(params[i].shape, generator=g) - 0.5) * 0.1
+    layout = M.mnist_layout()
+    W = layout.pack(params, device=cuda)
+    G = torch.zeros_like(W)
+    idx = torch.randperm(N, generator=g)[: 3 * b].to(torch.int32)
+    lr = torch.tensor([0.01], device=cuda)
+    step = M.FusedMnistTrainStep(X.to(cuda), Y.to(cuda), idx.to(cuda), W, G, layout, b, R, lr)
+    return X, Y, params, layout, W, G, idx, lr, step
+
+
+def _ref_grads(params, x, y, R):
+    p = [t.double().clone().requires_grad_(True) for t in params]
+    loss, logits, ce = M.reference_loss(p, x.double(), y, R)
+    loss.backward()
+    return [t.grad for t in p], logits.detach(), ce.detach()
+
+
+@pytest.mark.parametrize("b,R", [(64, 1), (64, 8), (17, 2), (1, 1), (128, 1)])
+def test_fused_grads_match_reference(cuda, b, R):
+    X, Y, params, layout, W, G, idx, lr, step = _setup(cuda, b, R)
+    off = b  # second chunk of idx
+    step.forward_backward(off)
+    step.finalize(False)
+    torch.cuda.synchronize()
+    ids = idx[off:off + b].long()
+    x, y = X[ids], Y[ids]
+    grads, logits, ce = _ref_grads(params, x, y, R)
+    got = layout.views(G.cpu())
+    names = [n for n, _ in M.MNIST_CNN_VARIABLES]
+    for name, gr, gg in zip(names, grads, got):
+        err = (gg.double() - gr).abs().max().item()
+        scale = gr.abs().max().item() + 1e-12
+        assert err <= 2e-5 * scale + 1e-9, f"{name}: max err {err} vs scale {scale}"
+    m = step.metrics.cpu()
+    assert abs(m[0].item() - ce.sum().item()) < 1e-3 * max(1.0, ce.sum().item())
+    correct = (logits.argmax(1) == y.long()).sum().item()
+    assert m[1].item() == correct
+    assert m[2].item() == b
+
+
+def test_fused_sgd_update(cuda):
+    b = 64
+    X, Y, params, layout, W, G, idx, lr, step = _setup(cuda, b, 1)
+    W0 = W.clone()
+    step.forward_backward(0)
+    step.finalize(True)
+    torch.cuda.synchronize()
+    assert torch.allclose(W, W0 - 0.01 * G, atol=1e-7, rtol=0)
+
+
+def test_fused_step_graph_capture(cuda):
+    b = 64
+    X, Y, params, layout, W, G, idx, lr, step = _setup(cuda, b, 1)
+    W_eager = W.clone()
+    # eager reference: 3 steps
+    Wsave = W.clone()
+    for k in range(3):
+        step.forward_backward(k * b)
+        step.finalize(True)
+    torch.cuda.synchronize()
+    W_eager = W.clone()
+    W.copy_(Wsave)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        step.forward_backward(0)  # warm-up (not captured)
+        step.finalize(False)
+    torch.cuda.synchronize()
+    with torch.cuda.graph(graph, stream=s):
+        for k in range(3):
+            step.forward_backward(k * b)
+            step.finalize(True)
+    W.copy_(Wsave)
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(W, W_eager), "graph replay must be bit-identical to eager execution"
+
+
+def test_fused_deterministic(cuda):
+    b = 64
+    X, Y, params, layout, W, G, idx, lr, step = _setup(cuda, b, 1)
+    step.forward_backward(0)
+    step.finalize(False)
+    g1 = G.clone()
+    step.forward_backward(0)
+    step.finalize(False)
+    torch.cuda.synchronize()
+    assert torch.equal(g1, G)
