@@ -85,21 +85,28 @@ __global__ __launch_bounds__(256) void k_conv2_pool(MnistArgs a) {
   const int oh = 2 * ph + (q >> 1), ow = 2 * pw + (q & 1);
   const float* abase = a.P1 + ((size_t)(bi * 13 + oh) * 13 + ow) * 32 + 4 * g;
   const float* bbase = a.W + a.ow2 + (4 * g) * 64 + n0 + i;
+  // Issue every load of the wave up front (18 k-steps x (float4 A + 4 B) = 144 VGPRs) so the
+  // whole K loop costs one memory round trip; the MFMAs then drain them in order.
+  f4 av[18];
+  float bv[18][4];
+#pragma unroll
+  for (int s = 0; s < 18; ++s) {
+    const int kk = s >> 1, cb = (s & 1) * 16, kh = kk / 3, kw = kk % 3;
+    av[s] = ld4(abase + (kh * 13 + kw) * 32 + cb);
+    const float* bp = bbase + (kk * 32 + cb) * 64;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) bv[s][t] = bp[t * 64];
+  }
+  __builtin_amdgcn_sched_barrier(0);  // keep every load above the MFMAs (one round trip)
   f4 acc0 = zero4(), acc1 = zero4();
+  const float vm = valid ? 1.f : 0.f;
 #pragma unroll
-  for (int kk = 0; kk < 9; ++kk) {
-    const int kh = kk / 3, kw = kk % 3;
-#pragma unroll
-    for (int cb = 0; cb < 32; cb += 16) {
-      f4 av = ld4(abase + (kh * 13 + kw) * 32 + cb);
-      if (!valid) av = zero4();
-      const float* bp = bbase + (kk * 32 + cb) * 64;
-      const float b0 = bp[0], b1 = bp[64], b2 = bp[128], b3 = bp[192];
-      acc0 = mfma16x16x4(av.x, b0, acc0);
-      acc1 = mfma16x16x4(av.y, b1, acc1);
-      acc0 = mfma16x16x4(av.z, b2, acc0);
-      acc1 = mfma16x16x4(av.w, b3, acc1);
-    }
+  for (int s = 0; s < 18; ++s) {
+    const f4 x = av[s] * vm;
+    acc0 = mfma16x16x4(x.x, bv[s][0], acc0);
+    acc1 = mfma16x16x4(x.y, bv[s][1], acc1);
+    acc0 = mfma16x16x4(x.z, bv[s][2], acc0);
+    acc1 = mfma16x16x4(x.w, bv[s][3], acc1);
   }
   const f4 acc = acc0 + acc1;
   // lane holds rows 4g..4g+3 == the 4 positions of pool window g, column n0+i.
@@ -128,17 +135,27 @@ __global__ __launch_bounds__(512) void k_dense1(MnistArgs a) {
   const bool valid = row < a.b;
   const float* ap = a.P2 + (size_t)(valid ? row : 0) * 1600 + 4 * g;
   const float* bp = a.W + a.ow3 + (4 * g) * 128 + nt * 16 + i;
-  f4 acc0 = zero4(), acc1 = zero4();
-  for (int c = wave; c < 100; c += 8) {
-    const int k0 = c * 16;
-    f4 av = ld4(ap + k0);
-    if (!valid) av = zero4();
+  // 13 k-chunks per wave (chunk c = wave + 8j < 100), all loads issued before the MFMAs.
+  f4 av[13];
+  float bv[13][4];
+#pragma unroll
+  for (int j = 0; j < 13; ++j) {
+    const int c = min(wave + 8 * j, 99), k0 = c * 16;
+    av[j] = ld4(ap + k0);
     const float* b = bp + k0 * 128;
-    const float b0 = b[0], b1 = b[128], b2 = b[256], b3 = b[384];
-    acc0 = mfma16x16x4(av.x, b0, acc0);
-    acc1 = mfma16x16x4(av.y, b1, acc1);
-    acc0 = mfma16x16x4(av.z, b2, acc0);
-    acc1 = mfma16x16x4(av.w, b3, acc1);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) bv[j][t] = b[t * 128];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  f4 acc0 = zero4(), acc1 = zero4();
+#pragma unroll
+  for (int j = 0; j < 13; ++j) {
+    const float m = (valid && wave + 8 * j < 100) ? 1.f : 0.f;
+    const f4 x = av[j] * m;
+    acc0 = mfma16x16x4(x.x, bv[j][0], acc0);
+    acc1 = mfma16x16x4(x.y, bv[j][1], acc1);
+    acc0 = mfma16x16x4(x.z, bv[j][2], acc0);
+    acc1 = mfma16x16x4(x.w, bv[j][3], acc1);
   }
   const f4 acc = acc0 + acc1;
 #pragma unroll
@@ -161,40 +178,56 @@ __global__ __launch_bounds__(1024) void k_head(MnistArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int b = a.b, tid = threadIdx.x;
   float* sH = sm;                 // b*128
-  float* sW = sH + b * 128;       // 1280 (+16 bias)
+  float* sW = sH + b * 128;       // 1280
   float* sB = sW + 1280;          // 16
   float* sD = sB + 16;            // b*16 logits -> dlogits
   float* sRed = sD + b * 16;      // 64
+  // every LDS-latency chain below is split over 4 independent accumulators and unrolled, so
+  // the single workgroup is issue-bound rather than LDS-latency-bound.
   for (int o = tid; o < b * 32; o += 1024) st4(sH + o * 4, ld4(a.H + o * 4));
   for (int o = tid; o < 1280; o += 1024) sW[o] = a.W[a.ow4 + o];
   if (tid < 10) sB[tid] = a.W[a.ob4 + tid];
+  const int yl = (tid < b) ? a.Y[a.idx[tid]] : 0;  // prefetch labels (b <= 1024 rows per pass)
   __syncthreads();
   for (int o = tid; o < b * 10; o += 1024) {
     const int r = o / 10, c = o - r * 10;
-    float s = sB[c];
-    const float* h = sH + r * 128;
+    const f4* h4 = reinterpret_cast<const f4*>(sH + r * 128);
+    float s0 = sB[c], s1 = 0.f, s2 = 0.f, s3 = 0.f;
 #pragma unroll 8
-    for (int k = 0; k < 128; ++k) s = fmaf(h[k], sW[k * 10 + c], s);
-    sD[r * 16 + c] = s;
+    for (int k4 = 0; k4 < 32; ++k4) {
+      const f4 h = h4[k4];
+      const float* w = sW + k4 * 40 + c;
+      s0 = fmaf(h.x, w[0], s0);
+      s1 = fmaf(h.y, w[10], s1);
+      s2 = fmaf(h.z, w[20], s2);
+      s3 = fmaf(h.w, w[30], s3);
+    }
+    sD[r * 16 + c] = (s0 + s1) + (s2 + s3);
   }
   __syncthreads();
   float lsum = 0.f, lcor = 0.f;
   for (int r = tid; r < b; r += 1024) {
     float* l = sD + r * 16;
-    const int y = a.Y[a.idx[r]];
-    float m = l[0];
+    const int y = (r < 1024 && r == tid) ? yl : a.Y[a.idx[r]];
+    float v[10];
+#pragma unroll
+    for (int c = 0; c < 10; ++c) v[c] = l[c];
+    float m = v[0];
     int am = 0;
 #pragma unroll
     for (int c = 1; c < 10; ++c)
-      if (l[c] > m) { m = l[c]; am = c; }
+      if (v[c] > m) { m = v[c]; am = c; }
     float se = 0.f;
 #pragma unroll
-    for (int c = 0; c < 10; ++c) se += expf(l[c] - m);
+    for (int c = 0; c < 10; ++c) se += expf(v[c] - m);
     const float lse = m + logf(se);
-    lsum += lse - l[y];
+    float ly = v[0];
+#pragma unroll
+    for (int c = 1; c < 10; ++c) ly = (c == y) ? v[c] : ly;
+    lsum += lse - ly;
     lcor += (am == y) ? 1.f : 0.f;
 #pragma unroll
-    for (int c = 0; c < 10; ++c) l[c] = (expf(l[c] - lse) - (c == y ? 1.f : 0.f)) * a.scale;
+    for (int c = 0; c < 10; ++c) l[c] = (expf(v[c] - lse) - (c == y ? 1.f : 0.f)) * a.scale;
   }
   lsum = wave_sum(lsum);
   lcor = wave_sum(lcor);
@@ -207,26 +240,33 @@ __global__ __launch_bounds__(1024) void k_head(MnistArgs a) {
     a.metrics[1] += c;
     a.metrics[2] += (float)b;
   }
-  for (int o = tid; o < 1280; o += 1024) {
-    const int k = o / 10, c = o - k * 10;
-    float s = 0.f;
-    for (int r = 0; r < b; ++r) s = fmaf(sH[r * 128 + k], sD[r * 16 + c], s);
-    a.G[a.ow4 + o] = s;
-  }
-  if (tid < 10) {
-    float s = 0.f;
-    for (int r = 0; r < b; ++r) s += sD[r * 16 + tid];
-    a.G[a.ob4 + tid] = s;
+  // dW4 (1280) and db4 (10): sum over rows, 4 accumulators
+  for (int o = tid; o < 1290; o += 1024) {
+    const bool bias = o >= 1280;
+    const int k = bias ? 0 : o / 10, c = bias ? o - 1280 : o - (o / 10) * 10;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int r = 0;
+    for (; r + 3 < b; r += 4) {
+      const float h0 = bias ? 1.f : sH[r * 128 + k], h1 = bias ? 1.f : sH[(r + 1) * 128 + k];
+      const float h2 = bias ? 1.f : sH[(r + 2) * 128 + k], h3 = bias ? 1.f : sH[(r + 3) * 128 + k];
+      s0 = fmaf(h0, sD[r * 16 + c], s0);
+      s1 = fmaf(h1, sD[(r + 1) * 16 + c], s1);
+      s2 = fmaf(h2, sD[(r + 2) * 16 + c], s2);
+      s3 = fmaf(h3, sD[(r + 3) * 16 + c], s3);
+    }
+    for (; r < b; ++r) s0 = fmaf(bias ? 1.f : sH[r * 128 + k], sD[r * 16 + c], s0);
+    a.G[(bias ? a.ob4 : a.ow4) + (bias ? c : o)] = (s0 + s1) + (s2 + s3);
   }
   for (int o = tid; o < b * 128; o += 1024) {
     const int r = o >> 7, k = o & 127;
     const float h = sH[o];
-    float s = 0.f;
-    if (h > 0.f) {
-#pragma unroll
-      for (int c = 0; c < 10; ++c) s = fmaf(sD[r * 16 + c], sW[k * 10 + c], s);
-    }
-    a.dH[o] = s;
+    const f4 d0 = ld4(sD + r * 16), d1 = ld4(sD + r * 16 + 4);
+    const float* w = sW + k * 10;
+    float s = d0.x * w[0];
+    s = fmaf(d0.y, w[1], s); s = fmaf(d0.z, w[2], s); s = fmaf(d0.w, w[3], s);
+    s = fmaf(d1.x, w[4], s); s = fmaf(d1.y, w[5], s); s = fmaf(d1.z, w[6], s); s = fmaf(d1.w, w[7], s);
+    s = fmaf(sD[r * 16 + 8], w[8], s); s = fmaf(sD[r * 16 + 9], w[9], s);
+    a.dH[o] = h > 0.f ? s : 0.f;
   }
 }
 
@@ -245,15 +285,23 @@ __global__ __launch_bounds__(256) void k_dense1_bwd(MnistArgs a) {
     // dW3[k][n] = sum_r P2[r][k] dH[r][n]   (M = 1600 features, N = 128, K = b)
     const int T = blk * 4 + wave, mt = T >> 3, nt = T & 7;
     const int kf = mt * 16 + i, n = nt * 16 + i;
+    // rows in batches of 64 (16 MFMA k-steps); all 32 loads of a batch in flight together.
     f4 acc0 = zero4(), acc1 = zero4();
-    for (int r0 = 0; r0 < b; r0 += 8) {
-      const int ra = r0 + g, rb = r0 + 4 + g;
-      const float a0 = ra < b ? a.P2[(size_t)ra * 1600 + kf] : 0.f;
-      const float b0 = ra < b ? a.dH[ra * 128 + n] : 0.f;
-      const float a1 = rb < b ? a.P2[(size_t)rb * 1600 + kf] : 0.f;
-      const float b1 = rb < b ? a.dH[rb * 128 + n] : 0.f;
-      acc0 = mfma16x16x4(a0, b0, acc0);
-      acc1 = mfma16x16x4(a1, b1, acc1);
+    for (int r0 = 0; r0 < b; r0 += 64) {
+      float av[16], bv[16];
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int rr = min(r0 + 4 * s + g, b - 1);
+        av[s] = a.P2[(size_t)rr * 1600 + kf];
+        bv[s] = a.dH[rr * 128 + n];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const float x = (r0 + 4 * s + g < b) ? av[s] : 0.f;
+        if (s & 1) acc1 = mfma16x16x4(x, bv[s], acc1);
+        else acc0 = mfma16x16x4(x, bv[s], acc0);
+      }
     }
     const f4 acc = acc0 + acc1;
 #pragma unroll
@@ -267,16 +315,22 @@ __global__ __launch_bounds__(256) void k_dense1_bwd(MnistArgs a) {
     const bool valid = row < b;
     const float* ap = a.dH + (valid ? row : 0) * 128 + 4 * g;
     const float* bp = a.W + a.ow3 + (size_t)(nt * 16 + i) * 128 + 4 * g;
+    f4 av[8], bv[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      av[s] = ld4(ap + s * 16);
+      bv[s] = ld4(bp + s * 16);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const float vm = valid ? 1.f : 0.f;
     f4 acc0 = zero4(), acc1 = zero4();
 #pragma unroll
-    for (int n0 = 0; n0 < 128; n0 += 16) {
-      f4 av = ld4(ap + n0);
-      if (!valid) av = zero4();
-      const f4 bv = ld4(bp + n0);
-      acc0 = mfma16x16x4(av.x, bv.x, acc0);
-      acc1 = mfma16x16x4(av.y, bv.y, acc1);
-      acc0 = mfma16x16x4(av.z, bv.z, acc0);
-      acc1 = mfma16x16x4(av.w, bv.w, acc1);
+    for (int s = 0; s < 8; ++s) {
+      const f4 x = av[s] * vm;
+      acc0 = mfma16x16x4(x.x, bv[s].x, acc0);
+      acc1 = mfma16x16x4(x.y, bv[s].y, acc1);
+      acc0 = mfma16x16x4(x.z, bv[s].z, acc0);
+      acc1 = mfma16x16x4(x.w, bv[s].w, acc1);
     }
     const f4 acc = acc0 + acc1;
     const int k = nt * 16 + i, pp = k >> 6, co = k & 63;
@@ -327,24 +381,45 @@ __global__ __launch_bounds__(256) void k_conv2_wgrad(MnistArgs a) {
   const float* pa = a.P1 + ((dy + kh) * 13 + (dx + kw)) * 32 + ci;
   const float* pb = a.dC2 + g * 64 + nt * 16 + i;
   const float one = (i == 0) ? 1.f : 0.f;
+  // windows in batches of 16, double-buffered: batch j+1's 32 loads are in flight while the
+  // MFMAs of batch j run.
   f4 acc0 = zero4(), acc1 = zero4();
-  int w = w0;
-  for (; w + 1 < w1; w += 2) {
-    const int bi0 = w / 25, pp0 = w - bi0 * 25, ph0 = pp0 / 5, pw0 = pp0 - ph0 * 5;
-    const int w_ = w + 1;
-    const int bi1 = w_ / 25, pp1 = w_ - bi1 * 25, ph1 = pp1 / 5, pw1 = pp1 - ph1 * 5;
-    const float a0 = bias_tile ? one : pa[((bi0 * 13 + 2 * ph0) * 13 + 2 * pw0) * 32];
-    const float a1 = bias_tile ? one : pa[((bi1 * 13 + 2 * ph1) * 13 + 2 * pw1) * 32];
-    const float b0 = pb[(size_t)w * 256];
-    const float b1 = pb[(size_t)w_ * 256];
-    acc0 = mfma16x16x4(a0, b0, acc0);
-    acc1 = mfma16x16x4(a1, b1, acc1);
-  }
-  if (w < w1) {
-    const int bi0 = w / 25, pp0 = w - bi0 * 25, ph0 = pp0 / 5, pw0 = pp0 - ph0 * 5;
-    const float a0 = bias_tile ? one : pa[((bi0 * 13 + 2 * ph0) * 13 + 2 * pw0) * 32];
-    const float b0 = pb[(size_t)w * 256];
-    acc0 = mfma16x16x4(a0, b0, acc0);
+  float ca[16], cb[16], na[16], nb[16];
+  auto load = [&](int base, float (&ra)[16], float (&rb)[16]) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int w = min(base + s, w1 - 1);
+      const int bi0 = w / 25, pp0 = w - bi0 * 25, ph0 = pp0 / 5, pw0 = pp0 - ph0 * 5;
+      ra[s] = pa[((bi0 * 13 + 2 * ph0) * 13 + 2 * pw0) * 32];
+      rb[s] = pb[(size_t)w * 256];
+    }
+  };
+  auto comp = [&](int base, const float (&ra)[16], const float (&rb)[16]) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const float x = (base + s < w1) ? (bias_tile ? one : ra[s]) : 0.f;
+      if (s & 1) acc1 = mfma16x16x4(x, rb[s], acc1);
+      else acc0 = mfma16x16x4(x, rb[s], acc0);
+    }
+  };
+  if (w0 < w1) {
+    load(w0, ca, cb);
+    int base = w0;
+    while (true) {
+      const int nxt = base + 16;
+      if (nxt < w1) load(nxt, na, nb);
+      __builtin_amdgcn_sched_barrier(0);
+      comp(base, ca, cb);
+      __builtin_amdgcn_sched_barrier(0);
+      if (nxt >= w1) break;
+      const int nn = nxt + 16;
+      if (nn < w1) load(nn, ca, cb);
+      __builtin_amdgcn_sched_barrier(0);
+      comp(nxt, na, nb);
+      __builtin_amdgcn_sched_barrier(0);
+      if (nn >= w1) break;
+      base = nn;
+    }
   }
   const f4 acc = acc0 + acc1;
 #pragma unroll
@@ -381,10 +456,10 @@ __global__ __launch_bounds__(512) void k_conv2_dgrad(MnistArgs a) {
     const int ohc = rv ? oh : 0, owc = rv ? ow : 0;
     const float* ap = a.dC2 + ((size_t)((bi * 25 + (ohc >> 1) * 5 + (owc >> 1)) * 4 + (ohc & 1) * 2 + (owc & 1))) * 64 + 4 * g;
     const float* bp = w2 + kk * 32 * 64;
+    const float m = rv ? 1.f : 0.f;
 #pragma unroll
     for (int c0 = 0; c0 < 64; c0 += 16) {
-      f4 av = ld4(ap + c0);
-      if (!rv) av = zero4();
+      const f4 av = ld4(ap + c0) * m;
       const f4 bv = ld4(bp + c0);
       acc0 = mfma16x16x4(av.x, bv.x, acc0);
       acc1 = mfma16x16x4(av.y, bv.y, acc1);
