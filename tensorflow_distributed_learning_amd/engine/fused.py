@@ -1,0 +1,306 @@
+"""The MI355X fast path of ``fit`` for the reference model (tf_dist_example.py:39-59).
+
+``compile()`` + ``fit()`` on the reference's Sequential (Conv2D(32,3,relu) MaxPool Conv2D(64,3,relu)
+MaxPool Flatten Dense(128,relu) Dense(10); SparseCategoricalCrossentropy(from_logits) ; SGD ;
+SparseCategoricalAccuracy) on a GPU replica is compiled into:
+
+* the model's flat parameter/gradient slabs (the same storage its MirroredVariables view);
+* a device-resident dataset (data/device.py) with per-step index vectors;
+* :class:`~..models.mnist_cnn.FusedMnistTrainStep` (8 hand-written gfx950 kernels);
+* the cross-replica gradient all-reduce on RCCL (``world > 1``) followed by the SGD kernel;
+* ONE hipGraph per execution of ``steps_per_execution`` steps, replayed with a new index vector
+  (the all-reduce is captured inside the graph when the communicator is capturable).
+
+Host work per execution: one H2D copy of K*B int32 indices and one graph launch.  Metrics (loss
+sum, correct count, sample count) are accumulated by the loss kernel on the device and reduced
+across replicas only when logs are read.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from ..data import device as DD
+from ..models import mnist_cnn as M
+from ..parallel import input_lib
+
+
+def _is_reference_cnn(model) -> bool:
+    from ..keras import activations as A
+    from ..keras import layers as L
+    from ..keras.models import Sequential
+
+    if not isinstance(model, Sequential):
+        return False
+    ls = [l for l in model.layers if not isinstance(l, L.InputLayer)]
+    pat = [L.Conv2D, L.MaxPooling2D, L.Conv2D, L.MaxPooling2D, L.Flatten, L.Dense, L.Dense]
+    if len(ls) != len(pat) or any(type(l) is not p for l, p in zip(ls, pat)):
+        return False
+    c1, p1, c2, p2, _, d1, d2 = ls
+    for c, f in ((c1, 32), (c2, 64)):
+        if not (c.filters == f and c.kernel_size == (3, 3) and c.strides == (1, 1) and c.padding == "valid" and
+                c.dilation_rate == (1, 1) and c.groups == 1 and c.use_bias and c.activation is A.relu):
+            return False
+    for p in (p1, p2):
+        if not (p.pool_size == (2, 2) and p.strides == (2, 2) and p.padding == "valid"):
+            return False
+    if not (d1.units == 128 and d1.use_bias and d1.activation is A.relu):
+        return False
+    if not (d2.units == 10 and d2.use_bias and d2.activation is A.linear):
+        return False
+    if tuple(model._built_input_shape[1:]) != (28, 28, 1):
+        return False
+    if any(getattr(l, "kernel_regularizer", None) or getattr(l, "bias_regularizer", None) for l in ls):
+        return False
+    return all(l.trainable for l in ls)
+
+
+def eligible(model, dataset=None) -> Optional[str]:
+    """None if the fused path applies, else the reason it does not."""
+    from .. import ops
+    from ..keras import losses, metrics, optimizers
+
+    if os.environ.get("TDL_DISABLE_FUSED") == "1":
+        return "disabled by TDL_DISABLE_FUSED"
+    s = model._get_strategy()
+    if s.extended.device.type != "cuda":
+        return "replica is not on a GPU"
+    if not ops.hip_available():
+        ops.hip()  # GPU replica without the HIP kernels: fail loudly
+    if not _is_reference_cnn(model):
+        return "model is not the reference CNN"
+    if model._dtype_policy() != "float32":
+        return "non-f32 dtype policy"
+    lo = model.loss
+    if not (isinstance(lo, losses.SparseCategoricalCrossentropy) and lo.from_logits and lo.ignore_class is None and
+            lo.reduction in (losses.Reduction.AUTO, losses.Reduction.SUM_OVER_BATCH_SIZE)):
+        return "loss is not SparseCategoricalCrossentropy(from_logits=True)"
+    opt = model.optimizer
+    if not isinstance(opt, optimizers.SGD) or opt.clipnorm or opt.clipvalue or opt.global_clipnorm or opt.weight_decay:
+        return "optimizer is not plain/momentum SGD"
+    for m in model.compiled_metrics:
+        if not isinstance(m, metrics.SparseCategoricalAccuracy):
+            return f"metric {m.name} not supported by the fused step"
+    return None
+
+
+class FusedMnistTrainer:
+    kind = "fused"
+
+    def __init__(self, model):
+        self.model = model
+        self.strategy = model._get_strategy()
+        self.device = self.strategy.extended.device
+        self.comm = self.strategy.extended.communicator
+        self.R = self.strategy.num_replicas_in_sync
+        self.rank = self.strategy.extended.rank
+        model._ensure_slabs()
+        self.layout = model._layout
+        self.W, self.G = model._W, model._G
+        for v in model._trainable_vars:
+            v._leaf = None
+        self.optimizer = model.optimizer
+        self.optimizer.build(self.W.numel(), self.device)
+        self.K = max(1, int(model._steps_per_execution))
+        self.metrics_dev = torch.zeros(4, dtype=torch.float32, device=self.device)
+        self._steps = {}
+        self._graphs = {}
+        self._data_key = None
+        self.capture = os.environ.get("TDL_GRAPH", "1") == "1"
+        # all-reduce inside the captured graph only when the communicator supports it
+        self.capture_comm = self.comm.world_size == 1 or (self.comm.capturable and
+                                                          os.environ.get("TDL_CAPTURE_ALLREDUCE", "1") == "1")
+
+    # ------------------------------------------------------------------ data
+    def prepare(self, dataset):
+        lp = DD.lower(dataset)
+        if lp is None:
+            return None
+        x, y = (lp.columns if isinstance(lp.columns, (tuple, list)) else (None, None))[:2]
+        if x is None or y is None or tuple(x.shape[1:]) not in ((28, 28, 1), (28, 28)) or \
+                x.dtype != torch.float32 or y.dim() != 1:
+            return None
+        if lp.batch_size % self.R:
+            raise ValueError(f"global batch {lp.batch_size} is not divisible by {self.R} replicas")
+        key = (id(x), id(y))
+        if key != self._data_key:
+            self.X = x.reshape(len(x), 28, 28, 1).to(self.device, torch.float32).contiguous()
+            self.Y = y.to(self.device, torch.int32).contiguous()
+            self._data_key = key
+            self._steps, self._graphs = {}, {}
+        policy = input_lib.effective_policy(dataset) if self.R > 1 else None
+        seed = input_lib.shared_seed(self.strategy) if policy is not None and policy.name in ("DATA", "FILE") else None
+        return DeviceHandler(lp, seed, self.rank, self.R)
+
+    # ------------------------------------------------------------------ steps
+    def _step(self, b: int, idx_buf: torch.Tensor, global_b: Optional[int] = None):
+        key = (b, idx_buf.data_ptr(), global_b)
+        st = self._steps.get(key)
+        if st is None:
+            st = M.FusedMnistTrainStep(self.X, self.Y, idx_buf, self.W, self.G, self.layout, b, self.R,
+                                       self.optimizer.lr_dev, self.metrics_dev, global_batch=global_b)
+            self._steps[key] = st
+        return st
+
+    def _apply(self, st, global_b: int):
+        """finalize + (all-reduce) + optimizer for one step."""
+        opt = self.optimizer
+        plain = opt.momentum == 0
+        if self.R == 1 and plain:
+            st.finalize(True)
+            return
+        st.finalize(False)
+        if self.R > 1:
+            self.comm.all_reduce(self.G, "sum")
+        from .. import ops
+
+        C = ops.hip()
+        if plain:
+            C.sgd(self.W, self.G, opt.lr_dev)
+        else:
+            C.sgd_momentum(self.W, self.G, opt._slots["momentum"], opt.lr_dev, opt.momentum, opt.nesterov)
+
+    def _run_eager(self, idx_np: np.ndarray, b: int, global_b: int):
+        if b == 0:
+            # this replica got no samples of a tiny final batch: contribute zero gradients
+            self.G.zero_()
+            if self.R > 1:
+                self.comm.all_reduce(self.G, "sum")
+            self.optimizer.apply_flat(self.W, self.G)
+            return
+        idx_buf = torch.from_numpy(idx_np.astype(np.int32)).to(self.device)
+        st = self._step(b, idx_buf, global_b)
+        st.forward_backward(0)
+        self._apply(st, global_b)
+        self.optimizer.iterations += 1
+
+    def _graph_for(self, K: int, b: int):
+        g = self._graphs.get((K, b))
+        if g is not None:
+            return g
+        idx_buf = torch.zeros(K * b, dtype=torch.int32, device=self.device)
+        st = self._step(b, idx_buf)
+        graph = None
+        if self.capture and (self.capture_comm or self.R == 1):
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            torch.cuda.synchronize(self.device)
+            graph = torch.cuda.CUDAGraph()
+            saved = (self.W.clone(), self.metrics_dev.clone(),
+                     {k: v.clone() for k, v in self.optimizer.slots().items()})
+            with torch.cuda.graph(graph, stream=s):
+                for k in range(K):
+                    st.forward_backward(k * b)
+                    self._apply(st, b * self.R)
+            torch.cuda.synchronize(self.device)
+            # capture does not execute, but be safe: restore state
+            self.W.copy_(saved[0])
+            self.metrics_dev.copy_(saved[1])
+            for k, v in saved[2].items():
+                self.optimizer.slots()[k].copy_(v)
+        g = (graph, idx_buf, st)
+        self._graphs[(K, b)] = g
+        return g
+
+    def run_train(self, handler: "DeviceHandler", steps: int) -> int:
+        done = 0
+        b = handler.b
+        opt = self.optimizer
+        while done < steps:
+            K = min(self.K, steps - done)
+            idx = handler.take(K)
+            if idx is None:
+                # ragged tail (end of finite data) -> eager steps of their own sizes
+                one = handler.next_ragged()
+                if one is None:
+                    break
+                opt._sync_lr()
+                self._run_eager(*one)
+                done += 1
+                continue
+            opt._sync_lr()
+            graph, idx_buf, st = self._graph_for(K, b)
+            idx_buf.copy_(torch.from_numpy(idx), non_blocking=False)
+            if graph is not None:
+                graph.replay()
+            else:
+                for k in range(K):
+                    st.forward_backward(k * b)
+                    self._apply(st, b * self.R)
+            opt.iterations += K
+            done += K
+        return done
+
+    def reset_metrics(self):
+        self.metrics_dev.zero_()
+        self.model._loss_tracker.reset_state()
+        for m in self.model.compiled_metrics:
+            m.reset_state()
+
+    def logs(self) -> Dict[str, float]:
+        t = self.metrics_dev.clone()
+        if self.R > 1:
+            self.comm.all_reduce(t, "sum")
+        loss_sum, correct, count = (float(v) for v in t[:3].cpu())
+        out = {"loss": loss_sum / max(count, 1.0)}
+        for m in self.model.compiled_metrics:
+            out[m.name] = correct / max(count, 1.0)
+        # mirror into the Keras metric objects so model.metrics results agree
+        lt = self.model._loss_tracker
+        lt._to(self.device)
+        lt.total._value.fill_(float(self.metrics_dev[0]))
+        lt.count._value.fill_(float(self.metrics_dev[2]))
+        for m in self.model.compiled_metrics:
+            m._to(self.device)
+            m.total._value.fill_(float(self.metrics_dev[1]))
+            m.count._value.fill_(float(self.metrics_dev[2]))
+        return out
+
+    def finish(self):
+        torch.cuda.synchronize(self.device)
+
+
+class DeviceHandler:
+    """Index vectors for this replica: its slice of every global batch."""
+
+    def __init__(self, lp: DD.LoweredPipeline, seed: Optional[int], rank: int, R: int):
+        self.lp = lp
+        self.rank, self.R = rank, R
+        self.B = lp.batch_size
+        self.b = lp.batch_size // R
+        self.stream = DD.IndexStream(lp, seed)
+        self._pending = []
+
+    def new_iterator(self):
+        self.stream = DD.IndexStream(self.lp, self.stream._seed)
+        self._pending = []
+
+    def _next_global(self):
+        if self._pending:
+            return self._pending.pop(0)
+        return self.stream.next_batch()
+
+    def take(self, K: int) -> Optional[np.ndarray]:
+        """K full global batches -> this replica's [K*b] indices (None if fewer remain)."""
+        got = []
+        for _ in range(K):
+            g = self._next_global()
+            if g is None or len(g) < self.B:
+                if g is not None:
+                    self._pending.insert(0, g)
+                self._pending = got + self._pending
+                return None
+            got.append(g)
+        return np.concatenate([g[self.rank * self.b:(self.rank + 1) * self.b] for g in got])
+
+    def next_ragged(self):
+        g = self._next_global()
+        if g is None:
+            return None
+        sizes = input_lib.split_sizes(len(g), self.R)
+        lo = sum(sizes[: self.rank])
+        n = sizes[self.rank]
+        return g[lo:lo + n], n, len(g)

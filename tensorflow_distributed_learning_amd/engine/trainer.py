@@ -1,0 +1,280 @@
+"""Training engines behind ``Model.fit`` / ``evaluate``.
+
+:class:`GenericTrainer` – any model: PyTorch autograd over the layer ``call``s, parameters as
+  autograd leaves that SHARE STORAGE with the replica's flat slab and whose ``.grad`` is a view of
+  the flat gradient slab; after backward the gradient slab is all-reduced (bucketed, overlapped
+  with backward through post-accumulate-grad hooks when the communicator is asynchronous) and the
+  optimizer updates the whole slab at once.  Mixed precision (``keras.mixed_precision`` policy
+  ``mixed_bfloat16``) runs the forward/backward under bf16 autocast with f32 master weights.
+
+:class:`~.fused.FusedMnistTrainer` – the reference model on MI355X: hand-written HIP kernels,
+  device-resident data, hipGraph-captured multi-step executions (engine/fused.py).
+
+Both share the data handling and the cross-replica metric reduction defined here.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from ..data import dataset as D
+from ..parallel import input_lib
+
+
+class LazyLogs(dict):
+    """Logs dict whose values are computed (host sync + cross-replica reduce) on first access."""
+
+    def __init__(self, fn):
+        super().__init__()
+        self._fn = fn
+        self._done = False
+
+    def _force(self):
+        if not self._done:
+            self._done = True
+            super().update(self._fn())
+
+    def __getitem__(self, k):
+        self._force()
+        return super().__getitem__(k)
+
+    def get(self, k, d=None):
+        self._force()
+        return super().get(k, d)
+
+    def items(self):
+        self._force()
+        return super().items()
+
+    def keys(self):
+        self._force()
+        return super().keys()
+
+    def values(self):
+        self._force()
+        return super().values()
+
+    def __iter__(self):
+        self._force()
+        return super().__iter__()
+
+    def __len__(self):
+        self._force()
+        return super().__len__()
+
+    def __contains__(self, k):
+        self._force()
+        return super().__contains__(k)
+
+    def __bool__(self):
+        return True
+
+
+def _to_device(batch, device):
+    return D.map_structure(lambda t: t.to(device, non_blocking=True) if isinstance(t, torch.Tensor) else t, batch)
+
+
+def _split_xy(batch):
+    if isinstance(batch, (tuple, list)):
+        if len(batch) == 1:
+            return batch[0], None, None
+        if len(batch) == 2:
+            return batch[0], batch[1], None
+        return batch[0], batch[1], batch[2]
+    if isinstance(batch, dict) and "x" in batch:
+        return batch["x"], batch.get("y"), batch.get("sample_weight")
+    return batch, None, None
+
+
+class HostDataHandler:
+    """Per-replica batches from a (distributed) host pipeline."""
+
+    def __init__(self, dataset: D.Dataset, strategy):
+        self.dist = input_lib.DistributedDataset(dataset, strategy)
+        self.strategy = strategy
+        self._it = None
+
+    def new_iterator(self):
+        self._it = iter(self.dist)
+
+    def next(self):
+        if self._it is None:
+            self.new_iterator()
+        return next(self._it)
+
+    def global_size(self, local_n: int) -> int:
+        """Actual global batch size of the current step (per-replica sizes follow split_sizes)."""
+        gb = self.dist.global_batch_size
+        R = self.dist.num_replicas
+        if R == 1:
+            return local_n
+        if gb is not None and local_n == gb // R and gb % R == 0:
+            return gb
+        t = torch.tensor([float(local_n)], dtype=torch.float64)
+        comm = self.strategy.extended.communicator
+        if comm.name == "rccl":
+            t = t.to(self.strategy.extended.device)
+        comm.all_reduce(t, "sum")
+        return int(t.item())
+
+
+class GenericTrainer:
+    kind = "generic"
+
+    def __init__(self, model):
+        self.model = model
+        self.strategy = model._get_strategy()
+        self.device = self.strategy.extended.device
+        self.comm = self.strategy.extended.communicator
+        model._ensure_slabs()
+        self.W, self.G = model._W, model._G
+        self._make_leaves()
+        self.optimizer = model.optimizer
+        self.optimizer.build(self.W.numel(), self.device)
+        self.loss = model.loss
+        self.loss_tracker = model._loss_tracker
+        self.metrics = model.compiled_metrics
+        self._policy = model._dtype_policy()
+        self._buckets = self._make_buckets()
+
+    # ------------------------------------------------------------------ parameters
+    def _make_leaves(self):
+        layout = self.model._layout
+        for v, view, gview in zip(self.model._trainable_vars, layout.views(self.W), layout.views(self.G)):
+            leaf = view.detach().requires_grad_(True)
+            leaf.grad = gview
+            v._leaf = leaf
+        self._leaves = [v._leaf for v in self.model._trainable_vars]
+
+    def _make_buckets(self):
+        """Overlap of the gradient all-reduce with backward: contiguous slab buckets (reverse
+        layer order) are launched asynchronously as soon as every gradient inside is final."""
+        if self.comm.world_size == 1 or self.comm.name != "rccl":
+            return None
+        bucket_bytes = self.model._bucket_bytes
+        if not bucket_bytes:
+            return None
+        layout = self.model._layout
+        ranges = layout.buckets(bucket_bytes)
+        if len(ranges) <= 1:
+            return None
+        var_bucket = {}
+        for bi, (s, e) in enumerate(ranges):
+            for i, off in enumerate(layout.offsets):
+                if s <= off < e:
+                    var_bucket[i] = bi
+        self._pending = [sum(1 for i in var_bucket if var_bucket[i] == b) for b in range(len(ranges))]
+        self._bucket_ranges = ranges
+        self._works = []
+        self._counts = list(self._pending)
+
+        def hook_for(i):
+            b = var_bucket[i]
+
+            def hook(_p):
+                self._counts[b] -= 1
+                if self._counts[b] == 0:
+                    s, e = self._bucket_ranges[b]
+                    self._works.append(self.comm.all_reduce_async(self.G[s:e], "sum"))
+            return hook
+
+        for i, leaf in enumerate(self._leaves):
+            leaf.register_post_accumulate_grad_hook(hook_for(i))
+        return ranges
+
+    # ------------------------------------------------------------------ steps
+    def _forward_loss(self, x, y, sw, global_n):
+        model = self.model
+        if self._policy == "mixed_bfloat16" and self.device.type == "cuda":
+            ctx = torch.autocast("cuda", dtype=torch.bfloat16)
+        else:
+            ctx = torch.autocast(self.device.type, enabled=False)
+        with ctx:
+            y_pred = model(x, training=True)
+        per_ex = self.loss.per_example(y, y_pred.float() if y_pred.dtype != torch.float32 else y_pred)
+        if sw is not None:
+            per_ex = per_ex * sw.to(per_ex.dtype)
+        # tf.nn.compute_average_loss: per-replica sum / GLOBAL batch -> SUM all-reduce = global mean
+        loss = per_ex.sum() / float(global_n)
+        reg = model._regularization_loss()
+        if reg is not None:
+            loss = loss + reg / self.strategy.num_replicas_in_sync
+        return loss, per_ex, y_pred
+
+    def train_step(self, batch, global_n: int):
+        x, y, sw = _split_xy(_to_device(batch, self.device))
+        G = self.G
+        G.zero_()
+        if self._buckets is not None:
+            self._counts = list(self._pending)
+            self._works = []
+        loss, per_ex, y_pred = self._forward_loss(x, y, sw, global_n)
+        loss.backward()
+        if self.comm.world_size > 1:
+            if self._buckets is not None:
+                for w in self._works:
+                    w.wait()
+                if len(self._works) != len(self._bucket_ranges):
+                    raise RuntimeError("gradient bucket hooks did not fire for every bucket (unused parameters?)")
+            else:
+                self.comm.all_reduce(G, "sum")
+        with torch.no_grad():
+            self.optimizer.apply_flat(self.W, G)
+            self.loss_tracker.update_state(per_ex.detach())
+            yp = y_pred.detach()
+            for m in self.metrics:
+                m.update_state(y, yp, sw)
+
+    def run_train(self, handler: HostDataHandler, steps: int) -> int:
+        done = 0
+        for _ in range(steps):
+            try:
+                batch = handler.next()
+            except StopIteration:
+                break
+            n = len(D.flatten(batch)[0])
+            self.train_step(batch, handler.global_size(n))
+            done += 1
+        return done
+
+    @torch.no_grad()
+    def test_step(self, batch):
+        x, y, sw = _split_xy(_to_device(batch, self.device))
+        y_pred = self.model(x, training=False)
+        per_ex = self.loss.per_example(y, y_pred.float())
+        if sw is not None:
+            per_ex = per_ex * sw.to(per_ex.dtype)
+        self.loss_tracker.update_state(per_ex)
+        for m in self.metrics:
+            m.update_state(y, y_pred, sw)
+
+    def run_test(self, handler: HostDataHandler, steps: Optional[int]) -> int:
+        done = 0
+        while steps is None or done < steps:
+            try:
+                batch = handler.next()
+            except StopIteration:
+                break
+            self.test_step(batch)
+            done += 1
+        return done
+
+    def reset_metrics(self):
+        self.loss_tracker.reset_state()
+        for m in self.metrics:
+            m.reset_state()
+
+    def logs(self) -> Dict[str, float]:
+        from ..parallel.strategy import _cross_replica
+
+        with _cross_replica():
+            out = {"loss": float(self.loss_tracker.result())}
+            for m in self.metrics:
+                out[m.name] = float(m.result())
+        return out
+
+    def finish(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)

@@ -1,0 +1,296 @@
+"""Keras optimizers over the flat parameter slab.
+
+Every replica applies the optimizer to its whole slab in ONE update after the gradient
+all-reduce (TF applies ``ResourceApplyGradientDescent`` once per variable).  On the GPU, SGD /
+momentum SGD run the hand-written gfx950 kernel (``_C.sgd`` / ``_C.sgd_momentum``, learning rate
+read from device memory so the update can sit inside a captured hipGraph); Adam/RMSprop/Adagrad
+use a handful of fused torch ops on the slab.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import torch
+
+from . import schedules as _sched
+
+
+class Optimizer:
+    def __init__(self, learning_rate=0.001, name="Optimizer", clipnorm=None, clipvalue=None, global_clipnorm=None,
+                 weight_decay=None, **kwargs):
+        self.name = name
+        self._lr = learning_rate
+        self.clipnorm, self.clipvalue, self.global_clipnorm = clipnorm, clipvalue, global_clipnorm
+        self.weight_decay = weight_decay
+        self.iterations = 0
+        self._slots: Dict[str, torch.Tensor] = {}
+        self._n = None
+        self._device = None
+        self.lr_dev: Optional[torch.Tensor] = None
+        unknown = set(kwargs) - {"decay", "amsgrad_legacy", "jit_compile", "is_legacy_optimizer",
+                                 "use_ema", "ema_momentum", "ema_overwrite_frequency"}
+        if unknown:
+            raise TypeError(f"{type(self).__name__}: unexpected arguments {sorted(unknown)}")
+
+    # ------------------------------------------------------------------ learning rate
+    @property
+    def learning_rate(self):
+        return self._lr
+
+    @learning_rate.setter
+    def learning_rate(self, v):
+        self._lr = v
+
+    lr = learning_rate
+
+    def current_lr(self, step: Optional[int] = None) -> float:
+        lr = self._lr
+        if isinstance(lr, _sched.LearningRateSchedule):
+            return float(lr(self.iterations if step is None else step))
+        if callable(lr):
+            return float(lr())
+        return float(lr)
+
+    def _sync_lr(self, step: Optional[int] = None):
+        if self.lr_dev is not None:
+            self.lr_dev.fill_(self.current_lr(step))
+
+    # ------------------------------------------------------------------ slots
+    def build(self, n: int, device: torch.device):
+        if self._n == n and self._device == device:
+            return
+        self._n, self._device = n, device
+        self.lr_dev = torch.full((1,), self.current_lr(), dtype=torch.float32, device=device)
+        for k in self._slot_names():
+            old = self._slots.get(k)
+            self._slots[k] = old.to(device) if (old is not None and old.numel() == n) else torch.zeros(
+                n, dtype=torch.float32, device=device)
+
+    def _slot_names(self) -> List[str]:
+        return []
+
+    def slots(self) -> Dict[str, torch.Tensor]:
+        return self._slots
+
+    # ------------------------------------------------------------------ update
+    def _clip(self, G: torch.Tensor):
+        if self.clipvalue is not None:
+            G.clamp_(-self.clipvalue, self.clipvalue)
+        norm = self.global_clipnorm or self.clipnorm
+        if norm is not None:
+            n = torch.linalg.vector_norm(G)
+            G.mul_(torch.clamp(norm / (n + 1e-12), max=1.0))
+
+    def apply_flat(self, W: torch.Tensor, G: torch.Tensor, sync_lr: bool = True):
+        """w <- update(w, g) over the whole slab (gradients already all-reduced)."""
+        if self._n != W.numel() or self._device != W.device:
+            self.build(W.numel(), W.device)
+        if sync_lr:
+            self._sync_lr()
+        self._clip(G)
+        if self.weight_decay:
+            W.mul_(1.0 - self.current_lr() * self.weight_decay)
+        with torch.no_grad():
+            self._update(W, G)
+        self.iterations += 1
+
+    def _update(self, W, G):
+        raise NotImplementedError
+
+    def apply_gradients(self, grads_and_vars):
+        """Eager per-variable path for custom training loops (tf.GradientTape style)."""
+        gv = [(g, v) for g, v in grads_and_vars if g is not None]
+        if not gv:
+            return
+        flat_g = torch.cat([torch.as_tensor(g).reshape(-1).float() for g, _ in gv])
+        flat_w = torch.cat([v.read_value().reshape(-1).float() for _, v in gv])
+        key = "_eager"
+        if getattr(self, key, None) is None or self._n != flat_w.numel():
+            self.build(flat_w.numel(), flat_w.device)
+            setattr(self, key, True)
+        self.apply_flat(flat_w, flat_g.to(flat_w.device))
+        off = 0
+        for _, v in gv:
+            n = int(math.prod(v.shape))
+            v.assign(flat_w[off : off + n].reshape(v.shape))
+            off += n
+
+    def variables(self):
+        return [self.iterations] + list(self._slots.values())
+
+    def get_config(self):
+        lr = self._lr
+        if isinstance(lr, _sched.LearningRateSchedule):
+            lr = _sched.serialize(lr)
+        return {"name": self.name, "learning_rate": lr, "clipnorm": self.clipnorm, "clipvalue": self.clipvalue,
+                "global_clipnorm": self.global_clipnorm}
+
+    @classmethod
+    def from_config(cls, cfg):
+        cfg = dict(cfg)
+        if isinstance(cfg.get("learning_rate"), dict):
+            cfg["learning_rate"] = _sched.deserialize(cfg["learning_rate"])
+        return cls(**cfg)
+
+    def state_dict(self):
+        return {"iterations": self.iterations, "slots": {k: v.detach().cpu() for k, v in self._slots.items()}}
+
+    def load_state_dict(self, st):
+        self.iterations = int(st.get("iterations", 0))
+        for k, v in st.get("slots", {}).items():
+            self._slots[k] = v.to(self._device) if self._device is not None else v.clone()
+
+
+def _hip_ok(t: torch.Tensor) -> bool:
+    if t.device.type != "cuda" or t.dtype != torch.float32:
+        return False
+    from .. import ops
+
+    ops.hip()  # raises loudly if the HIP kernels are missing on a GPU box
+    return True
+
+
+class SGD(Optimizer):
+    """tf.keras.optimizers.SGD(learning_rate=0.01, momentum=0.0, nesterov=False) (ex:51)."""
+
+    def __init__(self, learning_rate=0.01, momentum=0.0, nesterov=False, name="SGD", **kw):
+        super().__init__(learning_rate, name, **kw)
+        if not 0.0 <= momentum <= 1.0:
+            raise ValueError("momentum must be in [0, 1]")
+        self.momentum, self.nesterov = float(momentum), bool(nesterov)
+
+    def _slot_names(self):
+        return ["momentum"] if self.momentum > 0 else []
+
+    def _update(self, W, G):
+        if _hip_ok(W):
+            from .. import ops
+
+            C = ops.hip()
+            if self.momentum > 0:
+                C.sgd_momentum(W, G, self._slots["momentum"], self.lr_dev, self.momentum, self.nesterov)
+            else:
+                C.sgd(W, G, self.lr_dev)
+            return
+        lr = self.current_lr()
+        if self.momentum > 0:
+            v = self._slots["momentum"]
+            v.mul_(self.momentum).add_(G, alpha=-lr)
+            if self.nesterov:
+                W.add_(v, alpha=self.momentum).add_(G, alpha=-lr)
+            else:
+                W.add_(v)
+        else:
+            W.add_(G, alpha=-lr)
+
+    def get_config(self):
+        return dict(super().get_config(), momentum=self.momentum, nesterov=self.nesterov)
+
+
+class Adam(Optimizer):
+    def __init__(self, learning_rate=0.001, beta_1=0.9, beta_2=0.999, epsilon=1e-7, amsgrad=False, name="Adam", **kw):
+        super().__init__(learning_rate, name, **kw)
+        self.beta_1, self.beta_2, self.epsilon, self.amsgrad = beta_1, beta_2, epsilon, amsgrad
+
+    def _slot_names(self):
+        return ["m", "v"] + (["vhat"] if self.amsgrad else [])
+
+    def _update(self, W, G):
+        t = self.iterations + 1
+        lr = self.current_lr()
+        m, v = self._slots["m"], self._slots["v"]
+        m.mul_(self.beta_1).add_(G, alpha=1 - self.beta_1)
+        v.mul_(self.beta_2).addcmul_(G, G, value=1 - self.beta_2)
+        lr_t = lr * math.sqrt(1 - self.beta_2 ** t) / (1 - self.beta_1 ** t)
+        vv = v
+        if self.amsgrad:
+            torch.maximum(self._slots["vhat"], v, out=self._slots["vhat"])
+            vv = self._slots["vhat"]
+        W.addcdiv_(m, vv.sqrt().add_(self.epsilon), value=-lr_t)
+
+    def get_config(self):
+        return dict(super().get_config(), beta_1=self.beta_1, beta_2=self.beta_2, epsilon=self.epsilon,
+                    amsgrad=self.amsgrad)
+
+
+class AdamW(Adam):
+    def __init__(self, learning_rate=0.001, weight_decay=0.004, beta_1=0.9, beta_2=0.999, epsilon=1e-7, amsgrad=False,
+                 name="AdamW", **kw):
+        super().__init__(learning_rate, beta_1, beta_2, epsilon, amsgrad, name, weight_decay=weight_decay, **kw)
+
+
+class RMSprop(Optimizer):
+    def __init__(self, learning_rate=0.001, rho=0.9, momentum=0.0, epsilon=1e-7, centered=False, name="RMSprop", **kw):
+        super().__init__(learning_rate, name, **kw)
+        self.rho, self.momentum, self.epsilon, self.centered = rho, momentum, epsilon, centered
+
+    def _slot_names(self):
+        return ["rms"] + (["mom"] if self.momentum > 0 else []) + (["mg"] if self.centered else [])
+
+    def _update(self, W, G):
+        lr = self.current_lr()
+        rms = self._slots["rms"]
+        rms.mul_(self.rho).addcmul_(G, G, value=1 - self.rho)
+        denom = rms
+        if self.centered:
+            mg = self._slots["mg"]
+            mg.mul_(self.rho).add_(G, alpha=1 - self.rho)
+            denom = rms - mg * mg
+        step = G / (denom.sqrt() + self.epsilon)
+        if self.momentum > 0:
+            mom = self._slots["mom"]
+            mom.mul_(self.momentum).add_(step, alpha=lr)
+            W.sub_(mom)
+        else:
+            W.add_(step, alpha=-lr)
+
+
+class Adagrad(Optimizer):
+    def __init__(self, learning_rate=0.001, initial_accumulator_value=0.1, epsilon=1e-7, name="Adagrad", **kw):
+        super().__init__(learning_rate, name, **kw)
+        self.init_acc, self.epsilon = initial_accumulator_value, epsilon
+
+    def _slot_names(self):
+        return ["acc"]
+
+    def build(self, n, device):
+        fresh = "acc" not in self._slots
+        super().build(n, device)
+        if fresh:
+            self._slots["acc"].fill_(self.init_acc)
+
+    def _update(self, W, G):
+        acc = self._slots["acc"]
+        acc.addcmul_(G, G)
+        W.addcdiv_(G, acc.sqrt().add_(self.epsilon), value=-self.current_lr())
+
+
+_ALIASES = {"sgd": SGD, "adam": Adam, "adamw": AdamW, "rmsprop": RMSprop, "adagrad": Adagrad}
+
+
+def get(identifier) -> Optimizer:
+    if isinstance(identifier, Optimizer):
+        return identifier
+    if isinstance(identifier, str):
+        k = identifier.lower()
+        if k not in _ALIASES:
+            raise ValueError(f"unknown optimizer {identifier!r}")
+        return _ALIASES[k]()
+    if isinstance(identifier, dict):
+        return _ALIASES[identifier["class_name"].lower()].from_config(identifier.get("config", {}))
+    raise ValueError(f"could not interpret optimizer {identifier!r}")
+
+
+def serialize(opt: Optimizer):
+    return {"class_name": type(opt).__name__, "config": opt.get_config()}
+
+
+schedules = _sched
+
+
+class legacy:  # noqa: N801 - tf.keras.optimizers.legacy
+    SGD = SGD
+    Adam = Adam
+    RMSprop = RMSprop
+    Adagrad = Adagrad

@@ -104,7 +104,7 @@ class FusedMnistTrainStep:
 
     def __init__(self, X: torch.Tensor, Y: torch.Tensor, idx_buf: torch.Tensor, W: torch.Tensor,
                  G: torch.Tensor, layout: SlabLayout, per_replica_batch: int, num_replicas: int,
-                 lr: torch.Tensor, metrics: Optional[torch.Tensor] = None):
+                 lr: torch.Tensor, metrics: Optional[torch.Tensor] = None, global_batch: Optional[int] = None):
         from .. import ops
 
         C = ops.hip()
@@ -115,8 +115,9 @@ class FusedMnistTrainStep:
         self.metrics = metrics if metrics is not None else torch.zeros(4, device=W.device)
         self.lr = lr
         self.X, self.Y, self.idx_buf, self.W, self.G = X, Y, idx_buf, W, G
+        gb = int(global_batch) if global_batch is not None else self.b * self.R
         self._impl = C.MnistStep(X, Y, idx_buf, W, G, [int(o) for o in layout.offsets], self.b,
-                                 1.0 / (self.b * self.R), lr, self.metrics)
+                                 1.0 / gb, lr, self.metrics)
 
     def forward_backward(self, idx_offset: int) -> None:
         self._impl.forward_backward(int(idx_offset))

@@ -1,0 +1,57 @@
+"""Collective implementation selection (README.md:21-29, tf_dist_example.py:12).
+
+TF offers ``CollectiveCommunication.{AUTO, RING, NCCL}`` (TF 2.0-2.3 spelling, used by the
+reference) and ``CommunicationImplementation`` + ``CommunicationOptions`` (TF >= 2.4).  Both are
+accepted.  Mapping on this framework:
+
+* ``NCCL`` -> RCCL over xGMI through ``torch.distributed`` (backend ``"nccl"``); GPU replicas only.
+* ``RING`` -> the native C++ TCP ring (csrc/native/ring.cpp); GPU tensors are staged via host.
+* ``AUTO`` -> RCCL when every replica is a GPU, otherwise the native ring (gloo if the native
+  runtime is unavailable).
+"""
+from __future__ import annotations
+
+import enum
+from dataclasses import dataclass
+from typing import Optional
+
+
+class CommunicationImplementation(enum.Enum):
+    AUTO = "AUTO"
+    RING = "RING"
+    NCCL = "NCCL"
+
+
+# TF 2.0-2.3 name used by tf_dist_example.py:12
+CollectiveCommunication = CommunicationImplementation
+
+
+@dataclass
+class CommunicationOptions:
+    """tf.distribute.experimental.CommunicationOptions."""
+
+    bytes_per_pack: int = 0
+    timeout_seconds: Optional[float] = None
+    implementation: CommunicationImplementation = CommunicationImplementation.AUTO
+
+    def __post_init__(self):
+        if isinstance(self.implementation, str):
+            self.implementation = CommunicationImplementation(self.implementation.upper())
+        if self.bytes_per_pack < 0:
+            raise ValueError("bytes_per_pack must be >= 0")
+
+
+def normalize_options(communication=None, communication_options=None) -> CommunicationOptions:
+    if communication_options is not None and communication is not None:
+        raise ValueError("pass either `communication` or `communication_options`, not both")
+    if communication_options is not None:
+        if isinstance(communication_options, CommunicationImplementation):
+            return CommunicationOptions(implementation=communication_options)
+        return communication_options
+    if communication is None:
+        return CommunicationOptions()
+    if isinstance(communication, CommunicationOptions):
+        return communication
+    if isinstance(communication, str):
+        communication = CommunicationImplementation(communication.upper())
+    return CommunicationOptions(implementation=communication)

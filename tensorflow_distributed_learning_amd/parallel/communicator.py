@@ -1,0 +1,276 @@
+"""Cross-replica communicators (the DP communication backend).
+
+One process drives one replica (one GPU, or the CPU).  A communicator reduces tensors across all
+replicas of the job:
+
+* :class:`LocalCommunicator`  – single replica: every collective is the identity.
+* :class:`TorchCommunicator`  – ``torch.distributed`` process group.  Backend ``"nccl"`` is RCCL on
+  ROCm: ring/tree collectives over the xGMI links of an MI355X node, capturable into hipGraphs.
+  Backend ``"gloo"`` is kept as a CPU oracle for tests.
+* :class:`RingCommunicator`   – the native C++ TCP ring (``CollectiveCommunication.RING`` and CPU
+  replicas); GPU tensors are staged through pinned host memory.
+
+All communicators reduce in place and produce bit-identical results on every rank.
+"""
+from __future__ import annotations
+
+import os
+import socket
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from .. import ops
+
+_OPS = {"sum", "mean", "max", "min", "prod"}
+
+
+class Communicator:
+    name = "base"
+    capturable = False  # can be recorded inside a hipGraph capture
+
+    def __init__(self, rank: int, world_size: int, device: torch.device):
+        self.rank = int(rank)
+        self.world_size = int(world_size)
+        self.device = torch.device(device)
+
+    # -- collectives (in place) --------------------------------------------------------------
+    def all_reduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        raise NotImplementedError
+
+    def all_reduce_async(self, t: torch.Tensor, op: str = "sum"):
+        """Start an all-reduce; returns an object with ``wait()``.  Default: synchronous."""
+        self.all_reduce(t, op)
+        return _Done()
+
+    def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        raise NotImplementedError
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        """Returns a new tensor [world_size, *t.shape]."""
+        raise NotImplementedError
+
+    def barrier(self) -> None:
+        raise NotImplementedError
+
+    def shutdown(self) -> None:
+        pass
+
+    def __repr__(self):
+        return f"{type(self).__name__}(rank={self.rank}, world_size={self.world_size}, device={self.device})"
+
+
+class _Done:
+    def wait(self):
+        return None
+
+    def is_completed(self):
+        return True
+
+
+class LocalCommunicator(Communicator):
+    name = "local"
+    capturable = True
+
+    def __init__(self, device: torch.device):
+        super().__init__(0, 1, device)
+
+    def all_reduce(self, t, op="sum"):
+        if op not in _OPS:
+            raise ValueError(f"unknown reduce op {op}")
+        return t
+
+    def broadcast(self, t, src=0):
+        return t
+
+    def all_gather(self, t):
+        return t.unsqueeze(0).clone()
+
+    def barrier(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+
+_TORCH_OPS = {
+    "sum": dist.ReduceOp.SUM,
+    "max": dist.ReduceOp.MAX,
+    "min": dist.ReduceOp.MIN,
+    "prod": dist.ReduceOp.PRODUCT,
+}
+
+
+class TorchCommunicator(Communicator):
+    """torch.distributed process group (``nccl`` = RCCL over xGMI, or ``gloo``)."""
+
+    def __init__(self, backend: str, rank: int, world_size: int, device: torch.device, store=None,
+                 timeout: float = 1800.0, init: bool = True):
+        super().__init__(rank, world_size, device)
+        self.backend = backend
+        self.name = "rccl" if backend == "nccl" else backend
+        self.capturable = backend == "nccl"
+        self._owns_group = False
+        if init and not dist.is_initialized():
+            from datetime import timedelta
+
+            kw = {}
+            if backend == "nccl" and self.device.type == "cuda":
+                kw["device_id"] = self.device
+            if store is not None:
+                dist.init_process_group(backend, store=store, rank=rank, world_size=world_size,
+                                        timeout=timedelta(seconds=timeout), **kw)
+            else:
+                dist.init_process_group(backend, rank=rank, world_size=world_size,
+                                        timeout=timedelta(seconds=timeout), **kw)
+            self._owns_group = True
+        self._avg_native = backend == "nccl"
+
+    def all_reduce(self, t, op="sum"):
+        if op == "mean":
+            if self._avg_native:
+                dist.all_reduce(t, op=dist.ReduceOp.AVG)
+            else:
+                dist.all_reduce(t, op=dist.ReduceOp.SUM)
+                t.div_(self.world_size)
+            return t
+        dist.all_reduce(t, op=_TORCH_OPS[op])
+        return t
+
+    def all_reduce_async(self, t, op="sum"):
+        if op == "mean" and not self._avg_native:
+            work = dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True)
+            return _ScaleOnWait(work, t, 1.0 / self.world_size)
+        rop = dist.ReduceOp.AVG if op == "mean" else _TORCH_OPS[op]
+        return dist.all_reduce(t, op=rop, async_op=True)
+
+    def broadcast(self, t, src=0):
+        dist.broadcast(t, src=src)
+        return t
+
+    def all_gather(self, t):
+        out = torch.empty((self.world_size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.contiguous())
+        return out
+
+    def barrier(self):
+        if self.backend == "nccl" and self.device.type == "cuda":
+            dist.barrier(device_ids=[self.device.index or 0])
+        else:
+            dist.barrier()
+
+    def shutdown(self):
+        if self._owns_group and dist.is_initialized():
+            try:
+                dist.destroy_process_group()
+            except Exception:
+                pass
+            self._owns_group = False
+
+
+class _ScaleOnWait:
+    def __init__(self, work, t, s):
+        self.work, self.t, self.s = work, t, s
+
+    def wait(self):
+        self.work.wait()
+        self.t.mul_(self.s)
+
+    def is_completed(self):
+        return self.work.is_completed()
+
+
+def _my_ring_host(default: str) -> str:
+    h = os.environ.get("TDL_RING_HOST")
+    if h:
+        return h
+    if default in ("127.0.0.1", "localhost", ""):
+        return "127.0.0.1"
+    try:
+        return socket.gethostbyname(socket.gethostname())
+    except OSError:
+        return default
+
+
+class RingCommunicator(Communicator):
+    """Native C++ TCP ring collectives (csrc/native/ring.cpp)."""
+
+    name = "ring"
+
+    def __init__(self, rank: int, world_size: int, device: torch.device, store, host_hint: str = "127.0.0.1",
+                 timeout: float = 300.0, tag: str = "ring"):
+        super().__init__(rank, world_size, device)
+        N = ops.native()
+        self._ring = N.RingComm(self.rank, self.world_size, "0.0.0.0", int(timeout * 1000))
+        if self.world_size > 1:
+            me = _my_ring_host(host_hint)
+            store.set(f"{tag}/addr/{self.rank}", f"{me}:{self._ring.port}".encode())
+            right = (self.rank + 1) % self.world_size
+            addr = bytes(store.get(f"{tag}/addr/{right}")).decode()
+            h, p = addr.rsplit(":", 1)
+            self._ring.connect(h, int(p))
+        self._stage: Optional[torch.Tensor] = None
+
+    def _host(self, t: torch.Tensor):
+        if t.device.type == "cpu":
+            return t.contiguous(), False
+        n = t.numel() * t.element_size()
+        if self._stage is None or self._stage.numel() < n:
+            self._stage = torch.empty(max(n, 1 << 20), dtype=torch.uint8, pin_memory=torch.cuda.is_available())
+        h = self._stage[:n].view(t.dtype).view(t.shape)
+        h.copy_(t)
+        return h, True
+
+    def all_reduce(self, t, op="sum"):
+        if self.world_size == 1:
+            return t
+        rop = "sum" if op == "mean" else op
+        work = t
+        conv = None
+        if t.dtype in (torch.float16, torch.bfloat16):
+            conv = t
+            work = t.float()
+        h, staged = self._host(work)
+        self._ring.all_reduce(h, rop)
+        if op == "mean":
+            h.div_(self.world_size)
+        if staged or h.data_ptr() != work.data_ptr():
+            work.copy_(h)
+        if conv is not None:
+            conv.copy_(work)
+        return t
+
+    def broadcast(self, t, src=0):
+        if self.world_size == 1:
+            return t
+        h, staged = self._host(t)
+        self._ring.broadcast(h, int(src))
+        if staged or h.data_ptr() != t.data_ptr():
+            t.copy_(h)
+        return t
+
+    def all_gather(self, t):
+        src = t.detach().contiguous().cpu()
+        out = torch.empty((self.world_size,) + tuple(t.shape), dtype=t.dtype)
+        self._ring.all_gather(src, out)
+        return out.to(t.device)
+
+    def barrier(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        self._ring.barrier()
+
+    def shutdown(self):
+        self._ring.close()
+
+
+def all_reduce_coalesced(comm: Communicator, tensors: List[torch.Tensor], op: str = "sum") -> None:
+    """All-reduce a list of tensors as one flat buffer (TF's pack-by-size with one pack)."""
+    if comm.world_size == 1 or not tensors:
+        return
+    flat = torch.cat([x.reshape(-1) for x in tensors])
+    comm.all_reduce(flat, op)
+    off = 0
+    for x in tensors:
+        n = x.numel()
+        x.copy_(flat[off : off + n].view_as(x))
+        off += n

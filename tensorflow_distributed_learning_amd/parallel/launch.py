@@ -1,0 +1,226 @@
+"""Launcher: one process per replica (per GPU), optionally several TF_CONFIG tasks on one node.
+
+    # N replicas of a MirroredStrategy script on one node (torchrun-compatible env):
+    python -m tensorflow_distributed_learning_amd.launch --nproc-per-node 8 train.py
+
+    # K TF_CONFIG worker tasks x G GPUs each on one node (MultiWorkerMirroredStrategy, BASELINE
+    # config 5; README.md:61 "several cluster tasks on one physical machine"):
+    python -m tensorflow_distributed_learning_amd.launch --local-workers 2 --gpus-per-worker 4 train.py
+
+    # one task of a real multi-host cluster (README.md:156-162), G GPUs on this host:
+    TF_CONFIG='{"cluster": {...}, "task": {...}}' \\
+        python -m tensorflow_distributed_learning_amd.launch --nproc-per-node 4 train.py
+
+Children get RANK / WORLD_SIZE / LOCAL_RANK / LOCAL_WORLD_SIZE (+ MASTER_ADDR/PORT when no
+TF_CONFIG is used, + TF_CONFIG and HIP_VISIBLE_DEVICES for --local-workers).  If any child fails
+the others are terminated and the launcher exits with the failing code.
+"""
+from __future__ import annotations
+
+import argparse
+import atexit
+import json
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+from typing import Dict, List, Optional
+
+
+def free_port(host: str = "127.0.0.1") -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind((host, 0))
+        return s.getsockname()[1]
+
+
+def free_ports(n: int, host: str = "127.0.0.1") -> List[int]:
+    socks, ports = [], []
+    try:
+        for _ in range(n):
+            s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            s.bind((host, 0))
+            socks.append(s)
+            ports.append(s.getsockname()[1])
+    finally:
+        for s in socks:
+            s.close()
+    return ports
+
+
+class _Group:
+    def __init__(self):
+        self.procs: List[subprocess.Popen] = []
+
+    def start(self, cmd: List[str], env: Dict[str, str]):
+        p = subprocess.Popen(cmd, env=env, start_new_session=True)
+        self.procs.append(p)
+        return p
+
+    def terminate(self, sig=signal.SIGTERM):
+        for p in self.procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, sig)
+                except (ProcessLookupError, PermissionError):
+                    pass
+
+    def wait(self, poll: float = 0.1) -> int:
+        """Wait for all; on the first failure terminate the rest.  Returns the job exit code."""
+        try:
+            while True:
+                codes = [p.poll() for p in self.procs]
+                bad = [c for c in codes if c not in (None, 0)]
+                if bad:
+                    self.terminate()
+                    deadline = time.time() + 10
+                    while time.time() < deadline and any(p.poll() is None for p in self.procs):
+                        time.sleep(0.05)
+                    self.terminate(signal.SIGKILL)
+                    return bad[0]
+                if all(c == 0 for c in codes):
+                    return 0
+                time.sleep(poll)
+        except KeyboardInterrupt:
+            self.terminate()
+            return 130
+
+
+def _base_env(nprocs: int = 1) -> Dict[str, str]:
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if "OMP_NUM_THREADS" not in env:
+        # one replica process per GPU: do not let every process spawn a thread per core
+        env["OMP_NUM_THREADS"] = str(max(1, (os.cpu_count() or 1) // max(1, nprocs)))
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    return env
+
+
+def launch_replicas(cmd: List[str], nproc: int, master_addr: str = "127.0.0.1", master_port: Optional[int] = None,
+                    tf_config: Optional[str] = None) -> int:
+    env0 = _base_env(nproc)
+    port = master_port or free_port(master_addr)
+    g = _Group()
+    for lr in range(nproc):
+        env = dict(env0)
+        env.update(RANK=str(lr), WORLD_SIZE=str(nproc), LOCAL_RANK=str(lr), LOCAL_WORLD_SIZE=str(nproc),
+                   MASTER_ADDR=master_addr, MASTER_PORT=str(port), TDL_LAUNCHED="1")
+        if tf_config is not None:
+            env["TF_CONFIG"] = tf_config
+        g.start(cmd, env)
+    return g.wait()
+
+
+def launch_local_workers(cmd: List[str], workers: int, gpus_per_worker: int, base_port: Optional[int] = None,
+                         chief: bool = False) -> int:
+    """K TF_CONFIG tasks on this host, each with G replica processes (one per GPU)."""
+    env0 = _base_env(workers * max(1, gpus_per_worker))
+    ntasks = workers + (1 if chief else 0)
+    ports = [base_port + i for i in range(ntasks)] if base_port else free_ports(ntasks)
+    addrs = [f"127.0.0.1:{p}" for p in ports]
+    cluster = {"worker": addrs[1:] if chief else addrs}
+    if chief:
+        cluster["chief"] = [addrs[0]]
+    tasks = ([("chief", 0)] if chief else []) + [("worker", i) for i in range(workers)]
+    world = ntasks * gpus_per_worker
+    g = _Group()
+    for t_rank, (ttype, tidx) in enumerate(tasks):
+        tfc = json.dumps({"cluster": cluster, "task": {"type": ttype, "index": tidx}})
+        for lr in range(gpus_per_worker):
+            env = dict(env0)
+            env.update(TF_CONFIG=tfc, RANK=str(t_rank * gpus_per_worker + lr), WORLD_SIZE=str(world),
+                       LOCAL_RANK=str(lr), LOCAL_WORLD_SIZE=str(gpus_per_worker), TDL_LAUNCHED="1")
+            env.pop("MASTER_ADDR", None)
+            env.pop("MASTER_PORT", None)
+            if gpus_per_worker > 0 and os.environ.get("TDL_NO_GPU_PARTITION") != "1":
+                first = t_rank * gpus_per_worker
+                env["HIP_VISIBLE_DEVICES"] = ",".join(str(first + i) for i in range(gpus_per_worker))
+            g.start(cmd, env)
+    return g.wait()
+
+
+# ------------------------------------------------------------------------------------------------
+_SPAWNED: Optional[_Group] = None
+
+
+def maybe_spawn_local_replicas(n: int, spawn: Optional[bool] = None) -> Optional[dict]:
+    """MirroredStrategy started as a plain script with n > 1 devices: re-run the script once per
+    extra device (children are replicas 1..n-1, this process is replica 0).  Must run before this
+    process touches the GPU.  Returns the placement dict, or None to stay single-replica."""
+    global _SPAWNED
+    if spawn is None:
+        spawn = os.environ.get("TDL_AUTO_SPAWN", "1") == "1"
+    main = sys.argv[0] if sys.argv else ""
+    if not spawn or not main or not os.path.isfile(main) or "pytest" in os.path.basename(main) or \
+            os.environ.get("TDL_LAUNCHED") == "1":
+        return None
+    port = free_port()
+    env0 = _base_env(n)
+    g = _Group()
+    for lr in range(1, n):
+        env = dict(env0)
+        env.update(RANK=str(lr), WORLD_SIZE=str(n), LOCAL_RANK=str(lr), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TDL_LAUNCHED="1")
+        g.start([sys.executable] + sys.argv, env)
+    os.environ.update(RANK="0", WORLD_SIZE=str(n), LOCAL_RANK="0", LOCAL_WORLD_SIZE=str(n),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TDL_LAUNCHED="1")
+    _SPAWNED = g
+
+    def _join():
+        code = g.wait()
+        if code != 0:
+            sys.stderr.write(f"[tdl] a spawned replica exited with code {code}\n")
+
+    atexit.register(_join)
+    return {"rank": 0, "world_size": n, "local_rank": 0, "local_world_size": n}
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="python -m tensorflow_distributed_learning_amd.launch",
+                                 description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--nproc-per-node", "--nproc_per_node", type=int, default=None)
+    ap.add_argument("--local-workers", type=int, default=None)
+    ap.add_argument("--gpus-per-worker", type=int, default=1)
+    ap.add_argument("--chief", action="store_true", help="add a separate chief task (with --local-workers)")
+    ap.add_argument("--master-addr", default="127.0.0.1")
+    ap.add_argument("--master-port", type=int, default=None)
+    ap.add_argument("--base-port", type=int, default=None)
+    ap.add_argument("-m", dest="module", default=None, help="run a module instead of a script")
+    ap.add_argument("script", nargs="?")
+    ap.add_argument("args", nargs=argparse.REMAINDER)
+    a = ap.parse_args(argv)
+    if a.module:
+        cmd = [sys.executable, "-m", a.module] + ([a.script] if a.script else []) + a.args
+    else:
+        if not a.script:
+            ap.error("a training script is required")
+        cmd = [sys.executable, a.script] + a.args
+    if a.local_workers:
+        return launch_local_workers(cmd, a.local_workers, a.gpus_per_worker, a.base_port, chief=a.chief)
+    n = a.nproc_per_node
+    if n is None:
+        try:
+            import torch
+
+            n = max(1, torch.cuda.device_count())
+        except Exception:
+            n = 1
+    tfc = os.environ.get("TF_CONFIG")
+    if tfc:
+        # one TF_CONFIG task with n local replica processes: rank layout comes from the rendezvous
+        env0 = _base_env(n)
+        g = _Group()
+        port = a.master_port or free_port(a.master_addr)
+        for lr in range(n):
+            env = dict(env0)
+            env.update(RANK=str(lr), WORLD_SIZE=str(n), LOCAL_RANK=str(lr), LOCAL_WORLD_SIZE=str(n),
+                       MASTER_ADDR=a.master_addr, MASTER_PORT=str(port), TDL_LAUNCHED="1")
+            g.start(cmd, env)
+        return g.wait()
+    return launch_replicas(cmd, n, a.master_addr, a.master_port)
+
+
+if __name__ == "__main__":
+    sys.exit(main())
