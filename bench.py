@@ -1,0 +1,129 @@
+#!/usr/bin/env python3
+"""Headline benchmark: whole-node images/sec of the reference MNIST CNN (tf_dist_example.py)
+with global batch 64*N on N MI355X GPUs (BASELINE.json metric/config).
+
+    python bench.py                                   # N=1
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Runs the framework's real training path: MirroredStrategy (one process per GPU, RCCL over xGMI)
+-> Keras Sequential exactly as the reference builds it -> compile(SCCE from_logits, SGD 1e-3,
+SparseCategoricalAccuracy) -> the fused MI355X engine (hand-written gfx950 kernels, device-resident
+synthetic MNIST-shaped dataset with map(scale).cache().shuffle(10000).batch(64*N).repeat(),
+hipGraph-captured executions incl. the gradient all-reduce and the SGD update).
+W untimed warm-up steps, then EXACTLY K timed steps bracketed by barrier + device sync; the MAX
+time over ranks is reported by rank 0 as one JSON line.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--per-replica-batch", type=int, default=64)
+    ap.add_argument("--steps-per-execution", type=int, default=0, help="0 = auto")
+    args = ap.parse_args()
+
+    import torch
+
+    import tensorflow_distributed_learning_amd as tdl
+    from tensorflow_distributed_learning_amd.data import tfds
+    from tensorflow_distributed_learning_amd.models.mnist_cnn import build_mnist_cnn
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            print(f"bench.py: --gpus {args.gpus} needs a launcher (torch.distributed.run) with {args.gpus} ranks",
+                  file=sys.stderr)
+            sys.exit(2)
+    if world > 1 and "LOCAL_RANK" in os.environ:
+        torch.cuda.set_device(int(os.environ["LOCAL_RANK"]))
+
+    strategy = tdl.distribute.MirroredStrategy()
+    R = strategy.num_replicas_in_sync
+    rank = strategy.extended.rank
+    B = args.per_replica_batch * R
+    K, W = args.steps, args.warmup
+    spe = args.steps_per_execution or math.gcd(K, 50) or 1
+
+    # synthetic MNIST-shaped data (no network): the reference's input pipeline
+    (ds_all, info) = tfds.load("mnist", as_supervised=True, with_info=True)
+
+    def scale(image, label):
+        image = image.to(torch.float32)
+        image = image / 255
+        return image, label
+
+    train = ds_all["train"].map(scale).cache().shuffle(10000).batch(B).repeat()
+    options = tdl.data.Options()
+    options.experimental_distribute.auto_shard_policy = tdl.data.AutoShardPolicy.OFF
+    train = train.with_options(options)
+
+    with strategy.scope():
+        model = build_mnist_cnn()
+        model.compile(loss=tdl.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+                      optimizer=tdl.keras.optimizers.SGD(learning_rate=0.001),
+                      metrics=[tdl.keras.metrics.SparseCategoricalAccuracy()],
+                      steps_per_execution=spe)
+    trainer = model._get_trainer()
+    handler = trainer.prepare(train)
+    if trainer.kind != "fused" or handler is None:
+        raise SystemExit(f"bench: fused MI355X engine not selected ({getattr(model, '_fused_reason', '?')})")
+    comm = strategy.extended.communicator
+    dev = strategy.extended.device
+
+    trainer.warm_graphs(K)
+    trainer.warm_graphs(W)
+    trainer.run_train(handler, W)
+    torch.cuda.synchronize(dev)
+    comm.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    done = trainer.run_train(handler, K)
+    torch.cuda.synchronize(dev)
+    comm.barrier()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    if done != K:
+        raise SystemExit(f"bench: ran {done} steps instead of {K}")
+    t = torch.tensor([dt], dtype=torch.float64, device=dev if comm.name == "rccl" else "cpu")
+    comm.all_reduce(t, "max")
+    dt = float(t.item())
+    logs = trainer.logs()
+    ips = K * B / dt
+    if rank == 0:
+        print(json.dumps({
+            "metric": "images/sec (whole node) MNIST CNN global_batch=64*N",
+            "value": round(ips, 1),
+            "unit": "images/sec",
+            "n_gpus": R,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": round(dt / K * 1e3, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic MNIST-shaped (device-resident map(scale).cache().shuffle(10000).batch(64*N)); random init",
+            "config": {"model": "tf_dist_example.py MNIST CNN (Conv32-Pool-Conv64-Pool-Dense128-Dense10, 225,034 params)",
+                       "global_batch": B, "seq_len": None, "image_shape": [28, 28, 1],
+                       "parallelism": f"dp{R}", "engine": trainer.kind, "communicator": comm.name,
+                       "steps_per_execution": spe, "graph_captured": bool(trainer.capture),
+                       "allreduce_in_graph": bool(trainer.capture_comm and R > 1),
+                       "final_loss": round(logs["loss"], 4)},
+        }), flush=True)
+    strategy.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -133,7 +133,9 @@ class FusedMnistTrainer:
             self._steps, self._graphs = {}, {}
         policy = input_lib.effective_policy(dataset) if self.R > 1 else None
         seed = input_lib.shared_seed(self.strategy) if policy is not None and policy.name in ("DATA", "FILE") else None
-        return DeviceHandler(lp, seed, self.rank, self.R)
+        h = DeviceHandler(lp, seed, self.rank, self.R)
+        self._handlers_b = [h.b]
+        return h
 
     # ------------------------------------------------------------------ steps
     def _step(self, b: int, idx_buf: torch.Tensor, global_b: Optional[int] = None):
@@ -204,6 +206,18 @@ class FusedMnistTrainer:
         g = (graph, idx_buf, st)
         self._graphs[(K, b)] = g
         return g
+
+    def warm_graphs(self, steps: int, b: Optional[int] = None):
+        """Capture every graph ``run_train(steps)`` will replay, ahead of a timed region."""
+        if b is None and getattr(self, "_handlers_b", None):
+            b = self._handlers_b[0]
+        if b is None:
+            return
+        sizes = {self.K} if steps >= self.K else set()
+        if steps % self.K:
+            sizes.add(steps % self.K)
+        for K in sizes:
+            self._graph_for(K, b)
 
     def run_train(self, handler: "DeviceHandler", steps: int) -> int:
         done = 0
