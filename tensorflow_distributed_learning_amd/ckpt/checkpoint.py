@@ -196,6 +196,9 @@ def _restore_into(name: str, obj, tensors: Dict[str, torch.Tensor]):
                                            if k.startswith(name + "/slots/")}})
     elif hasattr(obj, "assign") and name in tensors:
         obj.assign(tensors[name])
+    elif isinstance(obj, torch.Tensor) and name in tensors:
+        with torch.no_grad():
+            obj.copy_(tensors[name].reshape(obj.shape))
     elif isinstance(obj, dict):
         for k, v in obj.items():
             _restore_into(f"{name}/{k}", v, tensors)
@@ -312,6 +315,10 @@ class CheckpointManager:
         os.makedirs(directory, exist_ok=True)
         _, allp = _read_state(directory)
         self._checkpoints = [os.path.join(directory, p) for p in allp]
+        # continue numbering after the checkpoints already in the directory
+        nums = [int(m.group(1)) for p in allp if (m := re.search(r"-(\d+)$", p))]
+        if nums:
+            checkpoint.save_counter = max(checkpoint.save_counter, max(nums))
 
     @property
     def latest_checkpoint(self) -> Optional[str]:
@@ -330,7 +337,7 @@ class CheckpointManager:
         ck.write(path)
         strategy = _strategy_of(next(iter(ck._objects.values()), None))
         if strategy.extended.is_chief:
-            self._checkpoints.append(path)
+            self._checkpoints = [p for p in self._checkpoints if p != path] + [path]
             if self.max_to_keep is not None:
                 while len(self._checkpoints) > self.max_to_keep:
                     old = self._checkpoints.pop(0)

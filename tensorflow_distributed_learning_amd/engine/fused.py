@@ -110,9 +110,12 @@ class FusedMnistTrainer:
         self._graphs = {}
         self._data_key = None
         self.capture = os.environ.get("TDL_GRAPH", "1") == "1"
-        # all-reduce inside the captured graph only when the communicator supports it
+        # all-reduce inside the captured graph only when the communicator supports it and it is
+        # enabled (TDL_CAPTURE_ALLREDUCE=1).  Default off: multi-rank RCCL capture cannot be
+        # validated on a one-GPU box (RCCL rejects two ranks on one device); the eager all-reduce
+        # costs ~30 us of host time per step, hidden behind the GPU step.
         self.capture_comm = self.comm.world_size == 1 or (self.comm.capturable and
-                                                          os.environ.get("TDL_CAPTURE_ALLREDUCE", "1") == "1")
+                                                          os.environ.get("TDL_CAPTURE_ALLREDUCE", "0") == "1")
 
     # ------------------------------------------------------------------ data
     def prepare(self, dataset):
@@ -155,6 +158,11 @@ class FusedMnistTrainer:
             st.finalize(True)
             return
         st.finalize(False)
+        self._reduce_and_update()
+
+    def _reduce_and_update(self):
+        opt = self.optimizer
+        plain = opt.momentum == 0
         if self.R > 1:
             self.comm.all_reduce(self.G, "sum")
         from .. import ops
@@ -186,17 +194,29 @@ class FusedMnistTrainer:
         idx_buf = torch.zeros(K * b, dtype=torch.int32, device=self.device)
         st = self._step(b, idx_buf)
         graph = None
-        if self.capture and (self.capture_comm or self.R == 1):
+        if self.capture:
             s = torch.cuda.Stream(self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
             torch.cuda.synchronize(self.device)
-            graph = torch.cuda.CUDAGraph()
             saved = (self.W.clone(), self.metrics_dev.clone(),
                      {k: v.clone() for k, v in self.optimizer.slots().items()})
-            with torch.cuda.graph(graph, stream=s):
+            if self.capture_comm or self.R == 1:
+                # whole execution (K steps incl. all-reduce + optimizer) in one graph
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph, stream=s):
+                    for k in range(K):
+                        st.forward_backward(k * b)
+                        self._apply(st, b * self.R)
+            else:
+                # one graph per step holding the fused fwd/bwd/finalize; the RCCL all-reduce and
+                # the SGD kernel are issued eagerly between replays
+                graph = []
                 for k in range(K):
-                    st.forward_backward(k * b)
-                    self._apply(st, b * self.R)
+                    gk = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(gk, stream=s):
+                        st.forward_backward(k * b)
+                        st.finalize(False)
+                    graph.append(gk)
             torch.cuda.synchronize(self.device)
             # capture does not execute, but be safe: restore state
             self.W.copy_(saved[0])
@@ -238,7 +258,11 @@ class FusedMnistTrainer:
             opt._sync_lr()
             graph, idx_buf, st = self._graph_for(K, b)
             idx_buf.copy_(torch.from_numpy(idx), non_blocking=False)
-            if graph is not None:
+            if isinstance(graph, list):
+                for gk in graph:
+                    gk.replay()
+                    self._reduce_and_update()
+            elif graph is not None:
                 graph.replay()
             else:
                 for k in range(K):

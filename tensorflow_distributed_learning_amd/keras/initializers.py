@@ -120,27 +120,32 @@ class VarianceScaling(Initializer):
         return {"scale": self.scale, "mode": self.mode, "distribution": self.distribution, "seed": self.seed}
 
 
-class GlorotUniform(VarianceScaling):
+class _Preset(VarianceScaling):
+    def get_config(self):
+        return {"seed": self.seed}
+
+
+class GlorotUniform(_Preset):
     def __init__(self, seed=None):
         super().__init__(1.0, "fan_avg", "uniform", seed)
 
 
-class GlorotNormal(VarianceScaling):
+class GlorotNormal(_Preset):
     def __init__(self, seed=None):
         super().__init__(1.0, "fan_avg", "truncated_normal", seed)
 
 
-class HeNormal(VarianceScaling):
+class HeNormal(_Preset):
     def __init__(self, seed=None):
         super().__init__(2.0, "fan_in", "truncated_normal", seed)
 
 
-class HeUniform(VarianceScaling):
+class HeUniform(_Preset):
     def __init__(self, seed=None):
         super().__init__(2.0, "fan_in", "uniform", seed)
 
 
-class LecunNormal(VarianceScaling):
+class LecunNormal(_Preset):
     def __init__(self, seed=None):
         super().__init__(1.0, "fan_in", "truncated_normal", seed)
 

@@ -458,7 +458,16 @@ class Model(Layer):
 
     def load_named_tensors(self, tensors: Dict[str, torch.Tensor], strict: bool = True):
         missing = []
-        by_name = {w.name: w for w in self.weights}
+        ws = self.weights
+        names = [w.name for w in ws]
+        cand = [(k, t) for k, t in tensors.items() if not k.startswith("optimizer/")]
+        if not any(n in tensors or n[:-2] in tensors for n in names) and len(cand) == len(ws) and \
+                all(tuple(t.shape) == tuple(w.shape) for (_, t), w in zip(cand, ws)):
+            # object-graph order matching (TF checkpoints match objects, not layer names)
+            for (_, t), w in zip(cand, ws):
+                w.assign(t)
+            return
+        by_name = {w.name: w for w in ws}
         for name, v in by_name.items():
             key = name if name in tensors else name[:-2] if name.endswith(":0") and name[:-2] in tensors else None
             if key is None:

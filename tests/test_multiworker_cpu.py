@@ -1,0 +1,162 @@
+"""Multi-process CPU tests: TF_CONFIG rendezvous, ring all-reduce, MultiWorkerMirroredStrategy
+world 2 end-to-end (BASELINE config 1), DATA sharding equivalence, chief-only checkpoints."""
+import json
+import os
+import subprocess
+import sys
+import textwrap
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.slow
+
+
+def _env(**kw):
+    e = dict(os.environ)
+    e["PYTHONPATH"] = ROOT
+    e["OMP_NUM_THREADS"] = "2"
+    e.pop("TF_CONFIG", None)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "TDL_LAUNCHED"):
+        e.pop(k, None)
+    e["CUDA_VISIBLE_DEVICES"] = ""
+    e["HIP_VISIBLE_DEVICES"] = ""
+    e.update(kw)
+    return e
+
+
+def _launch(tmp_path, body, args, timeout=240, env=None):
+    script = tmp_path / "job.py"
+    script.write_text(textwrap.dedent(body))
+    cmd = [sys.executable, "-m", "tensorflow_distributed_learning_amd.launch"] + args + [str(script), str(tmp_path)]
+    r = subprocess.run(cmd, env=_env(TDL_NO_GPU_PARTITION="1", **(env or {})), cwd=ROOT, capture_output=True,
+                       text=True, timeout=timeout)
+    return r
+
+
+def _results(tmp_path, n):
+    return [json.load(open(tmp_path / f"out{r}.json")) for r in range(n)]
+
+
+def test_mwms_world2_trains_identically(tmp_path):
+    body = """
+    import json, os, sys, numpy as np, torch
+    import tensorflow_distributed_learning_amd as tdl
+    from tensorflow_distributed_learning_amd.compat import tf, tfds
+    from tensorflow_distributed_learning_amd.models.mnist_cnn import build_mnist_cnn
+    out = sys.argv[1]
+    strategy = tf.distribute.experimental.MultiWorkerMirroredStrategy(
+        tf.distribute.experimental.CollectiveCommunication.AUTO)
+    R = strategy.num_replicas_in_sync
+    (ds, info) = tfds.load('mnist', as_supervised=True, with_info=True)
+    def scale(image, label):
+        image = tf.cast(image, tf.float32)
+        image /= 255
+        return image, label
+    train = ds['train'].take(2048).map(scale).cache().shuffle(1000).batch(64 * R)
+    opts = tf.data.Options()
+    opts.experimental_distribute.auto_shard_policy = tf.data.experimental.AutoShardPolicy.OFF
+    train = train.with_options(opts)
+    with strategy.scope():
+        m = build_mnist_cnn()
+        m.compile(loss=tf.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+                  optimizer=tf.keras.optimizers.SGD(learning_rate=0.05),
+                  metrics=[tf.keras.metrics.SparseCategoricalAccuracy()])
+    h = m.fit(x=train, epochs=3, steps_per_epoch=5, verbose=0)
+    ck = os.path.join(out, "ckpt")
+    m.save(os.path.join(out, "saved"))
+    w = np.concatenate([x.ravel() for x in m.get_weights()])
+    json.dump({"rank": strategy.extended.rank, "R": R, "comm": strategy.extended.communicator.name,
+               "task": [strategy.extended.task_type, strategy.extended.task_id],
+               "hash": float(np.abs(w).sum()), "w0": float(w[0]), "loss": h.history["loss"]},
+              open(os.path.join(out, f"out{strategy.extended.rank}.json"), "w"))
+    """
+    r = _launch(tmp_path, body, ["--local-workers", "2"])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    a, b = _results(tmp_path, 2)
+    assert a["R"] == 2 and a["comm"] == "ring" and a["task"] == ["worker", 0] and b["task"] == ["worker", 1]
+    assert a["hash"] == b["hash"] and a["w0"] == b["w0"]  # replicas stay bit-identical
+    assert a["loss"] == b["loss"]  # logged metrics are cross-replica reduced
+    assert a["loss"][-1] < a["loss"][0]
+    assert os.path.exists(tmp_path / "saved" / "saved_model.json")  # chief wrote
+    assert not any(p.startswith("workertemp") for p in os.listdir(tmp_path))  # non-chief temp removed
+
+
+def test_data_sharding_equals_single_replica_global_batch(tmp_path):
+    body = """
+    import json, os, sys, numpy as np, torch
+    import tensorflow_distributed_learning_amd as tdl
+    from tensorflow_distributed_learning_amd.models.mnist_cnn import build_mnist_cnn
+    out = sys.argv[1]
+    impl = os.environ.get("IMPL", "AUTO")
+    strategy = tdl.distribute.MirroredStrategy(communication=impl)
+    R = strategy.num_replicas_in_sync
+    tdl.keras.utils.set_random_seed(5)
+    from tensorflow_distributed_learning_amd.data.tfds import synthetic_mnist
+    x, y = synthetic_mnist(512, 2)
+    ds = tdl.data.Dataset.from_tensor_slices((x.reshape(-1, 28, 28, 1).astype(np.float32) / 255, y))
+    ds = ds.shuffle(512, seed=9).batch(128)   # AUTO -> DATA sharding: disjoint slices of each global batch
+    with strategy.scope():
+        m = build_mnist_cnn()
+        m.compile(loss=tdl.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+                  optimizer=tdl.keras.optimizers.SGD(0.1), metrics=["accuracy"])
+    h = m.fit(ds, epochs=2, verbose=0)
+    w = np.concatenate([v.ravel() for v in m.get_weights()])
+    np.save(os.path.join(out, f"w{strategy.extended.rank}_{R}.npy"), w)
+    json.dump({"loss": h.history["loss"], "comm": strategy.extended.communicator.name},
+              open(os.path.join(out, f"out{strategy.extended.rank}.json"), "w"))
+    """
+    r = _launch(tmp_path, body, ["--nproc-per-node", "1"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    single = np.load(tmp_path / "w0_1.npy")
+    l1 = _results(tmp_path, 1)[0]["loss"]
+    for impl in ("RING", "AUTO"):
+        r = _launch(tmp_path, body, ["--nproc-per-node", "2"], env={"IMPL": impl})
+        assert r.returncode == 0, r.stderr[-3000:]
+        w0, w1 = np.load(tmp_path / "w0_2.npy"), np.load(tmp_path / "w1_2.npy")
+        assert np.array_equal(w0, w1)
+        np.testing.assert_allclose(w0, single, rtol=1e-4, atol=1e-6)
+        res = _results(tmp_path, 2)
+        np.testing.assert_allclose(res[0]["loss"], l1, rtol=1e-4)
+
+
+def test_duplicate_task_rejected_and_ps_refused(tmp_path):
+    body = """
+    import sys
+    import tensorflow_distributed_learning_amd as tdl
+    try:
+        s = tdl.distribute.MultiWorkerMirroredStrategy(timeout=20)
+        print("JOINED", s.extended.rank, flush=True)
+        import time; time.sleep(6)  # keep the cluster up while the duplicate tries to join
+    except Exception as e:
+        print("ERR", type(e).__name__, e)
+        sys.exit(3)
+    """
+    from tensorflow_distributed_learning_amd.parallel.launch import free_ports
+
+    p0, p1 = free_ports(2)
+    tfc = json.dumps({"cluster": {"worker": [f"127.0.0.1:{p0}", f"127.0.0.1:{p1}"]}, "task": {"type": "worker", "index": 1}})
+    script = tmp_path / "dup.py"
+    script.write_text(textwrap.dedent(body))
+    chief = json.dumps({"cluster": {"worker": [f"127.0.0.1:{p0}", f"127.0.0.1:{p1}"]}, "task": {"type": "worker", "index": 0}})
+    procs = [subprocess.Popen([sys.executable, str(script)], env=_env(TF_CONFIG=c), stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True) for c in (chief, tfc, tfc)]
+    outs = [p.communicate(timeout=120)[0] for p in procs]
+    # exactly one of the two processes claiming worker/1 is rejected with a clear message
+    assert sum("already taken" in o for o in outs) == 1, outs
+    assert "JOINED 0" in outs[0]
+    ps = json.dumps({"cluster": {"worker": ["127.0.0.1:1"], "ps": ["127.0.0.1:2"]}, "task": {"type": "ps", "index": 0}})
+    r = subprocess.run([sys.executable, str(script)], env=_env(TF_CONFIG=ps), capture_output=True, text=True, timeout=60)
+    assert r.returncode == 3 and "ps" in r.stdout
+
+
+def test_launcher_propagates_failure(tmp_path):
+    body = """
+    import os, sys, time
+    if os.environ["RANK"] == "1":
+        sys.exit(7)
+    time.sleep(60)
+    """
+    r = _launch(tmp_path, body, ["--nproc-per-node", "2"], timeout=60)
+    assert r.returncode == 7
