@@ -379,7 +379,7 @@ class MirroredStrategy(Strategy):
                     raise ValueError(f"local rank {lr} has no device in {devices}")
                 dev = devs[lr]
             else:
-                dev = torch.device("cuda", lr) if torch.cuda.device_count() > lr else torch.device("cpu")
+                dev = _replica_device(lr)
             if dev.type == "cuda":
                 torch.cuda.set_device(dev)
             comm = _select_communicator(opts.implementation, dev, launched["rank"], launched["world_size"],
@@ -450,7 +450,7 @@ class MultiWorkerMirroredStrategy(Strategy):
                 raise ClusterConfigError(
                     "gpus_per_worker > 1 needs one process per GPU: start each task with "
                     "`python -m tensorflow_distributed_learning_amd.launch --nproc-per-node G`")
-            dev = (torch.device("cuda", lr) if torch.cuda.device_count() > lr else torch.device("cpu"))
+            dev = _replica_device(lr)
             if dev.type == "cuda":
                 torch.cuda.set_device(dev)
             rendezvous = Rendezvous(cfg, local_rank=lr, num_local=nlocal, timeout=timeout)
@@ -470,7 +470,7 @@ class _LocalPlacement:
     def resolve(launched, gpus_per_worker):
         if launched is not None:
             lr = launched["local_rank"]
-            dev = torch.device("cuda", lr) if torch.cuda.device_count() > lr else torch.device("cpu")
+            dev = _replica_device(lr)
             if dev.type == "cuda":
                 torch.cuda.set_device(dev)
             return launched["rank"], launched["world_size"], lr, dev
@@ -491,3 +491,15 @@ class experimental:  # noqa: N801 - tf.distribute.experimental namespace
     CollectiveCommunication = CollectiveCommunication
     CommunicationImplementation = CommunicationImplementation
     CommunicationOptions = CommunicationOptions
+
+
+def _replica_device(local_rank: int) -> torch.device:
+    """GPU of a replica process: cuda:<local_rank> (one process per GPU).  TDL_SHARE_GPU=1 maps
+    several replica processes onto the visible GPUs round-robin (tests with the RING communicator on
+    a one-GPU box; RCCL itself refuses two ranks on one device)."""
+    n = torch.cuda.device_count()
+    if n == 0:
+        return torch.device("cpu")
+    if os.environ.get("TDL_SHARE_GPU") == "1":
+        return torch.device("cuda", local_rank % n)
+    return torch.device("cuda", local_rank) if n > local_rank else torch.device("cpu")

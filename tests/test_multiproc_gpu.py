@@ -1,0 +1,60 @@
+"""Fused MI355X engine with 2 replica processes sharing the box's GPU over the native RING
+communicator: replicas stay bit-identical and train like one replica on the global batch."""
+import json
+import os
+import subprocess
+import sys
+import textwrap
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+BODY = """
+import json, os, sys, numpy as np, torch
+import tensorflow_distributed_learning_amd as tdl
+from tensorflow_distributed_learning_amd.models.mnist_cnn import build_mnist_cnn
+from tensorflow_distributed_learning_amd.data.tfds import synthetic_mnist
+out = sys.argv[1]
+strategy = tdl.distribute.MirroredStrategy(communication="RING")
+R = strategy.num_replicas_in_sync
+tdl.keras.utils.set_random_seed(5)
+x, y = synthetic_mnist(2048, 2)
+ds = tdl.data.Dataset.from_tensor_slices((x.reshape(-1, 28, 28, 1), y))
+ds = ds.map(lambda i, l: (i.to(torch.float32) / 255, l)).cache().shuffle(2048, seed=9).batch(128).repeat()
+with strategy.scope():
+    m = build_mnist_cnn()
+    m.compile(loss=tdl.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+              optimizer=tdl.keras.optimizers.SGD(0.1), metrics=["sparse_categorical_accuracy"],
+              steps_per_execution=4)
+h = m.fit(ds, epochs=2, steps_per_epoch=8, verbose=0)
+w = np.concatenate([v.ravel() for v in m.get_weights()])
+np.save(os.path.join(out, f"w{strategy.extended.rank}_{R}.npy"), w)
+json.dump({"loss": h.history["loss"], "engine": m._trainer.kind, "comm": strategy.extended.communicator.name},
+          open(os.path.join(out, f"r{strategy.extended.rank}_{R}.json"), "w"))
+"""
+
+
+def _run(tmp_path, n):
+    s = tmp_path / "job.py"
+    s.write_text(textwrap.dedent(BODY))
+    env = dict(os.environ, PYTHONPATH=ROOT, TDL_SHARE_GPU="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "TF_CONFIG"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-m", "tensorflow_distributed_learning_amd.launch", "--nproc-per-node", str(n),
+                        str(s), str(tmp_path)], env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+
+
+def test_fused_two_replicas_match_single(tmp_path):
+    _run(tmp_path, 1)
+    _run(tmp_path, 2)
+    r1 = json.load(open(tmp_path / "r0_1.json"))
+    a, b = (json.load(open(tmp_path / f"r{i}_2.json")) for i in range(2))
+    assert r1["engine"] == a["engine"] == "fused" and a["comm"] == "ring"
+    w0, w1, ws = (np.load(tmp_path / f) for f in ("w0_2.npy", "w1_2.npy", "w0_1.npy"))
+    assert np.array_equal(w0, w1)
+    np.testing.assert_allclose(w0, ws, rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(a["loss"], r1["loss"], rtol=1e-4)
