@@ -47,9 +47,10 @@ class MnistStep {
     A2_ = at::empty({b * 1600}, u8);
     H_ = at::empty({b * 128}, f);
     dH_ = at::empty({b * 128}, f);
-    dC2_ = at::empty({b * 25 * 4 * 64}, f);
-    part2_ = at::zeros({tdl::kMnistConv2Splits * tdl::kMnistPart2Rows * 64}, f);
-    part1_ = at::zeros({(int64_t)tdl::mnist_nb7((int)b) * tdl::kMnistPart1Cols}, f);
+    dC2_ = at::empty({b * 100 * 64}, f);
+    part2_ = at::zeros({b * tdl::kMnistPart2Rows * 64}, f);
+    part1_ = at::zeros({(int64_t)tdl::mnist_part1_rows((int)b) * tdl::kMnistPart1Cols}, f);
+    part4_ = at::zeros({(int64_t)tdl::mnist_head_blocks((int)b) * 1290}, f);
     a_ = tdl::MnistArgs{};
     a_.X = X_.data_ptr<float>();
     a_.Y = Y_.data_ptr<int>();
@@ -67,6 +68,7 @@ class MnistStep {
     a_.dC2 = dC2_.data_ptr<float>();
     a_.part2 = part2_.data_ptr<float>();
     a_.part1 = part1_.data_ptr<float>();
+    a_.part4 = part4_.data_ptr<float>();
     a_.metrics = metrics_.data_ptr<float>();
     a_.lr = lr_.data_ptr<float>();
     a_.b = (int)b;
@@ -88,8 +90,7 @@ class MnistStep {
       case 3: tdl::mnist_dense1(a_, s); break;
       case 4: tdl::mnist_head(a_, s); break;
       case 5: tdl::mnist_dense1_bwd(a_, s); break;
-      case 6: tdl::mnist_conv2_wgrad(a_, s); break;
-      case 7: tdl::mnist_conv2_dgrad(a_, s); break;
+      case 6: tdl::mnist_conv_bwd(a_, s); break;
       case 9: tdl::mnist_finalize(a_, apply_sgd, s); break;
       default: TORCH_CHECK(false, "unknown stage");
     }
@@ -104,8 +105,7 @@ class MnistStep {
     tdl::mnist_dense1(a_, s);
     tdl::mnist_head(a_, s);
     tdl::mnist_dense1_bwd(a_, s);
-    tdl::mnist_conv2_wgrad(a_, s);
-    tdl::mnist_conv2_dgrad(a_, s);
+    tdl::mnist_conv_bwd(a_, s);
   }
 
   void finalize(bool apply_sgd) { tdl::mnist_finalize(a_, apply_sgd, cur_stream()); }
@@ -123,7 +123,7 @@ class MnistStep {
 
  private:
   at::Tensor X_, Y_, idx_, W_, G_, lr_, metrics_;
-  at::Tensor P1_, A1_, P2_, A2_, H_, dH_, dC2_, part2_, part1_;
+  at::Tensor P1_, A1_, P2_, A2_, H_, dH_, dC2_, part2_, part1_, part4_;
   tdl::MnistArgs a_;
 };
 

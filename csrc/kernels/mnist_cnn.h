@@ -27,9 +27,10 @@ struct MnistArgs {
   uint8_t* A2;        // [b,1600]
   float* H;           // [b,128] relu(dense1)
   float* dH;          // [b,128]
-  float* dC2;         // [b,25,4,64] grad of conv2 output, pool-window-major
-  float* part2;       // [4][304][64] split-K partials of conv2 wgrad (+ bias row 288)
-  float* part1;       // [nb7][320] per-block partials of conv1 wgrad (+ bias)
+  float* dC2;         // [b,10,10,64] grad of the (used 10x10 part of the) conv2 output
+  float* part2;       // [b][289][64] per-image partials of conv2 wgrad (row 288 = bias)
+  float* part1;       // [2b][320] per-(image, pixel-half) partials of conv1 wgrad (+ bias)
+  float* part4;       // [ceil(b/4)][1290] per-workgroup partials of dense2 wgrad (+ bias)
   float* metrics;     // [0] loss sum, [1] correct, [2] count
   const float* lr;    // device scalar learning rate
   int b;              // per-replica batch
@@ -37,18 +38,17 @@ struct MnistArgs {
   int nslab;          // slab length (floats)
 };
 
-constexpr int kMnistConv2Splits = 4;
-constexpr int kMnistPart2Rows = 304;
+constexpr int kMnistPart2Rows = 289;
 constexpr int kMnistPart1Cols = 320;
-__host__ __device__ inline int mnist_nb7(int b) { return (b * 169 + 63) / 64; }
+__host__ __device__ inline int mnist_part1_rows(int b) { return 2 * b; }
+__host__ __device__ inline int mnist_head_blocks(int b) { return (b + 3) / 4; }
 
 void mnist_conv1_pool(const MnistArgs& a, hipStream_t s);
 void mnist_conv2_pool(const MnistArgs& a, hipStream_t s);
 void mnist_dense1(const MnistArgs& a, hipStream_t s);
 void mnist_head(const MnistArgs& a, hipStream_t s);
 void mnist_dense1_bwd(const MnistArgs& a, hipStream_t s);
-void mnist_conv2_wgrad(const MnistArgs& a, hipStream_t s);
-void mnist_conv2_dgrad(const MnistArgs& a, hipStream_t s);
+void mnist_conv_bwd(const MnistArgs& a, hipStream_t s);
 void mnist_finalize(const MnistArgs& a, bool apply_sgd, hipStream_t s);
 
 // Plain SGD over a flat slab: w -= lr * g  (lr read from device memory).

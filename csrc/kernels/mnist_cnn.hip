@@ -1,7 +1,7 @@
 // Fused MNIST-CNN training step for gfx950 (MI355X), f32 end to end.
 //
 // Replaces, for the reference model of tf_dist_example.py:40-52, the ~35 TF/cuDNN/Eigen kernels
-// of one replica step by eight launches:
+// of one replica step by seven launches:
 //
 //   K1 conv1_pool   : gather(idx) + conv1 3x3 (1->32) + bias + ReLU + maxpool2  (VALU; K=9)
 //   K2 conv2_pool   : conv2 3x3 (32->64) implicit GEMM on v_mfma_f32_16x16x4_f32, epilogue
@@ -10,10 +10,10 @@
 //   K4 head         : dense2 + softmax-xent + dlogits*(1/(b*R)) + loss/accuracy accumulators
 //                     + dW4/db4 + dH (ReLU mask), one workgroup
 //   K5 dense1_bwd   : dW3 = P2^T dH, db3, dP2 = dH W3^T -> pool2/ReLU backward scatter to dC2
-//   K6 conv2_wgrad  : dW2 (+db2 as an extra "ones" row) split-K MFMA partial slabs
-//   K7 conv2_dgrad  : dP1 = dC2 (*) W2^T on MFMA, epilogue = pool1/ReLU backward AND conv1
-//                     wgrad (dC1 is never materialised), per-block partial slabs
-//   K9 finalize     : deterministic reduction of the partial slabs into the flat gradient slab,
+//   KC conv_bwd     : per image (x4 parts), LDS-staged: dW2 (+db2 as an extra "ones" row) and
+//                     dP1 = dC2 (*) W2^T on MFMA with pool1/ReLU backward AND conv1 wgrad in
+//                     the epilogue (dC1 is never materialised); per-image partial slabs
+//   KF finalize     : deterministic reduction of the partial slabs into the flat gradient slab,
 //                     optionally fused with the SGD update (single replica)
 //
 // All reductions are slab-based (no float atomics) so every replica computes bit-identical
@@ -172,101 +172,62 @@ __global__ __launch_bounds__(512) void k_dense1(MnistArgs a) {
 }
 
 // --------------------------------------------------------------------------------------------
-// K4: dense2 + sparse softmax cross-entropy + metrics + dense2 grads + dH.  One workgroup.
+// K4: dense2 + sparse softmax cross-entropy + metrics + dense2 grads + dH.  ceil(b/4) workgroups.
 // --------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_head(MnistArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int b = a.b, tid = threadIdx.x;
-  float* sH = sm;                 // b*128
-  float* sW = sH + b * 128;       // 1280
-  float* sB = sW + 1280;          // 16
-  float* sD = sB + 16;            // b*16 logits -> dlogits
-  float* sRed = sD + b * 16;      // 64
-  // every LDS-latency chain below is split over 4 independent accumulators and unrolled, so
-  // the single workgroup is issue-bound rather than LDS-latency-bound.
-  for (int o = tid; o < b * 32; o += 1024) st4(sH + o * 4, ld4(a.H + o * 4));
-  for (int o = tid; o < 1280; o += 1024) sW[o] = a.W[a.ow4 + o];
-  if (tid < 10) sB[tid] = a.W[a.ob4 + tid];
-  const int yl = (tid < b) ? a.Y[a.idx[tid]] : 0;  // prefetch labels (b <= 1024 rows per pass)
+__global__ __launch_bounds__(256) void k_head(MnistArgs a) {
+  // One wave per batch row: lane l owns hidden features l and l+64.  Logits are wave
+  // reductions; softmax / loss / dlogits are computed redundantly by every lane; dH is written
+  // per lane; dW4/db4 per-workgroup partials (4 rows) go to part4, reduced by K5's tail blocks.
+  __shared__ float sP[4][1290 + 2];
+  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + wave;
+  const bool live = r < a.b;
+  const int rr = live ? r : 0;
+  const float* w4 = a.W + a.ow4;
+  float wa[10], wb[10];
+#pragma unroll
+  for (int c = 0; c < 10; ++c) { wa[c] = w4[l * 10 + c]; wb[c] = w4[(l + 64) * 10 + c]; }
+  const float h0 = a.H[rr * 128 + l], h1 = a.H[rr * 128 + l + 64];
+  const int y = a.Y[a.idx[rr]];
+  float lg[10];
+#pragma unroll
+  for (int c = 0; c < 10; ++c) lg[c] = wave_sum(fmaf(h0, wa[c], h1 * wb[c])) + a.W[a.ob4 + c];
+  float m = lg[0];
+  int am = 0;
+#pragma unroll
+  for (int c = 1; c < 10; ++c)
+    if (lg[c] > m) { m = lg[c]; am = c; }
+  float se = 0.f;
+#pragma unroll
+  for (int c = 0; c < 10; ++c) se += expf(lg[c] - m);
+  const float lse = m + logf(se);
+  float ly = lg[0];
+#pragma unroll
+  for (int c = 1; c < 10; ++c) ly = (c == y) ? lg[c] : ly;
+  float dl[10];
+  const float sc = live ? a.scale : 0.f;
+#pragma unroll
+  for (int c = 0; c < 10; ++c) dl[c] = (expf(lg[c] - lse) - (c == y ? 1.f : 0.f)) * sc;
+  float d0 = 0.f, d1 = 0.f;
+#pragma unroll
+  for (int c = 0; c < 10; ++c) { d0 = fmaf(dl[c], wa[c], d0); d1 = fmaf(dl[c], wb[c], d1); }
+  if (live) {
+    a.dH[r * 128 + l] = h0 > 0.f ? d0 : 0.f;
+    a.dH[r * 128 + l + 64] = h1 > 0.f ? d1 : 0.f;
+  }
+#pragma unroll
+  for (int c = 0; c < 10; ++c) {
+    sP[wave][l * 10 + c] = h0 * dl[c];
+    sP[wave][(l + 64) * 10 + c] = h1 * dl[c];
+  }
+  if (l < 10) sP[wave][1280 + l] = dl[l];
   __syncthreads();
-  for (int o = tid; o < b * 10; o += 1024) {
-    const int r = o / 10, c = o - r * 10;
-    const f4* h4 = reinterpret_cast<const f4*>(sH + r * 128);
-    float s0 = sB[c], s1 = 0.f, s2 = 0.f, s3 = 0.f;
-#pragma unroll 8
-    for (int k4 = 0; k4 < 32; ++k4) {
-      const f4 h = h4[k4];
-      const float* w = sW + k4 * 40 + c;
-      s0 = fmaf(h.x, w[0], s0);
-      s1 = fmaf(h.y, w[10], s1);
-      s2 = fmaf(h.z, w[20], s2);
-      s3 = fmaf(h.w, w[30], s3);
-    }
-    sD[r * 16 + c] = (s0 + s1) + (s2 + s3);
-  }
-  __syncthreads();
-  float lsum = 0.f, lcor = 0.f;
-  for (int r = tid; r < b; r += 1024) {
-    float* l = sD + r * 16;
-    const int y = (r < 1024 && r == tid) ? yl : a.Y[a.idx[r]];
-    float v[10];
-#pragma unroll
-    for (int c = 0; c < 10; ++c) v[c] = l[c];
-    float m = v[0];
-    int am = 0;
-#pragma unroll
-    for (int c = 1; c < 10; ++c)
-      if (v[c] > m) { m = v[c]; am = c; }
-    float se = 0.f;
-#pragma unroll
-    for (int c = 0; c < 10; ++c) se += expf(v[c] - m);
-    const float lse = m + logf(se);
-    float ly = v[0];
-#pragma unroll
-    for (int c = 1; c < 10; ++c) ly = (c == y) ? v[c] : ly;
-    lsum += lse - ly;
-    lcor += (am == y) ? 1.f : 0.f;
-#pragma unroll
-    for (int c = 0; c < 10; ++c) l[c] = (expf(v[c] - lse) - (c == y ? 1.f : 0.f)) * a.scale;
-  }
-  lsum = wave_sum(lsum);
-  lcor = wave_sum(lcor);
-  if ((tid & 63) == 0) { sRed[tid >> 6] = lsum; sRed[32 + (tid >> 6)] = lcor; }
-  __syncthreads();
-  if (tid == 0) {
-    float s = 0.f, c = 0.f;
-    for (int w = 0; w < 16; ++w) { s += sRed[w]; c += sRed[32 + w]; }
-    a.metrics[0] += s;
-    a.metrics[1] += c;
-    a.metrics[2] += (float)b;
-  }
-  // dW4 (1280) and db4 (10): sum over rows, 4 accumulators
-  for (int o = tid; o < 1290; o += 1024) {
-    const bool bias = o >= 1280;
-    const int k = bias ? 0 : o / 10, c = bias ? o - 1280 : o - (o / 10) * 10;
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    int r = 0;
-    for (; r + 3 < b; r += 4) {
-      const float h0 = bias ? 1.f : sH[r * 128 + k], h1 = bias ? 1.f : sH[(r + 1) * 128 + k];
-      const float h2 = bias ? 1.f : sH[(r + 2) * 128 + k], h3 = bias ? 1.f : sH[(r + 3) * 128 + k];
-      s0 = fmaf(h0, sD[r * 16 + c], s0);
-      s1 = fmaf(h1, sD[(r + 1) * 16 + c], s1);
-      s2 = fmaf(h2, sD[(r + 2) * 16 + c], s2);
-      s3 = fmaf(h3, sD[(r + 3) * 16 + c], s3);
-    }
-    for (; r < b; ++r) s0 = fmaf(bias ? 1.f : sH[r * 128 + k], sD[r * 16 + c], s0);
-    a.G[(bias ? a.ob4 : a.ow4) + (bias ? c : o)] = (s0 + s1) + (s2 + s3);
-  }
-  for (int o = tid; o < b * 128; o += 1024) {
-    const int r = o >> 7, k = o & 127;
-    const float h = sH[o];
-    const f4 d0 = ld4(sD + r * 16), d1 = ld4(sD + r * 16 + 4);
-    const float* w = sW + k * 10;
-    float s = d0.x * w[0];
-    s = fmaf(d0.y, w[1], s); s = fmaf(d0.z, w[2], s); s = fmaf(d0.w, w[3], s);
-    s = fmaf(d1.x, w[4], s); s = fmaf(d1.y, w[5], s); s = fmaf(d1.z, w[6], s); s = fmaf(d1.w, w[7], s);
-    s = fmaf(sD[r * 16 + 8], w[8], s); s = fmaf(sD[r * 16 + 9], w[9], s);
-    a.dH[o] = h > 0.f ? s : 0.f;
+  for (int o = threadIdx.x; o < 1290; o += 256)
+    a.part4[(size_t)blockIdx.x * 1290 + o] = (sP[0][o] + sP[1][o]) + (sP[2][o] + sP[3][o]);
+  if (l == 0 && live) {
+    atomicAdd(&a.metrics[0], lse - ly);
+    atomicAdd(&a.metrics[1], am == y ? 1.f : 0.f);
+    atomicAdd(&a.metrics[2], 1.f);
   }
 }
 
@@ -341,215 +302,254 @@ __global__ __launch_bounds__(256) void k_dense1_bwd(MnistArgs a) {
         const size_t e = (size_t)rr * 1600 + k;
         const float v = a.P2[e] > 0.f ? acc[r] : 0.f;
         const unsigned qa = a.A2[e];
-        float* d = a.dC2 + ((size_t)(rr * 25 + pp) * 4) * 64 + co;
+        const int ph = pp / 5, pw = pp - ph * 5;
+        float* d = a.dC2 + ((size_t)(rr * 10 + 2 * ph) * 10 + 2 * pw) * 64 + co;  // [b][10][10][64]
         d[0] = qa == 0 ? v : 0.f;
         d[64] = qa == 1 ? v : 0.f;
-        d[128] = qa == 2 ? v : 0.f;
-        d[192] = qa == 3 ? v : 0.f;
+        d[640] = qa == 2 ? v : 0.f;
+        d[704] = qa == 3 ? v : 0.f;
       }
     }
-  } else {
+  } else if (blk == 200 + nP) {
     if (threadIdx.x < 128) {
       float s = 0.f;
       for (int r = 0; r < b; ++r) s += a.dH[r * 128 + threadIdx.x];
       a.G[a.ob3 + threadIdx.x] = s;
     }
+  } else {
+    // dW4 / db4 = sum of the head's per-workgroup partials
+    const int o = (blk - 201 - nP) * 256 + threadIdx.x;
+    if (o < 1290) {
+      const int nh = mnist_head_blocks(b);
+      float s = 0.f;
+      for (int j = 0; j < nh; ++j) s += a.part4[(size_t)j * 1290 + o];
+      a.G[o < 1280 ? a.ow4 + o : a.ob4 + (o - 1280)] = s;
+    }
   }
 }
 
 // --------------------------------------------------------------------------------------------
-// K6: conv2 weight gradient.  M = 288 (+16 bias rows) = 19 tiles, N = 64 = 4 tiles,
-// K = b*25 pool windows x 4 positions; one MFMA k-step == one pool window (k-slot g == dy*2+dx).
-// grid = 76 tiles x 4 splits; each of the 4 waves takes 1/16 of the windows; the 4 waves of a
-// block reduce through LDS and the 4 splits are summed (deterministically) by K9.
+// KC: conv backward per image.  Workgroup = (image, part p in 0..3), 8 waves, LDS-staged:
+//   dCs  [15][15][68]  grad of conv2 output, zero border of 2 (no bounds checks in dgrad)
+//   P1s  [169][36]     pooled conv1 activations (stride 36: conflict-free ds_read_b128)
+//   Xs   [784]         input image
+//   Wd   [9][16][16][4] W2 for this part's 16 input channels in MFMA fragment order
+// Work of a part: conv2 wgrad for output channels [16p, 16p+16) over the image's 100 positions
+// (19 tiles incl. the bias row, 25 k-steps each) + conv2 dgrad for channel half h = p & 1 and
+// pixel half p >> 1 (6 tiles, 144 k-steps each) whose epilogue does pool1/relu backward and
+// conv1 wgrad.  Outputs are per-image partial slabs, reduced deterministically by KF.
 // --------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_conv2_wgrad(MnistArgs a) {
-  __shared__ float red[4][256];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+constexpr int kDcStride = 68, kDcDim = 15, kP1Stride = 36;
+constexpr int kLdsDc = kDcDim * kDcDim * kDcStride;   // 15300
+constexpr int kLdsP1 = 169 * kP1Stride;              // 6084
+constexpr int kLdsWd = 9 * 16 * 16 * 4;              // 9216
+constexpr int kLdsConvBwd = kLdsDc + kLdsP1 + 784 + kLdsWd + 8 * 10 * 16;
+
+__global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* dCs = sm;
+  float* P1s = dCs + kLdsDc;
+  float* Xs = P1s + kLdsP1;
+  float* Wd = Xs + 784;
+  float* red = Wd + kLdsWd;  // [8 waves][10][16]
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int i = lane & 15, g = lane >> 4;
-  const int tile = blockIdx.x >> 2, split = blockIdx.x & 3;
-  const int mt = tile >> 2, nt = tile & 3;
-  const int slice = split * 4 + wave;
-  const int NW = a.b * 25;
-  const int chunk = (NW + 15) / 16;
-  const int w0 = slice * chunk, w1 = min(NW, w0 + chunk);
-  const bool bias_tile = mt == 18;
-  const int k = mt * 16 + i;
-  const int kk9 = bias_tile ? 0 : (k >> 5), ci = k & 31;
-  const int kh = kk9 / 3, kw = kk9 - kh * 3;
-  const int dy = g >> 1, dx = g & 1;
-  const float* pa = a.P1 + ((dy + kh) * 13 + (dx + kw)) * 32 + ci;
-  const float* pb = a.dC2 + g * 64 + nt * 16 + i;
-  const float one = (i == 0) ? 1.f : 0.f;
-  // windows in batches of 16, double-buffered: batch j+1's 32 loads are in flight while the
-  // MFMAs of batch j run.
-  f4 acc0 = zero4(), acc1 = zero4();
-  float ca[16], cb[16], na[16], nb[16];
-  auto load = [&](int base, float (&ra)[16], float (&rb)[16]) {
+  const int bi = blockIdx.x >> 2, p = blockIdx.x & 3;
+  const int h = p & 1, half = p >> 1;
+  // ---- stage everything in LDS: every global load of the thread is issued first (one memory
+  // round trip for the whole staging), then all LDS stores.  Out-of-range slots load a valid
+  // address and are zeroed by a multiply (no per-element branch around a load). ----
+  constexpr int kIdc = (kLdsDc / 4 + 511) / 512, kIp1 = (169 * 8 + 511) / 512, kIwd = (kLdsWd / 4 + 511) / 512;
+  f4 vdc[kIdc], vp1[kIp1], vwd[kIwd], vx;
+  float mdc[kIdc];
+  const float* dcb = a.dC2 + (size_t)bi * 6400;
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int w = min(base + s, w1 - 1);
-      const int bi0 = w / 25, pp0 = w - bi0 * 25, ph0 = pp0 / 5, pw0 = pp0 - ph0 * 5;
-      ra[s] = pa[((bi0 * 13 + 2 * ph0) * 13 + 2 * pw0) * 32];
-      rb[s] = pb[(size_t)w * 256];
-    }
-  };
-  auto comp = [&](int base, const float (&ra)[16], const float (&rb)[16]) {
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const float x = (base + s < w1) ? (bias_tile ? one : ra[s]) : 0.f;
-      if (s & 1) acc1 = mfma16x16x4(x, rb[s], acc1);
-      else acc0 = mfma16x16x4(x, rb[s], acc0);
-    }
-  };
-  if (w0 < w1) {
-    load(w0, ca, cb);
-    int base = w0;
-    while (true) {
-      const int nxt = base + 16;
-      if (nxt < w1) load(nxt, na, nb);
-      __builtin_amdgcn_sched_barrier(0);
-      comp(base, ca, cb);
-      __builtin_amdgcn_sched_barrier(0);
-      if (nxt >= w1) break;
-      const int nn = nxt + 16;
-      if (nn < w1) load(nn, ca, cb);
-      __builtin_amdgcn_sched_barrier(0);
-      comp(nxt, na, nb);
-      __builtin_amdgcn_sched_barrier(0);
-      if (nn >= w1) break;
-      base = nn;
-    }
+  for (int j = 0; j < kIdc; ++j) {
+    const int e4 = tid + j * 512;
+    const int cell = e4 / 17, c4 = e4 - cell * 17;
+    const int y = cell / kDcDim - 2, x = cell - (cell / kDcDim) * kDcDim - 2;
+    const bool in = e4 < kLdsDc / 4 && c4 < 16 && y >= 0 && y < 10 && x >= 0 && x < 10;
+    mdc[j] = in ? 1.f : 0.f;
+    vdc[j] = ld4(dcb + (in ? (y * 10 + x) * 64 + c4 * 4 : 0));
   }
-  const f4 acc = acc0 + acc1;
+  const float* p1b = a.P1 + (size_t)bi * 169 * 32;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) red[wave][(4 * g + r) * 16 + i] = acc[r];
+  for (int j = 0; j < kIp1; ++j) {
+    const int e4 = min(tid + j * 512, 169 * 8 - 1);
+    vp1[j] = ld4(p1b + (e4 >> 3) * 32 + (e4 & 7) * 4);
+  }
+#pragma unroll
+  for (int j = 0; j < kIwd; ++j) {
+    const int e4 = min(tid + j * 512, kLdsWd / 4 - 1);
+    const int jj = e4 & 15, cq = (e4 >> 4) & 15, tap = e4 >> 8;
+    vwd[j] = ld4(a.W + a.ow2 + (size_t)(tap * 32 + 16 * h + jj) * 64 + cq * 4);
+  }
+  vx = ld4(a.X + (size_t)a.idx[bi] * 784 + min(tid, 195) * 4);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int j = 0; j < kIdc; ++j) {
+    const int e4 = tid + j * 512;
+    if (e4 < kLdsDc / 4) st4(dCs + e4 * 4, vdc[j] * mdc[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < kIp1; ++j) {
+    const int e4 = tid + j * 512;
+    if (e4 < 169 * 8) st4(P1s + (e4 >> 3) * kP1Stride + (e4 & 7) * 4, vp1[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < kIwd; ++j) {
+    const int e4 = tid + j * 512;
+    if (e4 < kLdsWd / 4) st4(Wd + e4 * 4, vwd[j]);
+  }
+  if (tid < 196) st4(Xs + tid * 4, vx);
   __syncthreads();
-  const int o = threadIdx.x;
-  const float s = red[0][o] + red[1][o] + red[2][o] + red[3][o];
-  const int row = mt * 16 + (o >> 4), col = nt * 16 + (o & 15);
-  a.part2[((size_t)split * kMnistPart2Rows + row) * 64 + col] = s;
-}
 
-// --------------------------------------------------------------------------------------------
-// K7: conv2 data gradient on MFMA (M = b*169 pooled-conv1 pixels, N = 32, K = 9 x 64) with the
-// pool1 + relu backward and the conv1 weight/bias gradient fused into the epilogue.
-// Workgroup = 8 waves = 4 row tiles x 2 column tiles = 64 pixels x 32 channels.
-// --------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(512) void k_conv2_dgrad(MnistArgs a) {
-  __shared__ float red[8][10][16];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int i = lane & 15, g = lane >> 4;
-  const int rt = wave & 3, ct = wave >> 2;
-  const int npix = a.b * 169;
-  const int P = blockIdx.x * 64 + rt * 16 + i;
-  const bool valid = P < npix;
-  const int Pc = valid ? P : 0;
-  const int bi = Pc / 169, rem = Pc - bi * 169, ih = rem / 13, iw = rem - ih * 13;
-  const float* w2 = a.W + a.ow2 + (size_t)(ct * 16 + i) * 64 + 4 * g;
-  f4 acc0 = zero4(), acc1 = zero4();
+  // ---- conv2 wgrad: tiles mt = wave, wave+8, wave+16 (< 19); columns 16p + i ----
+  for (int mt = wave; mt < 19; mt += 8) {
+    const bool bias_tile = mt == 18;
+    const int k = mt * 16 + i;
+    const int tap = bias_tile ? 0 : k >> 5, ci = k & 31;
+    const int kh = tap / 3, kw = tap - kh * 3;
+    const float* pa = P1s + (kh * 13 + kw) * kP1Stride + ci;
+    const float* pb = dCs + (2 * kDcDim + 2) * kDcStride + 16 * p + i;
+    const float one = (i == 0) ? 1.f : 0.f;
+    f4 acc0 = zero4(), acc1 = zero4();
+#pragma unroll 5
+    for (int s = 0; s < 25; ++s) {
+      const int pos = 4 * s + g, oh = pos / 10, ow = pos - oh * 10;
+      const float av = bias_tile ? one : pa[(oh * 13 + ow) * kP1Stride];
+      const float bv = pb[(oh * kDcDim + ow) * kDcStride];
+      if (s & 1) acc1 = mfma16x16x4(av, bv, acc1);
+      else acc0 = mfma16x16x4(av, bv, acc0);
+    }
+    const f4 acc = acc0 + acc1;
 #pragma unroll
-  for (int kk = 0; kk < 9; ++kk) {
-    const int kh = kk / 3, kw = kk % 3;
-    const int oh = ih - kh, ow = iw - kw;
-    const bool rv = valid && oh >= 0 && oh < 10 && ow >= 0 && ow < 10;
-    const int ohc = rv ? oh : 0, owc = rv ? ow : 0;
-    const float* ap = a.dC2 + ((size_t)((bi * 25 + (ohc >> 1) * 5 + (owc >> 1)) * 4 + (ohc & 1) * 2 + (owc & 1))) * 64 + 4 * g;
-    const float* bp = w2 + kk * 32 * 64;
-    const float m = rv ? 1.f : 0.f;
-#pragma unroll
-    for (int c0 = 0; c0 < 64; c0 += 16) {
-      const f4 av = ld4(ap + c0) * m;
-      const f4 bv = ld4(bp + c0);
-      acc0 = mfma16x16x4(av.x, bv.x, acc0);
-      acc1 = mfma16x16x4(av.y, bv.y, acc1);
-      acc0 = mfma16x16x4(av.z, bv.z, acc0);
-      acc1 = mfma16x16x4(av.w, bv.w, acc1);
+    for (int r = 0; r < 4; ++r) {
+      const int row = mt * 16 + 4 * g + r;
+      if (row < kMnistPart2Rows) a.part2[((size_t)bi * kMnistPart2Rows + row) * 64 + 16 * p + i] = acc[r];
     }
   }
-  const f4 acc = acc0 + acc1;
-  // epilogue: lane holds dP1 for pixels P_r = base + 4g + r, channel c.
-  const int c = ct * 16 + i;
+
+  // ---- conv2 dgrad (+ pool1/relu backward + conv1 wgrad): waves 2..7 take tiles 5..0 ----
   float dw[10];
 #pragma unroll
   for (int j = 0; j < 10; ++j) dw[j] = 0.f;
+  const int d = 7 - wave;
+  if (d < 6) {
+    const int pix0 = half * 85, pix1 = half ? 169 : 85;
+    const int P = pix0 + d * 16 + i;
+    const bool valid = P < pix1;
+    const int Pc = valid ? P : pix0;
+    const int ih = Pc / 13, iw = Pc - ih * 13;
+    const float* wb = Wd + (g * 16 + i) * 4;
+    f4 acc0 = zero4(), acc1 = zero4();
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int Pr = blockIdx.x * 64 + rt * 16 + 4 * g + r;
-    if (Pr < npix) {
-      const size_t e = (size_t)Pr * 32 + c;
-      const float v = a.P1[e] > 0.f ? acc[r] : 0.f;
-      const unsigned q1 = a.A1[e];
-      const int br = Pr / 169, rr = Pr - br * 169, ph = rr / 13, pw = rr - ph * 13;
-      const int y = 2 * ph + (q1 >> 1), x = 2 * pw + (q1 & 1);
-      const float* img = a.X + (size_t)a.idx[br] * 784 + y * 28 + x;
+    for (int tap = 0; tap < 9; ++tap) {
+      const int kh = tap / 3, kw = tap - kh * 3;
+      const float* ap = dCs + ((ih - kh + 2) * kDcDim + (iw - kw + 2)) * kDcStride + 4 * g;
 #pragma unroll
-      for (int kh = 0; kh < 3; ++kh)
+      for (int c0 = 0; c0 < 64; c0 += 16) {
+        const f4 av = ld4(ap + c0);
+        const f4 bv = ld4(wb + (tap * 16 + c0 / 4) * 64);
+        acc0 = mfma16x16x4(av.x, bv.x, acc0);
+        acc1 = mfma16x16x4(av.y, bv.y, acc1);
+        acc0 = mfma16x16x4(av.z, bv.z, acc0);
+        acc1 = mfma16x16x4(av.w, bv.w, acc1);
+      }
+    }
+    const f4 acc = acc0 + acc1;
+    const int c = 16 * h + i;
 #pragma unroll
-        for (int kw = 0; kw < 3; ++kw) dw[kh * 3 + kw] = fmaf(img[kh * 28 + kw], v, dw[kh * 3 + kw]);
-      dw[9] += v;
+    for (int r = 0; r < 4; ++r) {
+      const int Pr = pix0 + d * 16 + 4 * g + r;
+      if (Pr < pix1) {
+        const float v = P1s[Pr * kP1Stride + c] > 0.f ? acc[r] : 0.f;
+        const unsigned q1 = a.A1[((size_t)bi * 169 + Pr) * 32 + c];
+        const int ph = Pr / 13, pw = Pr - ph * 13;
+        const float* img = Xs + (2 * ph + (q1 >> 1)) * 28 + 2 * pw + (q1 & 1);
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw) dw[kh * 3 + kw] = fmaf(img[kh * 28 + kw], v, dw[kh * 3 + kw]);
+        dw[9] += v;
+      }
     }
   }
 #pragma unroll
   for (int j = 0; j < 10; ++j) dw[j] = sum_lane_groups(dw[j]);
   if (g == 0) {
 #pragma unroll
-    for (int j = 0; j < 10; ++j) red[wave][j][i] = dw[j];
+    for (int j = 0; j < 10; ++j) red[(wave * 10 + j) * 16 + i] = dw[j];
   }
   __syncthreads();
-  if (threadIdx.x < 320) {
-    const int j = threadIdx.x >> 5, cc = threadIdx.x & 31;
-    const int ctt = cc >> 4, ii = cc & 15;
-    const float s = red[ctt * 4 + 0][j][ii] + red[ctt * 4 + 1][j][ii] + red[ctt * 4 + 2][j][ii] +
-                    red[ctt * 4 + 3][j][ii];
-    a.part1[(size_t)blockIdx.x * kMnistPart1Cols + j * 32 + cc] = s;
+  if (tid < 160) {
+    const int j = tid >> 4, ii = tid & 15;
+    float s = 0.f;
+#pragma unroll
+    for (int w = 2; w < 8; ++w) s += red[(w * 10 + j) * 16 + ii];
+    a.part1[((size_t)bi * 2 + half) * kMnistPart1Cols + j * 32 + 16 * h + ii] = s;
   }
 }
 
 // --------------------------------------------------------------------------------------------
-// K9: reduce partial slabs into G (+ optional fused SGD).  Blocks [0, nbs) sweep the slab,
-// blocks [nbs, nbs+20) reduce the conv1 partials (16 outputs per block).
+// KF: reduce the per-image partial slabs into G (+ optional fused SGD).
+//   blocks [0, nbs)          : slab sweep (SGD of the parameters whose gradient is already in G)
+//   blocks [nbs, nbs + nb2)  : conv2 kernel/bias, 4 threads per output (16 images each)
+//   blocks [.., + 20)        : conv1 kernel/bias, 16 threads per output
 // --------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_finalize(MnistArgs a, int apply_sgd, int nbs) {
+__global__ __launch_bounds__(256) void k_finalize(MnistArgs a, int apply_sgd, int nbs, int nb2) {
   const float lr = *a.lr;
-  if ((int)blockIdx.x < nbs) {
-    const int e = blockIdx.x * 256 + threadIdx.x;
+  const int blk = blockIdx.x;
+  if (blk < nbs) {
+    const int e = blk * 256 + threadIdx.x;
     if (e >= a.nslab) return;
-    if ((e >= a.ow1 && e < a.ow1 + 288) || (e >= a.ob1 && e < a.ob1 + 32)) return;
-    float gv;
-    if (e >= a.ow2 && e < a.ow2 + 18432) {
-      const int k = e - a.ow2;
-      gv = 0.f;
-#pragma unroll
-      for (int s = 0; s < kMnistConv2Splits; ++s) gv += a.part2[(size_t)s * kMnistPart2Rows * 64 + k];
-      a.G[e] = gv;
-    } else if (e >= a.ob2 && e < a.ob2 + 64) {
-      const int co = e - a.ob2;
-      gv = 0.f;
-#pragma unroll
-      for (int s = 0; s < kMnistConv2Splits; ++s) gv += a.part2[((size_t)s * kMnistPart2Rows + 288) * 64 + co];
-      a.G[e] = gv;
-    } else {
-      gv = a.G[e];
-    }
-    if (apply_sgd) a.W[e] -= lr * gv;
+    const bool conv = (e >= a.ow1 && e < a.ow1 + 288) || (e >= a.ob1 && e < a.ob1 + 32) ||
+                      (e >= a.ow2 && e < a.ow2 + 18432) || (e >= a.ob2 && e < a.ob2 + 64);
+    if (conv || !apply_sgd) return;
+    a.W[e] -= lr * a.G[e];
     return;
   }
-  __shared__ float red[256];
-  const int ob = (blockIdx.x - nbs) * 16;
-  const int o = ob + (threadIdx.x & 15), u = threadIdx.x >> 4;
-  const int nb7 = mnist_nb7(a.b);
-  float s = 0.f;
-  for (int p = u; p < nb7; p += 16) s += a.part1[(size_t)p * kMnistPart1Cols + o];
-  red[threadIdx.x] = s;
-  __syncthreads();
-  if (threadIdx.x < 16) {
-    float t = 0.f;
+  if (blk < nbs + nb2) {
+    const int t = (blk - nbs) * 256 + threadIdx.x;
+    const int o = t >> 2, sub = t & 3;  // o in [0, 289*64)
+    const int n = kMnistPart2Rows * 64;
+    float s = 0.f;
+    const int oc = min(o, n - 1);
+    for (int base = 0; base < a.b; base += 64) {  // 16 independent loads in flight per thread
+      float v[16];
 #pragma unroll
-    for (int v = 0; v < 16; ++v) t += red[v * 16 + threadIdx.x];
-    const int e = (o < 288) ? a.ow1 + o : a.ob1 + (o - 288);
-    a.G[e] = t;
-    if (apply_sgd) a.W[e] -= lr * t;
+      for (int j = 0; j < 16; ++j) v[j] = a.part2[(size_t)min(base + sub + 4 * j, a.b - 1) * n + oc];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) s += (base + sub + 4 * j < a.b) ? v[j] : 0.f;
+    }
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    if (sub == 0 && o < n) {
+      const int row = o >> 6, col = o & 63;
+      const int e = row < 288 ? a.ow2 + o : a.ob2 + col;
+      a.G[e] = s;
+      if (apply_sgd) a.W[e] -= lr * s;
+    }
+    return;
+  }
+  const int t = (blk - nbs - nb2) * 256 + threadIdx.x;
+  const int o = t >> 4, sub = t & 15;  // o in [0, 320)
+  const int rows = mnist_part1_rows(a.b);
+  float s = 0.f;
+  const int oc = min(o, kMnistPart1Cols - 1);
+  for (int base = 0; base < rows; base += 128) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = a.part1[(size_t)min(base + sub + 16 * j, rows - 1) * kMnistPart1Cols + oc];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += (base + sub + 16 * j < rows) ? v[j] : 0.f;
+  }
+#pragma unroll
+  for (int m = 1; m < 16; m <<= 1) s += __shfl_xor(s, m, 64);
+  if (sub == 0 && o < kMnistPart1Cols) {
+    const int e = o < 288 ? a.ow1 + o : a.ob1 + (o - 288);
+    a.G[e] = s;
+    if (apply_sgd) a.W[e] -= lr * s;
   }
 }
 
@@ -605,28 +605,26 @@ void mnist_dense1(const MnistArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_dense1, dim3((a.b + 15) / 16, 8), dim3(512), 0, s, a);
 }
 void mnist_head(const MnistArgs& a, hipStream_t s) {
-  const size_t lds = (size_t)(a.b * 128 + 1280 + 16 + a.b * 16 + 64) * sizeof(float);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_head, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
-  hipLaunchKernelGGL(k_head, dim3(1), dim3(1024), lds, s, a);
+  hipLaunchKernelGGL(k_head, dim3(mnist_head_blocks(a.b)), dim3(256), 0, s, a);
 }
 void mnist_dense1_bwd(const MnistArgs& a, hipStream_t s) {
   const int MT = (a.b + 15) / 16;
   const int nP = (MT * 100 + 3) / 4;
-  hipLaunchKernelGGL(k_dense1_bwd, dim3(200 + nP + 1), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_dense1_bwd, dim3(200 + nP + 1 + 6), dim3(256), 0, s, a);
 }
-void mnist_conv2_wgrad(const MnistArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_conv2_wgrad, dim3(19 * 4 * kMnistConv2Splits), dim3(256), 0, s, a);
-}
-void mnist_conv2_dgrad(const MnistArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_conv2_dgrad, dim3(mnist_nb7(a.b)), dim3(512), 0, s, a);
+void mnist_conv_bwd(const MnistArgs& a, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_conv_bwd, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_conv_bwd, dim3(a.b * 4), dim3(512), kLdsConvBwd * sizeof(float), s, a);
 }
 void mnist_finalize(const MnistArgs& a, bool apply_sgd, hipStream_t s) {
   const int nbs = (a.nslab + 255) / 256;
-  hipLaunchKernelGGL(k_finalize, dim3(nbs + 20), dim3(256), 0, s, a, apply_sgd ? 1 : 0, nbs);
+  const int nb2 = (kMnistPart2Rows * 64 * 4 + 255) / 256;
+  const int nb1 = (kMnistPart1Cols * 16 + 255) / 256;
+  hipLaunchKernelGGL(k_finalize, dim3(nbs + nb2 + nb1), dim3(256), 0, s, a, apply_sgd ? 1 : 0, nbs, nb2);
 }
 void sgd_apply(float* w, const float* g, const float* lr, int64_t n, hipStream_t s) {
   const int64_t nt = (n + 3) / 4;
