@@ -50,6 +50,7 @@ class MnistStep {
     dC2_ = at::empty({b * 100 * 64}, f);
     part2_ = at::zeros({b * tdl::kMnistPart2Rows * 64}, f);
     part1_ = at::zeros({(int64_t)tdl::mnist_part1_rows((int)b) * tdl::kMnistPart1Cols}, f);
+    part3_ = at::zeros({(int64_t)tdl::kDense1Chunks * b * 128}, f);
     part4_ = at::zeros({(int64_t)tdl::mnist_head_blocks((int)b) * 1290}, f);
     a_ = tdl::MnistArgs{};
     a_.X = X_.data_ptr<float>();
@@ -68,6 +69,7 @@ class MnistStep {
     a_.dC2 = dC2_.data_ptr<float>();
     a_.part2 = part2_.data_ptr<float>();
     a_.part1 = part1_.data_ptr<float>();
+    a_.part3 = part3_.data_ptr<float>();
     a_.part4 = part4_.data_ptr<float>();
     a_.metrics = metrics_.data_ptr<float>();
     a_.lr = lr_.data_ptr<float>();
@@ -91,6 +93,7 @@ class MnistStep {
       case 4: tdl::mnist_head(a_, s); break;
       case 5: tdl::mnist_dense1_bwd(a_, s); break;
       case 6: tdl::mnist_conv_bwd(a_, s); break;
+      case 8: tdl::mnist_fwd_conv(a_, s); break;
       case 9: tdl::mnist_finalize(a_, apply_sgd, s); break;
       default: TORCH_CHECK(false, "unknown stage");
     }
@@ -100,8 +103,7 @@ class MnistStep {
   void forward_backward(int64_t idx_off) {
     set_idx_offset(idx_off);
     hipStream_t s = cur_stream();
-    tdl::mnist_conv1_pool(a_, s);
-    tdl::mnist_conv2_pool(a_, s);
+    tdl::mnist_fwd_conv(a_, s);
     tdl::mnist_dense1(a_, s);
     tdl::mnist_head(a_, s);
     tdl::mnist_dense1_bwd(a_, s);
@@ -114,16 +116,27 @@ class MnistStep {
   void forward_features(int64_t idx_off) {
     set_idx_offset(idx_off);
     hipStream_t s = cur_stream();
-    tdl::mnist_conv1_pool(a_, s);
-    tdl::mnist_conv2_pool(a_, s);
+    tdl::mnist_fwd_conv(a_, s);
     tdl::mnist_dense1(a_, s);
+  }
+
+  // diagnostics: per-workgroup phase timestamps of the next launches (None to disable)
+  void set_stamps(c10::optional<at::Tensor> t) {
+    if (t.has_value()) {
+      TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kLong, "stamps must be int64 on GPU");
+      stamps_ = *t;
+      a_.stamps = reinterpret_cast<unsigned long long*>(stamps_.data_ptr<int64_t>());
+    } else {
+      a_.stamps = nullptr;
+    }
   }
 
   std::vector<at::Tensor> buffers() { return {P1_, A1_, P2_, A2_, H_, dH_, dC2_, part2_, part1_}; }
 
  private:
   at::Tensor X_, Y_, idx_, W_, G_, lr_, metrics_;
-  at::Tensor P1_, A1_, P2_, A2_, H_, dH_, dC2_, part2_, part1_, part4_;
+  at::Tensor P1_, A1_, P2_, A2_, H_, dH_, dC2_, part2_, part1_, part3_, part4_;
+  at::Tensor stamps_;
   tdl::MnistArgs a_;
 };
 
@@ -159,7 +172,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("forward_backward", &MnistStep::forward_backward)
       .def("forward_features", &MnistStep::forward_features)
       .def("finalize", &MnistStep::finalize)
-      .def("buffers", &MnistStep::buffers);
+      .def("buffers", &MnistStep::buffers)
+      .def("set_stamps", &MnistStep::set_stamps);
   m.def("sgd", &sgd);
   m.def("sgd_momentum", &sgd_momentum);
   register_ops(m);

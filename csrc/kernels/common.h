@@ -38,4 +38,9 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// Phase timestamp (100 MHz s_memrealtime) of workgroup blockIdx.x, slot k; no-op when buf == null.
+__device__ __forceinline__ void stamp(unsigned long long* buf, int k) {
+  if (buf != nullptr && threadIdx.x == 0) buf[blockIdx.x * 8 + k] = __builtin_amdgcn_s_memrealtime();
+}
+
 }  // namespace tdl

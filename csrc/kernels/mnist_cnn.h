@@ -30,15 +30,18 @@ struct MnistArgs {
   float* dC2;         // [b,10,10,64] grad of the (used 10x10 part of the) conv2 output
   float* part2;       // [b][289][64] per-image partials of conv2 wgrad (row 288 = bias)
   float* part1;       // [2b][320] per-(image, pixel-half) partials of conv1 wgrad (+ bias)
+  float* part3;       // [25][b][128] split-K partials of dense1
   float* part4;       // [ceil(b/4)][1290] per-workgroup partials of dense2 wgrad (+ bias)
   float* metrics;     // [0] loss sum, [1] correct, [2] count
   const float* lr;    // device scalar learning rate
+  unsigned long long* stamps;  // optional [grid][8] phase timestamps (s_memrealtime), diagnostics
   int b;              // per-replica batch
   float scale;        // 1 / (b * R)
   int nslab;          // slab length (floats)
 };
 
 constexpr int kMnistPart2Rows = 289;
+constexpr int kDense1Chunks = 25;  // K = 1600 = 25 x 64
 constexpr int kMnistPart1Cols = 320;
 __host__ __device__ inline int mnist_part1_rows(int b) { return 2 * b; }
 __host__ __device__ inline int mnist_head_blocks(int b) { return (b + 3) / 4; }
@@ -49,6 +52,7 @@ void mnist_dense1(const MnistArgs& a, hipStream_t s);
 void mnist_head(const MnistArgs& a, hipStream_t s);
 void mnist_dense1_bwd(const MnistArgs& a, hipStream_t s);
 void mnist_conv_bwd(const MnistArgs& a, hipStream_t s);
+void mnist_fwd_conv(const MnistArgs& a, hipStream_t s);  // K1+K2 fused per image
 void mnist_finalize(const MnistArgs& a, bool apply_sgd, hipStream_t s);
 
 // Plain SGD over a flat slab: w -= lr * g  (lr read from device memory).

@@ -124,50 +124,45 @@ __global__ __launch_bounds__(256) void k_conv2_pool(MnistArgs a) {
 }
 
 // --------------------------------------------------------------------------------------------
-// K3: H = relu(P2 W3 + b3).  grid (ceil(b/16), 8); 8 waves split K=1600 (100 chunks of 16).
+// K3: dense1 GEMM P2 W3 as 25 split-K partial slabs (bias + ReLU + chunk sum in the head).
 // --------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(512) void k_dense1(MnistArgs a) {
-  __shared__ float red[8][256];
+__global__ __launch_bounds__(256) void k_dense1(MnistArgs a) {
+  // split-K GEMM: workgroup = (K chunk c of 64, row tile mt, column half); wave = 16 columns.
+  // Every load of a wave is issued up front (one memory round trip), 16 MFMAs, and the partial
+  // tile goes to part3[c]; the head sums the 25 chunks + bias + ReLU per row.
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int i = lane & 15, g = lane >> 4;
-  const int mt = blockIdx.x, nt = blockIdx.y;
+  const int MT = (a.b + 15) >> 4;
+  const int c = blockIdx.x / (MT * 2), rem = blockIdx.x - c * MT * 2;
+  const int mt = rem >> 1, nt = (rem & 1) * 4 + wave;
   const int row = mt * 16 + i;
   const bool valid = row < a.b;
-  const float* ap = a.P2 + (size_t)(valid ? row : 0) * 1600 + 4 * g;
-  const float* bp = a.W + a.ow3 + (4 * g) * 128 + nt * 16 + i;
-  // 13 k-chunks per wave (chunk c = wave + 8j < 100), all loads issued before the MFMAs.
-  f4 av[13];
-  float bv[13][4];
+  const float* ap = a.P2 + (size_t)(valid ? row : 0) * 1600 + c * 64 + 4 * g;
+  const float* bp = a.W + a.ow3 + (size_t)(c * 64 + 4 * g) * 128 + nt * 16 + i;
+  f4 av[4];
+  float bv[4][4];
 #pragma unroll
-  for (int j = 0; j < 13; ++j) {
-    const int c = min(wave + 8 * j, 99), k0 = c * 16;
-    av[j] = ld4(ap + k0);
-    const float* b = bp + k0 * 128;
+  for (int s = 0; s < 4; ++s) {
+    av[s] = ld4(ap + 16 * s);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) bv[j][t] = b[t * 128];
+    for (int t = 0; t < 4; ++t) bv[s][t] = bp[(16 * s + t) * 128];
   }
   __builtin_amdgcn_sched_barrier(0);
+  const float vm = valid ? 1.f : 0.f;
   f4 acc0 = zero4(), acc1 = zero4();
 #pragma unroll
-  for (int j = 0; j < 13; ++j) {
-    const float m = (valid && wave + 8 * j < 100) ? 1.f : 0.f;
-    const f4 x = av[j] * m;
-    acc0 = mfma16x16x4(x.x, bv[j][0], acc0);
-    acc1 = mfma16x16x4(x.y, bv[j][1], acc1);
-    acc0 = mfma16x16x4(x.z, bv[j][2], acc0);
-    acc1 = mfma16x16x4(x.w, bv[j][3], acc1);
+  for (int s = 0; s < 4; ++s) {
+    const f4 x = av[s] * vm;
+    acc0 = mfma16x16x4(x.x, bv[s][0], acc0);
+    acc1 = mfma16x16x4(x.y, bv[s][1], acc1);
+    acc0 = mfma16x16x4(x.z, bv[s][2], acc0);
+    acc1 = mfma16x16x4(x.w, bv[s][3], acc1);
   }
   const f4 acc = acc0 + acc1;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) red[wave][(4 * g + r) * 16 + i] = acc[r];
-  __syncthreads();
-  if (threadIdx.x < 256) {
-    const int o = threadIdx.x;
-    float s = 0.f;
-#pragma unroll
-    for (int w = 0; w < 8; ++w) s += red[w][o];
-    const int rr = mt * 16 + (o >> 4), cc = nt * 16 + (o & 15);
-    if (rr < a.b) a.H[rr * 128 + cc] = fmaxf(s + a.W[a.ob3 + cc], 0.f);
+  for (int r = 0; r < 4; ++r) {
+    const int rr = mt * 16 + 4 * g + r;
+    if (rr < a.b) a.part3[((size_t)c * a.b + rr) * 128 + nt * 16 + i] = acc[r];
   }
 }
 
@@ -187,7 +182,19 @@ __global__ __launch_bounds__(256) void k_head(MnistArgs a) {
   float wa[10], wb[10];
 #pragma unroll
   for (int c = 0; c < 10; ++c) { wa[c] = w4[l * 10 + c]; wb[c] = w4[(l + 64) * 10 + c]; }
-  const float h0 = a.H[rr * 128 + l], h1 = a.H[rr * 128 + l + 64];
+  // H = relu(b3 + sum of dense1's 25 split-K partials), 50 independent loads per lane
+  float hp0[kDense1Chunks], hp1[kDense1Chunks];
+#pragma unroll
+  for (int c = 0; c < kDense1Chunks; ++c) {
+    hp0[c] = a.part3[((size_t)c * a.b + rr) * 128 + l];
+    hp1[c] = a.part3[((size_t)c * a.b + rr) * 128 + l + 64];
+  }
+  float h0 = a.W[a.ob3 + l], h1 = a.W[a.ob3 + l + 64];
+#pragma unroll
+  for (int c = 0; c < kDense1Chunks; ++c) { h0 += hp0[c]; h1 += hp1[c]; }
+  h0 = fmaxf(h0, 0.f);
+  h1 = fmaxf(h1, 0.f);
+  if (live) { a.H[r * 128 + l] = h0; a.H[r * 128 + l + 64] = h1; }
   const int y = a.Y[a.idx[rr]];
   float lg[10];
 #pragma unroll
@@ -356,6 +363,7 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
   const int i = lane & 15, g = lane >> 4;
   const int bi = blockIdx.x >> 2, p = blockIdx.x & 3;
   const int h = p & 1, half = p >> 1;
+  stamp(a.stamps, 0);
   // ---- stage everything in LDS: every global load of the thread is issued first (one memory
   // round trip for the whole staging), then all LDS stores.  Out-of-range slots load a valid
   // address and are zeroed by a multiply (no per-element branch around a load). ----
@@ -402,7 +410,9 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
     if (e4 < kLdsWd / 4) st4(Wd + e4 * 4, vwd[j]);
   }
   if (tid < 196) st4(Xs + tid * 4, vx);
+  stamp(a.stamps, 1);
   __syncthreads();
+  stamp(a.stamps, 2);
 
   // ---- conv2 wgrad: tiles mt = wave, wave+8, wave+16 (< 19); columns 16p + i ----
   for (int mt = wave; mt < 19; mt += 8) {
@@ -430,6 +440,7 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
     }
   }
 
+  stamp(a.stamps, 3);
   // ---- conv2 dgrad (+ pool1/relu backward + conv1 wgrad): waves 2..7 take tiles 5..0 ----
   float dw[10];
 #pragma unroll
@@ -481,7 +492,9 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
 #pragma unroll
     for (int j = 0; j < 10; ++j) red[(wave * 10 + j) * 16 + i] = dw[j];
   }
+  stamp(a.stamps, 4);
   __syncthreads();
+  stamp(a.stamps, 5);
   if (tid < 160) {
     const int j = tid >> 4, ii = tid & 15;
     float s = 0.f;
@@ -489,6 +502,139 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
     for (int w = 2; w < 8; ++w) s += red[(w * 10 + j) * 16 + ii];
     a.part1[((size_t)bi * 2 + half) * kMnistPart1Cols + j * 32 + 16 * h + ii] = s;
   }
+}
+
+// --------------------------------------------------------------------------------------------
+// KA: forward convolutions per (image, output-channel quarter), 8 waves, LDS-staged:
+//   conv1 + bias + relu + maxpool into LDS (P1s, stride 36), then conv2 on MFMA for this
+//   quarter's 16 channels over the 100 used positions (7 row tiles of 4 pool windows) with the
+//   bias + relu + maxpool epilogue in registers.  Quarter 0 also writes P1 / A1 for backward.
+// --------------------------------------------------------------------------------------------
+constexpr int kLdsFwd = 784 + 320 + 169 * kP1Stride + 72 * 16 * 4;
+
+__global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* xs = sm;
+  float* w1s = xs + 784;
+  float* P1s = w1s + 320;
+  float* w2s = P1s + 169 * kP1Stride;  // [kc=72][j=16][t=4]: B[k=4kc+t][16cq+j]
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int i = lane & 15, g = lane >> 4;
+  const int bi = blockIdx.x >> 2, cq = blockIdx.x & 3;
+  stamp(a.stamps, 0);
+  // ---- staging: all global loads first ----
+  const f4 vx = ld4(a.X + (size_t)a.idx[bi] * 784 + min(tid, 195) * 4);
+  const float vw1 = tid < 288 ? a.W[a.ow1 + tid] : a.W[a.ob1 + min(tid - 288, 31)];
+  f4 vw2[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int e = min(tid + j * 512, 1151);  // (k, q): k = e >> 2, channels 16cq + 4q .. +3
+    vw2[j] = ld4(a.W + a.ow2 + (e >> 2) * 64 + 16 * cq + (e & 3) * 4);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  if (tid < 196) st4(xs + tid * 4, vx);
+  if (tid < 320) w1s[tid] = vw1;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int e = tid + j * 512;
+    if (e < 1152) {
+      const int k = e >> 2, q = e & 3;
+      float* d = w2s + ((k >> 2) * 16 + 4 * q) * 4 + (k & 3);
+      d[0] = vw2[j].x;
+      d[4] = vw2[j].y;
+      d[8] = vw2[j].z;
+      d[12] = vw2[j].w;
+    }
+  }
+  stamp(a.stamps, 1);
+  __syncthreads();
+  stamp(a.stamps, 2);
+  // ---- conv1 on MFMA (K = 9 taps padded to 12): rows = 676 conv1 positions in pool-window-major
+  // order, so a 16-row tile holds 4 whole 2x2 windows and the maxpool happens in registers.
+  // 43 row tiles x 2 channel tiles; bias + relu after the max (they commute with it). ----
+  {
+    float bw[2][3];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int s3 = 0; s3 < 3; ++s3) {
+        const int k = 4 * s3 + g;
+        bw[nt][s3] = k < 9 ? w1s[k * 32 + nt * 16 + i] : 0.f;
+      }
+    int tap_off[3];
+#pragma unroll
+    for (int s3 = 0; s3 < 3; ++s3) {
+      const int k = min(4 * s3 + g, 8);
+      tap_off[s3] = (k / 3) * 28 + (k % 3);
+    }
+    for (int job = wave; job < 86; job += 8) {
+      const int mt = job >> 1, nt = job & 1;
+      const int w = mt * 4 + (i >> 2), q = i & 3;
+      const int wc = min(w, 168);
+      const int y = 2 * (wc / 13) + (q >> 1), x = 2 * (wc % 13) + (q & 1);
+      const float* xb = xs + y * 28 + x;
+      f4 acc = zero4();
+#pragma unroll
+      for (int s3 = 0; s3 < 3; ++s3) acc = mfma16x16x4(xb[tap_off[s3]], bw[nt][s3], acc);
+      const int wo = mt * 4 + g;
+      if (wo < 169) {
+        float m = acc.x;
+        unsigned am = 0;
+        if (acc.y > m) { m = acc.y; am = 1; }
+        if (acc.z > m) { m = acc.z; am = 2; }
+        if (acc.w > m) { m = acc.w; am = 3; }
+        const int co = nt * 16 + i;
+        const float v = fmaxf(m + w1s[288 + co], 0.f);
+        P1s[wo * kP1Stride + co] = v;
+        if (cq == 0) {
+          const size_t gi = ((size_t)bi * 169 + wo) * 32 + co;
+          a.P1[gi] = v;
+          a.A1[gi] = (uint8_t)am;
+        }
+      }
+    }
+  }
+  stamp(a.stamps, 3);
+  __syncthreads();
+  stamp(a.stamps, 4);
+  // ---- conv2 on MFMA: wave w < 7 takes row tile w (windows 4w .. 4w+3) ----
+  if (wave >= 7) return;
+  const int wi = wave * 4 + (i >> 2), q = i & 3;
+  const bool valid = wi < 25;
+  const int wic = valid ? wi : 0;
+  const int ph = wic / 5, pw = wic - ph * 5;
+  const int oh = 2 * ph + (q >> 1), ow = 2 * pw + (q & 1);
+  const float* ab = P1s + (oh * 13 + ow) * kP1Stride + 4 * g;
+  const float* bb = w2s + (g * 16 + i) * 4;
+  f4 acc0 = zero4(), acc1 = zero4();
+#pragma unroll
+  for (int kk = 0; kk < 9; ++kk) {
+    const int kh = kk / 3, kw = kk % 3;
+#pragma unroll
+    for (int cb = 0; cb < 32; cb += 16) {
+      const f4 av = ld4(ab + (kh * 13 + kw) * kP1Stride + cb);
+      const f4 bv = ld4(bb + ((kk * 32 + cb) / 4) * 64);
+      acc0 = mfma16x16x4(av.x, bv.x, acc0);
+      acc1 = mfma16x16x4(av.y, bv.y, acc1);
+      acc0 = mfma16x16x4(av.z, bv.z, acc0);
+      acc1 = mfma16x16x4(av.w, bv.w, acc1);
+    }
+  }
+  const f4 acc = acc0 + acc1;
+  stamp(a.stamps, 5);
+  const int wo = wave * 4 + g;
+  if (wo < 25) {
+    float m = acc.x;
+    unsigned am = 0;
+    if (acc.y > m) { m = acc.y; am = 1; }
+    if (acc.z > m) { m = acc.z; am = 2; }
+    if (acc.w > m) { m = acc.w; am = 3; }
+    const int co = 16 * cq + i;
+    const size_t e = (size_t)bi * 1600 + wo * 64 + co;
+    a.P2[e] = fmaxf(m + a.W[a.ob2 + co], 0.f);
+    a.A2[e] = (uint8_t)am;
+  }
+  stamp(a.stamps, 6);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -602,7 +748,7 @@ void mnist_conv2_pool(const MnistArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_conv2_pool, dim3((a.b * 25 + 3) / 4), dim3(256), 0, s, a);
 }
 void mnist_dense1(const MnistArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_dense1, dim3((a.b + 15) / 16, 8), dim3(512), 0, s, a);
+  hipLaunchKernelGGL(k_dense1, dim3(kDense1Chunks * ((a.b + 15) / 16) * 2), dim3(256), 0, s, a);
 }
 void mnist_head(const MnistArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_head, dim3(mnist_head_blocks(a.b)), dim3(256), 0, s, a);
@@ -619,6 +765,14 @@ void mnist_conv_bwd(const MnistArgs& a, hipStream_t s) {
     attr = true;
   }
   hipLaunchKernelGGL(k_conv_bwd, dim3(a.b * 4), dim3(512), kLdsConvBwd * sizeof(float), s, a);
+}
+void mnist_fwd_conv(const MnistArgs& a, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_fwd_conv, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_fwd_conv, dim3(a.b * 4), dim3(512), kLdsFwd * sizeof(float), s, a);
 }
 void mnist_finalize(const MnistArgs& a, bool apply_sgd, hipStream_t s) {
   const int nbs = (a.nslab + 255) / 256;
