@@ -110,6 +110,18 @@ class MnistStep {
     tdl::mnist_conv_bwd(a_, s);
   }
 
+  // the same step split at the point where the dense-layer gradients are final in G (after K5):
+  // the engine all-reduces that bucket while backward_conv() runs
+  void forward_dense(int64_t idx_off) {
+    set_idx_offset(idx_off);
+    hipStream_t s = cur_stream();
+    tdl::mnist_fwd_conv(a_, s);
+    tdl::mnist_dense1(a_, s);
+    tdl::mnist_head(a_, s);
+    tdl::mnist_dense1_bwd(a_, s);
+  }
+  void backward_conv() { tdl::mnist_conv_bwd(a_, cur_stream()); }
+
   void finalize(bool apply_sgd) { tdl::mnist_finalize(a_, apply_sgd, cur_stream()); }
 
   // forward only (evaluation): K1..K3 + logits via head is training-only, so eval uses K1-K3.
@@ -171,6 +183,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("stage", &MnistStep::stage, pybind11::arg("k"), pybind11::arg("apply_sgd") = false)
       .def("forward_backward", &MnistStep::forward_backward)
       .def("forward_features", &MnistStep::forward_features)
+      .def("forward_dense", &MnistStep::forward_dense)
+      .def("backward_conv", &MnistStep::backward_conv)
       .def("finalize", &MnistStep::finalize)
       .def("buffers", &MnistStep::buffers)
       .def("set_stamps", &MnistStep::set_stamps);

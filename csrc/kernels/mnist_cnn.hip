@@ -775,7 +775,7 @@ void mnist_fwd_conv(const MnistArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_fwd_conv, dim3(a.b * 4), dim3(512), kLdsFwd * sizeof(float), s, a);
 }
 void mnist_finalize(const MnistArgs& a, bool apply_sgd, hipStream_t s) {
-  const int nbs = (a.nslab + 255) / 256;
+  const int nbs = apply_sgd ? (a.nslab + 255) / 256 : 0;
   const int nb2 = (kMnistPart2Rows * 64 * 4 + 255) / 256;
   const int nb1 = (kMnistPart1Cols * 16 + 255) / 256;
   hipLaunchKernelGGL(k_finalize, dim3(nbs + nb2 + nb1), dim3(256), 0, s, a, apply_sgd ? 1 : 0, nbs, nb2);

@@ -1,7 +1,9 @@
 // Python bindings of the C++ runtime (module `tensorflow_distributed_learning_amd._native`).
 #include <torch/extension.h>
 
+#include <algorithm>
 #include <array>
+#include <vector>
 
 #include "ring.h"
 #include "store.h"
@@ -54,6 +56,36 @@ uint32_t crc32c(const std::string& data, uint32_t crc) {
   crc = ~crc;
   for (unsigned char ch : data) crc = t[(crc ^ ch) & 0xff] ^ (crc >> 8);
   return ~crc;
+}
+
+// tf.data's buffered shuffle on an index sequence (data/dataset.py _shuffle_indices): keep a
+// window of `buffer_size` pending elements, emit slot r[k] mod |window|, refill that slot from the
+// source, or once the source is drained move the last pending element into it.  The random
+// stream r is drawn by the caller so the native and Python paths give the same order.
+at::Tensor buffered_shuffle(const at::Tensor& src, int64_t buffer_size, const at::Tensor& r) {
+  TORCH_CHECK(!src.is_cuda() && src.scalar_type() == at::kLong && src.is_contiguous(), "src: int64 CPU");
+  TORCH_CHECK(!r.is_cuda() && r.scalar_type() == at::kLong && r.numel() == src.numel(), "r: int64 CPU, |src|");
+  TORCH_CHECK(buffer_size > 0, "buffer_size must be > 0");
+  const int64_t n = src.numel();
+  const int64_t* s = src.data_ptr<int64_t>();
+  const int64_t* rv = r.data_ptr<int64_t>();
+  at::Tensor out = at::empty({n}, src.options());
+  int64_t* o = out.data_ptr<int64_t>();
+  const int64_t w0 = std::min(buffer_size, n);
+  std::vector<int64_t> buf(s, s + w0);
+  int64_t nxt = w0;
+  for (int64_t k = 0; k < n; ++k) {
+    const int64_t len = (int64_t)buf.size();
+    const int64_t j = rv[k] % len;
+    o[k] = buf[j];
+    if (nxt < n) {
+      buf[j] = s[nxt++];
+    } else {
+      buf[j] = buf.back();
+      buf.pop_back();
+    }
+  }
+  return out;
 }
 
 }  // namespace
@@ -145,6 +177,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("barrier", &tdl::RingComm::barrier, py::call_guard<py::gil_scoped_release>())
       .def("close", &tdl::RingComm::close);
 
+  m.def("buffered_shuffle", &buffered_shuffle, py::arg("src"), py::arg("buffer_size"), py::arg("r"));
   m.def("crc32c", [](py::bytes data, uint32_t crc) { return crc32c(std::string(data), crc); }, py::arg("data"),
         py::arg("crc") = 0u);
 }

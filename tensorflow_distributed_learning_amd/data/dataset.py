@@ -586,10 +586,27 @@ def _shuffle_indices(n: int, buffer_size: int, rng: np.random.Generator, source_
     src = np.arange(n) if source_order is None else np.asarray(source_order)
     if buffer_size >= n:
         return src[rng.permutation(n)]
+    r = rng.integers(0, 1 << 62, size=n)
+    N = _native_or_none()
+    if N is not None:
+        return N.buffered_shuffle(torch.from_numpy(np.ascontiguousarray(src, dtype=np.int64)), int(buffer_size),
+                                  torch.from_numpy(r)).numpy()
+    return _shuffle_indices_py(src, n, buffer_size, r)
+
+
+def _native_or_none():
+    from .. import ops
+
+    try:
+        return ops.native()
+    except Exception:
+        return None
+
+
+def _shuffle_indices_py(src, n, buffer_size, r):
     out = np.empty(n, dtype=np.int64)
     buf = list(src[:buffer_size])
     nxt = buffer_size
-    r = rng.integers(0, 1 << 62, size=n)
     for k in range(n):
         j = int(r[k] % len(buf))
         out[k] = buf[j]

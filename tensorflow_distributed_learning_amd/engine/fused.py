@@ -8,8 +8,9 @@ SparseCategoricalAccuracy) on a GPU replica is compiled into:
 * a device-resident dataset (data/device.py) with per-step index vectors;
 * :class:`~..models.mnist_cnn.FusedMnistTrainStep` (8 hand-written gfx950 kernels);
 * the cross-replica gradient all-reduce on RCCL (``world > 1``) followed by the SGD kernel;
-* ONE hipGraph per execution of ``steps_per_execution`` steps, replayed with a new index vector
-  (the all-reduce is captured inside the graph when the communicator is capturable).
+* ONE hipGraph per execution of ``steps_per_execution`` steps, replayed with a new index vector;
+  with R > 1 the RCCL all-reduce is captured inside it as two buckets on a side stream, the dense
+  bucket overlapping the conv backward kernel (``_train_step``).
 
 Host work per execution: one H2D copy of K*B int32 indices and one graph launch.  Metrics (loss
 sum, correct count, sample count) are accumulated by the loss kernel on the device and reduced
@@ -110,12 +111,23 @@ class FusedMnistTrainer:
         self._graphs = {}
         self._data_key = None
         self.capture = os.environ.get("TDL_GRAPH", "1") == "1"
-        # all-reduce inside the captured graph only when the communicator supports it and it is
-        # enabled (TDL_CAPTURE_ALLREDUCE=1).  Default off: multi-rank RCCL capture cannot be
-        # validated on a one-GPU box (RCCL rejects two ranks on one device); the eager all-reduce
-        # costs ~30 us of host time per step, hidden behind the GPU step.
-        self.capture_comm = self.comm.world_size == 1 or (self.comm.capturable and
-                                                          os.environ.get("TDL_CAPTURE_ALLREDUCE", "0") == "1")
+        # With R > 1 the cross-replica all-reduce is recorded inside the execution graph (RCCL
+        # supports hipGraph capture) unless TDL_CAPTURE_ALLREDUCE=0 or the collective capture probe
+        # fails on some rank; then each step's graph is followed by an eager all-reduce + update.
+        self._capture_comm = None
+        self._comm_stream = None
+        self.overlap = os.environ.get("TDL_OVERLAP_ALLREDUCE", "1") == "1"
+
+    @property
+    def capture_comm(self) -> bool:
+        if self._capture_comm is None:
+            if self.R == 1:
+                self._capture_comm = True
+            elif os.environ.get("TDL_CAPTURE_ALLREDUCE", "1") != "1" or not self.capture:
+                self._capture_comm = False
+            else:
+                self._capture_comm = bool(self.comm.capture_probe())
+        return self._capture_comm
 
     # ------------------------------------------------------------------ data
     def prepare(self, dataset):
@@ -160,18 +172,46 @@ class FusedMnistTrainer:
         st.finalize(False)
         self._reduce_and_update()
 
-    def _reduce_and_update(self):
-        opt = self.optimizer
-        plain = opt.momentum == 0
-        if self.R > 1:
-            self.comm.all_reduce(self.G, "sum")
+    def _train_step(self, st, off: int, global_b: int):
+        """One whole step on the current stream.  With R > 1 the gradient all-reduce runs as two
+        buckets on a side stream: the dense-layer bucket (G[dense_offset:], 91% of the bytes) is
+        final after forward_dense() and reduces while the conv backward runs; the conv bucket
+        follows finalize(); the optimizer waits for both."""
+        if self.R == 1 or not self.overlap:
+            st.forward_backward(off)
+            self._apply(st, global_b)
+            return
+        main = torch.cuda.current_stream(self.device)
+        if self._comm_stream is None:
+            self._comm_stream = torch.cuda.Stream(self.device)
+        cs = self._comm_stream
+        d0 = st.dense_offset
+        st.forward_dense(off)
+        cs.wait_stream(main)
+        with torch.cuda.stream(cs):
+            self.comm.all_reduce(self.G[d0:], "sum")
+        st.backward_conv()
+        st.finalize(False)
+        cs.wait_stream(main)
+        with torch.cuda.stream(cs):
+            self.comm.all_reduce(self.G[:d0], "sum")
+        main.wait_stream(cs)
+        self._update()
+
+    def _update(self):
         from .. import ops
 
+        opt = self.optimizer
         C = ops.hip()
-        if plain:
+        if opt.momentum == 0:
             C.sgd(self.W, self.G, opt.lr_dev)
         else:
             C.sgd_momentum(self.W, self.G, opt._slots["momentum"], opt.lr_dev, opt.momentum, opt.nesterov)
+
+    def _reduce_and_update(self):
+        if self.R > 1:
+            self.comm.all_reduce(self.G, "sum")
+        self._update()
 
     def _run_eager(self, idx_np: np.ndarray, b: int, global_b: int):
         if b == 0:
@@ -183,12 +223,13 @@ class FusedMnistTrainer:
             return
         idx_buf = torch.from_numpy(idx_np.astype(np.int32)).to(self.device)
         st = self._step(b, idx_buf, global_b)
-        st.forward_backward(0)
-        self._apply(st, global_b)
+        self._train_step(st, 0, global_b)
         self.optimizer.iterations += 1
 
-    def _graph_for(self, K: int, b: int):
-        g = self._graphs.get((K, b))
+    def _graph_for(self, K: int, b: int, slot: int = 0):
+        """Graph of one K-step execution reading its sample ids from its own index buffer; two
+        slots alternate so the host uploads execution i+1's indices while execution i runs."""
+        g = self._graphs.get((K, b, slot))
         if g is not None:
             return g
         idx_buf = torch.zeros(K * b, dtype=torch.int32, device=self.device)
@@ -200,13 +241,12 @@ class FusedMnistTrainer:
             torch.cuda.synchronize(self.device)
             saved = (self.W.clone(), self.metrics_dev.clone(),
                      {k: v.clone() for k, v in self.optimizer.slots().items()})
-            if self.capture_comm or self.R == 1:
+            if self.capture_comm:
                 # whole execution (K steps incl. all-reduce + optimizer) in one graph
                 graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(graph, stream=s):
                     for k in range(K):
-                        st.forward_backward(k * b)
-                        self._apply(st, b * self.R)
+                        self._train_step(st, k * b, b * self.R)
             else:
                 # one graph per step holding the fused fwd/bwd/finalize; the RCCL all-reduce and
                 # the SGD kernel are issued eagerly between replays
@@ -224,7 +264,7 @@ class FusedMnistTrainer:
             for k, v in saved[2].items():
                 self.optimizer.slots()[k].copy_(v)
         g = (graph, idx_buf, st)
-        self._graphs[(K, b)] = g
+        self._graphs[(K, b, slot)] = g
         return g
 
     def warm_graphs(self, steps: int, b: Optional[int] = None):
@@ -237,12 +277,30 @@ class FusedMnistTrainer:
         if steps % self.K:
             sizes.add(steps % self.K)
         for K in sizes:
-            self._graph_for(K, b)
+            for slot in (0, 1):
+                self._graph_for(K, b, slot)
+
+    def _upload(self, idx: np.ndarray, idx_buf: torch.Tensor, slot: int):
+        """Asynchronous H2D copy of an execution's indices through a pinned staging buffer."""
+        n = idx.size
+        stage = self._stage[slot]
+        if stage is None or stage.numel() < n:
+            stage = torch.empty(max(n, 1024), dtype=torch.int32, pin_memory=True)
+            self._stage[slot] = stage
+        else:
+            self._stage_ev[slot].synchronize()  # the previous copy out of this buffer has run
+        stage[:n].numpy()[:] = idx
+        idx_buf.copy_(stage[:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._stage_ev[slot] = ev
 
     def run_train(self, handler: "DeviceHandler", steps: int) -> int:
         done = 0
         b = handler.b
         opt = self.optimizer
+        if not hasattr(self, "_stage"):
+            self._stage, self._stage_ev, self._slot = [None, None], [None, None], 0
         while done < steps:
             K = min(self.K, steps - done)
             idx = handler.take(K)
@@ -256,8 +314,10 @@ class FusedMnistTrainer:
                 done += 1
                 continue
             opt._sync_lr()
-            graph, idx_buf, st = self._graph_for(K, b)
-            idx_buf.copy_(torch.from_numpy(idx), non_blocking=False)
+            slot = self._slot
+            self._slot ^= 1
+            graph, idx_buf, st = self._graph_for(K, b, slot)
+            self._upload(idx, idx_buf, slot)
             if isinstance(graph, list):
                 for gk in graph:
                     gk.replay()
@@ -266,8 +326,7 @@ class FusedMnistTrainer:
                 graph.replay()
             else:
                 for k in range(K):
-                    st.forward_backward(k * b)
-                    self._apply(st, b * self.R)
+                    self._train_step(st, k * b, b * self.R)
             opt.iterations += K
             done += K
         return done

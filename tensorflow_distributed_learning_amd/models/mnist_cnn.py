@@ -118,9 +118,20 @@ class FusedMnistTrainStep:
         gb = int(global_batch) if global_batch is not None else self.b * self.R
         self._impl = C.MnistStep(X, Y, idx_buf, W, G, [int(o) for o in layout.offsets], self.b,
                                  1.0 / gb, lr, self.metrics)
+        # G[dense_offset:] (dense kernels/biases) is final after forward_dense(); G[:dense_offset]
+        # (conv kernels/biases) after backward_conv() + finalize()
+        self.dense_offset = int(layout.offsets[4])
 
     def forward_backward(self, idx_offset: int) -> None:
         self._impl.forward_backward(int(idx_offset))
+
+    def forward_dense(self, idx_offset: int) -> None:
+        """Forward, loss and the dense-layer backward (their gradients land in G)."""
+        self._impl.forward_dense(int(idx_offset))
+
+    def backward_conv(self) -> None:
+        """Conv backward into per-image partial slabs (reduced into G by finalize)."""
+        self._impl.backward_conv()
 
     def finalize(self, apply_sgd: bool) -> None:
         self._impl.finalize(bool(apply_sgd))

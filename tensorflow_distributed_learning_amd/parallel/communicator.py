@@ -54,6 +54,10 @@ class Communicator:
     def barrier(self) -> None:
         raise NotImplementedError
 
+    def capture_probe(self) -> bool:
+        """True when this communicator's collectives can be recorded into a hipGraph."""
+        return self.capturable
+
     def shutdown(self) -> None:
         pass
 
@@ -157,6 +161,46 @@ class TorchCommunicator(Communicator):
             dist.barrier(device_ids=[self.device.index or 0])
         else:
             dist.barrier()
+
+    def capture_probe(self) -> bool:
+        """Collectively decide whether RCCL all-reduces can live inside a hipGraph on this job.
+
+        Every rank captures a graph with one all-reduce; the ranks agree (eager MIN) on whether
+        all captures succeeded before any of them replays, replay once, verify the sum, and agree
+        again — so all ranks take the same path and issue the same collective sequence.
+        """
+        if getattr(self, "_capture_ok", None) is not None:
+            return self._capture_ok
+        if not self.capturable or self.device.type != "cuda":
+            self._capture_ok = False
+            return False
+        dev = self.device
+        flag = torch.ones(1, device=dev)
+        t = torch.full((64,), float(self.rank + 1), device=dev)
+        dist.all_reduce(t)  # warm the communicator outside capture
+        g = None
+        try:
+            s = torch.cuda.Stream(dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                dist.all_reduce(t)
+            torch.cuda.synchronize(dev)
+        except Exception:  # capture unsupported by this RCCL/torch build
+            g = None
+            flag.zero_()
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        ok = bool(flag.item() > 0.5)
+        if ok:
+            t.fill_(float(self.rank + 1))
+            g.replay()
+            torch.cuda.synchronize(dev)
+            want = float(self.world_size * (self.world_size + 1) // 2)
+            flag.fill_(1.0 if bool(torch.all(t == want)) else 0.0)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            ok = bool(flag.item() > 0.5)
+        self._capture_ok = ok
+        return ok
 
     def shutdown(self):
         if self._owns_group and dist.is_initialized():
