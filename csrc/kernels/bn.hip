@@ -1,0 +1,347 @@
+// Training-mode batch normalisation for NHWC activations on gfx950 (see bn.h).
+//
+// HBM-bound work; the design minimises passes and keeps every wave streaming 16-byte loads:
+//   forward : [partial sums x, x^2 per channel]  -> [finalize: mean/invstd, scale/shift, moving
+//             stats]  -> [apply y = act(x*scale + shift)]                (2 reads + 1 write of x)
+//   backward: [partial sums dy, dy*x]  -> [finalize: dgamma, dbeta, dx coefficients]
+//             -> [dx = A*dy + B*x + D]                                    (2x2 reads + 1 write)
+// A thread owns 8 consecutive channels (one 16-byte bf16 vector); a 256-thread workgroup covers
+// 256/(C/8) rows per iteration, unrolled 4 deep so each wave keeps 4 independent loads in flight.
+// Partials are per workgroup ([parts][2][C]) and reduced in a fixed order (deterministic).
+#include "bn.h"
+#include "common.h"
+
+namespace tdl {
+namespace {
+
+constexpr int kUnroll = 4;
+constexpr int kMaxParts = 1024;
+
+__device__ __forceinline__ float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+__device__ __forceinline__ uint32_t f2bf(float f) {  // round to nearest even
+  uint32_t u = __float_as_uint(f);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+
+template <BnDType D>
+struct Io;
+
+template <>
+struct Io<BnDType::kF32> {
+  static __device__ __forceinline__ void load(const void* p, int64_t e, float* o) {
+    const f4* q = reinterpret_cast<const f4*>(static_cast<const float*>(p) + e);
+    const f4 a = q[0], b = q[1];
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
+    o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+  }
+  static __device__ __forceinline__ void store(void* p, int64_t e, const float* v) {
+    f4* q = reinterpret_cast<f4*>(static_cast<float*>(p) + e);
+    q[0] = f4{v[0], v[1], v[2], v[3]};
+    q[1] = f4{v[4], v[5], v[6], v[7]};
+  }
+};
+
+template <>
+struct Io<BnDType::kBF16> {
+  static __device__ __forceinline__ void load(const void* p, int64_t e, float* o) {
+    const uint4 u = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(p) + e);
+    o[0] = bf_lo(u.x); o[1] = bf_hi(u.x); o[2] = bf_lo(u.y); o[3] = bf_hi(u.y);
+    o[4] = bf_lo(u.z); o[5] = bf_hi(u.z); o[6] = bf_lo(u.w); o[7] = bf_hi(u.w);
+  }
+  static __device__ __forceinline__ void store(void* p, int64_t e, const float* v) {
+    uint4 u;
+    u.x = f2bf(v[0]) | (f2bf(v[1]) << 16);
+    u.y = f2bf(v[2]) | (f2bf(v[3]) << 16);
+    u.z = f2bf(v[4]) | (f2bf(v[5]) << 16);
+    u.w = f2bf(v[6]) | (f2bf(v[7]) << 16);
+    *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p) + e) = u;
+  }
+};
+
+// Partial per-channel sums over a workgroup's rows.
+//   MODE 0 (forward)      : (sum x, sum x*x)                     a = x
+//   MODE 1 (backward)     : (sum dy, sum dy*x)                   a = dy, b = x
+//   MODE 2 (bwd, relu)    : dz = dy masked by x*scale+shift > 0  (the fused ReLU, recomputed from x)
+//   MODE 3 (bwd, add+relu): dz = dy masked by y > 0, written to dz_out (the residual's gradient)
+template <BnDType D, int MODE>
+__global__ __launch_bounds__(256) void k_bn_partial(const void* __restrict__ a, const void* __restrict__ b,
+                                                    const void* __restrict__ y, const float* __restrict__ scale,
+                                                    const float* __restrict__ shift, void* __restrict__ dz_out,
+                                                    int64_t M, int C, int64_t rows_wg, float* __restrict__ part) {
+  __shared__ float red[2][2048];
+  const int G = C >> 3, R = 256 / G;
+  const int t = threadIdx.x, cg = t % G, rr = t / G;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_wg;
+  const int64_t r1 = min(M, r0 + rows_wg);
+  float s[8], q[8], sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    s[j] = q[j] = 0.f;
+    sc[j] = MODE == 2 ? scale[cg * 8 + j] : 0.f;
+    sh[j] = MODE == 2 ? shift[cg * 8 + j] : 0.f;
+  }
+  if (rr < R) {
+    int64_t r = r0 + rr;
+    for (; r + (kUnroll - 1) * R < r1; r += kUnroll * R) {
+      float va[kUnroll][8], vb[kUnroll][8], vy[kUnroll][8];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        Io<D>::load(a, (r + u * R) * C + cg * 8, va[u]);
+        if (MODE != 0) Io<D>::load(b, (r + u * R) * C + cg * 8, vb[u]);
+        if (MODE == 3) Io<D>::load(y, (r + u * R) * C + cg * 8, vy[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (MODE == 2 && !(fmaf(vb[u][j], sc[j], sh[j]) > 0.f)) va[u][j] = 0.f;
+          if (MODE == 3 && !(vy[u][j] > 0.f)) va[u][j] = 0.f;
+          s[j] += va[u][j];
+          q[j] = fmaf(va[u][j], MODE == 0 ? va[u][j] : vb[u][j], q[j]);
+        }
+        if (MODE == 3) Io<D>::store(dz_out, (r + u * R) * C + cg * 8, va[u]);
+      }
+    }
+    for (; r < r1; r += R) {
+      float va[8], vb[8], vy[8];
+      Io<D>::load(a, r * C + cg * 8, va);
+      if (MODE != 0) Io<D>::load(b, r * C + cg * 8, vb);
+      if (MODE == 3) Io<D>::load(y, r * C + cg * 8, vy);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (MODE == 2 && !(fmaf(vb[j], sc[j], sh[j]) > 0.f)) va[j] = 0.f;
+        if (MODE == 3 && !(vy[j] > 0.f)) va[j] = 0.f;
+        s[j] += va[j];
+        q[j] = fmaf(va[j], MODE == 0 ? va[j] : vb[j], q[j]);
+      }
+      if (MODE == 3) Io<D>::store(dz_out, r * C + cg * 8, va);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[0][rr * C + cg * 8 + j] = s[j];
+      red[1][rr * C + cg * 8 + j] = q[j];
+    }
+  }
+  __syncthreads();
+  for (int c = t; c < C; c += 256) {
+    float S = 0.f, Q = 0.f;
+    for (int k = 0; k < R; ++k) {
+      S += red[0][k * C + c];
+      Q += red[1][k * C + c];
+    }
+    part[((int64_t)blockIdx.x * 2) * C + c] = S;
+    part[((int64_t)blockIdx.x * 2 + 1) * C + c] = Q;
+  }
+}
+
+// Sum the partial rows of channel c (64 channels x 4 partial-row phases per workgroup), f64.
+__device__ __forceinline__ bool reduce_parts(const float* __restrict__ part, int P, int C, double& S, double& Q) {
+  __shared__ double rs[4][64], rq[4][64];
+  const int lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  double s = 0.0, q = 0.0;
+  if (c < C) {
+#pragma unroll 8
+    for (int p = ph; p < P; p += 4) {
+      s += part[((int64_t)p * 2) * C + c];
+      q += part[((int64_t)p * 2 + 1) * C + c];
+    }
+  }
+  rs[ph][lane] = s;
+  rq[ph][lane] = q;
+  __syncthreads();
+  if (ph != 0 || c >= C) return false;
+  S = rs[0][lane] + rs[1][lane] + rs[2][lane] + rs[3][lane];
+  Q = rq[0][lane] + rq[1][lane] + rq[2][lane] + rq[3][lane];
+  return true;
+}
+
+__global__ __launch_bounds__(256) void k_bn_fwd_finalize(const float* __restrict__ part, int P, int64_t M, int C,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta,
+                                                         const float* __restrict__ mean_off, float* __restrict__ mean,
+                                                         float* __restrict__ invstd, float* __restrict__ scale,
+                                                         float* __restrict__ shift, float* __restrict__ mm,
+                                                         float* __restrict__ mv, float momentum, float eps) {
+  double S, Q;
+  if (!reduce_parts(part, P, C, S, Q)) return;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const double mu = S / (double)M;
+  const double var = fmax(Q / (double)M - mu * mu, 0.0);
+  const float inv = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = gamma ? gamma[c] : 1.f, be = beta ? beta[c] : 0.f;
+  mean[c] = (float)mu;
+  invstd[c] = inv;
+  scale[c] = g * inv;
+  shift[c] = be - (float)mu * g * inv;
+  if (mm != nullptr) {
+    const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    // mean_off: bias of a preceding conv folded into this BN (it shifts only the batch mean)
+    const float mu_o = (float)mu + (mean_off ? mean_off[c] : 0.f);
+    mm[c] = mm[c] * momentum + mu_o * (1.f - momentum);
+    mv[c] = mv[c] * momentum + (float)unb * (1.f - momentum);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_bn_bwd_finalize(const float* __restrict__ part, int P, int64_t M, int C,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ mean,
+                                                         const float* __restrict__ invstd, float* __restrict__ dgamma,
+                                                         float* __restrict__ dbeta, float* __restrict__ coef) {
+  double S, Q;
+  if (!reduce_parts(part, P, C, S, Q)) return;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const double mu = mean[c], inv = invstd[c];
+  const double g = gamma ? gamma[c] : 1.0;
+  const double dg = (Q - mu * S) * inv;  // sum dy * xhat
+  const double db = S;                   // sum dy
+  if (dgamma) dgamma[c] = (float)dg;
+  if (dbeta) dbeta[c] = (float)db;
+  // dx = g*inv/M * (M*dy - db - xhat*dg) = A*dy + B*x + D
+  const double A = g * inv, B = -g * inv * inv * dg / (double)M;
+  coef[c] = (float)A;
+  coef[C + c] = (float)B;
+  coef[2 * C + c] = (float)(-A * db / (double)M - B * mu);
+}
+
+template <BnDType D>
+__global__ __launch_bounds__(256) void k_bn_apply(const void* __restrict__ x, const void* __restrict__ res,
+                                                  void* __restrict__ y, int64_t n8, int C,
+                                                  const float* __restrict__ scale, const float* __restrict__ shift,
+                                                  int relu) {
+  __shared__ float sc[2048], sh[2048];
+  for (int c = threadIdx.x; c < C; c += 256) {
+    sc[c] = scale[c];
+    sh[c] = shift[c];
+  }
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < n8; v += stride) {
+    const int c0 = (int)((v * 8) % C);
+    float xv[8], rv[8];
+    Io<D>::load(x, v * 8, xv);
+    if (res != nullptr) Io<D>::load(res, v * 8, rv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float o = fmaf(xv[j], sc[c0 + j], sh[c0 + j]);
+      if (res != nullptr) o += rv[j];
+      xv[j] = relu ? fmaxf(o, 0.f) : o;
+    }
+    Io<D>::store(y, v * 8, xv);
+  }
+}
+
+// dx = A*dz + B*x + D with dz = dy (modes 1, 3: dy is the masked dz) or dy masked by the
+// recomputed relu condition x*scale + shift > 0 (mode 2)
+template <BnDType D, bool MASK>
+__global__ __launch_bounds__(256) void k_bn_dx(const void* __restrict__ dy, const void* __restrict__ x,
+                                               void* __restrict__ dx, int64_t n8, int C, const float* __restrict__ coef,
+                                               const float* __restrict__ scale, const float* __restrict__ shift) {
+  __shared__ float cA[2048], cB[2048], cD[2048], cS[MASK ? 2048 : 1], cT[MASK ? 2048 : 1];
+  for (int c = threadIdx.x; c < C; c += 256) {
+    cA[c] = coef[c];
+    cB[c] = coef[C + c];
+    cD[c] = coef[2 * C + c];
+    if (MASK) {
+      cS[c] = scale[c];
+      cT[c] = shift[c];
+    }
+  }
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < n8; v += stride) {
+    const int c0 = (int)((v * 8) % C);
+    float g[8], xv[8];
+    Io<D>::load(dy, v * 8, g);
+    Io<D>::load(x, v * 8, xv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (MASK && !(fmaf(xv[j], cS[c0 + j], cT[c0 + j]) > 0.f)) g[j] = 0.f;
+      g[j] = fmaf(cA[c0 + j], g[j], fmaf(cB[c0 + j], xv[j], cD[c0 + j]));
+    }
+    Io<D>::store(dx, v * 8, g);
+  }
+}
+
+int elementwise_grid(int64_t n8) {
+  const int64_t b = (n8 + 255) / 256;
+  return (int)std::min<int64_t>(b, 256 * 16);
+}
+
+}  // namespace
+
+BnPlan bn_plan(int64_t M, int C) {
+  BnPlan p;
+  p.groups = C / 8;
+  p.rows_iter = 256 / p.groups;
+  const int64_t chunk = (int64_t)p.rows_iter * kUnroll;
+  const int64_t nchunks = (M + chunk - 1) / chunk;
+  const int64_t parts = std::min<int64_t>(std::max<int64_t>(nchunks, 1), kMaxParts);
+  p.rows_wg = ((nchunks + parts - 1) / parts) * chunk;
+  p.parts = (int)std::max<int64_t>(1, (M + p.rows_wg - 1) / p.rows_wg);
+  return p;
+}
+
+void bn_forward_stats(const void* x, BnDType dt, int64_t M, int C, float* part, const float* gamma, const float* beta,
+                      const float* mean_off, float* mean, float* invstd, float* scale, float* shift,
+                      float* moving_mean, float* moving_var, float momentum, float eps, hipStream_t s) {
+  const BnPlan p = bn_plan(M, C);
+  if (dt == BnDType::kBF16)
+    hipLaunchKernelGGL((k_bn_partial<BnDType::kBF16, 0>), dim3(p.parts), dim3(256), 0, s, x, nullptr, nullptr, nullptr,
+                       nullptr, nullptr, M, C, p.rows_wg, part);
+  else
+    hipLaunchKernelGGL((k_bn_partial<BnDType::kF32, 0>), dim3(p.parts), dim3(256), 0, s, x, nullptr, nullptr, nullptr,
+                       nullptr, nullptr, M, C, p.rows_wg, part);
+  hipLaunchKernelGGL(k_bn_fwd_finalize, dim3((C + 63) / 64), dim3(256), 0, s, part, p.parts, M, C, gamma, beta,
+                     mean_off, mean, invstd, scale, shift, moving_mean, moving_var, momentum, eps);
+}
+
+void bn_apply(const void* x, const void* residual, void* y, BnDType dt, int64_t M, int C, const float* scale,
+              const float* shift, int relu, hipStream_t s) {
+  const int64_t n8 = M * C / 8;
+  if (dt == BnDType::kBF16)
+    hipLaunchKernelGGL(k_bn_apply<BnDType::kBF16>, dim3(elementwise_grid(n8)), dim3(256), 0, s, x, residual, y, n8, C,
+                       scale, shift, relu);
+  else
+    hipLaunchKernelGGL(k_bn_apply<BnDType::kF32>, dim3(elementwise_grid(n8)), dim3(256), 0, s, x, residual, y, n8, C,
+                       scale, shift, relu);
+}
+
+template <BnDType D>
+static void bn_backward_t(const void* dy, const void* x, const void* y, void* dz, void* dx, int64_t M, int C,
+                          float* part, const float* gamma, const float* mean, const float* invstd, const float* scale,
+                          const float* shift, float* dgamma, float* dbeta, float* coef, int mode, hipStream_t s) {
+  const BnPlan p = bn_plan(M, C);
+  const dim3 gp(p.parts), blk(256);
+  if (mode == 0)
+    hipLaunchKernelGGL((k_bn_partial<D, 1>), gp, blk, 0, s, dy, x, nullptr, nullptr, nullptr, nullptr, M, C, p.rows_wg,
+                       part);
+  else if (mode == 1)
+    hipLaunchKernelGGL((k_bn_partial<D, 2>), gp, blk, 0, s, dy, x, nullptr, scale, shift, nullptr, M, C, p.rows_wg,
+                       part);
+  else
+    hipLaunchKernelGGL((k_bn_partial<D, 3>), gp, blk, 0, s, dy, x, y, nullptr, nullptr, dz, M, C, p.rows_wg, part);
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), blk, 0, s, part, p.parts, M, C, gamma, mean, invstd,
+                     dgamma, dbeta, coef);
+  const int64_t n8 = M * C / 8;
+  const dim3 ge(elementwise_grid(n8));
+  if (mode == 1)
+    hipLaunchKernelGGL((k_bn_dx<D, true>), ge, blk, 0, s, dy, x, dx, n8, C, coef, scale, shift);
+  else
+    hipLaunchKernelGGL((k_bn_dx<D, false>), ge, blk, 0, s, mode == 2 ? dz : dy, x, dx, n8, C, coef, nullptr, nullptr);
+}
+
+void bn_backward(const void* dy, const void* x, const void* y, void* dz, void* dx, BnDType dt, int64_t M, int C,
+                 float* part, const float* gamma, const float* mean, const float* invstd, const float* scale,
+                 const float* shift, float* dgamma, float* dbeta, float* coef, int mode, hipStream_t s) {
+  if (dt == BnDType::kBF16)
+    bn_backward_t<BnDType::kBF16>(dy, x, y, dz, dx, M, C, part, gamma, mean, invstd, scale, shift, dgamma, dbeta,
+                                   coef, mode, s);
+  else
+    bn_backward_t<BnDType::kF32>(dy, x, y, dz, dx, M, C, part, gamma, mean, invstd, scale, shift, dgamma, dbeta, coef,
+                                  mode, s);
+}
+
+}  // namespace tdl

@@ -98,6 +98,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("port", &tdl::KVServer::port)
       .def("stop", &tdl::KVServer::stop, py::call_guard<py::gil_scoped_release>())
       .def("heartbeat_ages", &tdl::KVServer::heartbeat_ages)
+      .def("lost_clients", &tdl::KVServer::lost_clients)
       .def("num_keys", &tdl::KVServer::num_keys);
 
   py::class_<tdl::KVClient>(m, "KVClient")

@@ -29,6 +29,7 @@ struct KVServer::Impl {
   std::map<std::string, std::string> kv;
   std::map<std::string, double> last_seen;  // client name -> monotonic seconds
   std::set<std::string> departed;
+  std::set<std::string> lost;  // clients whose connection dropped without BYE (crashed peers)
   int listen_fd = -1;
   int port = 0;
   bool stopping = false;
@@ -71,6 +72,7 @@ struct KVServer::Impl {
             std::lock_guard<std::mutex> g(mu);
             touch(who);
             departed.erase(who);
+            lost.erase(who);
             send_u64(fd, 1);
             break;
           }
@@ -207,7 +209,9 @@ struct KVServer::Impl {
         }
       }
     } catch (const std::exception&) {
-      // client went away; nothing to clean up besides the socket
+      // connection ended: a client that never said BYE died (or lost the network)
+      std::lock_guard<std::mutex> g(mu);
+      if (!who.empty() && !departed.count(who) && !stopping) lost.insert(who);
     }
     ::close(fd);
   }
@@ -271,6 +275,11 @@ std::map<std::string, double> KVServer::heartbeat_ages() const {
   for (auto& kv : impl_->last_seen)
     if (!impl_->departed.count(kv.first)) out[kv.first] = t - kv.second;
   return out;
+}
+
+std::vector<std::string> KVServer::lost_clients() const {
+  std::lock_guard<std::mutex> g(impl_->mu);
+  return std::vector<std::string>(impl_->lost.begin(), impl_->lost.end());
 }
 
 size_t KVServer::num_keys() const {

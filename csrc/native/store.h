@@ -18,6 +18,8 @@ class KVServer {
   void stop();
   // client name -> seconds since that client was last heard from (departed clients excluded)
   std::map<std::string, double> heartbeat_ages() const;
+  // names of clients whose connection dropped without an orderly BYE (crashed peers)
+  std::vector<std::string> lost_clients() const;
   size_t num_keys() const;
 
  private:

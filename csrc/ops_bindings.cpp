@@ -2,6 +2,7 @@
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 
+#include "kernels/bn.h"
 #include "kernels/ops.h"
 
 namespace {
@@ -35,9 +36,95 @@ at::Tensor gather_labels(at::Tensor src, at::Tensor idx) {
   tdl::gather_i32(src.data_ptr<int>(), idx.data_ptr<int>(), out.data_ptr<int>(), idx.numel(), cur_stream());
   return out;
 }
+tdl::BnDType bn_dtype(const at::Tensor& x) {
+  if (x.scalar_type() == at::kFloat) return tdl::BnDType::kF32;
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16, "batch_norm: float32 or bfloat16 activations expected");
+  return tdl::BnDType::kBF16;
+}
+
+void bn_check(const at::Tensor& x) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() >= 2, "batch_norm: contiguous [..., C] GPU tensor expected");
+  const int64_t C = x.size(-1);
+  TORCH_CHECK(C % 8 == 0 && C <= 2048, "batch_norm: C must be a multiple of 8 and <= 2048");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "batch_norm: 16-byte aligned data expected");
+}
+
+const float* opt_f32(const c10::optional<at::Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous(), "batch_norm: f32 GPU params");
+  return t->data_ptr<float>();
+}
+
+// training forward: y = act(bn(x) [+ residual]); returns (y, stats[4][C] = mean, invstd, scale, shift);
+// moving statistics updated in place (mean_off: folded conv bias, moving mean only)
+std::vector<at::Tensor> bn_forward_train(at::Tensor x, c10::optional<at::Tensor> gamma, c10::optional<at::Tensor> beta,
+                                         c10::optional<at::Tensor> moving_mean, c10::optional<at::Tensor> moving_var,
+                                         double momentum, double eps, bool relu, c10::optional<at::Tensor> residual,
+                                         c10::optional<at::Tensor> mean_off) {
+  bn_check(x);
+  const int64_t C = x.size(-1), M = x.numel() / C;
+  const void* res = nullptr;
+  if (residual.has_value() && residual->defined()) {
+    bn_check(*residual);
+    TORCH_CHECK(residual->scalar_type() == x.scalar_type() && residual->numel() == x.numel(),
+                "batch_norm: residual must match x");
+    res = residual->data_ptr();
+  }
+  const tdl::BnPlan plan = tdl::bn_plan(M, (int)C);
+  auto f = x.options().dtype(at::kFloat);
+  auto part = at::empty({(int64_t)plan.parts * 2 * C}, f);
+  auto st = at::empty({4, C}, f);  // mean, invstd, scale, shift
+  float* mm = const_cast<float*>(opt_f32(moving_mean));
+  float* mv = const_cast<float*>(opt_f32(moving_var));
+  TORCH_CHECK((mm == nullptr) == (mv == nullptr), "batch_norm: moving mean and variance go together");
+  hipStream_t s = cur_stream();
+  float* sp = st.data_ptr<float>();
+  tdl::bn_forward_stats(x.data_ptr(), bn_dtype(x), M, (int)C, part.data_ptr<float>(), opt_f32(gamma), opt_f32(beta),
+                        opt_f32(mean_off), sp, sp + C, sp + 2 * C, sp + 3 * C, mm, mv, (float)momentum, (float)eps, s);
+  auto y = at::empty_like(x);
+  tdl::bn_apply(x.data_ptr(), res, y.data_ptr(), bn_dtype(x), M, (int)C, sp + 2 * C, sp + 3 * C, relu ? 1 : 0, s);
+  return {y, st};
+}
+
+// backward (mode 0 plain, 1 relu, 2 add+relu using y); returns (dx, dgamma, dbeta[, dz])
+std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> y,
+                                    c10::optional<at::Tensor> gamma, at::Tensor st, int64_t mode) {
+  bn_check(x);
+  bn_check(dy);
+  TORCH_CHECK(dy.scalar_type() == x.scalar_type() && dy.numel() == x.numel(), "batch_norm backward: dy/x mismatch");
+  TORCH_CHECK(mode >= 0 && mode <= 2, "batch_norm backward: bad mode");
+  const int64_t C = x.size(-1), M = x.numel() / C;
+  TORCH_CHECK(st.is_contiguous() && st.numel() == 4 * C && st.scalar_type() == at::kFloat, "batch_norm: stats [4][C]");
+  const void* yp = nullptr;
+  at::Tensor dz;
+  if (mode == 2) {
+    TORCH_CHECK(y.has_value() && y->defined(), "batch_norm backward mode 2 needs y");
+    bn_check(*y);
+    yp = y->data_ptr();
+    dz = at::empty_like(x);
+  }
+  const tdl::BnPlan plan = tdl::bn_plan(M, (int)C);
+  auto f = x.options().dtype(at::kFloat);
+  auto part = at::empty({(int64_t)plan.parts * 2 * C}, f);
+  auto out = at::empty({5, C}, f);  // dgamma, dbeta, coef[3]
+  auto dx = at::empty_like(x);
+  float* o = out.data_ptr<float>();
+  const float* sp = st.data_ptr<float>();
+  tdl::bn_backward(dy.data_ptr(), x.data_ptr(), yp, mode == 2 ? dz.data_ptr() : nullptr, dx.data_ptr(), bn_dtype(x), M,
+                   (int)C, part.data_ptr<float>(), opt_f32(gamma), sp, sp + C, sp + 2 * C, sp + 3 * C, o, o + C,
+                   o + 2 * C, (int)mode, cur_stream());
+  if (mode == 2) return {dx, out[0], out[1], dz};
+  return {dx, out[0], out[1]};
+}
 }  // namespace
 
 void register_ops(pybind11::module& m) {
   m.def("gather_rows", &gather_rows, "row gather (+u8->f32 scale) of a device-resident dataset");
   m.def("gather_labels", &gather_labels);
+  m.def("bn_forward_train", &bn_forward_train, "NHWC batch-norm training forward (+relu)", pybind11::arg("x"),
+        pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("moving_mean"), pybind11::arg("moving_var"),
+        pybind11::arg("momentum"), pybind11::arg("eps"), pybind11::arg("relu") = false,
+        pybind11::arg("residual") = pybind11::none(), pybind11::arg("mean_off") = pybind11::none());
+  m.def("bn_backward", &bn_backward, "NHWC batch-norm training backward", pybind11::arg("dy"), pybind11::arg("x"),
+        pybind11::arg("y"), pybind11::arg("gamma"), pybind11::arg("stats"), pybind11::arg("mode"));
 }

@@ -1,0 +1,109 @@
+#!/usr/bin/env python3
+"""ResNet-50 training throughput (BASELINE configs 4/5): synthetic ImageNet-shaped data, random init,
+Keras ResNet50 built with this framework, mixed_bfloat16 policy, SGD momentum 0.9, MirroredStrategy
+(one process per GPU, RCCL bucketed all-reduce overlapped with backward).
+
+    python scripts/bench_resnet50.py [--batch 256] [--steps 20] [--warmup 5]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 scripts/bench_resnet50.py
+
+Prints one JSON line (rank 0) in the bench.py format.  ``--engine`` picks the generic autograd
+engine ("generic") or the MI355X ResNet engine ("resnet", whole-step hipGraph + fused HIP kernels).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256, help="per-replica batch")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--classes", type=int, default=1000)
+    ap.add_argument("--dtype", default="mixed_bfloat16", choices=["mixed_bfloat16", "float32"])
+    ap.add_argument("--engine", default="auto")
+    args = ap.parse_args()
+
+    import torch
+
+    import tensorflow_distributed_learning_amd as tdl
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 and "LOCAL_RANK" in os.environ:
+        torch.cuda.set_device(int(os.environ["LOCAL_RANK"]))
+    if args.engine != "auto":
+        os.environ["TDL_ENGINE"] = args.engine
+    tdl.keras.mixed_precision.set_global_policy(args.dtype)
+    strategy = tdl.distribute.MirroredStrategy()
+    R = strategy.num_replicas_in_sync
+    dev = strategy.extended.device
+    b = args.batch
+    B = b * R
+    # device-resident synthetic ImageNet-shaped dataset: 4 distinct global batches, repeated
+    g = torch.Generator(device="cpu").manual_seed(0)
+    n = 4 * B
+    x = torch.empty(n, args.image, args.image, 3, dtype=torch.float32, device=dev)
+    x.uniform_(0, 1)
+    y = torch.randint(0, args.classes, (n,), generator=g).to(torch.int64).to(dev)
+    ds = tdl.data.Dataset.from_tensor_slices((x, y)).batch(B, drop_remainder=True).repeat()
+    opts = tdl.data.Options()
+    opts.experimental_distribute.auto_shard_policy = tdl.data.AutoShardPolicy.OFF
+    ds = ds.with_options(opts)
+
+    with strategy.scope():
+        model = tdl.keras.applications.ResNet50(weights=None, classes=args.classes, classifier_activation=None,
+                                                input_shape=(args.image, args.image, 3))
+        model.compile(loss=tdl.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+                      optimizer=tdl.keras.optimizers.SGD(learning_rate=0.1, momentum=0.9),
+                      metrics=["sparse_categorical_accuracy"])
+    trainer = model._get_trainer()
+    handler = trainer.prepare(ds) if hasattr(trainer, "prepare") else None
+    if handler is None:
+        from tensorflow_distributed_learning_amd.engine.trainer import HostDataHandler
+
+        handler = HostDataHandler(ds, strategy)
+    comm = strategy.extended.communicator
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    if hasattr(trainer, "warm_graphs"):
+        trainer.warm_graphs(args.steps)
+    trainer.run_train(handler, args.warmup)
+    sync()
+    comm.barrier()
+    sync()
+    t0 = time.perf_counter()
+    done = trainer.run_train(handler, args.steps)
+    sync()
+    comm.barrier()
+    sync()
+    dt = time.perf_counter() - t0
+    assert done == args.steps, done
+    t = torch.tensor([dt], dtype=torch.float64, device=dev if comm.name == "rccl" else "cpu")
+    comm.all_reduce(t, "max")
+    dt = float(t.item())
+    logs = trainer.logs()
+    if strategy.extended.rank == 0:
+        print(json.dumps({
+            "metric": "images/sec (whole node) ResNet-50 synthetic ImageNet-shaped",
+            "value": round(args.steps * B / dt, 1), "unit": "images/sec", "n_gpus": R,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16" if args.dtype == "mixed_bfloat16" else "fp32",
+            "data": "synthetic ImageNet-shaped, device-resident; random init",
+            "config": {"model": "keras.applications.ResNet50 (25.6M params)", "global_batch": B,
+                       "image": args.image, "parallelism": f"dp{R}", "engine": trainer.kind,
+                       "communicator": comm.name, "final_loss": round(logs["loss"], 4)},
+        }), flush=True)
+    strategy.shutdown()
+
+
+if __name__ == "__main__":
+    main()

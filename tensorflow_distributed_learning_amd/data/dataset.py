@@ -104,8 +104,19 @@ def _stack(elems: List[Any]):
 
 
 def _take_rows(cols, idx: torch.Tensor):
-    return map_structure(lambda c: c.index_select(0, idx) if isinstance(c, torch.Tensor) else [c[i] for i in idx.tolist()],
-                         cols)
+    n = int(idx.numel())
+    lo = int(idx[0]) if n else 0
+    # a contiguous run of rows (unshuffled batch) is a view, not a gather
+    contiguous = n > 0 and int(idx[-1]) - lo == n - 1 and bool(torch.all(idx[1:] - idx[:-1] == 1))
+
+    def take(c):
+        if not isinstance(c, torch.Tensor):
+            return [c[i] for i in idx.tolist()]
+        if contiguous:
+            return c.narrow(0, lo, n)
+        return c.index_select(0, idx.to(c.device))
+
+    return map_structure(take, cols)
 
 
 def _num_rows(cols) -> int:

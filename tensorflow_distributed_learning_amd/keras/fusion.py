@@ -1,0 +1,116 @@
+"""Graph-level fusion for training-mode functional models on the GPU.
+
+The functional executor (models.Model._run_graph) asks :func:`plan` for a fusion plan of its node
+list; the plan rewrites, at execution time only (the layer graph, variables, checkpoints and
+``model.summary()`` are untouched):
+
+* ``Conv2D(use_bias, linear) -> BatchNormalization``: the conv runs without its bias; the bias is
+  folded into the BN (only the moving mean sees it; its gradient is exactly zero in training mode).
+* ``BatchNormalization -> ReLU``: one fused kernel pass (ops/batchnorm.py).
+* ``BatchNormalization -> Add(other) -> ReLU``: the ResNet block tail, one fused pass that also
+  produces the residual's gradient.
+
+Every intermediate tensor of a fused group must have exactly one consumer.  A group executes at
+the position of its last node, when all its external inputs exist.  Eval / CPU calls run the
+original node by node.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, List, Optional
+
+from . import activations as A
+from . import layers as L
+
+
+class Group:
+    __slots__ = ("bn_node", "relu", "residual", "conv_layer", "out", "last")
+
+    def __init__(self, bn_node, relu, residual, conv_layer, out, last):
+        self.bn_node, self.relu, self.residual, self.conv_layer, self.out, self.last = (
+            bn_node, relu, residual, conv_layer, out, last)
+
+
+class Plan:
+    def __init__(self):
+        self.skip = set()        # node ids absorbed into a group that runs elsewhere
+        self.conv_nobias = set()  # conv node ids whose bias is folded into their BN
+        self.groups: Dict[int, Group] = {}  # id(last node) -> group
+
+    def __len__(self):
+        return len(self.groups)
+
+
+def _is_plain_relu(layer) -> bool:
+    if isinstance(layer, L.Activation):
+        return layer.activation is A.relu
+    if isinstance(layer, L.ReLU):
+        return layer.max_value is None and layer.negative_slope == 0 and layer.threshold == 0
+    return False
+
+
+def _single_tensor(x):
+    return x if isinstance(x, L.KerasTensor) else None
+
+
+def plan(nodes: List[L.Node], outputs) -> Plan:
+    p = Plan()
+    if os.environ.get("TDL_FUSE", "1") != "1":
+        return p
+    consumers: Dict[int, List[L.Node]] = {}
+    for n in nodes:
+        for t in L._flat(n.inputs):
+            consumers.setdefault(id(t), []).append(n)
+    outs = {id(t) for t in L._flat(outputs)}
+
+    def only_consumer(t) -> Optional[L.Node]:
+        if t is None or id(t) in outs:
+            return None
+        c = consumers.get(id(t), [])
+        return c[0] if len(c) == 1 else None
+
+    producer = {id(t): n for n in nodes for t in L._flat(n.outputs)}
+    for n in nodes:
+        bn = n.layer
+        if not (isinstance(bn, L.BatchNormalization) and bn.trainable and bn.axis in (-1, 3)):
+            continue
+        x_t = _single_tensor(n.inputs)
+        out_t = _single_tensor(n.outputs)
+        if x_t is None or out_t is None or len(x_t.shape) != 4:
+            continue
+        conv_layer = None
+        prod = producer.get(id(x_t))
+        if prod is not None and isinstance(prod.layer, L.Conv2D) and prod.layer.use_bias and \
+                prod.layer.activation is A.linear and prod.layer.trainable and only_consumer(x_t) is n:
+            conv_layer = prod.layer
+            p.conv_nobias.add(id(prod))
+        relu, residual, last, out = False, None, n, out_t
+        c1 = only_consumer(out_t)
+        if c1 is not None and _is_plain_relu(c1.layer):
+            relu, last, out = True, c1, _single_tensor(c1.outputs)
+        elif c1 is not None and isinstance(c1.layer, L.Add) and isinstance(c1.inputs, (list, tuple)) and \
+                len(c1.inputs) == 2 and id(c1) not in p.skip:  # (a projection shortcut's BN may own it)
+            add_out = _single_tensor(c1.outputs)
+            c2 = only_consumer(add_out)
+            other = c1.inputs[1] if c1.inputs[0] is out_t else c1.inputs[0]
+            if c2 is not None and _is_plain_relu(c2.layer) and other is not out_t and \
+                    tuple(other.shape) == tuple(out_t.shape):
+                relu, residual, last, out = True, other, c2, _single_tensor(c2.outputs)
+                p.skip.add(id(c1))
+        if last is not n:
+            p.skip.add(id(n))
+        p.groups[id(last)] = Group(n, relu, residual, conv_layer, out, last)
+    return p
+
+
+def run_group(g: Group, vals, training):
+    from ..ops.batchnorm import batch_norm_train
+
+    bn = g.bn_node.layer
+    x = vals[id(g.bn_node.inputs)]
+    r = vals[id(g.residual)] if g.residual is not None else None
+    cb = g.conv_layer.bias.value if g.conv_layer is not None else None
+    y = batch_norm_train(x, bn.gamma.value if bn.gamma is not None else None,
+                         bn.beta.value if bn.beta is not None else None, bn.moving_mean.value,
+                         bn.moving_variance.value, bn.momentum, bn.epsilon, relu=g.relu, residual=r, conv_bias=cb)
+    vals[id(g.out)] = y

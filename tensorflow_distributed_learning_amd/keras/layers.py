@@ -308,7 +308,9 @@ class Conv2D(Layer):
                                     regularizer=self.bias_regularizer) if self.use_bias else None
         self.built = True
 
-    def call(self, x, training=None):
+    def call(self, x, training=None, _fold_bias=False):
+        """``_fold_bias``: the functional executor folded this bias into the following training-mode
+        BatchNormalization (keras/fusion.py), so the convolution runs without it."""
         w = self.kernel.value.to(x.dtype).permute(3, 2, 0, 1)  # HWIO -> OIHW
         h = x.permute(0, 3, 1, 2)  # NHWC data viewed as NCHW (channels_last memory format)
         pad = 0
@@ -319,7 +321,7 @@ class Conv2D(Layer):
                 pad = (ph[0], pw[0])
             else:
                 h = F.pad(h, (pw[0], pw[1], ph[0], ph[1]))
-        b = self.bias.value.to(x.dtype) if self.bias is not None else None
+        b = self.bias.value.to(x.dtype) if (self.bias is not None and not _fold_bias) else None
         y = F.conv2d(h, w, b, stride=self.strides, padding=pad, dilation=self.dilation_rate, groups=self.groups)
         return self.activation(y.permute(0, 2, 3, 1))
 
@@ -562,6 +564,15 @@ class BatchNormalization(Layer):
 
     def call(self, x, training=None):
         axis = self.axis % x.dim()
+        if training and self.trainable and axis == x.dim() - 1 and x.is_cuda:
+            # NHWC training on the GPU: hand-written batch-norm kernels (ops/batchnorm.py)
+            from ..ops import batchnorm as _bn
+
+            if _bn.supported(x):
+                return _bn.batch_norm_train(x, self.gamma.value if self.gamma is not None else None,
+                                            self.beta.value if self.beta is not None else None,
+                                            self.moving_mean.value, self.moving_variance.value, self.momentum,
+                                            self.epsilon)
         perm = None
         if axis != 1:
             perm = [0, axis] + [i for i in range(1, x.dim()) if i != axis]

@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import math
 import sys
+import time
 import warnings
 from typing import Any, Dict, List, Optional
 
@@ -27,6 +28,9 @@ from . import optimizers as _opt
 from .layers import InputLayer, KerasTensor, Layer, Node, _flat, _map
 
 _GLOBAL_POLICY = ["float32"]
+
+
+_FUSE_CPU = [False]  # tests: apply the training-graph fusion plan to CPU tensors too
 
 
 class Model(Layer):
@@ -103,12 +107,38 @@ class Model(Layer):
         self._built_input_shape = self._inputs[0].shape if len(self._inputs) == 1 else [i.shape for i in self._inputs]
         self.built = True
 
+    def _fusion(self):
+        fp = self.__dict__.get("_fusion_plan")
+        if fp is None or fp[0] is not self._nodes:
+            from . import fusion
+
+            fp = (self._nodes, fusion.plan(self._nodes, self._outputs))
+            self.__dict__["_fusion_plan"] = fp
+        return fp[1]
+
     def _run_graph(self, inputs, training):
         xs = inputs if isinstance(inputs, (list, tuple)) else [inputs]
         vals = {id(k): v for k, v in zip(self._inputs, xs)}
+        fp = None
+        if training and isinstance(xs[0], torch.Tensor) and (xs[0].is_cuda or _FUSE_CPU[0]):
+            fp = self._fusion()  # keras/fusion.py: conv-bias/BN/ReLU/Add groups (training, GPU)
+            if not fp.groups:
+                fp = None
         for n in self._nodes:
+            if fp is not None:
+                nid = id(n)
+                if nid in fp.skip:
+                    continue
+                g = fp.groups.get(nid)
+                if g is not None:
+                    from .fusion import run_group
+
+                    run_group(g, vals, training)
+                    continue
             args = _map(lambda t: vals[id(t)], n.inputs)
             kw = {k: v for k, v in n.kwargs.items() if k != "training"}
+            if fp is not None and id(n) in fp.conv_nobias:
+                kw["_fold_bias"] = True
             out = n.layer(args, training=training, **kw)
             if isinstance(n.outputs, list):
                 for t, o in zip(n.outputs, out):
@@ -346,7 +376,7 @@ class Model(Layer):
                 n = K if steps is None else min(K, steps - done)
                 if want_batch:
                     cb_list.on_train_batch_begin(done)
-                got = trainer.run_train(handler, n)
+                got = _run_guarded(trainer, handler, n, strategy)
                 done += got
                 if want_batch and got:
                     cb_list.on_train_batch_end(done - 1, _LazyLogs(trainer))
@@ -686,3 +716,26 @@ def load_model(path, compile=True, custom_objects=None):
 
 def clone_model(model):
     return model_from_config(model.get_config_full())
+
+
+def _run_guarded(trainer, handler, n, strategy):
+    """One execution of ``n`` steps with failure detection (utils/fault.py): a collective that
+    fails because a peer died is re-raised as PeerLostError with the watchdog's diagnosis, and the
+    fault-injection hook runs at the execution boundary."""
+    from ..utils import fault
+
+    wd = getattr(strategy.extended, "watchdog", None)
+    try:
+        got = trainer.run_train(handler, n)
+    except Exception as e:
+        if wd is not None:
+            deadline = time.monotonic() + 3 * wd.interval + 1.0
+            while wd.reason is None and time.monotonic() < deadline:
+                time.sleep(wd.interval / 4)
+            if wd.reason is not None:
+                wd.acknowledged = True
+                raise fault.PeerLostError(f"{wd.reason} (collective failed: {e})") from e
+        raise
+    fault.check()
+    fault.maybe_inject(strategy.extended.rank, int(trainer.optimizer.iterations))
+    return got

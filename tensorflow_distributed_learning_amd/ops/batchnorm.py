@@ -1,0 +1,85 @@
+"""Training-mode batch normalisation on the hand-written NHWC kernels (csrc/kernels/bn.hip).
+
+``batch_norm_train(x, gamma, beta, moving_mean, moving_var, momentum, eps, relu, residual,
+conv_bias)`` normalises the last axis of a ``[..., C]`` tensor with its batch statistics, updates
+the moving statistics in place (Keras momentum convention; unbiased moving variance) and fuses the
+neighbours the functional-model executor hands it (keras/models.py ``_fusion_plan``):
+
+* ``relu=True``                   : BN -> ReLU
+* ``residual=r, relu=True``       : BN -> Add(r) -> ReLU (ResNet block tail)
+* ``conv_bias=b``                 : the preceding Conv2D's bias, folded in.  In training mode a
+  per-channel bias before BN only shifts the batch mean, so the output is unchanged, the moving mean
+  gets ``+ b`` and the bias gradient is exactly zero (returned as zeros).
+
+On a GPU tensor the HIP kernels are the only path (:func:`..ops.hip` raises if the extension is not
+built); CPU tensors use PyTorch ops with the same semantics.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import hip
+
+
+def supported(x: torch.Tensor) -> bool:
+    C = x.shape[-1]
+    return x.is_cuda and x.dim() >= 2 and C % 8 == 0 and C <= 2048 and x.dtype in (torch.float32, torch.bfloat16)
+
+
+def _aligned(t: torch.Tensor) -> torch.Tensor:
+    t = t.contiguous()
+    return t if t.data_ptr() % 16 == 0 else t.clone()
+
+
+class _BatchNormTrain(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, residual, conv_bias, moving_mean, moving_var, momentum, eps, relu):
+        C = hip()
+        xc = _aligned(x)
+        rc = _aligned(residual.to(xc.dtype)) if residual is not None else None
+        y, st = C.bn_forward_train(xc, gamma, beta, moving_mean, moving_var, float(momentum), float(eps), bool(relu),
+                                   rc, conv_bias.detach() if conv_bias is not None else None)
+        ctx.mode = 2 if residual is not None else (1 if relu else 0)
+        ctx.flags = (gamma is not None, beta is not None, residual is not None, conv_bias is not None)
+        ctx.res_dtype = residual.dtype if residual is not None else None
+        ctx.save_for_backward(xc, gamma if gamma is not None else st, st, y if ctx.mode == 2 else st,
+                              conv_bias if conv_bias is not None else st)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = hip()
+        xc, gamma, st, y, conv_bias = ctx.saved_tensors
+        has_g, has_b, has_r, has_cb = ctx.flags
+        dy = _aligned(dy.to(xc.dtype))
+        out = C.bn_backward(dy, xc, y if ctx.mode == 2 else None, gamma if has_g else None, st, ctx.mode)
+        dx, dgamma, dbeta = out[0], out[1], out[2]
+        dres = out[3].to(ctx.res_dtype) if has_r else None
+        dcb = torch.zeros_like(conv_bias) if has_cb else None
+        return (dx, dgamma if has_g else None, dbeta if has_b else None, dres, dcb, None, None, None, None, None)
+
+
+def batch_norm_train(x: torch.Tensor, gamma: Optional[torch.Tensor], beta: Optional[torch.Tensor],
+                     moving_mean: Optional[torch.Tensor], moving_var: Optional[torch.Tensor], momentum: float,
+                     eps: float, relu: bool = False, residual: Optional[torch.Tensor] = None,
+                     conv_bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Keras-convention ``momentum`` (moving = moving*momentum + batch*(1-momentum))."""
+    if residual is not None and not relu:
+        raise ValueError("the fused residual form is BN -> Add -> ReLU")
+    if supported(x) and (residual is None or tuple(residual.shape) == tuple(x.shape)):
+        return _BatchNormTrain.apply(x, gamma, beta, residual, conv_bias, moving_mean, moving_var, momentum, eps, relu)
+    h = x if conv_bias is None else x + conv_bias.to(x.dtype)
+    perm = [0, h.dim() - 1] + list(range(1, h.dim() - 1))
+    hp = h.permute(*perm)
+    y = F.batch_norm(hp, moving_mean, moving_var, gamma.to(hp.dtype) if gamma is not None else None,
+                     beta.to(hp.dtype) if beta is not None else None, training=True, momentum=1.0 - momentum, eps=eps)
+    inv = [0] * len(perm)
+    for i, p in enumerate(perm):
+        inv[p] = i
+    y = y.permute(*inv)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y) if relu else y

@@ -288,6 +288,10 @@ class Strategy:
         if self._closed:
             return
         self._closed = True
+        wd = getattr(self.extended, "watchdog", None)
+        if wd is not None:
+            wd.stop()
+            self.extended.watchdog = None
         try:
             self.extended.communicator.shutdown()
         except Exception:
@@ -461,6 +465,11 @@ class MultiWorkerMirroredStrategy(Strategy):
                                         host_hint=host_hint, timeout=opts.timeout_seconds or 1800.0)
         ext = StrategyExtended(self, dev, rank, world, lr, comm, opts, tf_config=cfg, rendezvous=rendezvous)
         super().__init__(ext, cluster_resolver=resolver)
+        if rendezvous is not None and world > 1 and os.environ.get("TDL_WATCHDOG", "1") == "1":
+            from ..utils.fault import PeerWatchdog
+
+            ext.watchdog = PeerWatchdog(rendezvous, stale_after=float(os.environ.get("TDL_HEARTBEAT_TIMEOUT", "60")),
+                                        grace=float(os.environ.get("TDL_ABORT_GRACE", "30"))).start()
         if world > 1:
             comm.barrier()
 

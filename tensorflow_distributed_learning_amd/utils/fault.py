@@ -1,0 +1,142 @@
+"""Failure detection and fault injection for multi-worker jobs (test tier T-fault).
+
+The reference assumes every gRPC server comes up and stays up (README.md:65-68): a dead worker
+stalls the job.  Here a job fails fast and says why:
+
+* **Detection.**  The chief's native KV server (csrc/native/store.cpp) marks a client whose TCP
+  connection drops without an orderly BYE as *lost*, and every rank keeps a heartbeat connection
+  (cluster/rendezvous.py).  :class:`PeerWatchdog` runs on every rank: on the chief it turns a lost or
+  stale heartbeat into the job-wide key ``job/abort``; on every rank it polls that key and notices
+  when the chief itself disappears.
+* **Reaction.**  ``Model.fit`` calls :func:`check` at every execution boundary, which raises
+  :class:`PeerLostError` on a fault.  A rank blocked inside a collective cannot reach that check,
+  so after ``grace`` seconds the watchdog ends the process with exit status
+  :data:`EXIT_PEER_LOST`, having printed the reason.  (The collective timeouts of the TCP ring and
+  of RCCL/gloo stay as the last line of defence.)
+* **Injection.**  ``TDL_FAULT_KILL_AT_STEP="rank:step"`` makes that rank die abruptly
+  (``os._exit``) once its optimizer has taken ``step`` steps — the fault the tests inject.
+
+The job is not elastic: recovery is a restart that resumes from the chief's checkpoint
+(``keras.callbacks.BackupAndRestore``), as with TF.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import threading
+import time
+from typing import Optional
+
+EXIT_PEER_LOST = 75
+EXIT_INJECTED = 43
+
+_ACTIVE: Optional["PeerWatchdog"] = None
+
+
+class PeerLostError(RuntimeError):
+    """A peer of this multi-worker job died, hung, or the job was aborted."""
+
+
+def _kill_spec():
+    spec = os.environ.get("TDL_FAULT_KILL_AT_STEP")
+    if not spec:
+        return None
+    r, s = spec.split(":")
+    return int(r), int(s)
+
+
+def maybe_inject(rank: int, step: int) -> None:
+    """Fault injection hook: die abruptly when ``TDL_FAULT_KILL_AT_STEP`` names this rank/step."""
+    spec = _kill_spec()
+    if spec is not None and spec[0] == rank and step >= spec[1]:
+        sys.stderr.write(f"[tdl] fault injection: rank {rank} exits at step {step}\n")
+        sys.stderr.flush()
+        os._exit(EXIT_INJECTED)
+
+
+def check() -> None:
+    """Raise :class:`PeerLostError` if the job has been aborted."""
+    w = _ACTIVE
+    if w is not None and w.reason is not None:
+        w.acknowledged = True
+        raise PeerLostError(w.reason)
+
+
+class PeerWatchdog:
+    """Per-rank failure detector over the rendezvous store (see module docstring)."""
+
+    def __init__(self, rendezvous, interval: float = 0.5, stale_after: float = 60.0, grace: float = 30.0):
+        from .. import ops
+
+        self.rdv = rendezvous
+        self.interval = float(interval)
+        self.stale_after = float(stale_after)
+        self.grace = float(grace)
+        self.reason: Optional[str] = None
+        self.acknowledged = False
+        self._stop = threading.Event()
+        lay = rendezvous.layout
+        self.rank = lay.rank
+        self.world = lay.world_size
+        self._client = ops.native().KVClient(rendezvous.store_host, rendezvous.store_port, 10000,
+                                             f"watchdog/{self.rank}")
+        self._thread = threading.Thread(target=self._run, name="tdl-watchdog", daemon=True)
+
+    def start(self) -> "PeerWatchdog":
+        global _ACTIVE
+        _ACTIVE = self
+        self._thread.start()
+        return self
+
+    def stop(self):
+        global _ACTIVE
+        self._stop.set()
+        if _ACTIVE is self:
+            _ACTIVE = None
+        self._thread.join(timeout=5 * self.interval + 1)
+        try:
+            self._client.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------------------------------
+    def _chief_scan(self) -> Optional[str]:
+        srv = self.rdv.server
+        lost = [c for c in srv.lost_clients() if c.startswith("hb/")]
+        if lost:
+            return f"lost connection to {', '.join(sorted('rank ' + c[3:] for c in lost))} (process died)"
+        stale = self.rdv.dead_peers(self.stale_after)
+        if stale:
+            return f"no heartbeat from {', '.join(sorted('rank ' + c[3:] for c in stale))} for {self.stale_after:.0f}s"
+        return None
+
+    def _abort(self, reason: str):
+        if self.reason is None:
+            self.reason = reason
+            sys.stderr.write(f"[tdl] rank {self.rank}: aborting multi-worker job: {reason}\n")
+            sys.stderr.flush()
+
+    def _run(self):
+        aborted_at = None
+        while not self._stop.wait(self.interval):
+            if self.reason is None:
+                try:
+                    if self.rdv.server is not None:
+                        why = self._chief_scan()
+                        if why is not None:
+                            self._client.set("job/abort", why.encode())
+                    if self._client.check(["job/abort"]):
+                        self._abort(bytes(self._client.get("job/abort")).decode())
+                except Exception as e:  # the chief's store is gone
+                    if self._stop.is_set():
+                        return
+                    self._abort(f"lost connection to the chief's rendezvous store ({e})")
+            if self.reason is not None:
+                aborted_at = aborted_at or time.monotonic()
+                if not self.acknowledged and time.monotonic() - aborted_at > self.grace:
+                    sys.stderr.write(f"[tdl] rank {self.rank}: still blocked {self.grace:.0f}s after the abort; "
+                                     f"exiting ({self.reason})\n")
+                    sys.stderr.flush()
+                    os._exit(EXIT_PEER_LOST)
+                if self.acknowledged:
+                    return

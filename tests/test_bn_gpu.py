@@ -1,0 +1,152 @@
+"""NHWC batch-norm HIP kernels (csrc/kernels/bn.hip) vs a float64 PyTorch reference of the same op:
+outputs, moving statistics, and input/gamma/beta gradients."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [((4, 7, 7, 64), torch.float32), ((3, 5, 5, 96), torch.float32), ((2, 5, 5, 2048), torch.bfloat16),
+          ((16, 56, 56, 64), torch.bfloat16), ((6, 9, 9, 256), torch.float32), ((1, 1, 3, 8), torch.float32)]
+
+
+def _ref(x, g, b, mm, mv, mom, eps, relu):
+    x64 = x.double().detach().requires_grad_(True)
+    g64 = g.double().detach().requires_grad_(True)
+    b64 = b.double().detach().requires_grad_(True)
+    mm64, mv64 = mm.double().clone(), mv.double().clone()
+    h = x64.movedim(-1, 1)
+    y = F.batch_norm(h, mm64, mv64, g64, b64, training=True, momentum=1 - mom, eps=eps).movedim(1, -1)
+    if relu:
+        y = F.relu(y)
+    return x64, g64, b64, y, mm64, mv64
+
+
+@pytest.mark.parametrize("shape,dtype", SHAPES)
+@pytest.mark.parametrize("relu", [False, True])
+def test_bn_train_matches_fp64(shape, dtype, relu):
+    from tensorflow_distributed_learning_amd.ops.batchnorm import batch_norm_train
+
+    torch.manual_seed(0)
+    dev = torch.device("cuda:0")
+    C = shape[-1]
+    x = (torch.randn(shape, device=dev) * 2 + 0.5).to(dtype)
+    g = (torch.rand(C, device=dev) + 0.5).requires_grad_(True)
+    b = torch.randn(C, device=dev).requires_grad_(True)
+    mm, mv = torch.randn(C, device=dev), torch.rand(C, device=dev) + 0.5
+    x64, g64, b64, y64, mm64, mv64 = _ref(x, g, b, mm, mv, 0.9, 1e-3, relu)
+    xin = x.clone().requires_grad_(True)
+    y = batch_norm_train(xin, g, b, mm, mv, 0.9, 1e-3, relu=relu)
+    assert y.dtype == dtype and y.shape == x.shape
+    tol = dict(atol=2e-4, rtol=2e-4) if dtype == torch.float32 else dict(atol=4e-2, rtol=2e-2)
+    torch.testing.assert_close(y.double(), y64, **tol)
+    torch.testing.assert_close(mm.double(), mm64, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(mv.double(), mv64, atol=1e-4, rtol=1e-4)
+    dy = torch.randn(shape, device=dev).to(dtype)
+    y.backward(dy)
+    y64.backward(dy.double())
+    n = x.numel() // C
+    gtol = dict(atol=5e-4, rtol=1e-3) if dtype == torch.float32 else dict(atol=6e-2, rtol=3e-2)
+    torch.testing.assert_close(xin.grad.double(), x64.grad, **gtol)
+    scale = max(1.0, n ** 0.5 / 8)
+    torch.testing.assert_close(g.grad.double(), g64.grad, atol=gtol["atol"] * scale * 4, rtol=gtol["rtol"])
+    torch.testing.assert_close(b.grad.double(), b64.grad, atol=gtol["atol"] * scale * 4, rtol=gtol["rtol"])
+
+
+def test_bn_layer_uses_hip_kernels():
+    import tensorflow_distributed_learning_amd as tdl
+    from tensorflow_distributed_learning_amd.ops import loaded_paths
+
+    x = torch.randn(4, 6, 6, 32, device="cuda:0")
+    with tdl.distribute.OneDeviceStrategy("/gpu:0").scope():
+        layer = tdl.keras.layers.BatchNormalization()
+        layer.build(x.shape)
+    for v in (layer.gamma, layer.beta, layer.moving_mean, layer.moving_variance):
+        v._value = v._value.to("cuda:0")
+    y = layer(x, training=True)
+    assert "_C" in loaded_paths()
+    ref = F.batch_norm(x.movedim(-1, 1), None, None, training=True, eps=1e-3).movedim(1, -1)
+    torch.testing.assert_close(y, ref, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_bn_add_relu_with_folded_conv_bias(dtype):
+    from tensorflow_distributed_learning_amd.ops.batchnorm import batch_norm_train
+
+    torch.manual_seed(1)
+    dev = torch.device("cuda:0")
+    shape, C = (4, 9, 9, 128), 128
+    x = torch.randn(shape, device=dev).to(dtype)
+    r = torch.randn(shape, device=dev).to(dtype)
+    g = (torch.rand(C, device=dev) + 0.5).requires_grad_(True)
+    b = torch.randn(C, device=dev).requires_grad_(True)
+    cb = torch.randn(C, device=dev).requires_grad_(True)
+    mm, mv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    # reference: relu(BN(x + cb) + r) in float64
+    x64 = x.double().requires_grad_(True)
+    r64 = r.double().requires_grad_(True)
+    g64, b64, cb64 = (t.detach().double().requires_grad_(True) for t in (g, b, cb))
+    mm64, mv64 = mm.double().clone(), mv.double().clone()
+    h = (x64 + cb64).movedim(-1, 1)
+    y64 = F.relu(F.batch_norm(h, mm64, mv64, g64, b64, training=True, momentum=0.01, eps=1e-3).movedim(1, -1) + r64)
+    xin, rin = x.clone().requires_grad_(True), r.clone().requires_grad_(True)
+    y = batch_norm_train(xin, g, b, mm, mv, 0.99, 1e-3, relu=True, residual=rin, conv_bias=cb)
+    tol = dict(atol=2e-4, rtol=2e-4) if dtype == torch.float32 else dict(atol=4e-2, rtol=2e-2)
+    torch.testing.assert_close(y.double(), y64, **tol)
+    torch.testing.assert_close(mm.double(), mm64, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(mv.double(), mv64, atol=1e-4, rtol=1e-4)
+    dy = torch.randn(shape, device=dev).to(dtype)
+    y.backward(dy)
+    y64.backward(dy.double())
+    gtol = dict(atol=5e-4, rtol=1e-3) if dtype == torch.float32 else dict(atol=6e-2, rtol=3e-2)
+    torch.testing.assert_close(xin.grad.double(), x64.grad, **gtol)
+    torch.testing.assert_close(rin.grad.double(), r64.grad, **gtol)
+    torch.testing.assert_close(g.grad.double(), g64.grad, atol=gtol["atol"] * 20, rtol=gtol["rtol"])
+    torch.testing.assert_close(b.grad.double(), b64.grad, atol=gtol["atol"] * 20, rtol=gtol["rtol"])
+    assert float(cb.grad.abs().max()) == 0.0 and float(cb64.grad.abs().max()) < 1e-6
+
+
+def test_resnet50_fused_training_graph_matches_unfused():
+    import sys
+
+    import tensorflow_distributed_learning_amd as tdl
+
+    tdl.keras.utils.set_random_seed(0)
+    m = tdl.keras.applications.ResNet50(weights=None, classes=10, classifier_activation=None,
+                                        input_shape=(32, 32, 3))
+    for v in m.weights:
+        v._value = v._value.to("cuda:0")
+    x = torch.randn(4, 32, 32, 3, device="cuda:0")
+    init = [v._value.clone() for v in m.non_trainable_weights]
+
+    def run(fuse):
+        import os
+
+        os.environ["TDL_FUSE"] = "1" if fuse else "0"
+        m.__dict__.pop("_fusion_plan", None)
+        for v, t in zip(m.non_trainable_weights, init):
+            v._value.copy_(t)
+        leaves = []
+        for v in m.trainable_weights:
+            v._leaf = v._value.detach().clone().requires_grad_(True)
+            leaves.append(v._leaf)
+        y = m(x, training=True)
+        (y.float() ** 2).sum().backward()
+        out = y.detach().clone(), [l.grad.clone() for l in leaves], [v._value.clone() for v in m.non_trainable_weights]
+        for v in m.trainable_weights:
+            v._leaf = None
+        os.environ["TDL_FUSE"] = "1"
+        return out
+
+    y0, g0, s0 = run(False)
+    y1, g1, s1 = run(True)
+    assert sys.modules["tensorflow_distributed_learning_amd.keras.fusion"] is not None
+    torch.testing.assert_close(y1, y0, atol=2e-3, rtol=2e-3)
+    for a, b, v in zip(g1, g0, m.trainable_weights):
+        if "conv" in v.name and v.name.endswith("bias:0"):
+            assert float(a.abs().max()) == 0.0
+            continue
+        scale = float(b.abs().max()) + 1e-6
+        assert float((a - b).abs().max()) / scale < 2e-2, v.name
+    for a, b in zip(s1, s0):
+        torch.testing.assert_close(a, b, atol=1e-4, rtol=1e-3)

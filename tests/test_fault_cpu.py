@@ -1,0 +1,108 @@
+"""T-fault: kill one worker mid-training; the survivor must abort within a bounded
+time with a clear error (no hang), and a restart resumes from the chief's BackupAndRestore state.
+
+Workers are started as independent processes with their own TF_CONFIG (README.md:158-162 style),
+not through the launcher, which would tear the job down itself on the first failure."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import textwrap
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.slow
+
+BODY = """
+import json, os, sys, torch
+import tensorflow_distributed_learning_amd as tdl
+from tensorflow_distributed_learning_amd.models.mnist_cnn import build_mnist_cnn
+from tensorflow_distributed_learning_amd.data.tfds import synthetic_mnist
+from tensorflow_distributed_learning_amd.utils.fault import PeerLostError
+out = sys.argv[1]
+strategy = tdl.distribute.MultiWorkerMirroredStrategy(communication="RING")
+rank = strategy.extended.rank
+tdl.keras.utils.set_random_seed(1)
+x, y = synthetic_mnist(1024, 3)
+ds = tdl.data.Dataset.from_tensor_slices((x.reshape(-1, 28, 28, 1), y))
+ds = ds.map(lambda i, l: (i.to(torch.float32) / 255, l)).batch(64).repeat()
+with strategy.scope():
+    m = build_mnist_cnn()
+    m.compile(loss=tdl.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+              optimizer=tdl.keras.optimizers.SGD(0.05), metrics=["sparse_categorical_accuracy"])
+cb = tdl.keras.callbacks.BackupAndRestore(os.path.join(out, "backup"))
+res = {"rank": rank}
+try:
+    h = m.fit(ds, epochs=6, steps_per_epoch=4, verbose=0, callbacks=[cb])
+    res.update(status="ok", epochs=h.epoch, iterations=int(m.optimizer.iterations))
+except PeerLostError as e:
+    res.update(status="peer_lost", error=str(e))
+json.dump(res, open(os.path.join(out, f"res{rank}_{os.environ['RUN']}.json"), "w"))
+strategy.shutdown()
+"""
+
+
+def _ports(n):
+    socks = [socket.socket() for _ in range(n)]
+    for s in socks:
+        s.bind(("127.0.0.1", 0))
+    ports = [s.getsockname()[1] for s in socks]
+    for s in socks:
+        s.close()
+    return ports
+
+
+def _start(tmp_path, run, extra_env):
+    script = tmp_path / "job.py"
+    script.write_text(textwrap.dedent(BODY))
+    ports = _ports(2)
+    cluster = {"worker": [f"127.0.0.1:{p}" for p in ports]}
+    procs = []
+    for i in range(2):
+        env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="",
+                   RUN=run, TF_CONFIG=json.dumps({"cluster": cluster, "task": {"type": "worker", "index": i}}),
+                   TDL_ABORT_GRACE="20", **extra_env)
+        for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "TDL_LAUNCHED"):
+            env.pop(k, None)
+        procs.append(subprocess.Popen([sys.executable, str(script), str(tmp_path)], env=env, cwd=ROOT,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    return procs
+
+
+def _finish(procs, timeout):
+    outs = []
+    for p in procs:
+        try:
+            o, e = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise AssertionError("a worker hung after the fault")
+        outs.append((p.returncode, o, e))
+    return outs
+
+
+def test_worker_death_is_detected_and_training_resumes(tmp_path):
+    t0 = time.time()
+    procs = _start(tmp_path, "a", {"TDL_FAULT_KILL_AT_STEP": "1:10"})
+    (rc0, _, e0), (rc1, _, e1) = _finish(procs, timeout=180)
+    assert rc1 == 43, e1[-2000:]  # injected abrupt exit of rank 1 after 10 steps
+    assert "fault injection" in e1
+    r0 = json.load(open(tmp_path / "res0_a.json"))
+    assert r0["status"] == "peer_lost", (r0, e0[-2000:])
+    assert "rank 1" in r0["error"], r0
+    assert time.time() - t0 < 150
+
+    # restart without the fault: BackupAndRestore resumes after the last completed epoch (epoch 2:
+    # 10 steps = 2 full epochs of 4, the chief saved at each epoch end)
+    procs = _start(tmp_path, "b", {})
+    outs = _finish(procs, timeout=180)
+    for rc, _, e in outs:
+        assert rc == 0, e[-3000:]
+    a, b = (json.load(open(tmp_path / f"res{i}_b.json")) for i in range(2))
+    assert a["status"] == b["status"] == "ok"
+    assert a["epochs"] == [2, 3, 4, 5], a
+    assert a["iterations"] == b["iterations"] == 24

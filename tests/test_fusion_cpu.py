@@ -1,0 +1,86 @@
+"""keras/fusion.py: the training-graph fusion plan (conv bias folded into BN, BN+ReLU,
+BN+Add+ReLU) must not change a functional model's outputs, gradients or moving statistics.
+Checked on CPU, where the fused groups run through the PyTorch path of ops/batchnorm.py."""
+import numpy as np
+import torch
+
+import tensorflow_distributed_learning_amd as tdl
+import sys
+
+from tensorflow_distributed_learning_amd.keras import fusion
+
+models = sys.modules["tensorflow_distributed_learning_amd.keras.models"]
+
+
+def _tiny_resnet():
+    L = tdl.keras.layers
+    inp = L.Input(shape=(8, 8, 3))
+    x = L.Conv2D(8, 3, padding="same")(inp)
+    x = L.BatchNormalization()(x)
+    x = L.Activation("relu")(x)
+    sc = L.Conv2D(16, 1)(x)
+    sc = L.BatchNormalization()(sc)
+    y = L.Conv2D(16, 3, padding="same")(x)
+    y = L.BatchNormalization()(y)
+    y = L.Add()([sc, y])
+    y = L.ReLU()(y)
+    z = L.Conv2D(16, 1)(y)
+    z = L.BatchNormalization()(z)
+    z = L.Add()([y, z])
+    z = L.Activation("relu")(z)
+    z = L.GlobalAveragePooling2D()(z)
+    out = L.Dense(4)(z)
+    return tdl.keras.Model(inp, out)
+
+
+def test_plan_shapes_resnet50():
+    m = tdl.keras.applications.ResNet50(weights=None, classes=10, classifier_activation=None, input_shape=(32, 32, 3))
+    p = fusion.plan(m._nodes, m._outputs)
+    assert len(p.groups) == 53 and len(p.conv_nobias) == 53
+    assert sum(g.residual is not None for g in p.groups.values()) == 16
+    assert sum(g.relu and g.residual is None for g in p.groups.values()) == 33
+
+
+def _run(m, x, fuse):
+    models._FUSE_CPU[0] = fuse
+    try:
+        for v in m.trainable_weights:
+            v.value.grad = None
+        leaves = []
+        for v in m.trainable_weights:
+            v._leaf = v._value.detach().clone().requires_grad_(True)
+            leaves.append(v._leaf)
+        y = m(x, training=True)
+        (y ** 2).sum().backward()
+        mstats = [v._value.clone() for v in m.non_trainable_weights]
+        out = y.detach().clone(), [l.grad.clone() for l in leaves], mstats
+        for v in m.trainable_weights:
+            v._leaf = None
+        return out
+    finally:
+        models._FUSE_CPU[0] = False
+
+
+def test_fused_training_graph_matches_unfused():
+    tdl.keras.utils.set_random_seed(0)
+    m = _tiny_resnet()
+    for v in m.trainable_weights:
+        if v.name.endswith("bias:0"):
+            v.assign(np.random.RandomState(1).randn(*v.shape).astype(np.float32))
+    p = fusion.plan(m._nodes, m._outputs)
+    assert len(p.groups) == 4 and len(p.conv_nobias) == 4
+    x = torch.randn(5, 8, 8, 3)
+    init = [v._value.clone() for v in m.non_trainable_weights]
+    y0, g0, s0 = _run(m, x, False)
+    for v, t in zip(m.non_trainable_weights, init):
+        v._value.copy_(t)
+    y1, g1, s1 = _run(m, x, True)
+    torch.testing.assert_close(y1, y0, atol=1e-5, rtol=1e-5)
+    for a, b, v in zip(g1, g0, m.trainable_weights):
+        if v.name.endswith("bias:0") and "conv" in v.name:
+            assert float(b.abs().max()) < 1e-4  # analytically zero through training-mode BN
+            assert float(a.abs().max()) < 1e-4  # (exactly 0 on the GPU kernels)
+        else:
+            torch.testing.assert_close(a, b, atol=1e-4, rtol=1e-4)
+    for a, b in zip(s1, s0):
+        torch.testing.assert_close(a, b, atol=1e-6, rtol=1e-6)
