@@ -1,0 +1,158 @@
+// NHWC max pooling on gfx950, bf16 / f32, 8 channels (16 B of bf16) per thread.
+//
+// forward : y = max over the window; arg = window position of the (first) maximum per element
+//           (255 when an implicit zero-padding element won).  Padding is either -inf (TF 'same'
+//           max pool) or zero (a fused ZeroPadding2D in front, the ResNet stem).
+// backward: gather form — each input element sums dy over the <= ceil(k/s)^2 windows whose
+//           argmax points at it: no atomics, deterministic, one pass over dx.
+#include "common.h"
+#include "pool.h"
+
+namespace tdl {
+namespace {
+
+__device__ __forceinline__ float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+__device__ __forceinline__ uint32_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+
+template <bool BF>
+__device__ __forceinline__ void ld8(const void* p, int64_t e, float* o) {
+  if (BF) {
+    const uint4 u = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(p) + e);
+    o[0] = bf_lo(u.x); o[1] = bf_hi(u.x); o[2] = bf_lo(u.y); o[3] = bf_hi(u.y);
+    o[4] = bf_lo(u.z); o[5] = bf_hi(u.z); o[6] = bf_lo(u.w); o[7] = bf_hi(u.w);
+  } else {
+    const f4* q = reinterpret_cast<const f4*>(static_cast<const float*>(p) + e);
+    const f4 a = q[0], b = q[1];
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+  }
+}
+
+template <bool BF>
+__device__ __forceinline__ void st8(void* p, int64_t e, const float* v) {
+  if (BF) {
+    uint4 u;
+    u.x = f2bf(v[0]) | (f2bf(v[1]) << 16);
+    u.y = f2bf(v[2]) | (f2bf(v[3]) << 16);
+    u.z = f2bf(v[4]) | (f2bf(v[5]) << 16);
+    u.w = f2bf(v[6]) | (f2bf(v[7]) << 16);
+    *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p) + e) = u;
+  } else {
+    f4* q = reinterpret_cast<f4*>(static_cast<float*>(p) + e);
+    q[0] = f4{v[0], v[1], v[2], v[3]};
+    q[1] = f4{v[4], v[5], v[6], v[7]};
+  }
+}
+
+template <bool BF>
+__global__ __launch_bounds__(256) void k_maxpool_fwd(const void* __restrict__ x, void* __restrict__ y,
+                                                     uint8_t* __restrict__ arg, PoolGeom g) {
+  const int G = g.C >> 3;
+  const int64_t total = (int64_t)g.N * g.OH * g.OW * G;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int cg = (int)(t % G);
+    int64_t r = t / G;
+    const int ow = (int)(r % g.OW);
+    r /= g.OW;
+    const int oh = (int)(r % g.OH);
+    const int n = (int)(r / g.OH);
+    float best[8];
+    uint32_t am[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      best[j] = -INFINITY;
+      am[j] = 255;
+    }
+    for (int i = 0; i < g.kh; ++i) {
+      const int h = oh * g.sh - g.pt + i;
+      for (int k = 0; k < g.kw; ++k) {
+        const int w = ow * g.sw - g.pl + k;
+        const uint32_t pos = (uint32_t)(i * g.kw + k);
+        float v[8];
+        if (h >= 0 && h < g.H && w >= 0 && w < g.W) {
+          ld8<BF>(x, (((int64_t)n * g.H + h) * g.W + w) * g.C + cg * 8, v);
+        } else if (g.pad_zero) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = 0.f;
+        } else {
+          continue;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (v[j] > best[j]) {
+            best[j] = v[j];
+            am[j] = (h >= 0 && h < g.H && w >= 0 && w < g.W) ? pos : 255u;
+          }
+      }
+    }
+    const int64_t o = (((int64_t)n * g.OH + oh) * g.OW + ow) * g.C + cg * 8;
+    st8<BF>(y, o, best);
+    uint2 a;
+    a.x = am[0] | (am[1] << 8) | (am[2] << 16) | (am[3] << 24);
+    a.y = am[4] | (am[5] << 8) | (am[6] << 16) | (am[7] << 24);
+    *reinterpret_cast<uint2*>(arg + o) = a;
+  }
+}
+
+template <bool BF>
+__global__ __launch_bounds__(256) void k_maxpool_bwd(const void* __restrict__ dy, const uint8_t* __restrict__ arg,
+                                                     void* __restrict__ dx, PoolGeom g) {
+  const int G = g.C >> 3;
+  const int64_t total = (int64_t)g.N * g.H * g.W * G;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int cg = (int)(t % G);
+    int64_t r = t / G;
+    const int w = (int)(r % g.W);
+    r /= g.W;
+    const int h = (int)(r % g.H);
+    const int n = (int)(r / g.H);
+    const int hp = h + g.pt, wp = w + g.pl;
+    const int oh0 = hp - g.kh + 1 <= 0 ? 0 : (hp - g.kh + g.sh) / g.sh;
+    const int oh1 = min(g.OH - 1, hp / g.sh);
+    const int ow0 = wp - g.kw + 1 <= 0 ? 0 : (wp - g.kw + g.sw) / g.sw;
+    const int ow1 = min(g.OW - 1, wp / g.sw);
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    for (int oh = oh0; oh <= oh1; ++oh)
+      for (int ow = ow0; ow <= ow1; ++ow) {
+        const uint32_t pos = (uint32_t)((hp - oh * g.sh) * g.kw + (wp - ow * g.sw));
+        const int64_t o = (((int64_t)n * g.OH + oh) * g.OW + ow) * g.C + cg * 8;
+        const uint2 a = *reinterpret_cast<const uint2*>(arg + o);
+        float d[8];
+        ld8<BF>(dy, o, d);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t aj = ((j < 4 ? a.x : a.y) >> (8 * (j & 3))) & 0xffu;
+          if (aj == pos) acc[j] += d[j];
+        }
+      }
+    st8<BF>(dx, (((int64_t)n * g.H + h) * g.W + w) * g.C + cg * 8, acc);
+  }
+}
+
+int grid_for(int64_t n) { return (int)std::min<int64_t>((n + 255) / 256, 256 * 32); }
+
+}  // namespace
+
+void maxpool_forward(const void* x, void* y, uint8_t* arg, bool bf16, const PoolGeom& g, hipStream_t s) {
+  const int64_t n = (int64_t)g.N * g.OH * g.OW * (g.C / 8);
+  if (bf16)
+    hipLaunchKernelGGL(k_maxpool_fwd<true>, dim3(grid_for(n)), dim3(256), 0, s, x, y, arg, g);
+  else
+    hipLaunchKernelGGL(k_maxpool_fwd<false>, dim3(grid_for(n)), dim3(256), 0, s, x, y, arg, g);
+}
+
+void maxpool_backward(const void* dy, const uint8_t* arg, void* dx, bool bf16, const PoolGeom& g, hipStream_t s) {
+  const int64_t n = (int64_t)g.N * g.H * g.W * (g.C / 8);
+  if (bf16)
+    hipLaunchKernelGGL(k_maxpool_bwd<true>, dim3(grid_for(n)), dim3(256), 0, s, dy, arg, dx, g);
+  else
+    hipLaunchKernelGGL(k_maxpool_bwd<false>, dim3(grid_for(n)), dim3(256), 0, s, dy, arg, dx, g);
+}
+
+}  // namespace tdl

@@ -4,6 +4,7 @@
 
 #include "kernels/bn.h"
 #include "kernels/ops.h"
+#include "kernels/pool.h"
 
 namespace {
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
@@ -116,6 +117,34 @@ std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, c10::optional<a
   if (mode == 2) return {dx, out[0], out[1], dz};
   return {dx, out[0], out[1]};
 }
+// max pool NHWC: returns (y, argmax bytes); pads = (top, left), output size given
+std::vector<at::Tensor> maxpool_fwd(at::Tensor x, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t pt,
+                                    int64_t pl, int64_t OH, int64_t OW, bool pad_zero) {
+  bn_check(x);
+  TORCH_CHECK(x.dim() == 4, "maxpool: NHWC input expected");
+  TORCH_CHECK(kh * kw < 255 && kh > 0 && kw > 0 && sh > 0 && sw > 0 && OH > 0 && OW > 0, "maxpool: bad geometry");
+  tdl::PoolGeom g{(int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3), (int)OH, (int)OW,
+                  (int)kh, (int)kw, (int)sh, (int)sw, (int)pt, (int)pl, pad_zero ? 1 : 0};
+  auto y = at::empty({x.size(0), OH, OW, x.size(3)}, x.options());
+  auto arg = at::empty({x.size(0), OH, OW, x.size(3)}, x.options().dtype(at::kByte));
+  tdl::maxpool_forward(x.data_ptr(), y.data_ptr(), arg.data_ptr<uint8_t>(), bn_dtype(x) == tdl::BnDType::kBF16, g,
+                       cur_stream());
+  return {y, arg};
+}
+
+at::Tensor maxpool_bwd(at::Tensor dy, at::Tensor arg, std::vector<int64_t> in_shape, int64_t kh, int64_t kw,
+                       int64_t sh, int64_t sw, int64_t pt, int64_t pl) {
+  bn_check(dy);
+  TORCH_CHECK(dy.dim() == 4 && arg.sizes() == dy.sizes() && arg.scalar_type() == at::kByte && arg.is_contiguous(),
+              "maxpool backward: dy / argmax mismatch");
+  TORCH_CHECK(in_shape.size() == 4 && in_shape[3] == dy.size(3) && in_shape[0] == dy.size(0), "maxpool: bad shape");
+  tdl::PoolGeom g{(int)in_shape[0], (int)in_shape[1], (int)in_shape[2], (int)in_shape[3], (int)dy.size(1),
+                  (int)dy.size(2), (int)kh, (int)kw, (int)sh, (int)sw, (int)pt, (int)pl, 0};
+  auto dx = at::empty(in_shape, dy.options());
+  tdl::maxpool_backward(dy.data_ptr(), arg.data_ptr<uint8_t>(), dx.data_ptr(), bn_dtype(dy) == tdl::BnDType::kBF16, g,
+                        cur_stream());
+  return dx;
+}
 }  // namespace
 
 void register_ops(pybind11::module& m) {
@@ -125,6 +154,8 @@ void register_ops(pybind11::module& m) {
         pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("moving_mean"), pybind11::arg("moving_var"),
         pybind11::arg("momentum"), pybind11::arg("eps"), pybind11::arg("relu") = false,
         pybind11::arg("residual") = pybind11::none(), pybind11::arg("mean_off") = pybind11::none());
+  m.def("maxpool_fwd", &maxpool_fwd, "NHWC max pool forward (+argmax)");
+  m.def("maxpool_bwd", &maxpool_bwd, "NHWC max pool backward (gather form)");
   m.def("bn_backward", &bn_backward, "NHWC batch-norm training backward", pybind11::arg("dy"), pybind11::arg("x"),
         pybind11::arg("y"), pybind11::arg("gamma"), pybind11::arg("stats"), pybind11::arg("mode"));
 }

@@ -9,6 +9,7 @@ list; the plan rewrites, at execution time only (the layer graph, variables, che
 * ``BatchNormalization -> ReLU``: one fused kernel pass (ops/batchnorm.py).
 * ``BatchNormalization -> Add(other) -> ReLU``: the ResNet block tail, one fused pass that also
   produces the residual's gradient.
+* ``ZeroPadding2D -> MaxPooling2D('valid')``: one pooling pass with implicit zero padding.
 
 Every intermediate tensor of a fused group must have exactly one consumer.  A group executes at
 the position of its last node, when all its external inputs exist.  Eval / CPU calls run the
@@ -36,6 +37,7 @@ class Plan:
         self.skip = set()        # node ids absorbed into a group that runs elsewhere
         self.conv_nobias = set()  # conv node ids whose bias is folded into their BN
         self.groups: Dict[int, Group] = {}  # id(last node) -> group
+        self.pool_pad: Dict[int, tuple] = {}  # id(max-pool node) -> (padding input, padding)
 
     def __len__(self):
         return len(self.groups)
@@ -70,6 +72,13 @@ def plan(nodes: List[L.Node], outputs) -> Plan:
         return c[0] if len(c) == 1 else None
 
     producer = {id(t): n for n in nodes for t in L._flat(n.outputs)}
+    for n in nodes:  # ZeroPadding2D -> MaxPooling2D('valid'): one pooling pass with zero padding
+        if isinstance(n.layer, L.MaxPooling2D) and n.layer.padding == "valid":
+            x_t = _single_tensor(n.inputs)
+            prod = producer.get(id(x_t)) if x_t is not None else None
+            if prod is not None and isinstance(prod.layer, L.ZeroPadding2D) and only_consumer(x_t) is n:
+                p.pool_pad[id(n)] = (prod.inputs, prod.layer.padding)
+                p.skip.add(id(prod))
     for n in nodes:
         bn = n.layer
         if not (isinstance(bn, L.BatchNormalization) and bn.trainable and bn.axis in (-1, 3)):

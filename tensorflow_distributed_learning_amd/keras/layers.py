@@ -311,6 +311,18 @@ class Conv2D(Layer):
     def call(self, x, training=None, _fold_bias=False):
         """``_fold_bias``: the functional executor folded this bias into the following training-mode
         BatchNormalization (keras/fusion.py), so the convolution runs without it."""
+        if self.kernel_size == (1, 1) and self.groups == 1 and self.dilation_rate == (1, 1) and x.is_cuda:
+            # a 1x1 convolution over NHWC rows is a plain GEMM [N*H*W, Cin] x [Cin, Cout] (library
+            # GEMM, hipBLASLt); 'same' and 'valid' coincide for 1x1 kernels
+            sh, sw = self.strides
+            xs = x if (sh, sw) == (1, 1) else x[:, ::sh, ::sw, :]
+            n, hh, ww, c = xs.shape
+            w2 = self.kernel.value.view(c, self.filters)
+            b = self.bias.value if (self.bias is not None and not _fold_bias) else None
+            y2 = xs.reshape(-1, c) @ w2.to(xs.dtype)
+            if b is not None:
+                y2 = y2 + b.to(y2.dtype)
+            return self.activation(y2.view(n, hh, ww, self.filters))
         w = self.kernel.value.to(x.dtype).permute(3, 2, 0, 1)  # HWIO -> OIHW
         h = x.permute(0, 3, 1, 2)  # NHWC data viewed as NCHW (channels_last memory format)
         pad = 0
@@ -374,7 +386,21 @@ class _Pool2D(Layer):
 
 
 class MaxPooling2D(_Pool2D):
-    def call(self, x, training=None):
+    def call(self, x, training=None, _zero_pad=None):
+        """``_zero_pad``: padding of a ZeroPadding2D fused in front (keras/fusion.py)."""
+        from ..ops import pooling as _pool
+
+        if _zero_pad is not None or _pool.supported(x):
+            pads = ((0, 0), (0, 0))
+            if self.padding == "same":
+                pads = (_same_pads(x.shape[1], self.pool_size[0], self.strides[0]),
+                        _same_pads(x.shape[2], self.pool_size[1], self.strides[1]))
+            if _zero_pad is not None:
+                if self.padding == "same":
+                    x = F.pad(x, (0, 0, _zero_pad[1][0], _zero_pad[1][1], _zero_pad[0][0], _zero_pad[0][1]))
+                else:
+                    return _pool.max_pool_nhwc(x, self.pool_size, self.strides, _zero_pad, pad_zero=True)
+            return _pool.max_pool_nhwc(x, self.pool_size, self.strides, pads, pad_zero=False)
         h = x.permute(0, 3, 1, 2)
         if self.padding == "same":
             ph, pw = self._pads(h)

@@ -122,7 +122,7 @@ class Model(Layer):
         fp = None
         if training and isinstance(xs[0], torch.Tensor) and (xs[0].is_cuda or _FUSE_CPU[0]):
             fp = self._fusion()  # keras/fusion.py: conv-bias/BN/ReLU/Add groups (training, GPU)
-            if not fp.groups:
+            if not fp.groups and not fp.pool_pad:
                 fp = None
         for n in self._nodes:
             if fp is not None:
@@ -135,10 +135,16 @@ class Model(Layer):
 
                     run_group(g, vals, training)
                     continue
-            args = _map(lambda t: vals[id(t)], n.inputs)
             kw = {k: v for k, v in n.kwargs.items() if k != "training"}
-            if fp is not None and id(n) in fp.conv_nobias:
-                kw["_fold_bias"] = True
+            src = n.inputs
+            if fp is not None:
+                if id(n) in fp.conv_nobias:
+                    kw["_fold_bias"] = True
+                pp = fp.pool_pad.get(id(n))
+                if pp is not None:  # fused ZeroPadding2D: read the padding layer's input
+                    src = pp[0]
+                    kw["_zero_pad"] = pp[1]
+            args = _map(lambda t: vals[id(t)], src)
             out = n.layer(args, training=training, **kw)
             if isinstance(n.outputs, list):
                 for t, o in zip(n.outputs, out):

@@ -84,3 +84,22 @@ def test_fused_training_graph_matches_unfused():
             torch.testing.assert_close(a, b, atol=1e-4, rtol=1e-4)
     for a, b in zip(s1, s0):
         torch.testing.assert_close(a, b, atol=1e-6, rtol=1e-6)
+
+
+def test_zero_pad_max_pool_fusion_matches():
+    L = tdl.keras.layers
+    inp = L.Input(shape=(9, 9, 8))
+    x = L.ZeroPadding2D(((1, 1), (1, 1)))(inp)
+    x = L.MaxPooling2D(3, strides=2)(x)
+    m = tdl.keras.Model(inp, L.Flatten()(x))
+    p = fusion.plan(m._nodes, m._outputs)
+    assert len(p.pool_pad) == 1 and len(p.skip) == 1
+    xin = torch.randn(2, 9, 9, 8) - 0.5
+    y0 = m(xin, training=True)
+    models._FUSE_CPU[0] = True
+    try:
+        m.__dict__.pop("_fusion_plan", None)
+        y1 = m(xin, training=True)
+    finally:
+        models._FUSE_CPU[0] = False
+    torch.testing.assert_close(y1, y0)
