@@ -15,7 +15,8 @@ namespace tdl {
 namespace {
 
 constexpr int kUnroll = 4;
-constexpr int kMaxParts = 1024;
+constexpr int kMaxParts = 512;
+constexpr int kFinPhases = 16;  // partial-row phases per channel in the finalize kernels (1024 threads)
 
 __device__ __forceinline__ float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
@@ -136,15 +137,15 @@ __global__ __launch_bounds__(256) void k_bn_partial(const void* __restrict__ a, 
   }
 }
 
-// Sum the partial rows of channel c (64 channels x 4 partial-row phases per workgroup), f64.
+// Sum the partial rows of channel c: 64 channels x kFinPhases phases per 1024-thread workgroup, f64.
 __device__ __forceinline__ bool reduce_parts(const float* __restrict__ part, int P, int C, double& S, double& Q) {
-  __shared__ double rs[4][64], rq[4][64];
+  __shared__ double rs[kFinPhases][64], rq[kFinPhases][64];
   const int lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
   double s = 0.0, q = 0.0;
   if (c < C) {
-#pragma unroll 8
-    for (int p = ph; p < P; p += 4) {
+#pragma unroll 4
+    for (int p = ph; p < P; p += kFinPhases) {
       s += part[((int64_t)p * 2) * C + c];
       q += part[((int64_t)p * 2 + 1) * C + c];
     }
@@ -153,12 +154,17 @@ __device__ __forceinline__ bool reduce_parts(const float* __restrict__ part, int
   rq[ph][lane] = q;
   __syncthreads();
   if (ph != 0 || c >= C) return false;
-  S = rs[0][lane] + rs[1][lane] + rs[2][lane] + rs[3][lane];
-  Q = rq[0][lane] + rq[1][lane] + rq[2][lane] + rq[3][lane];
+  S = 0.0;
+  Q = 0.0;
+#pragma unroll
+  for (int k = 0; k < kFinPhases; ++k) {
+    S += rs[k][lane];
+    Q += rq[k][lane];
+  }
   return true;
 }
 
-__global__ __launch_bounds__(256) void k_bn_fwd_finalize(const float* __restrict__ part, int P, int64_t M, int C,
+__global__ __launch_bounds__(1024) void k_bn_fwd_finalize(const float* __restrict__ part, int P, int64_t M, int C,
                                                          const float* __restrict__ gamma,
                                                          const float* __restrict__ beta,
                                                          const float* __restrict__ mean_off, float* __restrict__ mean,
@@ -185,7 +191,7 @@ __global__ __launch_bounds__(256) void k_bn_fwd_finalize(const float* __restrict
   }
 }
 
-__global__ __launch_bounds__(256) void k_bn_bwd_finalize(const float* __restrict__ part, int P, int64_t M, int C,
+__global__ __launch_bounds__(1024) void k_bn_bwd_finalize(const float* __restrict__ part, int P, int64_t M, int C,
                                                          const float* __restrict__ gamma,
                                                          const float* __restrict__ mean,
                                                          const float* __restrict__ invstd, float* __restrict__ dgamma,
@@ -294,7 +300,7 @@ void bn_forward_stats(const void* x, BnDType dt, int64_t M, int C, float* part, 
   else
     hipLaunchKernelGGL((k_bn_partial<BnDType::kF32, 0>), dim3(p.parts), dim3(256), 0, s, x, nullptr, nullptr, nullptr,
                        nullptr, nullptr, M, C, p.rows_wg, part);
-  hipLaunchKernelGGL(k_bn_fwd_finalize, dim3((C + 63) / 64), dim3(256), 0, s, part, p.parts, M, C, gamma, beta,
+  hipLaunchKernelGGL(k_bn_fwd_finalize, dim3((C + 63) / 64), dim3(64 * kFinPhases), 0, s, part, p.parts, M, C, gamma, beta,
                      mean_off, mean, invstd, scale, shift, moving_mean, moving_var, momentum, eps);
 }
 
@@ -323,7 +329,7 @@ static void bn_backward_t(const void* dy, const void* x, const void* y, void* dz
                        part);
   else
     hipLaunchKernelGGL((k_bn_partial<D, 3>), gp, blk, 0, s, dy, x, y, nullptr, nullptr, dz, M, C, p.rows_wg, part);
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), blk, 0, s, part, p.parts, M, C, gamma, mean, invstd,
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), dim3(64 * kFinPhases), 0, s, part, p.parts, M, C, gamma, mean, invstd,
                      dgamma, dbeta, coef);
   const int64_t n8 = M * C / 8;
   const dim3 ge(elementwise_grid(n8));

@@ -311,18 +311,8 @@ class Conv2D(Layer):
     def call(self, x, training=None, _fold_bias=False):
         """``_fold_bias``: the functional executor folded this bias into the following training-mode
         BatchNormalization (keras/fusion.py), so the convolution runs without it."""
-        if self.kernel_size == (1, 1) and self.groups == 1 and self.dilation_rate == (1, 1) and x.is_cuda:
-            # a 1x1 convolution over NHWC rows is a plain GEMM [N*H*W, Cin] x [Cin, Cout] (library
-            # GEMM, hipBLASLt); 'same' and 'valid' coincide for 1x1 kernels
-            sh, sw = self.strides
-            xs = x if (sh, sw) == (1, 1) else x[:, ::sh, ::sw, :]
-            n, hh, ww, c = xs.shape
-            w2 = self.kernel.value.view(c, self.filters)
-            b = self.bias.value if (self.bias is not None and not _fold_bias) else None
-            y2 = xs.reshape(-1, c) @ w2.to(xs.dtype)
-            if b is not None:
-                y2 = y2 + b.to(y2.dtype)
-            return self.activation(y2.view(n, hh, ww, self.filters))
+        # (1x1 convs stay on MIOpen: routing them through hipBLASLt GEMMs measured slower on MI355X,
+        #  scripts/probe_1x1_gemm.py)
         w = self.kernel.value.to(x.dtype).permute(3, 2, 0, 1)  # HWIO -> OIHW
         h = x.permute(0, 3, 1, 2)  # NHWC data viewed as NCHW (channels_last memory format)
         pad = 0
