@@ -21,6 +21,7 @@ import torch
 
 from ..data import dataset as D
 from ..parallel import input_lib
+from ..utils.tracing import trace_range
 
 
 class LazyLogs(dict):
@@ -210,17 +211,20 @@ class GenericTrainer:
         if self._buckets is not None:
             self._counts = list(self._pending)
             self._works = []
-        loss, per_ex, y_pred = self._forward_loss(x, y, sw, global_n)
-        loss.backward()
+        with trace_range("tdl.forward"):
+            loss, per_ex, y_pred = self._forward_loss(x, y, sw, global_n)
+        with trace_range("tdl.backward"):
+            loss.backward()
         if self.comm.world_size > 1:
-            if self._buckets is not None:
-                for w in self._works:
-                    w.wait()
-                if len(self._works) != len(self._bucket_ranges):
-                    raise RuntimeError("gradient bucket hooks did not fire for every bucket (unused parameters?)")
-            else:
-                self.comm.all_reduce(G, "sum")
-        with torch.no_grad():
+            with trace_range("tdl.allreduce"):
+                if self._buckets is not None:
+                    for w in self._works:
+                        w.wait()
+                    if len(self._works) != len(self._bucket_ranges):
+                        raise RuntimeError("gradient bucket hooks did not fire for every bucket (unused parameters?)")
+                else:
+                    self.comm.all_reduce(G, "sum")
+        with torch.no_grad(), trace_range("tdl.optimizer"):
             self.optimizer.apply_flat(self.W, G)
             self.loss_tracker.update_state(per_ex.detach())
             yp = y_pred.detach()

@@ -729,10 +729,12 @@ def _run_guarded(trainer, handler, n, strategy):
     fails because a peer died is re-raised as PeerLostError with the watchdog's diagnosis, and the
     fault-injection hook runs at the execution boundary."""
     from ..utils import fault
+    from ..utils.tracing import trace_range
 
     wd = getattr(strategy.extended, "watchdog", None)
     try:
-        got = trainer.run_train(handler, n)
+        with trace_range(f"tdl.execution[{n} steps]"):
+            got = trainer.run_train(handler, n)
     except Exception as e:
         if wd is not None:
             deadline = time.monotonic() + 3 * wd.interval + 1.0
