@@ -47,11 +47,11 @@ class MnistStep {
     A2_ = at::empty({b * 1600}, u8);
     H_ = at::empty({b * 128}, f);
     dH_ = at::empty({b * 128}, f);
+    part4_ = at::zeros({(int64_t)tdl::mnist_head_blocks((int)b) * 1290}, f);
     dC2_ = at::empty({b * 100 * 64}, f);
     part2_ = at::zeros({b * tdl::kMnistPart2Rows * 64}, f);
     part1_ = at::zeros({(int64_t)tdl::mnist_part1_rows((int)b) * tdl::kMnistPart1Cols}, f);
     part3_ = at::zeros({(int64_t)tdl::kDense1Chunks * b * 128}, f);
-    part4_ = at::zeros({(int64_t)tdl::mnist_head_blocks((int)b) * 1290}, f);
     a_ = tdl::MnistArgs{};
     a_.X = X_.data_ptr<float>();
     a_.Y = Y_.data_ptr<int>();
@@ -66,11 +66,11 @@ class MnistStep {
     a_.A2 = A2_.data_ptr<uint8_t>();
     a_.H = H_.data_ptr<float>();
     a_.dH = dH_.data_ptr<float>();
+    a_.part4 = part4_.data_ptr<float>();
     a_.dC2 = dC2_.data_ptr<float>();
     a_.part2 = part2_.data_ptr<float>();
     a_.part1 = part1_.data_ptr<float>();
     a_.part3 = part3_.data_ptr<float>();
-    a_.part4 = part4_.data_ptr<float>();
     a_.metrics = metrics_.data_ptr<float>();
     a_.lr = lr_.data_ptr<float>();
     a_.b = (int)b;
@@ -83,13 +83,10 @@ class MnistStep {
     a_.idx = idx_.data_ptr<int>() + off;
   }
 
-  // Individual stages (tests / profiling): 1..7, 9.
+  // Individual stages (tests / profiling): 4 head, 5 dense1 bwd, 6 conv bwd, 8 fwd conv (+dense1), 9 finalize.
   void stage(int64_t k, bool apply_sgd) {
     hipStream_t s = cur_stream();
     switch (k) {
-      case 1: tdl::mnist_conv1_pool(a_, s); break;
-      case 2: tdl::mnist_conv2_pool(a_, s); break;
-      case 3: tdl::mnist_dense1(a_, s); break;
       case 4: tdl::mnist_head(a_, s); break;
       case 5: tdl::mnist_dense1_bwd(a_, s); break;
       case 6: tdl::mnist_conv_bwd(a_, s); break;
@@ -104,7 +101,6 @@ class MnistStep {
     set_idx_offset(idx_off);
     hipStream_t s = cur_stream();
     tdl::mnist_fwd_conv(a_, s);
-    tdl::mnist_dense1(a_, s);
     tdl::mnist_head(a_, s);
     tdl::mnist_dense1_bwd(a_, s);
     tdl::mnist_conv_bwd(a_, s);
@@ -116,7 +112,6 @@ class MnistStep {
     set_idx_offset(idx_off);
     hipStream_t s = cur_stream();
     tdl::mnist_fwd_conv(a_, s);
-    tdl::mnist_dense1(a_, s);
     tdl::mnist_head(a_, s);
     tdl::mnist_dense1_bwd(a_, s);
   }
@@ -129,7 +124,6 @@ class MnistStep {
     set_idx_offset(idx_off);
     hipStream_t s = cur_stream();
     tdl::mnist_fwd_conv(a_, s);
-    tdl::mnist_dense1(a_, s);
   }
 
   // diagnostics: per-workgroup phase timestamps of the next launches (None to disable)
@@ -143,7 +137,7 @@ class MnistStep {
     }
   }
 
-  std::vector<at::Tensor> buffers() { return {P1_, A1_, P2_, A2_, H_, dH_, dC2_, part2_, part1_}; }
+  std::vector<at::Tensor> buffers() { return {P1_, A1_, P2_, A2_, H_, dH_, dC2_, part2_, part1_, part3_}; }
 
  private:
   at::Tensor X_, Y_, idx_, W_, G_, lr_, metrics_;

@@ -38,9 +38,11 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-// Phase timestamp (100 MHz s_memrealtime) of workgroup blockIdx.x, slot k; no-op when buf == null.
+// Phase timestamp (100 MHz s_memrealtime) of wave (threadIdx.x / 64) of workgroup blockIdx.x,
+// slot k < 8, into buf[grid][8 waves][8 slots]; no-op when buf == null.
 __device__ __forceinline__ void stamp(unsigned long long* buf, int k) {
-  if (buf != nullptr && threadIdx.x == 0) buf[blockIdx.x * 8 + k] = __builtin_amdgcn_s_memrealtime();
+  if (buf != nullptr && (threadIdx.x & 63) == 0)
+    buf[((size_t)blockIdx.x * 8 + (threadIdx.x >> 6)) * 8 + k] = __builtin_amdgcn_s_memrealtime();
 }
 
 }  // namespace tdl

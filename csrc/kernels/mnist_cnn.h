@@ -26,11 +26,11 @@ struct MnistArgs {
   float* P2;          // [b,5,5,64] == [b,1600]
   uint8_t* A2;        // [b,1600]
   float* H;           // [b,128] relu(dense1)
-  float* dH;          // [b,128]
+  float* dH;          // [b,128] grad of dense1 out (ReLU-masked)
   float* dC2;         // [b,10,10,64] grad of the (used 10x10 part of the) conv2 output
   float* part2;       // [b][289][64] per-image partials of conv2 wgrad (row 288 = bias)
   float* part1;       // [2b][320] per-(image, pixel-half) partials of conv1 wgrad (+ bias)
-  float* part3;       // [25][b][128] split-K partials of dense1
+  float* part3;       // [4][b][128] dense1 partials, one per conv2 channel quarter
   float* part4;       // [ceil(b/4)][1290] per-workgroup partials of dense2 wgrad (+ bias)
   float* metrics;     // [0] loss sum, [1] correct, [2] count
   const float* lr;    // device scalar learning rate
@@ -41,18 +41,16 @@ struct MnistArgs {
 };
 
 constexpr int kMnistPart2Rows = 289;
-constexpr int kDense1Chunks = 25;  // K = 1600 = 25 x 64
+constexpr int kDense1Chunks = 4;  // dense1 partials: one per conv2 channel quarter (k_fwd_conv)
 constexpr int kMnistPart1Cols = 320;
 __host__ __device__ inline int mnist_part1_rows(int b) { return 2 * b; }
+
 __host__ __device__ inline int mnist_head_blocks(int b) { return (b + 3) / 4; }
 
-void mnist_conv1_pool(const MnistArgs& a, hipStream_t s);
-void mnist_conv2_pool(const MnistArgs& a, hipStream_t s);
-void mnist_dense1(const MnistArgs& a, hipStream_t s);
 void mnist_head(const MnistArgs& a, hipStream_t s);
 void mnist_dense1_bwd(const MnistArgs& a, hipStream_t s);
 void mnist_conv_bwd(const MnistArgs& a, hipStream_t s);
-void mnist_fwd_conv(const MnistArgs& a, hipStream_t s);  // K1+K2 fused per image
+void mnist_fwd_conv(const MnistArgs& a, hipStream_t s);  // conv1 + conv2 + dense1 partials per image
 void mnist_finalize(const MnistArgs& a, bool apply_sgd, hipStream_t s);
 
 // Plain SGD over a flat slab: w -= lr * g  (lr read from device memory).

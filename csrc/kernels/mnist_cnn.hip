@@ -1,14 +1,14 @@
 // Fused MNIST-CNN training step for gfx950 (MI355X), f32 end to end.
 //
 // Replaces, for the reference model of tf_dist_example.py:40-52, the ~35 TF/cuDNN/Eigen kernels
-// of one replica step by seven launches:
+// of one replica step by five launches:
 //
-//   K1 conv1_pool   : gather(idx) + conv1 3x3 (1->32) + bias + ReLU + maxpool2  (VALU; K=9)
-//   K2 conv2_pool   : conv2 3x3 (32->64) implicit GEMM on v_mfma_f32_16x16x4_f32, epilogue
-//                     bias + ReLU + maxpool2 done in registers (a 16-row MFMA tile = 4 windows)
-//   K3 dense1       : [b,1600]x[1600,128] MFMA, 8-wave in-workgroup split-K, bias + ReLU
-//   K4 head         : dense2 + softmax-xent + dlogits*(1/(b*R)) + loss/accuracy accumulators
-//                     + dW4/db4 + dH (ReLU mask), one workgroup
+//   KA fwd_conv     : per (image, channel quarter), LDS-staged: gather(idx) + conv1 3x3 (1->32)
+//                     and conv2 3x3 (32->64) on v_mfma_f32_16x16x4_f32 with bias + ReLU + maxpool2
+//                     in registers (a 16-row MFMA tile = 4 pool windows), then this quarter's
+//                     dense1 partial [1600/4 features] x W3 (W3 slice prefetched in registers)
+//   K4 head         : dense1 partial sum + bias + ReLU, dense2 + softmax-xent + dlogits*(1/(b*R))
+//                     + loss/accuracy accumulators + dW4/db4 partials + dH (ReLU mask)
 //   K5 dense1_bwd   : dW3 = P2^T dH, db3, dP2 = dH W3^T -> pool2/ReLU backward scatter to dC2
 //   KC conv_bwd     : per image (x4 parts), LDS-staged: dW2 (+db2 as an extra "ones" row) and
 //                     dP1 = dC2 (*) W2^T on MFMA with pool1/ReLU backward AND conv1 wgrad in
@@ -22,149 +22,6 @@
 #include "mnist_cnn.h"
 
 namespace tdl {
-
-// --------------------------------------------------------------------------------------------
-// K1: conv1 + bias + relu + maxpool.  One thread = one pooled pixel x 4 output channels.
-// --------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_conv1_pool(MnistArgs a) {
-  __shared__ float sw[320];
-  for (int i = threadIdx.x; i < 320; i += 256)
-    sw[i] = (i < 288) ? a.W[a.ow1 + i] : a.W[a.ob1 + i - 288];
-  __syncthreads();
-  const int t = blockIdx.x * 256 + threadIdx.x;
-  if (t >= a.b * 169 * 8) return;
-  const int cg = t & 7, pix = t >> 3;
-  const int bi = pix / 169, p = pix - bi * 169, ph = p / 13, pw = p - ph * 13;
-  const float* img = a.X + (size_t)a.idx[bi] * 784 + (2 * ph) * 28 + 2 * pw;
-  float in[4][4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) in[r][c] = img[r * 28 + c];
-  const int co = cg * 4;
-  float best[4];
-  unsigned arg[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int dy = q >> 1, dx = q & 1;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float acc = 0.f;
-#pragma unroll
-      for (int kh = 0; kh < 3; ++kh)
-#pragma unroll
-        for (int kw = 0; kw < 3; ++kw) acc = fmaf(in[dy + kh][dx + kw], sw[(kh * 3 + kw) * 32 + co + j], acc);
-      if (q == 0 || acc > best[j]) { best[j] = acc; arg[j] = q; }
-    }
-  }
-  f4 o;
-  o.x = fmaxf(best[0] + sw[288 + co + 0], 0.f);
-  o.y = fmaxf(best[1] + sw[288 + co + 1], 0.f);
-  o.z = fmaxf(best[2] + sw[288 + co + 2], 0.f);
-  o.w = fmaxf(best[3] + sw[288 + co + 3], 0.f);
-  st4(a.P1 + (size_t)pix * 32 + co, o);
-  *reinterpret_cast<unsigned*>(a.A1 + (size_t)pix * 32 + co) =
-      arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
-}
-
-// --------------------------------------------------------------------------------------------
-// K2: conv2 + bias + relu + maxpool on MFMA.  Workgroup = 4 waves = one 16-row tile (4 pool
-// windows x 4 positions) x 4 column tiles of 16 output channels.  K = 9 taps x 32 ci.
-// Lane group g owns k-slot g; each lane loads 4 consecutive ci (float4) and feeds them to 4
-// successive MFMAs, so the same permuted k order is used for A and B.
-// --------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_conv2_pool(MnistArgs a) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int i = lane & 15, g = lane >> 4;
-  const int n0 = wave * 16;
-  const int npp = a.b * 25;
-  const int pp = blockIdx.x * 4 + (i >> 2), q = i & 3;
-  const bool valid = pp < npp;
-  const int ppc = valid ? pp : 0;
-  const int bi = ppc / 25, r = ppc - bi * 25, ph = r / 5, pw = r - ph * 5;
-  const int oh = 2 * ph + (q >> 1), ow = 2 * pw + (q & 1);
-  const float* abase = a.P1 + ((size_t)(bi * 13 + oh) * 13 + ow) * 32 + 4 * g;
-  const float* bbase = a.W + a.ow2 + (4 * g) * 64 + n0 + i;
-  // Issue every load of the wave up front (18 k-steps x (float4 A + 4 B) = 144 VGPRs) so the
-  // whole K loop costs one memory round trip; the MFMAs then drain them in order.
-  f4 av[18];
-  float bv[18][4];
-#pragma unroll
-  for (int s = 0; s < 18; ++s) {
-    const int kk = s >> 1, cb = (s & 1) * 16, kh = kk / 3, kw = kk % 3;
-    av[s] = ld4(abase + (kh * 13 + kw) * 32 + cb);
-    const float* bp = bbase + (kk * 32 + cb) * 64;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) bv[s][t] = bp[t * 64];
-  }
-  __builtin_amdgcn_sched_barrier(0);  // keep every load above the MFMAs (one round trip)
-  f4 acc0 = zero4(), acc1 = zero4();
-  const float vm = valid ? 1.f : 0.f;
-#pragma unroll
-  for (int s = 0; s < 18; ++s) {
-    const f4 x = av[s] * vm;
-    acc0 = mfma16x16x4(x.x, bv[s][0], acc0);
-    acc1 = mfma16x16x4(x.y, bv[s][1], acc1);
-    acc0 = mfma16x16x4(x.z, bv[s][2], acc0);
-    acc1 = mfma16x16x4(x.w, bv[s][3], acc1);
-  }
-  const f4 acc = acc0 + acc1;
-  // lane holds rows 4g..4g+3 == the 4 positions of pool window g, column n0+i.
-  const int ppo = blockIdx.x * 4 + g;
-  if (ppo < npp) {
-    float m = acc.x;
-    unsigned am = 0;
-    if (acc.y > m) { m = acc.y; am = 1; }
-    if (acc.z > m) { m = acc.z; am = 2; }
-    if (acc.w > m) { m = acc.w; am = 3; }
-    const int co = n0 + i;
-    a.P2[(size_t)ppo * 64 + co] = fmaxf(m + a.W[a.ob2 + co], 0.f);
-    a.A2[(size_t)ppo * 64 + co] = (uint8_t)am;
-  }
-}
-
-// --------------------------------------------------------------------------------------------
-// K3: dense1 GEMM P2 W3 as 25 split-K partial slabs (bias + ReLU + chunk sum in the head).
-// --------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_dense1(MnistArgs a) {
-  // split-K GEMM: workgroup = (K chunk c of 64, row tile mt, column half); wave = 16 columns.
-  // Every load of a wave is issued up front (one memory round trip), 16 MFMAs, and the partial
-  // tile goes to part3[c]; the head sums the 25 chunks + bias + ReLU per row.
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int i = lane & 15, g = lane >> 4;
-  const int MT = (a.b + 15) >> 4;
-  const int c = blockIdx.x / (MT * 2), rem = blockIdx.x - c * MT * 2;
-  const int mt = rem >> 1, nt = (rem & 1) * 4 + wave;
-  const int row = mt * 16 + i;
-  const bool valid = row < a.b;
-  const float* ap = a.P2 + (size_t)(valid ? row : 0) * 1600 + c * 64 + 4 * g;
-  const float* bp = a.W + a.ow3 + (size_t)(c * 64 + 4 * g) * 128 + nt * 16 + i;
-  f4 av[4];
-  float bv[4][4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    av[s] = ld4(ap + 16 * s);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) bv[s][t] = bp[(16 * s + t) * 128];
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  const float vm = valid ? 1.f : 0.f;
-  f4 acc0 = zero4(), acc1 = zero4();
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const f4 x = av[s] * vm;
-    acc0 = mfma16x16x4(x.x, bv[s][0], acc0);
-    acc1 = mfma16x16x4(x.y, bv[s][1], acc1);
-    acc0 = mfma16x16x4(x.z, bv[s][2], acc0);
-    acc1 = mfma16x16x4(x.w, bv[s][3], acc1);
-  }
-  const f4 acc = acc0 + acc1;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int rr = mt * 16 + 4 * g + r;
-    if (rr < a.b) a.part3[((size_t)c * a.b + rr) * 128 + nt * 16 + i] = acc[r];
-  }
-}
 
 // --------------------------------------------------------------------------------------------
 // K4: dense2 + sparse softmax cross-entropy + metrics + dense2 grads + dH.  ceil(b/4) workgroups.
@@ -350,7 +207,7 @@ constexpr int kDcStride = 68, kDcDim = 15, kP1Stride = 36;
 constexpr int kLdsDc = kDcDim * kDcDim * kDcStride;   // 15300
 constexpr int kLdsP1 = 169 * kP1Stride;              // 6084
 constexpr int kLdsWd = 9 * 16 * 16 * 4;              // 9216
-constexpr int kLdsConvBwd = kLdsDc + kLdsP1 + 784 + kLdsWd + 8 * 10 * 16;
+constexpr int kLdsConvBwd = kLdsDc + kLdsP1 + 784 + kLdsWd + 8 * 10 * 16 + 16;
 
 __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -359,6 +216,7 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
   float* Xs = P1s + kLdsP1;
   float* Wd = Xs + 784;
   float* red = Wd + kLdsWd;  // [8 waves][10][16]
+  float* unit = red + 8 * 10 * 16;  // [16] = e_0 (A operand of the bias row)
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int i = lane & 15, g = lane >> 4;
   const int bi = blockIdx.x >> 2, p = blockIdx.x & 3;
@@ -410,33 +268,54 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
     if (e4 < kLdsWd / 4) st4(Wd + e4 * 4, vwd[j]);
   }
   if (tid < 196) st4(Xs + tid * 4, vx);
+  if (tid < 16) unit[tid] = tid == 0 ? 1.f : 0.f;
   stamp(a.stamps, 1);
   __syncthreads();
   stamp(a.stamps, 2);
 
-  // ---- conv2 wgrad: tiles mt = wave, wave+8, wave+16 (< 19); columns 16p + i ----
-  for (int mt = wave; mt < 19; mt += 8) {
-    const bool bias_tile = mt == 18;
-    const int k = mt * 16 + i;
-    const int tap = bias_tile ? 0 : k >> 5, ci = k & 31;
-    const int kh = tap / 3, kw = tap - kh * 3;
-    const float* pa = P1s + (kh * 13 + kw) * kP1Stride + ci;
-    const float* pb = dCs + (2 * kDcDim + 2) * kDcStride + 16 * p + i;
-    const float one = (i == 0) ? 1.f : 0.f;
-    f4 acc0 = zero4(), acc1 = zero4();
-#pragma unroll 5
-    for (int s = 0; s < 25; ++s) {
-      const int pos = 4 * s + g, oh = pos / 10, ow = pos - oh * 10;
-      const float av = bias_tile ? one : pa[(oh * 13 + ow) * kP1Stride];
-      const float bv = pb[(oh * kDcDim + ow) * kDcStride];
-      if (s & 1) acc1 = mfma16x16x4(av, bv, acc1);
-      else acc0 = mfma16x16x4(av, bv, acc0);
-    }
-    const f4 acc = acc0 + acc1;
+  // ---- conv2 wgrad (19 row tiles of 25 k-steps, columns 16p + i).  MFMA work per SIMD (waves w
+  // and w+4 share one): wave 0 takes tiles 0..5 + 18 (the bias row), wave 1 tiles 6..11, waves
+  // 2..7 tile 10 + wave next to their 144-step dgrad tile -> at most 344 MFMAs per SIMD. ----
+  {
+    const int ntiles = wave == 0 ? 7 : (wave == 1 ? 6 : 1);
+    for (int j = 0; j < ntiles; ++j) {
+      const int mt = wave == 0 ? (j < 6 ? j : 18) : (wave == 1 ? 6 + j : 10 + wave);
+      const bool bias_tile = mt == 18;
+      const int k = mt * 16 + i;
+      const int tap = bias_tile ? 0 : k >> 5, ci = k & 31;
+      const int kh = tap / 3, kw = tap - kh * 3;
+      // the bias row reads the LDS unit vector (1 for i == 0) at every position: stride 0
+      const float* pa = bias_tile ? unit + i : P1s + (kh * 13 + kw) * kP1Stride + ci;
+      const int sa = bias_tile ? 0 : 1;
+      const float* pb = dCs + (2 * kDcDim + 2) * kDcStride + 16 * p + i;
+      // this lane's k-step s covers position 4s + g of the 10x10 grid: advance incrementally
+      int ow = g, offA = sa * g * kP1Stride, offB = g * kDcStride;
+      f4 acc0 = zero4(), acc1 = zero4();
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = mt * 16 + 4 * g + r;
-      if (row < kMnistPart2Rows) a.part2[((size_t)bi * kMnistPart2Rows + row) * 64 + 16 * p + i] = acc[r];
+      for (int s0 = 0; s0 < 25; s0 += 5) {
+        float av[5], bv[5];
+#pragma unroll
+        for (int u = 0; u < 5; ++u) {
+          av[u] = pa[offA];
+          bv[u] = pb[offB];
+          const int ow2 = ow + 4;
+          const bool wrap = ow2 >= 10;
+          ow = wrap ? ow2 - 10 : ow2;
+          offA += sa * (wrap ? 7 * kP1Stride : 4 * kP1Stride);
+          offB += wrap ? 9 * kDcStride : 4 * kDcStride;
+        }
+#pragma unroll
+        for (int u = 0; u < 5; ++u) {
+          if ((s0 + u) & 1) acc1 = mfma16x16x4(av[u], bv[u], acc1);
+          else acc0 = mfma16x16x4(av[u], bv[u], acc0);
+        }
+      }
+      const f4 acc = acc0 + acc1;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = mt * 16 + 4 * g + r;
+        if (row < kMnistPart2Rows) a.part2[((size_t)bi * kMnistPart2Rows + row) * 64 + 16 * p + i] = acc[r];
+      }
     }
   }
 
@@ -453,6 +332,14 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
     const int Pc = valid ? P : pix0;
     const int ih = Pc / 13, iw = Pc - ih * 13;
     const float* wb = Wd + (g * 16 + i) * 4;
+    const int c = 16 * h + i;
+    // pool-1 argmax bytes of the epilogue's 4 rows: issued now, consumed after the MFMAs
+    unsigned q1v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int Pr = min(pix0 + d * 16 + 4 * g + r, pix1 - 1);
+      q1v[r] = a.A1[((size_t)bi * 169 + Pr) * 32 + c];
+    }
     f4 acc0 = zero4(), acc1 = zero4();
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
@@ -469,13 +356,13 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
       }
     }
     const f4 acc = acc0 + acc1;
-    const int c = 16 * h + i;
+    stamp(a.stamps, 6);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int Pr = pix0 + d * 16 + 4 * g + r;
       if (Pr < pix1) {
         const float v = P1s[Pr * kP1Stride + c] > 0.f ? acc[r] : 0.f;
-        const unsigned q1 = a.A1[((size_t)bi * 169 + Pr) * 32 + c];
+        const unsigned q1 = q1v[r];
         const int ph = Pr / 13, pw = Pr - ph * 13;
         const float* img = Xs + (2 * ph + (q1 >> 1)) * 28 + 2 * pw + (q1 & 1);
 #pragma unroll
@@ -509,8 +396,11 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
 //   conv1 + bias + relu + maxpool into LDS (P1s, stride 36), then conv2 on MFMA for this
 //   quarter's 16 channels over the 100 used positions (7 row tiles of 4 pool windows) with the
 //   bias + relu + maxpool epilogue in registers.  Quarter 0 also writes P1 / A1 for backward.
+//   Then dense1 for this quarter's 400 of the 1600 features: H_part[cq][bi][:] = P2_q . W3_q,
+//   with the 205 KB W3 slice loaded into registers at kernel start (its latency hides behind the
+//   convolutions); the head sums the 4 quarter partials + bias + ReLU.
 // --------------------------------------------------------------------------------------------
-constexpr int kLdsFwd = 784 + 320 + 169 * kP1Stride + 72 * 16 * 4;
+constexpr int kLdsFwd = 784 + 320 + 169 * kP1Stride + 72 * 16 * 4 + 400;
 
 __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -518,6 +408,7 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   float* w1s = xs + 784;
   float* P1s = w1s + 320;
   float* w2s = P1s + 169 * kP1Stride;  // [kc=72][j=16][t=4]: B[k=4kc+t][16cq+j]
+  float* p2s = w2s + 72 * 16 * 4;      // [25 windows][16 channels] pooled conv2 output
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int i = lane & 15, g = lane >> 4;
   const int bi = blockIdx.x >> 2, cq = blockIdx.x & 3;
@@ -549,6 +440,16 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   stamp(a.stamps, 1);
   __syncthreads();
   stamp(a.stamps, 2);
+  // ---- dense1 operand prefetch (after the staging loads, overlapping the convolutions): thread
+  // (row group rg, 4 columns n4) needs W3 rows of features kk = 25 rg .. 25 rg + 24 of this quarter
+  // (feature kk = window (kk >> 4), channel 16cq + (kk & 15))
+  const int n4 = (tid & 31) * 4, rg = tid >> 5;
+  f4 w3v[25];
+#pragma unroll
+  for (int j = 0; j < 25; ++j) {
+    const int kk = rg * 25 + j;
+    w3v[j] = ld4(a.W + a.ow3 + (size_t)((kk >> 4) * 64 + 16 * cq + (kk & 15)) * 128 + n4);
+  }
   // ---- conv1 on MFMA (K = 9 taps padded to 12): rows = 676 conv1 positions in pool-window-major
   // order, so a 16-row tile holds 4 whole 2x2 windows and the maxpool happens in registers.
   // 43 row tiles x 2 channel tiles; bias + relu after the max (they commute with it). ----
@@ -567,29 +468,51 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
       const int k = min(4 * s3 + g, 8);
       tap_off[s3] = (k / 3) * 28 + (k % 3);
     }
-    for (int job = wave; job < 86; job += 8) {
-      const int mt = job >> 1, nt = job & 1;
-      const int w = mt * 4 + (i >> 2), q = i & 3;
-      const int wc = min(w, 168);
-      const int y = 2 * (wc / 13) + (q >> 1), x = 2 * (wc % 13) + (q & 1);
-      const float* xb = xs + y * 28 + x;
-      f4 acc = zero4();
+    // row tiles mt0 and mt0 + 8 per iteration, both channel tiles each: 4 independent MFMA
+    // chains sharing 6 LDS loads (the two channel tiles read the same image values)
+    for (int mt0 = wave; mt0 < 43; mt0 += 16) {
+      float xa[2][3];
 #pragma unroll
-      for (int s3 = 0; s3 < 3; ++s3) acc = mfma16x16x4(xb[tap_off[s3]], bw[nt][s3], acc);
-      const int wo = mt * 4 + g;
-      if (wo < 169) {
-        float m = acc.x;
-        unsigned am = 0;
-        if (acc.y > m) { m = acc.y; am = 1; }
-        if (acc.z > m) { m = acc.z; am = 2; }
-        if (acc.w > m) { m = acc.w; am = 3; }
-        const int co = nt * 16 + i;
-        const float v = fmaxf(m + w1s[288 + co], 0.f);
-        P1s[wo * kP1Stride + co] = v;
-        if (cq == 0) {
-          const size_t gi = ((size_t)bi * 169 + wo) * 32 + co;
-          a.P1[gi] = v;
-          a.A1[gi] = (uint8_t)am;
+      for (int u = 0; u < 2; ++u) {
+        const int mt = min(mt0 + 8 * u, 42);
+        const int w = mt * 4 + (i >> 2), q = i & 3;
+        const int wc = min(w, 168);
+        const int y = 2 * (wc / 13) + (q >> 1), x = 2 * (wc % 13) + (q & 1);
+        const float* xb = xs + y * 28 + x;
+#pragma unroll
+        for (int s3 = 0; s3 < 3; ++s3) xa[u][s3] = xb[tap_off[s3]];
+      }
+      f4 acc[2][2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) acc[u][nt] = zero4();
+#pragma unroll
+      for (int s3 = 0; s3 < 3; ++s3)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) acc[u][nt] = mfma16x16x4(xa[u][s3], bw[nt][s3], acc[u][nt]);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int wo = (mt0 + 8 * u) * 4 + g;
+        if (mt0 + 8 * u >= 43 || wo >= 169) continue;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const f4 ac = acc[u][nt];
+          float m = ac.x;
+          unsigned am = 0;
+          if (ac.y > m) { m = ac.y; am = 1; }
+          if (ac.z > m) { m = ac.z; am = 2; }
+          if (ac.w > m) { m = ac.w; am = 3; }
+          const int co = nt * 16 + i;
+          const float v = fmaxf(m + w1s[288 + co], 0.f);
+          P1s[wo * kP1Stride + co] = v;
+          if (cq == 0) {
+            const size_t gi = ((size_t)bi * 169 + wo) * 32 + co;
+            a.P1[gi] = v;
+            a.A1[gi] = (uint8_t)am;
+          }
         }
       }
     }
@@ -598,41 +521,59 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   __syncthreads();
   stamp(a.stamps, 4);
   // ---- conv2 on MFMA: wave w < 7 takes row tile w (windows 4w .. 4w+3) ----
-  if (wave >= 7) return;
-  const int wi = wave * 4 + (i >> 2), q = i & 3;
-  const bool valid = wi < 25;
-  const int wic = valid ? wi : 0;
-  const int ph = wic / 5, pw = wic - ph * 5;
-  const int oh = 2 * ph + (q >> 1), ow = 2 * pw + (q & 1);
-  const float* ab = P1s + (oh * 13 + ow) * kP1Stride + 4 * g;
-  const float* bb = w2s + (g * 16 + i) * 4;
-  f4 acc0 = zero4(), acc1 = zero4();
+  if (wave < 7) {
+    const int wi = wave * 4 + (i >> 2), q = i & 3;
+    const bool valid = wi < 25;
+    const int wic = valid ? wi : 0;
+    const int ph = wic / 5, pw = wic - ph * 5;
+    const int oh = 2 * ph + (q >> 1), ow = 2 * pw + (q & 1);
+    const float* ab = P1s + (oh * 13 + ow) * kP1Stride + 4 * g;
+    const float* bb = w2s + (g * 16 + i) * 4;
+    f4 acc0 = zero4(), acc1 = zero4();
 #pragma unroll
-  for (int kk = 0; kk < 9; ++kk) {
-    const int kh = kk / 3, kw = kk % 3;
+    for (int kk = 0; kk < 9; ++kk) {
+      const int kh = kk / 3, kw = kk % 3;
 #pragma unroll
-    for (int cb = 0; cb < 32; cb += 16) {
-      const f4 av = ld4(ab + (kh * 13 + kw) * kP1Stride + cb);
-      const f4 bv = ld4(bb + ((kk * 32 + cb) / 4) * 64);
-      acc0 = mfma16x16x4(av.x, bv.x, acc0);
-      acc1 = mfma16x16x4(av.y, bv.y, acc1);
-      acc0 = mfma16x16x4(av.z, bv.z, acc0);
-      acc1 = mfma16x16x4(av.w, bv.w, acc1);
+      for (int cb = 0; cb < 32; cb += 16) {
+        const f4 av = ld4(ab + (kh * 13 + kw) * kP1Stride + cb);
+        const f4 bv = ld4(bb + ((kk * 32 + cb) / 4) * 64);
+        acc0 = mfma16x16x4(av.x, bv.x, acc0);
+        acc1 = mfma16x16x4(av.y, bv.y, acc1);
+        acc0 = mfma16x16x4(av.z, bv.z, acc0);
+        acc1 = mfma16x16x4(av.w, bv.w, acc1);
+      }
+    }
+    const f4 acc = acc0 + acc1;
+    stamp(a.stamps, 5);
+    const int wo = wave * 4 + g;
+    if (wo < 25) {
+      float m = acc.x;
+      unsigned am = 0;
+      if (acc.y > m) { m = acc.y; am = 1; }
+      if (acc.z > m) { m = acc.z; am = 2; }
+      if (acc.w > m) { m = acc.w; am = 3; }
+      const int co = 16 * cq + i;
+      const size_t e = (size_t)bi * 1600 + wo * 64 + co;
+      const float v = fmaxf(m + a.W[a.ob2 + co], 0.f);
+      a.P2[e] = v;
+      a.A2[e] = (uint8_t)am;
+      p2s[wo * 16 + i] = v;
     }
   }
-  const f4 acc = acc0 + acc1;
-  stamp(a.stamps, 5);
-  const int wo = wave * 4 + g;
-  if (wo < 25) {
-    float m = acc.x;
-    unsigned am = 0;
-    if (acc.y > m) { m = acc.y; am = 1; }
-    if (acc.z > m) { m = acc.z; am = 2; }
-    if (acc.w > m) { m = acc.w; am = 3; }
-    const int co = 16 * cq + i;
-    const size_t e = (size_t)bi * 1600 + wo * 64 + co;
-    a.P2[e] = fmaxf(m + a.W[a.ob2 + co], 0.f);
-    a.A2[e] = (uint8_t)am;
+  __syncthreads();
+  // ---- dense1 quarter partial: 25 features x 4 columns per thread, 16 row groups reduced in LDS
+  {
+    f4 hs = zero4();
+#pragma unroll
+    for (int j = 0; j < 25; ++j) hs += p2s[rg * 25 + j] * w3v[j];
+    st4(P1s + rg * 128 + n4, hs);  // P1s is free after conv2
+  }
+  __syncthreads();
+  if (tid < 128) {
+    float hsum = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) hsum += P1s[k * 128 + tid];
+    a.part3[((size_t)cq * a.b + bi) * 128 + tid] = hsum;
   }
   stamp(a.stamps, 6);
 }
@@ -740,16 +681,6 @@ __global__ __launch_bounds__(256) void k_sgd_momentum(float* __restrict__ w, con
 // --------------------------------------------------------------------------------------------
 // launchers
 // --------------------------------------------------------------------------------------------
-void mnist_conv1_pool(const MnistArgs& a, hipStream_t s) {
-  const int n = a.b * 169 * 8;
-  hipLaunchKernelGGL(k_conv1_pool, dim3((n + 255) / 256), dim3(256), 0, s, a);
-}
-void mnist_conv2_pool(const MnistArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_conv2_pool, dim3((a.b * 25 + 3) / 4), dim3(256), 0, s, a);
-}
-void mnist_dense1(const MnistArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_dense1, dim3(kDense1Chunks * ((a.b + 15) / 16) * 2), dim3(256), 0, s, a);
-}
 void mnist_head(const MnistArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_head, dim3(mnist_head_blocks(a.b)), dim3(256), 0, s, a);
 }

@@ -1,40 +1,66 @@
-"""Phase timestamps (s_memrealtime, 10 ns ticks) of the per-image kernels: median over workgroups
-of each phase duration and of the kernel span, after warm-up."""
-import os, sys
+"""Per-wave phase timestamps (s_memrealtime, 10 ns ticks) of the per-image MNIST kernels.
+
+For every wave slot, prints the median (over workgroups) time from the kernel's first wave start
+to each stamped point, so phases of different waves can be compared on one clock."""
+import os
+import sys
+
 import numpy as np
 import torch
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from tensorflow_distributed_learning_amd.models import mnist_cnn as M
 
-dev = torch.device("cuda:0")
-b, N = 64, 60000
-X = torch.rand(N, 28, 28, 1, device=dev)
-Y = torch.randint(0, 10, (N,), device=dev, dtype=torch.int32)
-layout = M.mnist_layout()
-W = layout.pack(M.init_mnist_params(0), device=dev)
-G = torch.zeros_like(W)
-idx = torch.randperm(N, device=dev)[:b].to(torch.int32)
-lr = torch.tensor([1e-3], device=dev)
-st = M.FusedMnistTrainStep(X, Y, idx, W, G, layout, b, 1, lr)
-for _ in range(20):
-    st.forward_backward(0); st.finalize(True)
-for name, k, grid, phases in (("fwd_conv", 8, b * 4, ["stage-issue", "stage-barrier", "conv1", "barrier2", "conv2-mfma", "epilogue"]),
-                               ("conv_bwd", 6, b * 4, ["stage-issue", "stage-barrier", "wgrad", "dgrad+epi", "final-barrier"])):
-    buf = torch.zeros(grid * 8, dtype=torch.int64, device=dev)
-    res = []
-    for rep in range(5):
-        st.forward_backward(0); st.finalize(True)
-        buf.zero_()
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tensorflow_distributed_learning_amd.models import mnist_cnn as M  # noqa: E402
+
+KERNELS = {
+    "fwd_conv": (8, 8, {0: "start", 1: "stage-issued", 2: "stage-barrier", 3: "conv1-done", 4: "barrier2",
+                        5: "conv2-mfma", 6: "end"}, 256),
+    "conv_bwd": (6, 8, {0: "start", 1: "stage-issued", 2: "stage-barrier", 3: "wgrad-done", 6: "dgrad-mfma",
+                        4: "dgrad-epi", 5: "final-barrier"}, 256),
+}
+
+
+def main():
+    dev = torch.device("cuda:0")
+    b, N = 64, 60000
+    X = torch.rand(N, 28, 28, 1, device=dev)
+    Y = torch.randint(0, 10, (N,), device=dev, dtype=torch.int32)
+    layout = M.mnist_layout()
+    W = layout.pack(M.init_mnist_params(0), device=dev)
+    G = torch.zeros_like(W)
+    idx = torch.randperm(N, device=dev)[:b].to(torch.int32)
+    lr = torch.tensor([1e-3], device=dev)
+    st = M.FusedMnistTrainStep(X, Y, idx, W, G, layout, b, 1, lr)
+    for _ in range(20):
+        st.forward_backward(0)
+        st.finalize(True)
+    for name, (k, waves, slots, grid) in KERNELS.items():
+        if grid is None:  # dense_bwd: 4 row tiles x 13 dP2 blocks + 25 dW3 blocks
+            grid = 4 * 13 + 25
+        buf = torch.zeros(grid * 64, dtype=torch.int64, device=dev)
+        st.forward_backward(0)
+        st.finalize(True)
         st._impl.set_stamps(buf)
         st.stage(k)
         st._impl.set_stamps(None)
         torch.cuda.synchronize()
-        res.append(buf.view(grid, 8).cpu().numpy().astype(np.int64))
-    r = res[-1]
-    n = len(phases) + 1
-    d = np.diff(r[:, :n], axis=1) * 10 / 1000.0  # us
-    span = (r[:, n - 1].max() - r[:, 0].min()) * 10 / 1000.0
-    starts = (r[:, 0] - r[:, 0].min()) * 10 / 1000.0
-    print(f"{name}: kernel span {span:.2f} us; WG start spread {starts.max():.2f} us")
-    for j, ph in enumerate(phases):
-        print(f"   {ph:14s} median {np.median(d[:, j]):6.2f}  max {d[:, j].max():6.2f} us")
+        r = buf.view(grid, 8, 8).cpu().numpy().astype(np.int64)
+        t0 = r[:, :waves, 0].min(axis=1, keepdims=True)
+        rel = (r - t0[:, :, None]) * 10 / 1000.0  # us since the workgroup's first wave started
+        span = (r[:, :waves][r[:, :waves] > 0].max() - r[:, :waves, 0].min()) * 10 / 1000.0
+        starts = r[:, 0, 0]
+        print(f"{name}: kernel span {span:.2f} us; workgroup start spread {(starts.max() - starts.min()) / 100:.2f} us"
+              "  (median us since workgroup start, per wave)")
+        if name == "dense_bwd":
+            for lo, hi, lab in ((0, 52, "dP2"), (52, grid, "dW3")):
+                ph = [np.median((r[lo:hi, 0, k] - r[lo:hi, 0, 0]) / 100) for k in (3, 4, 5, 1, 2)]
+                print(f"  {lab:4s} blocks (median us): loads+H {ph[0]:.2f}  logits {ph[1]:.2f}  softmax {ph[2]:.2f}  "
+                      f"dH/head {ph[3]:.2f}  end {ph[4]:.2f}")
+            continue
+        print("  slot/wave " + " ".join(f"{w:>6d}" for w in range(waves)))
+        for s, label in sorted(slots.items(), key=lambda kv: np.median(rel[:, 0, kv[0]])):
+            vals = [np.median(rel[:, w, s]) if (r[:, w, s] > 0).all() else float("nan") for w in range(waves)]
+            print(f"  {label:14s}" + " ".join(f"{v:6.2f}" for v in vals))
+
+
+if __name__ == "__main__":
+    main()

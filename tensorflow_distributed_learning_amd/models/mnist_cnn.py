@@ -143,5 +143,5 @@ class FusedMnistTrainStep:
         self._impl.set_idx_offset(int(off))
 
     def buffers(self) -> Dict[str, torch.Tensor]:
-        names = ["P1", "A1", "P2", "A2", "H", "dH", "dC2", "part2", "part1"]
+        names = ["P1", "A1", "P2", "A2", "H", "dH", "dC2", "part2", "part1", "part3"]
         return dict(zip(names, self._impl.buffers()))
