@@ -35,6 +35,7 @@ __global__ __launch_bounds__(256) void k_head(MnistArgs a) {
   const int r = blockIdx.x * 4 + wave;
   const bool live = r < a.b;
   const int rr = live ? r : 0;
+  const int y = a.Y[a.idx[rr]];  // dependent pair of loads: issued first
   const float* w4 = a.W + a.ow4;
   float wa[10], wb[10];
 #pragma unroll
@@ -52,7 +53,6 @@ __global__ __launch_bounds__(256) void k_head(MnistArgs a) {
   h0 = fmaxf(h0, 0.f);
   h1 = fmaxf(h1, 0.f);
   if (live) { a.H[r * 128 + l] = h0; a.H[r * 128 + l + 64] = h1; }
-  const int y = a.Y[a.idx[rr]];
   float lg[10];
 #pragma unroll
   for (int c = 0; c < 10; ++c) lg[c] = wave_sum(fmaf(h0, wa[c], h1 * wb[c])) + a.W[a.ob4 + c];
@@ -146,6 +146,15 @@ __global__ __launch_bounds__(256) void k_dense1_bwd(MnistArgs a) {
       av[s] = ld4(ap + s * 16);
       bv[s] = ld4(bp + s * 16);
     }
+    // epilogue operands (pool2 output and argmax of the tile's 4 rows) in the same round trip
+    float p2v[4];
+    unsigned a2v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const size_t e = (size_t)min(mt * 16 + 4 * g + r, b - 1) * 1600 + nt * 16 + i;
+      p2v[r] = a.P2[e];
+      a2v[r] = a.A2[e];
+    }
     __builtin_amdgcn_sched_barrier(0);
     const float vm = valid ? 1.f : 0.f;
     f4 acc0 = zero4(), acc1 = zero4();
@@ -163,9 +172,8 @@ __global__ __launch_bounds__(256) void k_dense1_bwd(MnistArgs a) {
     for (int r = 0; r < 4; ++r) {
       const int rr = mt * 16 + 4 * g + r;
       if (rr < b) {
-        const size_t e = (size_t)rr * 1600 + k;
-        const float v = a.P2[e] > 0.f ? acc[r] : 0.f;
-        const unsigned qa = a.A2[e];
+        const float v = p2v[r] > 0.f ? acc[r] : 0.f;
+        const unsigned qa = a2v[r];
         const int ph = pp / 5, pw = pp - ph * 5;
         float* d = a.dC2 + ((size_t)(rr * 10 + 2 * ph) * 10 + 2 * pw) * 64 + co;  // [b][10][10][64]
         d[0] = qa == 0 ? v : 0.f;
@@ -508,7 +516,7 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
           const int co = nt * 16 + i;
           const float v = fmaxf(m + w1s[288 + co], 0.f);
           P1s[wo * kP1Stride + co] = v;
-          if (cq == 0) {
+          if (((mt0 + 8 * u) & 3) == cq) {  // each quarter stores a quarter of P1 / A1 for backward
             const size_t gi = ((size_t)bi * 169 + wo) * 32 + co;
             a.P1[gi] = v;
             a.A1[gi] = (uint8_t)am;
@@ -584,7 +592,7 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
 //   blocks [nbs, nbs + nb2)  : conv2 kernel/bias, 4 threads per output (16 images each)
 //   blocks [.., + 20)        : conv1 kernel/bias, 16 threads per output
 // --------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_finalize(MnistArgs a, int apply_sgd, int nbs, int nb2) {
+__global__ __launch_bounds__(256) void k_finalize(MnistArgs a, int apply_sgd, int nbs, int nb2, int nb1) {
   const float lr = *a.lr;
   const int blk = blockIdx.x;
   if (blk < nbs) {
@@ -709,7 +717,7 @@ void mnist_finalize(const MnistArgs& a, bool apply_sgd, hipStream_t s) {
   const int nbs = apply_sgd ? (a.nslab + 255) / 256 : 0;
   const int nb2 = (kMnistPart2Rows * 64 * 4 + 255) / 256;
   const int nb1 = (kMnistPart1Cols * 16 + 255) / 256;
-  hipLaunchKernelGGL(k_finalize, dim3(nbs + nb2 + nb1), dim3(256), 0, s, a, apply_sgd ? 1 : 0, nbs, nb2);
+  hipLaunchKernelGGL(k_finalize, dim3(nbs + nb2 + nb1), dim3(256), 0, s, a, apply_sgd ? 1 : 0, nbs, nb2, nb1);
 }
 void sgd_apply(float* w, const float* g, const float* lr, int64_t n, hipStream_t s) {
   const int64_t nt = (n + 3) / 4;
