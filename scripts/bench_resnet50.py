@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--classes", type=int, default=1000)
     ap.add_argument("--dtype", default="mixed_bfloat16", choices=["mixed_bfloat16", "float32"])
     ap.add_argument("--engine", default="auto")
+    ap.add_argument("--strategy", default="mirrored", choices=["mirrored", "mwms"],
+                    help="mwms: MultiWorkerMirroredStrategy over TF_CONFIG workers (BASELINE config 5)")
     args = ap.parse_args()
 
     import torch
@@ -34,12 +36,15 @@ def main():
     import tensorflow_distributed_learning_amd as tdl
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1 and "LOCAL_RANK" in os.environ:
-        torch.cuda.set_device(int(os.environ["LOCAL_RANK"]))
+    if world > 1 and "LOCAL_RANK" in os.environ and torch.cuda.device_count() > 0:
+        torch.cuda.set_device(int(os.environ["LOCAL_RANK"]) % torch.cuda.device_count())
     if args.engine != "auto":
         os.environ["TDL_ENGINE"] = args.engine
     tdl.keras.mixed_precision.set_global_policy(args.dtype)
-    strategy = tdl.distribute.MirroredStrategy()
+    if args.strategy == "mwms":
+        strategy = tdl.distribute.MultiWorkerMirroredStrategy()
+    else:
+        strategy = tdl.distribute.MirroredStrategy()
     R = strategy.num_replicas_in_sync
     dev = strategy.extended.device
     b = args.batch
@@ -99,7 +104,10 @@ def main():
             "dtype": "bf16" if args.dtype == "mixed_bfloat16" else "fp32",
             "data": "synthetic ImageNet-shaped, device-resident; random init",
             "config": {"model": "keras.applications.ResNet50 (25.6M params)", "global_batch": B,
-                       "image": args.image, "parallelism": f"dp{R}", "engine": trainer.kind,
+                       "image": args.image, "parallelism": f"dp{R}", "strategy": type(strategy).__name__,
+                       "workers": (len(strategy.extended.tf_config.cluster.training_tasks())
+                                   if getattr(strategy.extended, "tf_config", None) else 1),
+                       "engine": trainer.kind,
                        "communicator": comm.name, "final_loss": round(logs["loss"], 4)},
         }), flush=True)
     strategy.shutdown()
