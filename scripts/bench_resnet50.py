@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--classes", type=int, default=1000)
     ap.add_argument("--dtype", default="mixed_bfloat16", choices=["mixed_bfloat16", "float32"])
     ap.add_argument("--engine", default="auto")
+    ap.add_argument("--conv-search", type=int, default=1,
+                    help="1: MIOpen find-mode solver search per conv shape (torch.backends.cudnn.benchmark)")
     ap.add_argument("--strategy", default="mirrored", choices=["mirrored", "mwms"],
                     help="mwms: MultiWorkerMirroredStrategy over TF_CONFIG workers (BASELINE config 5)")
     args = ap.parse_args()
@@ -34,6 +36,8 @@ def main():
     import torch
 
     import tensorflow_distributed_learning_amd as tdl
+
+    torch.backends.cudnn.benchmark = bool(args.conv_search)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1 and "LOCAL_RANK" in os.environ and torch.cuda.device_count() > 0:
