@@ -208,10 +208,17 @@ __global__ __launch_bounds__(256) void k_dense1_bwd(MnistArgs a) {
 //   Wd   [9][16][16][4] W2 for this part's 16 input channels in MFMA fragment order
 // Work of a part: conv2 wgrad for output channels [16p, 16p+16) over the image's 100 positions
 // (19 tiles incl. the bias row, 25 k-steps each) + conv2 dgrad for channel half h = p & 1 and
-// pixel half p >> 1 (6 tiles, 144 k-steps each) whose epilogue does pool1/relu backward and
-// conv1 wgrad.  Outputs are per-image partial slabs, reduced deterministically by KF.
+// pixel part p >> 1 (pixels [0, 80) or [80, 169), 16-pixel tiles of up to 9 taps x 16 k-steps)
+// whose epilogue does pool1/relu backward and conv1 wgrad.  Kernel rows kh whose taps read only
+// the zero border of dC2 for every pixel of a tile are skipped (exact).  Outputs are per-image
+// partial slabs, reduced deterministically by KF.
 // --------------------------------------------------------------------------------------------
 constexpr int kDcStride = 68, kDcDim = 15, kP1Stride = 36;
+constexpr int kDgSplit = 80;  // pixel split of the dgrad parts: balances their MFMA work after tap skipping
+// conv2 wgrad tiles (first, count) per (pixel part, wave): waves w and w+4 share a SIMD, so each
+// SIMD's wgrad + dgrad MFMAs come to <= 294 (part 0) / 292 (part 1)
+__constant__ int kWgradTiles[2][8][2] = {{{0, 6}, {6, 5}, {11, 6}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {17, 2}},
+                                         {{0, 5}, {5, 5}, {10, 5}, {15, 4}, {0, 0}, {0, 0}, {0, 0}, {0, 0}}};
 constexpr int kLdsDc = kDcDim * kDcDim * kDcStride;   // 15300
 constexpr int kLdsP1 = 169 * kP1Stride;              // 6084
 constexpr int kLdsWd = 9 * 16 * 16 * 4;              // 9216
@@ -281,13 +288,12 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
   __syncthreads();
   stamp(a.stamps, 2);
 
-  // ---- conv2 wgrad (19 row tiles of 25 k-steps, columns 16p + i).  MFMA work per SIMD (waves w
-  // and w+4 share one): wave 0 takes tiles 0..5 + 18 (the bias row), wave 1 tiles 6..11, waves
-  // 2..7 tile 10 + wave next to their 144-step dgrad tile -> at most 344 MFMAs per SIMD. ----
+  // ---- conv2 wgrad (19 row tiles of 25 k-steps, columns 16p + i; tile 18 = the bias row), placed
+  // per wave by kWgradTiles next to the wave's dgrad work ----
   {
-    const int ntiles = wave == 0 ? 7 : (wave == 1 ? 6 : 1);
+    const int t0 = kWgradTiles[half][wave][0], ntiles = kWgradTiles[half][wave][1];
     for (int j = 0; j < ntiles; ++j) {
-      const int mt = wave == 0 ? (j < 6 ? j : 18) : (wave == 1 ? 6 + j : 10 + wave);
+      const int mt = t0 + j;
       const bool bias_tile = mt == 18;
       const int k = mt * 16 + i;
       const int tap = bias_tile ? 0 : k >> 5, ci = k & 31;
@@ -328,13 +334,13 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
   }
 
   stamp(a.stamps, 3);
-  // ---- conv2 dgrad (+ pool1/relu backward + conv1 wgrad): waves 2..7 take tiles 5..0 ----
+  // ---- conv2 dgrad (+ pool1/relu backward + conv1 wgrad): waves 7, 6, ... take tiles 0, 1, ... ----
   float dw[10];
 #pragma unroll
   for (int j = 0; j < 10; ++j) dw[j] = 0.f;
   const int d = 7 - wave;
-  if (d < 6) {
-    const int pix0 = half * 85, pix1 = half ? 169 : 85;
+  const int pix0 = half ? kDgSplit : 0, pix1 = half ? 169 : kDgSplit;
+  if (d < (pix1 - pix0 + 15) / 16) {
     const int P = pix0 + d * 16 + i;
     const bool valid = P < pix1;
     const int Pc = valid ? P : pix0;
@@ -348,19 +354,24 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
       const int Pr = min(pix0 + d * 16 + 4 * g + r, pix1 - 1);
       q1v[r] = a.A1[((size_t)bi * 169 + Pr) * 32 + c];
     }
+    // kernel rows kh with 0 <= ih - kh <= 9 for some pixel row ih of the tile (wave-uniform)
+    const int ih_lo = (pix0 + d * 16) / 13, ih_hi = min(pix0 + d * 16 + 15, pix1 - 1) / 13;
+    const int kh_lo = max(0, ih_lo - 9), kh_hi = min(2, ih_hi);
     f4 acc0 = zero4(), acc1 = zero4();
+    for (int kh = kh_lo; kh <= kh_hi; ++kh) {
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int kh = tap / 3, kw = tap - kh * 3;
-      const float* ap = dCs + ((ih - kh + 2) * kDcDim + (iw - kw + 2)) * kDcStride + 4 * g;
+      for (int kw = 0; kw < 3; ++kw) {
+        const int tap = kh * 3 + kw;
+        const float* ap = dCs + ((ih - kh + 2) * kDcDim + (iw - kw + 2)) * kDcStride + 4 * g;
 #pragma unroll
-      for (int c0 = 0; c0 < 64; c0 += 16) {
-        const f4 av = ld4(ap + c0);
-        const f4 bv = ld4(wb + (tap * 16 + c0 / 4) * 64);
-        acc0 = mfma16x16x4(av.x, bv.x, acc0);
-        acc1 = mfma16x16x4(av.y, bv.y, acc1);
-        acc0 = mfma16x16x4(av.z, bv.z, acc0);
-        acc1 = mfma16x16x4(av.w, bv.w, acc1);
+        for (int c0 = 0; c0 < 64; c0 += 16) {
+          const f4 av = ld4(ap + c0);
+          const f4 bv = ld4(wb + (tap * 16 + c0 / 4) * 64);
+          acc0 = mfma16x16x4(av.x, bv.x, acc0);
+          acc1 = mfma16x16x4(av.y, bv.y, acc1);
+          acc0 = mfma16x16x4(av.z, bv.z, acc0);
+          acc1 = mfma16x16x4(av.w, bv.w, acc1);
+        }
       }
     }
     const f4 acc = acc0 + acc1;
