@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--per-replica-batch", type=int, default=64)
     ap.add_argument("--steps-per-execution", type=int, default=0, help="0 = auto")
+    ap.add_argument("--take", type=int, default=0, help="diagnostics: train on the first N images only")
     args = ap.parse_args()
 
     import torch
@@ -64,7 +65,8 @@ def main():
         image = image / 255
         return image, label
 
-    train = ds_all["train"].map(scale).cache().shuffle(10000).batch(B).repeat()
+    src = ds_all["train"].take(args.take) if args.take else ds_all["train"]
+    train = src.map(scale).cache().shuffle(10000).batch(B).repeat()
     options = tdl.data.Options()
     options.experimental_distribute.auto_shard_policy = tdl.data.AutoShardPolicy.OFF
     train = train.with_options(options)
@@ -101,6 +103,13 @@ def main():
     dt = float(t.item())
     logs = trainer.logs()
     ips = K * B / dt
+    ht = getattr(trainer, "_host_times", None)
+    if ht:
+        import numpy as np
+
+        a = np.array(ht[-(K // max(1, spe)):]) * 1e6
+        print(f"host us per execution (take, upload, launch): median {np.median(a, 0).round(1).tolist()} "
+              f"max {a.max(0).round(1).tolist()}", file=sys.stderr)
     if rank == 0:
         print(json.dumps({
             "metric": "images/sec (whole node) MNIST CNN global_batch=64*N",

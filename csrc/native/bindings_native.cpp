@@ -60,23 +60,30 @@ uint32_t crc32c(const std::string& data, uint32_t crc) {
 
 // tf.data's buffered shuffle on an index sequence (data/dataset.py _shuffle_indices): keep a
 // window of `buffer_size` pending elements, emit slot r[k] mod |window|, refill that slot from the
-// source, or once the source is drained move the last pending element into it.  The random
-// stream r is drawn by the caller so the native and Python paths give the same order.
-at::Tensor buffered_shuffle(const at::Tensor& src, int64_t buffer_size, const at::Tensor& r) {
+// source, or once the source is drained move the last pending element into it.  r[k] is the k-th
+// output of splitmix64 seeded with `seed` (>> 2, i.e. 62 bits); the whole epoch runs without the
+// GIL so an input pipeline's producer thread never stalls the launch loop.
+static inline uint64_t splitmix64(uint64_t& state) {
+  uint64_t z = (state += 0x9E3779B97F4A7C15ULL);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+at::Tensor buffered_shuffle(const at::Tensor& src, int64_t buffer_size, uint64_t seed) {
   TORCH_CHECK(!src.is_cuda() && src.scalar_type() == at::kLong && src.is_contiguous(), "src: int64 CPU");
-  TORCH_CHECK(!r.is_cuda() && r.scalar_type() == at::kLong && r.numel() == src.numel(), "r: int64 CPU, |src|");
   TORCH_CHECK(buffer_size > 0, "buffer_size must be > 0");
   const int64_t n = src.numel();
   const int64_t* s = src.data_ptr<int64_t>();
-  const int64_t* rv = r.data_ptr<int64_t>();
   at::Tensor out = at::empty({n}, src.options());
   int64_t* o = out.data_ptr<int64_t>();
   const int64_t w0 = std::min(buffer_size, n);
   std::vector<int64_t> buf(s, s + w0);
   int64_t nxt = w0;
+  uint64_t state = seed;
   for (int64_t k = 0; k < n; ++k) {
     const int64_t len = (int64_t)buf.size();
-    const int64_t j = rv[k] % len;
+    const int64_t j = (int64_t)((splitmix64(state) >> 2) % (uint64_t)len);
     o[k] = buf[j];
     if (nxt < n) {
       buf[j] = s[nxt++];
@@ -178,7 +185,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("barrier", &tdl::RingComm::barrier, py::call_guard<py::gil_scoped_release>())
       .def("close", &tdl::RingComm::close);
 
-  m.def("buffered_shuffle", &buffered_shuffle, py::arg("src"), py::arg("buffer_size"), py::arg("r"));
+  m.def("buffered_shuffle", &buffered_shuffle, py::arg("src"), py::arg("buffer_size"), py::arg("seed"),
+        py::call_guard<py::gil_scoped_release>());
   m.def("crc32c", [](py::bytes data, uint32_t crc) { return crc32c(std::string(data), crc); }, py::arg("data"),
         py::arg("crc") = 0u);
 }

@@ -592,17 +592,31 @@ class CacheDataset(Dataset):
             yield from self._cache
 
 
+_MASK64 = (1 << 64) - 1
+
+
+def _splitmix64_stream(seed: int, n: int) -> np.ndarray:
+    """The 62-bit random stream r[k] of the buffered shuffle: splitmix64(seed) outputs >> 2."""
+    with np.errstate(over="ignore"):
+        k = np.arange(1, n + 1, dtype=np.uint64)
+        z = np.uint64(seed) + k * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return (z >> np.uint64(2)).astype(np.int64)
+
+
 def _shuffle_indices(n: int, buffer_size: int, rng: np.random.Generator, source_order=None) -> np.ndarray:
-    """TF's buffered shuffle on indices: fill a buffer, emit a random slot, refill it."""
+    """TF's buffered shuffle on indices: fill a buffer, emit a random slot, refill it.  One 64-bit
+    seed is drawn from ``rng``; the per-element random stream is splitmix64 of that seed, so the
+    native implementation (csrc/native, GIL released) and the Python one give the same order."""
     src = np.arange(n) if source_order is None else np.asarray(source_order)
-    if buffer_size >= n:
-        return src[rng.permutation(n)]
-    r = rng.integers(0, 1 << 62, size=n)
+    seed = int(rng.integers(0, 1 << 63))
     N = _native_or_none()
     if N is not None:
         return N.buffered_shuffle(torch.from_numpy(np.ascontiguousarray(src, dtype=np.int64)), int(buffer_size),
-                                  torch.from_numpy(r)).numpy()
-    return _shuffle_indices_py(src, n, buffer_size, r)
+                                  seed).numpy()
+    return _shuffle_indices_py(src, n, buffer_size, _splitmix64_stream(seed, n))
 
 
 def _native_or_none():
@@ -617,7 +631,7 @@ def _native_or_none():
 def _shuffle_indices_py(src, n, buffer_size, r):
     out = np.empty(n, dtype=np.int64)
     buf = list(src[:buffer_size])
-    nxt = buffer_size
+    nxt = min(buffer_size, n)
     for k in range(n):
         j = int(r[k] % len(buf))
         out[k] = buf[j]
@@ -644,17 +658,25 @@ class ShuffleDataset(Dataset):
     def cardinality(self):
         return self._inputs[0].cardinality()
 
-    def _rng(self):
+    def _rng_at(self, epoch: int, seed_override: Optional[int] = None):
+        """The shuffle RNG of iteration ``epoch`` (pure: no counter advances).  ``seed_override``
+        stands in for an unset ``seed`` (synchronised DATA sharding, parallel/input_lib.reseed)."""
         seed = _seed_state.override if _seed_state.override is not None else self.seed
+        if seed is None:
+            seed = seed_override
         if seed is None and _global_seed is not None:
             seed = _global_seed
         if seed is None:
             if self._base is None:
                 self._base = int(np.random.SeedSequence().entropy % (1 << 63))
             seed = self._base
-        ep = self._epoch if self.reshuffle else 0
-        self._epoch += 1
+        ep = epoch if self.reshuffle else 0
         return np.random.default_rng([int(seed) & ((1 << 63) - 1), ep])
+
+    def _rng(self):
+        r = self._rng_at(self._epoch)
+        self._epoch += 1
+        return r
 
     def _columns(self):
         return self._inputs[0]._columns()

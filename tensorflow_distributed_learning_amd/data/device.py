@@ -80,7 +80,14 @@ def lower(ds: D.Dataset) -> Optional[LoweredPipeline]:
 
 
 class IndexStream:
-    """Global-batch sample indices of a lowered pipeline, epoch after epoch."""
+    """Global-batch sample indices of a lowered pipeline, epoch after epoch.
+
+    Epoch ``e`` of the stream shuffles with the dataset's RNG of iteration ``ep0 + e``, ``ep0``
+    being the dataset's iteration counter when the stream was created (so a stream reproduces the
+    host pipeline's order); the stream never mutates the dataset, which makes it safe to run ahead
+    in a producer thread.  :meth:`commit` advances the dataset's counter by the epochs a consumer
+    actually used.
+    """
 
     def __init__(self, lp: LoweredPipeline, seed: Optional[int] = None):
         self.lp = lp
@@ -89,24 +96,27 @@ class IndexStream:
         self._done = False
         self._seed = seed
         self._shuffle_seed_base = None
+        self._ep0 = lp.shuffle._epoch if lp.shuffle is not None else 0
+
+    def commit(self, epochs_used: int) -> None:
+        sh = self.lp.shuffle
+        if sh is not None:
+            sh._epoch = max(sh._epoch, self._ep0 + int(epochs_used))
 
     def _epoch_order(self) -> Optional[np.ndarray]:
         lp = self.lp
         if lp.repeat is not None and self._epoch >= lp.repeat:
             return None
+        e = self._epoch
         self._epoch += 1
         if lp.shuffle is None:
             return np.arange(lp.n, dtype=np.int64)
         sh = lp.shuffle
+        override = None
         if self._seed is not None and sh.seed is None:
             # synchronised (DATA) sharding: same derivation as input_lib.reseed
-            saved = sh.seed
-            sh.seed = (int(self._seed) * 1_000_003 + 1) & ((1 << 62) - 1)
-            rng = sh._rng()
-            sh.seed = saved
-        else:
-            rng = sh._rng()
-        return D._shuffle_indices(lp.n, sh.buffer_size, rng)
+            override = (int(self._seed) * 1_000_003 + 1) & ((1 << 62) - 1)
+        return D._shuffle_indices(lp.n, sh.buffer_size, sh._rng_at(self._ep0 + e, override))
 
     def next_batch(self) -> Optional[np.ndarray]:
         """Indices of the next global batch (may be short at the very end), or None."""

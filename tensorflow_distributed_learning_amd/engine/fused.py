@@ -19,6 +19,9 @@ across replicas only when logs are read.
 from __future__ import annotations
 
 import os
+import queue
+import threading
+import time
 from typing import Dict, Optional
 
 import numpy as np
@@ -117,6 +120,12 @@ class FusedMnistTrainer:
         self._capture_comm = None
         self._comm_stream = None
         self.overlap = os.environ.get("TDL_OVERLAP_ALLREDUCE", "1") == "1"
+        # index-upload slots (one captured graph each): the host may run this many executions ahead
+        # of the GPU, which absorbs host hiccups such as an epoch's shuffle (~ms) without starving it
+        self._nslots = max(2, int(os.environ.get("TDL_INDEX_SLOTS", "4")))
+        self._ragged_bufs, self._ragged_stage, self._ragged_ev = {}, None, None
+        # diagnostics: host seconds per execution (index take, upload, graph launch)
+        self._host_times = [] if os.environ.get("TDL_HOST_TIMING") == "1" else None
 
     @property
     def capture_comm(self) -> bool:
@@ -221,14 +230,28 @@ class FusedMnistTrainer:
                 self.comm.all_reduce(self.G, "sum")
             self.optimizer.apply_flat(self.W, self.G)
             return
-        idx_buf = torch.from_numpy(idx_np.astype(np.int32)).to(self.device)
+        # one persistent index buffer per ragged size (the step object is cached by its address),
+        # filled through a pinned staging buffer without a host sync
+        key = ("ragged", b)
+        idx_buf = self._ragged_bufs.get(key)
+        if idx_buf is None:
+            idx_buf = torch.zeros(b, dtype=torch.int32, device=self.device)
+            self._ragged_bufs[key] = idx_buf
+        if self._ragged_ev is not None:
+            self._ragged_ev.synchronize()
+        if self._ragged_stage is None or self._ragged_stage.numel() < b:
+            self._ragged_stage = torch.empty(max(b, 256), dtype=torch.int32, pin_memory=True)
+        self._ragged_stage[:b].numpy()[:] = idx_np
+        idx_buf.copy_(self._ragged_stage[:b], non_blocking=True)
+        self._ragged_ev = torch.cuda.Event()
+        self._ragged_ev.record(torch.cuda.current_stream(self.device))
         st = self._step(b, idx_buf, global_b)
         self._train_step(st, 0, global_b)
         self.optimizer.iterations += 1
 
     def _graph_for(self, K: int, b: int, slot: int = 0):
-        """Graph of one K-step execution reading its sample ids from its own index buffer; two
-        slots alternate so the host uploads execution i+1's indices while execution i runs."""
+        """Graph of one K-step execution reading its sample ids from its own index buffer; the
+        slots rotate so the host uploads execution i+1's indices while execution i runs."""
         g = self._graphs.get((K, b, slot))
         if g is not None:
             return g
@@ -277,7 +300,7 @@ class FusedMnistTrainer:
         if steps % self.K:
             sizes.add(steps % self.K)
         for K in sizes:
-            for slot in (0, 1):
+            for slot in range(self._nslots):
                 self._graph_for(K, b, slot)
 
     def _upload(self, idx: np.ndarray, idx_buf: torch.Tensor, slot: int):
@@ -300,9 +323,11 @@ class FusedMnistTrainer:
         b = handler.b
         opt = self.optimizer
         if not hasattr(self, "_stage"):
-            self._stage, self._stage_ev, self._slot = [None, None], [None, None], 0
+            self._stage, self._stage_ev, self._slot = [None] * self._nslots, [None] * self._nslots, 0
+        timing = self._host_times is not None
         while done < steps:
             K = min(self.K, steps - done)
+            t0 = time.perf_counter() if timing else 0.0
             idx = handler.take(K)
             if idx is None:
                 # ragged tail (end of finite data) -> eager steps of their own sizes
@@ -315,9 +340,11 @@ class FusedMnistTrainer:
                 continue
             opt._sync_lr()
             slot = self._slot
-            self._slot ^= 1
+            self._slot = (slot + 1) % self._nslots
             graph, idx_buf, st = self._graph_for(K, b, slot)
+            t1 = time.perf_counter() if timing else 0.0
             self._upload(idx, idx_buf, slot)
+            t2 = time.perf_counter() if timing else 0.0
             if isinstance(graph, list):
                 for gk in graph:
                     gk.replay()
@@ -327,6 +354,8 @@ class FusedMnistTrainer:
             else:
                 for k in range(K):
                     self._train_step(st, k * b, b * self.R)
+            if timing:
+                self._host_times.append((t1 - t0, t2 - t1, time.perf_counter() - t2))
             opt.iterations += K
             done += K
         return done
@@ -360,6 +389,50 @@ class FusedMnistTrainer:
         torch.cuda.synchronize(self.device)
 
 
+class _IndexProducer:
+    """Background thread producing the global-batch index arrays of an IndexStream into a bounded
+    queue, so an epoch's shuffle (native, GIL released) never stalls the launch loop."""
+
+    def __init__(self, stream: "DD.IndexStream", depth: int = 512):
+        self.stream = stream
+        self.q: "queue.Queue" = queue.Queue(maxsize=depth)
+        self._stop = threading.Event()
+        self._ended = False
+        self.t = threading.Thread(target=self._run, name="tdl-index-producer", daemon=True)
+        self.t.start()
+
+    def _run(self):
+        while not self._stop.is_set():
+            g = self.stream.next_batch()
+            item = (g, self.stream._epoch)  # epochs the stream had to generate to produce g
+            while not self._stop.is_set():
+                try:
+                    self.q.put(item, timeout=0.1)
+                    break
+                except queue.Full:
+                    continue
+            if g is None:
+                return
+
+    def get(self):
+        """(batch or None at the end, epochs generated up to it)."""
+        if self._ended:
+            return None, None
+        g, ep = self.q.get()
+        if g is None:
+            self._ended = True
+        return g, ep
+
+    def close(self):
+        self._stop.set()
+        while True:
+            try:
+                self.q.get_nowait()
+            except queue.Empty:
+                break
+        self.t.join(timeout=5)
+
+
 class DeviceHandler:
     """Index vectors for this replica: its slice of every global batch."""
 
@@ -370,15 +443,41 @@ class DeviceHandler:
         self.b = lp.batch_size // R
         self.stream = DD.IndexStream(lp, seed)
         self._pending = []
+        self._async = os.environ.get("TDL_ASYNC_INDICES", "1") == "1"
+        self._producer: Optional[_IndexProducer] = None
+        self._epochs_used = 0
 
     def new_iterator(self):
+        self.close()
         self.stream = DD.IndexStream(self.lp, self.stream._seed)
         self._pending = []
+        self._epochs_used = 0
+
+    def close(self):
+        if self._producer is not None:
+            self._producer.close()
+            self._producer = None
+        self.stream.commit(self._epochs_used)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     def _next_global(self):
         if self._pending:
             return self._pending.pop(0)
-        return self.stream.next_batch()
+        if not self._async:
+            g = self.stream.next_batch()
+            self._epochs_used = self.stream._epoch
+            return g
+        if self._producer is None:
+            self._producer = _IndexProducer(self.stream)
+        g, ep = self._producer.get()
+        if ep is not None:
+            self._epochs_used = ep
+        return g
 
     def take(self, K: int) -> Optional[np.ndarray]:
         """K full global batches -> this replica's [K*b] indices (None if fewer remain)."""

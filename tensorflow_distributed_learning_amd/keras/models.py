@@ -410,6 +410,8 @@ class Model(Layer):
             if self.stop_training:
                 break
         trainer.finish()
+        if hasattr(handler, "close"):  # stop an index producer, commit the epochs it consumed
+            handler.close()
         cb_list.on_train_end(logs)
         self.history = history
         return history

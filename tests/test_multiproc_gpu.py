@@ -27,7 +27,7 @@ ds = ds.map(lambda i, l: (i.to(torch.float32) / 255, l)).cache().shuffle(2048, s
 with strategy.scope():
     m = build_mnist_cnn()
     m.compile(loss=tdl.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
-              optimizer=tdl.keras.optimizers.SGD(0.1), metrics=["sparse_categorical_accuracy"],
+              optimizer=tdl.keras.optimizers.SGD(0.01), metrics=["sparse_categorical_accuracy"],
               steps_per_execution=4)
 h = m.fit(ds, epochs=2, steps_per_epoch=8, verbose=0)
 w = np.concatenate([v.ravel() for v in m.get_weights()])
@@ -56,5 +56,6 @@ def test_fused_two_replicas_match_single(tmp_path):
     assert r1["engine"] == a["engine"] == "fused" and a["comm"] == "ring"
     w0, w1, ws = (np.load(tmp_path / f) for f in ("w0_2.npy", "w1_2.npy", "w0_1.npy"))
     assert np.array_equal(w0, w1)
+    # lr 0.01: R=2 vs R=1 differ only by fp32 summation order (at lr 0.1 ReLU flips amplify it)
     np.testing.assert_allclose(w0, ws, rtol=1e-3, atol=1e-5)
     np.testing.assert_allclose(a["loss"], r1["loss"], rtol=1e-4)

@@ -96,10 +96,7 @@ def test_slab_layout_aligned_disjoint(shapes, align):
 def test_native_buffered_shuffle_matches_python(n, buf, seed):
     src = np.arange(n)
     a = D._shuffle_indices(n, buf, np.random.default_rng(seed))
-    r = np.random.default_rng(seed)
-    if buf >= n:
-        b = src[r.permutation(n)]
-    else:
-        b = D._shuffle_indices_py(src, n, buf, r.integers(0, 1 << 62, size=n))
+    s64 = int(np.random.default_rng(seed).integers(0, 1 << 63))
+    b = D._shuffle_indices_py(src, n, buf, D._splitmix64_stream(s64, n))
     assert np.array_equal(a, b)
     assert sorted(a.tolist()) == list(range(n))
