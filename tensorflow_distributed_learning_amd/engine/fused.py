@@ -313,7 +313,7 @@ class FusedMnistTrainer:
         else:
             self._stage_ev[slot].synchronize()  # the previous copy out of this buffer has run
         stage[:n].numpy()[:] = idx
-        idx_buf.copy_(stage[:n], non_blocking=True)
+        idx_buf[:n].copy_(stage[:n], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.device))
         self._stage_ev[slot] = ev
@@ -345,7 +345,14 @@ class FusedMnistTrainer:
             t1 = time.perf_counter() if timing else 0.0
             self._upload(idx, idx_buf, slot)
             t2 = time.perf_counter() if timing else 0.0
-            if isinstance(graph, list):
+            Kr = idx.size // b
+            if Kr < K:
+                # the full batches in front of an epoch's partial batch: same slot buffers and
+                # step object, launched eagerly (no per-step host sync, no new graph size)
+                for k in range(Kr):
+                    self._train_step(st, k * b, b * self.R)
+                K = Kr
+            elif isinstance(graph, list):
                 for gk in graph:
                     gk.replay()
                     self._reduce_and_update()
@@ -480,16 +487,19 @@ class DeviceHandler:
         return g
 
     def take(self, K: int) -> Optional[np.ndarray]:
-        """K full global batches -> this replica's [K*b] indices (None if fewer remain)."""
+        """Up to K full global batches -> this replica's [K'*b] indices.  Stops early in front of
+        a partial batch (the epoch's remainder, left pending for ``next_ragged``) or the end of
+        finite data; None when the next batch is not a full one."""
         got = []
         for _ in range(K):
             g = self._next_global()
             if g is None or len(g) < self.B:
                 if g is not None:
                     self._pending.insert(0, g)
-                self._pending = got + self._pending
-                return None
+                break
             got.append(g)
+        if not got:
+            return None
         return np.concatenate([g[self.rank * self.b:(self.rank + 1) * self.b] for g in got])
 
     def next_ragged(self):
