@@ -127,6 +127,7 @@ def main():
             "config": {"model": "tf_dist_example.py MNIST CNN (Conv32-Pool-Conv64-Pool-Dense128-Dense10, 225,034 params)",
                        "global_batch": B, "seq_len": None, "image_shape": [28, 28, 1],
                        "parallelism": f"dp{R}", "engine": trainer.kind, "communicator": comm.name,
+                       "allreduce": getattr(comm, "algorithm", comm.name),
                        "steps_per_execution": spe, "graph_captured": bool(trainer.capture),
                        "allreduce_in_graph": bool(trainer.capture_comm and R > 1),
                        "final_loss": round(logs["loss"], 4)},

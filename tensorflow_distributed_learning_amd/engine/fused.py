@@ -183,9 +183,11 @@ class FusedMnistTrainer:
 
     def _train_step(self, st, off: int, global_b: int):
         """One whole step on the current stream.  With R > 1 the gradient all-reduce runs as two
-        buckets on a side stream: the dense-layer bucket (G[dense_offset:], 91% of the bytes) is
-        final after forward_dense() and reduces while the conv backward runs; the conv bucket
-        follows finalize(); the optimizer waits for both."""
+        buckets: the dense-layer bucket (G[dense_offset:], 91% of the bytes) is final after
+        forward_dense() and reduces on a side stream while the conv backward runs; the conv bucket
+        follows finalize().  With the xGMI one-shot communicator each bucket's all-reduce also
+        applies plain SGD to its own parameter range (W[dense_offset:] is not read again in the
+        step), so no separate optimizer kernel runs; otherwise the optimizer waits for both."""
         if self.R == 1 or not self.overlap:
             st.forward_backward(off)
             self._apply(st, global_b)
@@ -195,27 +197,47 @@ class FusedMnistTrainer:
             self._comm_stream = torch.cuda.Stream(self.device)
         cs = self._comm_stream
         d0 = st.dense_offset
+        G, W = self.G, self.W
+        fuse = self.optimizer.momentum == 0
+        lr = self.optimizer.lr_dev
         st.forward_dense(off)
         cs.wait_stream(main)
         with torch.cuda.stream(cs):
-            self.comm.all_reduce(self.G[d0:], "sum")
+            dense_fused = fuse and self.comm.all_reduce_sgd(G[d0:], W[d0:], lr)
+            if not dense_fused:
+                self.comm.all_reduce(G[d0:], "sum")
         st.backward_conv()
         st.finalize(False)
+        if dense_fused and self.comm.all_reduce_sgd(G[:d0], W[:d0], lr):
+            main.wait_stream(cs)
+            return
         cs.wait_stream(main)
         with torch.cuda.stream(cs):
-            self.comm.all_reduce(self.G[:d0], "sum")
+            self.comm.all_reduce(G[:d0], "sum")
         main.wait_stream(cs)
-        self._update()
+        if dense_fused:
+            self._update(0, d0)
+        else:
+            self._update()
 
-    def _update(self):
+    def _prepare_comm(self, d0: int):
+        """Collective set-up of the communicator's all-reduce channels for this step's buckets
+        (must precede any graph capture; every rank reaches it at the same point)."""
+        if self.R > 1 and not getattr(self, "_comm_prepared", False):
+            n = self.W.numel()
+            self.comm.prepare_all_reduce(n - d0, d0, n)
+            self._comm_prepared = True
+
+    def _update(self, lo: int = 0, hi: Optional[int] = None):
         from .. import ops
 
         opt = self.optimizer
         C = ops.hip()
+        W, G = self.W[lo:hi], self.G[lo:hi]
         if opt.momentum == 0:
-            C.sgd(self.W, self.G, opt.lr_dev)
+            C.sgd(W, G, opt.lr_dev)
         else:
-            C.sgd_momentum(self.W, self.G, opt._slots["momentum"], opt.lr_dev, opt.momentum, opt.nesterov)
+            C.sgd_momentum(W, G, opt._slots["momentum"][lo:hi], opt.lr_dev, opt.momentum, opt.nesterov)
 
     def _reduce_and_update(self):
         if self.R > 1:
@@ -246,6 +268,7 @@ class FusedMnistTrainer:
         self._ragged_ev = torch.cuda.Event()
         self._ragged_ev.record(torch.cuda.current_stream(self.device))
         st = self._step(b, idx_buf, global_b)
+        self._prepare_comm(st.dense_offset)
         self._train_step(st, 0, global_b)
         self.optimizer.iterations += 1
 
@@ -257,6 +280,7 @@ class FusedMnistTrainer:
             return g
         idx_buf = torch.zeros(K * b, dtype=torch.int32, device=self.device)
         st = self._step(b, idx_buf)
+        self._prepare_comm(st.dense_offset)
         graph = None
         if self.capture:
             s = torch.cuda.Stream(self.device)
@@ -376,6 +400,7 @@ class FusedMnistTrainer:
     def logs(self) -> Dict[str, float]:
         t = self.metrics_dev.clone()
         if self.R > 1:
+            self.comm.check_health()
             self.comm.all_reduce(t, "sum")
         loss_sum, correct, count = (float(v) for v in t[:3].cpu())
         out = {"loss": loss_sum / max(count, 1.0)}

@@ -58,6 +58,17 @@ class Communicator:
         """True when this communicator's collectives can be recorded into a hipGraph."""
         return self.capturable
 
+    def check_health(self) -> None:
+        """Raise if an asynchronous collective failed (host sync; called when logs are read)."""
+
+    def prepare_all_reduce(self, *numels: int) -> None:
+        """Collective set-up for all-reduces of these sizes (before any graph capture)."""
+
+    def all_reduce_sgd(self, g: torch.Tensor, w: torch.Tensor, lr: torch.Tensor) -> bool:
+        """``w -= lr * all_reduce_sum(g)`` as one fused operation when the communicator has one
+        (returns False otherwise; the caller then all-reduces and applies SGD itself)."""
+        return False
+
     def shutdown(self) -> None:
         pass
 
@@ -128,8 +139,41 @@ class TorchCommunicator(Communicator):
                                         timeout=timedelta(seconds=timeout), **kw)
             self._owns_group = True
         self._avg_native = backend == "nccl"
+        self.xgmi = None  # parallel/xgmi.py one-shot path for small f32 messages (single node)
+        self.algorithm = "ring" if backend == "gloo" else "rccl"
+
+    def enable_xgmi(self) -> bool:
+        """Route small f32 sum/mean all-reduces through the xGMI one-shot kernel when every rank
+        is on this node (collective; the self-test runs on the first prepared channel).  Over a
+        gloo group (replica processes sharing one GPU, where RCCL cannot run) the kernel is the
+        only device data plane; gloo carries the control messages."""
+        from . import xgmi
+
+        if self.device.type != "cuda" or self.world_size > 8 or not xgmi.enabled_by_env():
+            return False
+        if not xgmi.single_node():
+            return False
+        ctrl = self.device if self.backend == "nccl" else torch.device("cpu")
+        self.xgmi = xgmi.XgmiAllReduce(self.rank, self.world_size, self.device, ctrl_device=ctrl)
+        return True
+
+    def prepare_all_reduce(self, *numels):
+        if self.xgmi is not None:
+            if self.xgmi.prepare(*numels):
+                self.algorithm = "xgmi-oneshot+" + ("rccl" if self.backend == "nccl" else self.backend)
+            else:
+                self.xgmi = None
+
+    def all_reduce_sgd(self, g, w, lr):
+        return self.xgmi is not None and self.xgmi.all_reduce_sgd(g, w, lr)
+
+    def check_health(self):
+        if self.xgmi is not None:
+            self.xgmi.check()
 
     def all_reduce(self, t, op="sum"):
+        if self.xgmi is not None and self.xgmi.all_reduce(t, op):
+            return t
         if op == "mean":
             if self._avg_native:
                 dist.all_reduce(t, op=dist.ReduceOp.AVG)
@@ -171,6 +215,10 @@ class TorchCommunicator(Communicator):
         """
         if getattr(self, "_capture_ok", None) is not None:
             return self._capture_ok
+        if self.backend != "nccl" and self.xgmi is not None:
+            # gloo control plane: the device collectives are the (capturable) xGMI kernels
+            self._capture_ok = bool(self.xgmi._ensure_tested())
+            return self._capture_ok
         if not self.capturable or self.device.type != "cuda":
             self._capture_ok = False
             return False
@@ -203,6 +251,13 @@ class TorchCommunicator(Communicator):
         return ok
 
     def shutdown(self):
+        if self.xgmi is not None:
+            try:
+                self.barrier()  # no peer may still be reading our exchange buffers
+            except Exception:
+                pass
+            self.xgmi.close()
+            self.xgmi = None
         if self._owns_group and dist.is_initialized():
             try:
                 dist.destroy_process_group()

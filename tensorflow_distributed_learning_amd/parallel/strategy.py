@@ -342,7 +342,21 @@ def _select_communicator(impl: CommunicationImplementation, device: torch.device
 
         return TorchCommunicator("gloo", rank, world, device, store=None if dist.is_initialized() else store,
                                  timeout=timeout)
-    return TorchCommunicator("nccl", rank, world, device, store=store, timeout=timeout)
+    if impl == CommunicationImplementation.AUTO and os.environ.get("TDL_SHARE_GPU") == "1":
+        # replica processes sharing one GPU: RCCL refuses duplicate devices; gloo control plane +
+        # the xGMI kernel over IPC-mapped buffers of the same device
+        import torch.distributed as dist
+
+        if store is None and not dist.is_initialized():
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        comm = TorchCommunicator("gloo", rank, world, device, store=None if dist.is_initialized() else store,
+                                 timeout=timeout)
+        comm.enable_xgmi()
+        return comm
+    comm = TorchCommunicator("nccl", rank, world, device, store=store, timeout=timeout)
+    if impl != CommunicationImplementation.NCCL:  # AUTO: topology/size-aware algorithm choice
+        comm.enable_xgmi()
+    return comm
 
 
 def _PGStore():

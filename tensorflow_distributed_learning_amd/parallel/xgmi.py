@@ -1,0 +1,196 @@
+"""One-shot xGMI all-reduce for small messages (SURVEY.md §2.8 "algorithm selection", §5 comm row).
+
+RCCL's ring all-reduce of a sub-MiB message pays 2(R-1) dependent hops over one xGMI link per hop.
+On one MI355X node every GPU has a direct link to every other GPU, so for messages up to a few MiB
+each rank pulls every peer's slice in ONE hop and reduces it locally
+(``csrc/kernels/xgmi.hip``); the SGD update can ride in the same kernel.  TF's ``AUTO``
+collective selection by "hardware, network topology, tensor size" (README.md:21) is this choice:
+xGMI one-shot below ``TDL_XGMI_MAX_BYTES`` (default 4 MiB) on a single node, RCCL otherwise.
+
+Exchange buffers are exported with HIP IPC and opened by every peer (one channel per message size;
+channel set-up is collective, so it happens outside graph capture: :meth:`XgmiAllReduce.prepare`).
+A self-test against an all-gather reference runs when the first channel is made; if any rank
+fails it (or cannot map its peers), every rank falls back to RCCL.  Waits inside the kernel are
+bounded (``TDL_XGMI_TIMEOUT`` seconds): a peer that never arrives raises an error on the host at
+the next :meth:`check` instead of hanging the GPU.
+"""
+from __future__ import annotations
+
+import os
+import socket
+import warnings
+from typing import Dict, Optional
+
+import torch
+import torch.distributed as dist
+
+BLOCK = 1024  # f32 elements per workgroup (kXgmiBlockElems)
+
+
+def enabled_by_env() -> bool:
+    return os.environ.get("TDL_XGMI", "1") == "1"
+
+
+def max_bytes() -> int:
+    return int(os.environ.get("TDL_XGMI_MAX_BYTES", str(4 << 20)))
+
+
+class XgmiAllReduce:
+    """Channel manager of one process group (every rank on this node, one GPU each)."""
+
+    def __init__(self, rank: int, world: int, device: torch.device, group=None, ctrl_device=None):
+        from .. import ops
+
+        self.C = ops.hip()
+        self.rank, self.world, self.device, self.group = rank, world, torch.device(device), group
+        # device of the small control collectives (the process group's own: cpu for gloo)
+        self.ctrl = torch.device(ctrl_device) if ctrl_device is not None else self.device
+        self.timeout = float(os.environ.get("TDL_XGMI_TIMEOUT", "600"))
+        self.limit = max_bytes() // 4
+        self._chans: Dict[int, object] = {}
+        self.ok: Optional[bool] = None  # None = not yet tested
+        self.reason = ""
+
+    # ------------------------------------------------------------------ set-up (collective)
+    def _make(self, numel: int):
+        cap = ((numel + BLOCK - 1) // BLOCK) * BLOCK
+        ch = self.C.XgmiChannel(self.rank, self.world, cap, self.device.index or 0, self.timeout)
+        mine = (bytes(ch.handle(False)), bytes(ch.handle(True)))
+        allh = [None] * self.world
+        dist.all_gather_object(allh, mine, group=self.group)
+        err = ""
+        try:
+            ch.open([h[0] for h in allh], [h[1] for h in allh])
+        except Exception as e:  # noqa: BLE001 - reported collectively below
+            err = f"{type(e).__name__}: {e}"
+        if not self._agree(not err):
+            raise RuntimeError(f"xgmi: peer buffers could not be mapped on every rank ({err or 'another rank failed'})")
+        return ch
+
+    def _agree(self, ok: bool) -> bool:
+        f = torch.tensor([1.0 if ok else 0.0], device=self.ctrl)
+        dist.all_reduce(f, op=dist.ReduceOp.MIN, group=self.group)
+        return bool(f.item() > 0.5)
+
+    def prepare(self, *numels: int) -> bool:
+        """Create (collectively) the channels for these message sizes; False if disabled."""
+        if not self._ensure_tested():
+            return False
+        for n in numels:
+            n = int(n)
+            if 0 < n <= self.limit and n not in self._chans:
+                self._chans[n] = self._make(n)
+        return True
+
+    def _ensure_tested(self) -> bool:
+        if self.ok is None and torch.cuda.is_current_stream_capturing():
+            return False  # the self-test is collective: never inside a capture (all ranks agree)
+        if self.ok is None:
+            try:
+                self.ok = self._selftest()
+                if not self.ok:
+                    self.reason = "self-test mismatch"
+            except Exception as e:  # noqa: BLE001 - any failure means RCCL
+                self.ok, self.reason = False, f"{type(e).__name__}: {e}"
+            if not self.ok and self.rank == 0:
+                warnings.warn(f"xGMI one-shot all-reduce disabled, using RCCL ({self.reason})")
+        return self.ok
+
+    def _selftest(self) -> bool:
+        """Eager, repeated (both buffer halves), graph-replayed and fused-SGD calls against an
+        exact all-gather reference summed in rank order (bit-identical expected)."""
+        n = 3 * BLOCK + 37
+        ch = self._make(n)
+        dev = self.device
+        g = torch.Generator(device="cpu").manual_seed(1234 + self.rank)
+        ok = True
+
+        def ref(x):
+            parts = [torch.empty(x.numel(), dtype=x.dtype, device=self.ctrl) for _ in range(self.world)]
+            dist.all_gather(parts, x.to(self.ctrl), group=self.group)
+            acc = parts[0].clone()
+            for r in range(1, self.world):
+                acc += parts[r]
+            return acc.to(dev)
+
+        for it in range(3):
+            x = torch.randn(n, generator=g).to(dev)
+            y = torch.empty_like(x)
+            ch.all_reduce(x, y, 1.0)
+            ok &= bool(torch.equal(y, ref(x)))
+        x = torch.randn(n, generator=g).to(dev)
+        want = ref(x)
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        y = torch.zeros_like(x)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=s):
+            ch.all_reduce(x, y, 1.0)
+        torch.cuda.synchronize(dev)
+        for _ in range(3):
+            y.zero_()
+            graph.replay()
+            torch.cuda.synchronize(dev)
+            ok &= bool(torch.equal(y, want))
+        w = torch.randn(n, generator=g).to(dev)
+        w_ref = w - 0.5 * want
+        lr = torch.tensor([0.5], device=dev)
+        ch.all_reduce_sgd(x, w, lr, 1.0)
+        torch.cuda.synchronize(dev)
+        ok &= bool(torch.allclose(w, w_ref, rtol=0, atol=1e-6))
+        ok &= ch.error() == 0
+        ok = self._agree(ok)
+        self._chans[n] = ch
+        return ok
+
+    # ------------------------------------------------------------------ collectives
+    def _channel(self, n: int):
+        ch = self._chans.get(n)
+        if ch is not None or n > self.limit or not self.ok:
+            return ch
+        if torch.cuda.is_current_stream_capturing():
+            return None  # set-up is collective and cannot run inside a capture: RCCL for this one
+        self._chans[n] = self._make(n)
+        return self._chans[n]
+
+    def applicable(self, t: torch.Tensor) -> bool:
+        return (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.data_ptr() % 16 == 0 and
+                0 < t.numel() <= self.limit)
+
+    def all_reduce(self, t: torch.Tensor, op: str) -> bool:
+        """In-place sum/mean of ``t`` on the current stream; False = not handled (use RCCL)."""
+        if op not in ("sum", "mean") or not self.applicable(t) or not self._ensure_tested():
+            return False
+        ch = self._channel(t.numel())
+        if ch is None:
+            return False
+        ch.all_reduce(t, t, 1.0 / self.world if op == "mean" else 1.0)
+        return True
+
+    def all_reduce_sgd(self, g: torch.Tensor, w: torch.Tensor, lr: torch.Tensor) -> bool:
+        """``w -= lr * sum_over_ranks(g)`` in one kernel; False = not handled."""
+        if not (self.applicable(g) and self.applicable(w)) or not self._ensure_tested():
+            return False
+        ch = self._channel(g.numel())
+        if ch is None:
+            return False
+        ch.all_reduce_sgd(g, w, lr, 1.0)
+        return True
+
+    def check(self) -> None:
+        """Raise if any kernel of this rank timed out waiting for a peer (host sync)."""
+        for n, ch in self._chans.items():
+            if ch.error():
+                raise RuntimeError(f"xgmi all-reduce: a peer did not arrive within {self.timeout:.0f} s "
+                                   f"(channel of {n} elements); the job's ranks are out of step or one died")
+
+    def close(self) -> None:
+        self._chans.clear()
+
+
+def single_node(group=None) -> bool:
+    """True when every rank of the (initialised) default group runs on this host."""
+    me = socket.gethostname()
+    names = [None] * dist.get_world_size(group)
+    dist.all_gather_object(names, me, group=group)
+    return all(n == me for n in names)

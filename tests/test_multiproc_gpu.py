@@ -18,7 +18,7 @@ import tensorflow_distributed_learning_amd as tdl
 from tensorflow_distributed_learning_amd.models.mnist_cnn import build_mnist_cnn
 from tensorflow_distributed_learning_amd.data.tfds import synthetic_mnist
 out = sys.argv[1]
-strategy = tdl.distribute.MirroredStrategy(communication="RING")
+strategy = tdl.distribute.MirroredStrategy(communication=os.environ.get("JOB_COMM") or None)
 R = strategy.num_replicas_in_sync
 tdl.keras.utils.set_random_seed(5)
 x, y = synthetic_mnist(2048, 2)
@@ -32,15 +32,17 @@ with strategy.scope():
 h = m.fit(ds, epochs=2, steps_per_epoch=8, verbose=0)
 w = np.concatenate([v.ravel() for v in m.get_weights()])
 np.save(os.path.join(out, f"w{strategy.extended.rank}_{R}.npy"), w)
-json.dump({"loss": h.history["loss"], "engine": m._trainer.kind, "comm": strategy.extended.communicator.name},
+comm = strategy.extended.communicator
+json.dump({"loss": h.history["loss"], "engine": m._trainer.kind, "comm": comm.name,
+           "algorithm": getattr(comm, "algorithm", comm.name), "graph": bool(m._trainer.capture_comm)},
           open(os.path.join(out, f"r{strategy.extended.rank}_{R}.json"), "w"))
 """
 
 
-def _run(tmp_path, n):
+def _run(tmp_path, n, comm="RING"):
     s = tmp_path / "job.py"
     s.write_text(textwrap.dedent(BODY))
-    env = dict(os.environ, PYTHONPATH=ROOT, TDL_SHARE_GPU="1")
+    env = dict(os.environ, PYTHONPATH=ROOT, TDL_SHARE_GPU="1", JOB_COMM=comm)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "TF_CONFIG"):
         env.pop(k, None)
     r = subprocess.run([sys.executable, "-m", "tensorflow_distributed_learning_amd.launch", "--nproc-per-node", str(n),
@@ -59,3 +61,17 @@ def test_fused_two_replicas_match_single(tmp_path):
     # lr 0.01: R=2 vs R=1 differ only by fp32 summation order (at lr 0.1 ReLU flips amplify it)
     np.testing.assert_allclose(w0, ws, rtol=1e-3, atol=1e-5)
     np.testing.assert_allclose(a["loss"], r1["loss"], rtol=1e-4)
+
+
+def test_fused_two_replicas_xgmi_auto(tmp_path):
+    """AUTO on replicas sharing one GPU: gloo control plane + the xGMI one-shot kernels (IPC),
+    all-reduce + SGD fused and captured in the execution graph."""
+    _run(tmp_path, 1, comm="")
+    _run(tmp_path, 2, comm="")
+    a, b = (json.load(open(tmp_path / f"r{i}_2.json")) for i in range(2))
+    assert a["engine"] == "fused" and a["comm"] == "gloo"
+    assert a["algorithm"] == "xgmi-oneshot+gloo" and a["graph"], a
+    w0, w1, ws = (np.load(tmp_path / f) for f in ("w0_2.npy", "w1_2.npy", "w0_1.npy"))
+    assert np.array_equal(w0, w1)
+    np.testing.assert_allclose(w0, ws, rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(a["loss"], json.load(open(tmp_path / "r0_1.json"))["loss"], rtol=2e-3)
