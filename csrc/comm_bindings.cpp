@@ -1,5 +1,5 @@
-// Host side of the xGMI one-shot all-reduce (csrc/kernels/xgmi.hip): exchange buffers, IPC
-// handles and launches.  One XgmiChannel serves one message size class of one communicator.
+// Host side of the xGMI one-/two-shot all-reduce (csrc/kernels/xgmi.hip): exchange buffers, IPC
+// handles and launches.  One XgmiChannel serves one message size of one communicator.
 #include <torch/extension.h>
 #include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
@@ -17,17 +17,22 @@ void hip_ok(hipError_t e, const char* what) {
 
 class XgmiChannel {
  public:
-  XgmiChannel(int64_t rank, int64_t world, int64_t cap, int64_t device, double timeout_s)
-      : rank_((int)rank), world_((int)world), device_((int)device) {
+  // `numel`: the message size of this channel (one-shot calls may be shorter; two-shot calls must
+  // use exactly this size, their shard layout depends on it); `algo`: 0 one-shot, 1 two-shot
+  XgmiChannel(int64_t rank, int64_t world, int64_t numel, int64_t device, double timeout_s, int64_t algo)
+      : rank_((int)rank), world_((int)world), device_((int)device), algo_((int)algo), n_(numel) {
     TORCH_CHECK(world >= 1 && world <= tdl::kXgmiMaxRanks, "xgmi: 1..8 ranks supported");
     TORCH_CHECK(rank >= 0 && rank < world, "xgmi: bad rank");
-    TORCH_CHECK(cap > 0, "xgmi: empty channel");
+    TORCH_CHECK(numel > 0, "xgmi: empty channel");
+    TORCH_CHECK(algo == 0 || algo == 1, "xgmi: algo is 0 (one-shot) or 1 (two-shot)");
     c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
-    blocks_ = tdl::xgmi_blocks(cap);
+    blocks_ = tdl::xgmi_blocks(numel);
     cap_ = (int64_t)blocks_ * tdl::kXgmiBlockElems;
+    shard_ = tdl::xgmi_shard(numel, world_);
     timeout_ = (int64_t)(timeout_s * 1e8);
-    hip_ok(hipMalloc(&buf_, (size_t)(2 * cap_) * sizeof(float)), "hipMalloc(exchange)");
-    const size_t sig_bytes = (size_t)blocks_ * tdl::kXgmiMaxRanks * sizeof(uint32_t);
+    // 2 parity halves x [input | result]
+    hip_ok(hipMalloc(&buf_, (size_t)(4 * cap_) * sizeof(float)), "hipMalloc(exchange)");
+    const size_t sig_bytes = (size_t)2 * blocks_ * tdl::kXgmiMaxRanks * sizeof(uint32_t);
     // signal words are polled across the fabric: uncached device memory where the runtime has it
     if (hipExtMallocWithFlags(reinterpret_cast<void**>(&sig_), sig_bytes, hipDeviceMallocUncached) != hipSuccess) {
       (void)hipGetLastError();
@@ -35,7 +40,7 @@ class XgmiChannel {
     }
     hip_ok(hipMalloc(&epoch_, (size_t)blocks_ * sizeof(uint32_t)), "hipMalloc(epochs)");
     hip_ok(hipMalloc(&err_, sizeof(uint32_t)), "hipMalloc(error)");
-    hip_ok(hipMemset(buf_, 0, (size_t)(2 * cap_) * sizeof(float)), "hipMemset");
+    hip_ok(hipMemset(buf_, 0, (size_t)(4 * cap_) * sizeof(float)), "hipMemset");
     hip_ok(hipMemset(sig_, 0, sig_bytes), "hipMemset");
     hip_ok(hipMemset(epoch_, 0, (size_t)blocks_ * sizeof(uint32_t)), "hipMemset");
     hip_ok(hipMemset(err_, 0, sizeof(uint32_t)), "hipMemset");
@@ -59,6 +64,7 @@ class XgmiChannel {
   }
 
   int64_t cap() const { return cap_; }
+  int64_t algo() const { return algo_; }
   bool connected() const { return connected_; }
 
   pybind11::bytes handle(bool signals) const {
@@ -138,6 +144,7 @@ class XgmiChannel {
 
   void launch(const at::Tensor& src, float* dst, float* w, const float* lr, double scale, int mode) {
     TORCH_CHECK(connected_, "xgmi: channel is not connected");
+    TORCH_CHECK(algo_ == 0 || src.numel() == n_, "xgmi: a two-shot channel serves exactly ", n_, " elements");
     tdl::XgmiArgs a;
     a.p = peers_;
     a.src = src.data_ptr<float>();
@@ -148,17 +155,20 @@ class XgmiChannel {
     a.err = err_;
     a.n = src.numel();
     a.cap = cap_;
+    a.shard = shard_;
+    a.sig_blocks = blocks_;
     a.timeout = timeout_;
     a.scale = (float)scale;
     a.rank = rank_;
     a.world = world_;
     c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
-    tdl::xgmi_all_reduce(a, mode, c10::hip::getCurrentHIPStream().stream());
+    tdl::xgmi_all_reduce(a, mode, algo_, c10::hip::getCurrentHIPStream().stream());
   }
 
-  int rank_, world_, device_;
+  int rank_, world_, device_, algo_;
+  int64_t n_;
   int blocks_ = 0;
-  int64_t cap_ = 0, timeout_ = 0;
+  int64_t cap_ = 0, shard_ = 0, timeout_ = 0;
   float* buf_ = nullptr;
   uint32_t* sig_ = nullptr;
   uint32_t* epoch_ = nullptr;
@@ -172,9 +182,11 @@ class XgmiChannel {
 
 void register_comm(pybind11::module& m) {
   pybind11::class_<XgmiChannel>(m, "XgmiChannel")
-      .def(pybind11::init<int64_t, int64_t, int64_t, int64_t, double>(), pybind11::arg("rank"),
-           pybind11::arg("world"), pybind11::arg("cap"), pybind11::arg("device"), pybind11::arg("timeout_s") = 60.0)
+      .def(pybind11::init<int64_t, int64_t, int64_t, int64_t, double, int64_t>(), pybind11::arg("rank"),
+           pybind11::arg("world"), pybind11::arg("numel"), pybind11::arg("device"), pybind11::arg("timeout_s") = 60.0,
+           pybind11::arg("algo") = 0)
       .def_property_readonly("cap", &XgmiChannel::cap)
+      .def_property_readonly("algo", &XgmiChannel::algo)
       .def_property_readonly("connected", &XgmiChannel::connected)
       .def("handle", &XgmiChannel::handle, pybind11::arg("signals"))
       .def("open", &XgmiChannel::open)

@@ -38,15 +38,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--marker", required=True, help="substring of the first kernel of each step")
+    ap.add_argument("--marker-grid-min", type=int, default=0, help="only marker dispatches with a grid >= this")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--top", type=int, default=25)
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    marks = [i for i, r in enumerate(rows) if a.marker in r["Kernel_Name"]]
-    if len(marks) < a.steps:
+    marks = [i for i, r in enumerate(rows)
+             if a.marker in r["Kernel_Name"] and int(r.get("Grid_Size_X") or 0) >= a.marker_grid_min]
+    # the window spans the last `steps` complete steps: marker[-steps-1] .. marker[-1]
+    if len(marks) < a.steps + 1:
         raise SystemExit(f"only {len(marks)} marker dispatches")
-    win = rows[marks[-a.steps]:]
+    win = rows[marks[-a.steps - 1]:marks[-1]]
     t0 = int(win[0]["Start_Timestamp"])
     t1 = max(int(r["End_Timestamp"]) for r in win)
     busy = defaultdict(float)

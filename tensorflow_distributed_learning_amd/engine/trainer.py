@@ -140,6 +140,12 @@ class GenericTrainer:
         self.metrics = model.compiled_metrics
         self._policy = model._dtype_policy()
         self._buckets = self._make_buckets()
+        # whole-step hipGraphs (forward + backward + all-reduce + optimizer + metrics), keyed by
+        # the batch signature; the first two steps of a signature run eagerly (solver search,
+        # allocator warm-up), the third is captured and every later one is a single replay
+        self._graphs: Dict[tuple, tuple] = {}
+        self._seen: Dict[tuple, int] = {}
+        self._graph_ok: Optional[bool] = None
         if self.device.type == "cuda" and os.environ.get("TDL_CONV_AUTOTUNE", "1") == "1":
             # like TF's cuDNN autotuning (TF_CUDNN_USE_AUTOTUNE=1): MIOpen find-mode search of the
             # conv solvers per shape on first use (+12% ResNet-50 step rate on MI355X)
@@ -194,7 +200,8 @@ class GenericTrainer:
     def _forward_loss(self, x, y, sw, global_n):
         model = self.model
         if self._policy == "mixed_bfloat16" and self.device.type == "cuda":
-            ctx = torch.autocast("cuda", dtype=torch.bfloat16)
+            # no cast cache: a cached bf16 weight copy must not outlive a captured step graph
+            ctx = torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False)
         else:
             ctx = torch.autocast(self.device.type, enabled=False)
         with ctx:
@@ -209,7 +216,7 @@ class GenericTrainer:
             loss = loss + reg / self.strategy.num_replicas_in_sync
         return loss, per_ex, y_pred
 
-    def train_step(self, batch, global_n: int):
+    def train_step(self, batch, global_n: int, sync_lr: bool = True):
         x, y, sw = _split_xy(_to_device(batch, self.device))
         G = self.G
         G.zero_()
@@ -230,7 +237,7 @@ class GenericTrainer:
                 else:
                     self.comm.all_reduce(G, "sum")
         with torch.no_grad(), trace_range("tdl.optimizer"):
-            self.optimizer.apply_flat(self.W, G)
+            self.optimizer.apply_flat(self.W, G, sync_lr=sync_lr)
             self.loss_tracker.update_state(per_ex.detach())
             yp = y_pred.detach()
             for m in self.metrics:
@@ -244,9 +251,71 @@ class GenericTrainer:
             except StopIteration:
                 break
             n = len(D.flatten(batch)[0])
-            self.train_step(batch, handler.global_size(n))
+            gn = handler.global_size(n)
+            if not self._graphed_step(batch, gn):
+                self.train_step(batch, gn)
             done += 1
         return done
+
+    # ------------------------------------------------------------------ whole-step graphs
+    def _graphable(self) -> bool:
+        if self._graph_ok is None:
+            ok = (self.device.type == "cuda" and os.environ.get("TDL_GRAPH_STEP", "1") == "1" and
+                  getattr(self.optimizer, "graph_safe", False) and not self.optimizer.weight_decay)
+            if ok and self.comm.world_size > 1:
+                ok = self.comm.capture_probe()  # collective: every rank takes the same decision
+            self._graph_ok = bool(ok)
+        return self._graph_ok
+
+    def _graphed_step(self, batch, global_n: int) -> bool:
+        flat = D.flatten(batch)
+        if not all(isinstance(t, torch.Tensor) for t in flat):
+            return False
+        if not self._graphable():
+            return False
+        key = (global_n,) + tuple((tuple(t.shape), t.dtype) for t in flat)
+        ent = self._graphs.get(key)
+        if ent is None:
+            seen = self._seen.get(key, 0) + 1
+            self._seen[key] = seen
+            if seen <= 2:
+                return False
+            try:
+                ent = self._capture(batch, global_n)
+            except Exception as e:  # noqa: BLE001 - a layer with host-side logic: stay eager
+                import warnings
+
+                warnings.warn(f"whole-step graph capture failed, training eagerly: {type(e).__name__}: {e}")
+                torch.cuda.synchronize(self.device)
+                self._graph_ok = False
+                return False
+            self._graphs[key] = ent
+        static, graph = ent
+        for s_, t in zip(static, flat):
+            s_.copy_(t, non_blocking=True)
+        self.optimizer._sync_lr()
+        graph.replay()
+        self.optimizer.iterations += 1
+        return True
+
+    def _capture(self, batch, global_n: int):
+        flat = D.flatten(batch)
+        static = [torch.empty_like(t, device=self.device).copy_(t) for t in flat]
+        it = iter(static)
+        sbatch = D.map_structure(lambda _t: next(it), batch)
+        dev = self.device
+        torch.cuda.synchronize(dev)
+        graph = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        it0 = self.optimizer.iterations
+        try:
+            with torch.cuda.graph(graph, stream=s):
+                self.train_step(sbatch, global_n, sync_lr=False)
+        finally:
+            self.optimizer.iterations = it0  # capture records, it does not run a step
+        torch.cuda.current_stream(dev).wait_stream(s)
+        return static, graph
 
     @torch.no_grad()
     def test_step(self, batch):

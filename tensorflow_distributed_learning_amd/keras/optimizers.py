@@ -154,6 +154,10 @@ def _hip_ok(t: torch.Tensor) -> bool:
 class SGD(Optimizer):
     """tf.keras.optimizers.SGD(learning_rate=0.01, momentum=0.0, nesterov=False) (ex:51)."""
 
+    # the GPU update reads the learning rate from ``lr_dev`` (refreshed before every step), so a
+    # captured step graph stays correct under learning-rate schedules
+    graph_safe = True
+
     def __init__(self, learning_rate=0.01, momentum=0.0, nesterov=False, name="SGD", **kw):
         super().__init__(learning_rate, name, **kw)
         if not 0.0 <= momentum <= 1.0:

@@ -35,6 +35,14 @@ def max_bytes() -> int:
     return int(os.environ.get("TDL_XGMI_MAX_BYTES", str(4 << 20)))
 
 
+def choose_algo(numel: int, world: int) -> int:
+    """0 = one-shot, 1 = two-shot.  One-shot moves (R-1) x n bytes over a rank's links, two-shot
+    2 (R-1)/R x n in two hops: above ``TDL_XGMI_ONESHOT_MAX_BYTES`` (256 KiB) at R >= 3 the
+    bandwidth term wins over the extra hop."""
+    lim = int(os.environ.get("TDL_XGMI_ONESHOT_MAX_BYTES", str(256 << 10)))
+    return 1 if world >= 3 and 4 * numel > lim else 0
+
+
 class XgmiAllReduce:
     """Channel manager of one process group (every rank on this node, one GPU each)."""
 
@@ -53,8 +61,8 @@ class XgmiAllReduce:
 
     # ------------------------------------------------------------------ set-up (collective)
     def _make(self, numel: int):
-        cap = ((numel + BLOCK - 1) // BLOCK) * BLOCK
-        ch = self.C.XgmiChannel(self.rank, self.world, cap, self.device.index or 0, self.timeout)
+        ch = self.C.XgmiChannel(self.rank, self.world, numel, self.device.index or 0, self.timeout,
+                                choose_algo(numel, self.world))
         mine = (bytes(ch.handle(False)), bytes(ch.handle(True)))
         allh = [None] * self.world
         dist.all_gather_object(allh, mine, group=self.group)
@@ -97,9 +105,15 @@ class XgmiAllReduce:
         return self.ok
 
     def _selftest(self) -> bool:
-        """Eager, repeated (both buffer halves), graph-replayed and fused-SGD calls against an
-        exact all-gather reference summed in rank order (bit-identical expected)."""
-        n = 3 * BLOCK + 37
+        """Both algorithms (a small and a large message): eager, repeated (both buffer halves),
+        graph-replayed and fused-SGD calls against an exact all-gather reference summed in rank
+        order (bit-identical expected)."""
+        ok = True
+        for n in (3 * BLOCK + 37, 70 * BLOCK + 5):
+            ok &= self._selftest_one(n)
+        return self._agree(ok)
+
+    def _selftest_one(self, n: int) -> bool:
         ch = self._make(n)
         dev = self.device
         g = torch.Generator(device="cpu").manual_seed(1234 + self.rank)
@@ -139,9 +153,8 @@ class XgmiAllReduce:
         torch.cuda.synchronize(dev)
         ok &= bool(torch.allclose(w, w_ref, rtol=0, atol=1e-6))
         ok &= ch.error() == 0
-        ok = self._agree(ok)
         self._chans[n] = ch
-        return ok
+        return bool(ok)
 
     # ------------------------------------------------------------------ collectives
     def _channel(self, n: int):

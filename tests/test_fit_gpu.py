@@ -65,7 +65,61 @@ def test_fused_epoch_boundary_partial_batches_match_generic():
     front of it (eager remainder) and the partial batch runs as its own step."""
     mf, hf = _train(True, steps=14, spe=3, n=300)
     assert mf._trainer.kind == "fused", mf._fused_reason
-    mg, hg = _train(False, steps=14, spe=3, n=300)
+    os.environ["TDL_GRAPH_STEP"] = "0"  # the generic reference step by step (graphs: next test)
+    try:
+        mg, hg = _train(False, steps=14, spe=3, n=300)
+    finally:
+        os.environ.pop("TDL_GRAPH_STEP", None)
     for a, b in zip(mf.get_weights(), mg.get_weights()):
         np.testing.assert_allclose(a, b, rtol=2e-3, atol=2e-4)
     np.testing.assert_allclose(hf.history["loss"], hg.history["loss"], rtol=1e-3, atol=1e-4)
+
+
+def _small_resnet(seed):
+    """Conv/BN/ReLU/residual/pool model on the generic engine (fused BN kernels, MIOpen convs)."""
+    tdl.keras.utils.set_random_seed(seed)
+    L = tdl.keras.layers
+    inp = L.Input(shape=(16, 16, 8))
+    x = L.Conv2D(16, 3, padding="same")(inp)
+    x = L.BatchNormalization()(x)
+    x = L.Activation("relu")(x)
+    y = L.Conv2D(16, 3, padding="same")(x)
+    y = L.BatchNormalization()(y)
+    x = L.Activation("relu")(L.Add()([x, y]))
+    x = L.GlobalAveragePooling2D()(x)
+    out = L.Dense(10)(x)
+    return tdl.keras.Model(inp, out)
+
+
+def _train_small_resnet(graph: bool, steps=8):
+    os.environ["TDL_GRAPH_STEP"] = "1" if graph else "0"
+    try:
+        tdl.keras.backend.clear_session()
+        g = torch.Generator().manual_seed(0)
+        x = torch.rand(512, 16, 16, 8, generator=g)
+        y = torch.randint(0, 10, (512,), generator=g)
+        ds = tdl.data.Dataset.from_tensor_slices((x, y)).batch(64).repeat()
+        strategy = tdl.distribute.MirroredStrategy(devices=["/gpu:0"])
+        with strategy.scope():
+            m = _small_resnet(1)
+            m.compile(loss=tdl.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+                      optimizer=tdl.keras.optimizers.SGD(
+                          learning_rate=tdl.keras.optimizers.schedules.ExponentialDecay(0.1, 2, 0.5), momentum=0.9),
+                      metrics=["sparse_categorical_accuracy"])
+        h = m.fit(ds, epochs=2, steps_per_epoch=steps // 2, verbose=0)
+        return m, h
+    finally:
+        os.environ.pop("TDL_GRAPH_STEP", None)
+
+
+def test_generic_whole_step_graph_matches_eager():
+    """Steps 3+ of the generic engine replay one captured hipGraph (forward, backward, optimizer,
+    metrics, BN moving statistics); a decaying learning rate must still apply per step."""
+    mg, hg = _train_small_resnet(True)
+    assert mg._trainer.kind == "generic" and len(mg._trainer._graphs) == 1
+    me, he = _train_small_resnet(False)
+    assert not me._trainer._graphs
+    assert mg.optimizer.iterations == me.optimizer.iterations == 8
+    for a, b in zip(mg.get_weights(), me.get_weights()):
+        np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(hg.history["loss"], he.history["loss"], rtol=1e-4)

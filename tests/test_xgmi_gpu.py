@@ -42,13 +42,16 @@ IPC_BODY = """
 import os, sys, torch, torch.distributed as dist
 sys.path.insert(0, sys.argv[2])
 from tensorflow_distributed_learning_amd import ops
+from tensorflow_distributed_learning_amd.parallel.xgmi import choose_algo
 rank, R = int(sys.argv[1]), int(sys.argv[4])
 dist.init_process_group("gloo", rank=rank, world_size=R, init_method="tcp://127.0.0.1:" + sys.argv[3])
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 C = ops.hip()
-for n in (37, 70000, 206218):
-    ch = C.XgmiChannel(rank, R, n, 0, 20.0)
+keep = []  # (freeing an exported buffer a peer still maps, then re-allocating it, breaks IPC export)
+for n, algo in [(37, 0), (70000, 0), (70000, 1), (206218, choose_algo(206218, R)), (18816, 1)]:
+    ch = C.XgmiChannel(rank, R, n, 0, 20.0, algo)
+    assert ch.algo == algo
     mine = (bytes(ch.handle(False)), bytes(ch.handle(True)))
     allh = [None] * R
     dist.all_gather_object(allh, mine)
@@ -65,7 +68,7 @@ for n in (37, 70000, 206218):
         ch.all_reduce(x, y, 1.0)
         torch.cuda.synchronize(dev)
         assert ch.error() == 0, "timeout"
-        assert torch.equal(y.cpu(), want), f"mismatch n={n} it={it}"
+        assert torch.equal(y.cpu(), want), f"mismatch n={n} algo={algo} it={it}"
     # graph replay with two calls per replay, then fused SGD
     s = torch.cuda.Stream(dev)
     gr = torch.cuda.CUDAGraph()
@@ -87,7 +90,7 @@ for n in (37, 70000, 206218):
     torch.testing.assert_close(w.cpu(), 1 - 0.25 * want, rtol=0, atol=1e-6)
     assert ch.error() == 0
     dist.barrier()
-    del ch
+    keep.append(ch)
 print("ipc ok", rank, flush=True)
 """
 
