@@ -56,13 +56,14 @@ class XgmiAllReduce:
         self.timeout = float(os.environ.get("TDL_XGMI_TIMEOUT", "600"))
         self.limit = max_bytes() // 4
         self._chans: Dict[int, object] = {}
+        self._selftest_chans = []
         self.ok: Optional[bool] = None  # None = not yet tested
         self.reason = ""
 
     # ------------------------------------------------------------------ set-up (collective)
-    def _make(self, numel: int):
-        ch = self.C.XgmiChannel(self.rank, self.world, numel, self.device.index or 0, self.timeout,
-                                choose_algo(numel, self.world))
+    def _make(self, numel: int, timeout: Optional[float] = None):
+        ch = self.C.XgmiChannel(self.rank, self.world, numel, self.device.index or 0,
+                                self.timeout if timeout is None else timeout, choose_algo(numel, self.world))
         mine = (bytes(ch.handle(False)), bytes(ch.handle(True)))
         allh = [None] * self.world
         dist.all_gather_object(allh, mine, group=self.group)
@@ -114,7 +115,8 @@ class XgmiAllReduce:
         return self._agree(ok)
 
     def _selftest_one(self, n: int) -> bool:
-        ch = self._make(n)
+        # short bounded waits: a protocol failure on this machine must fall back, not stall
+        ch = self._make(n, timeout=10.0)
         dev = self.device
         g = torch.Generator(device="cpu").manual_seed(1234 + self.rank)
         ok = True
@@ -153,7 +155,7 @@ class XgmiAllReduce:
         torch.cuda.synchronize(dev)
         ok &= bool(torch.allclose(w, w_ref, rtol=0, atol=1e-6))
         ok &= ch.error() == 0
-        self._chans[n] = ch
+        self._selftest_chans.append(ch)  # kept alive (see close); not reused for traffic
         return bool(ok)
 
     # ------------------------------------------------------------------ collectives
@@ -199,6 +201,7 @@ class XgmiAllReduce:
 
     def close(self) -> None:
         self._chans.clear()
+        self._selftest_chans.clear()
 
 
 def single_node(group=None) -> bool:
