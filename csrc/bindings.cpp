@@ -47,7 +47,8 @@ class MnistStep {
     A2_ = at::empty({b * 1600}, u8);
     H_ = at::empty({b * 128}, f);
     dH_ = at::empty({b * 128}, f);
-    part4_ = at::zeros({(int64_t)tdl::mnist_head_blocks((int)b) * 1290}, f);
+    dL_ = at::zeros({b * 10}, f);
+    cnt_ = at::zeros({b}, f.dtype(at::kInt));
     dC2_ = at::empty({b * 100 * 64}, f);
     part2_ = at::zeros({b * tdl::kMnistPart2Rows * 64}, f);
     part1_ = at::zeros({(int64_t)tdl::mnist_part1_rows((int)b) * tdl::kMnistPart1Cols}, f);
@@ -66,7 +67,9 @@ class MnistStep {
     a_.A2 = A2_.data_ptr<uint8_t>();
     a_.H = H_.data_ptr<float>();
     a_.dH = dH_.data_ptr<float>();
-    a_.part4 = part4_.data_ptr<float>();
+    a_.dL = dL_.data_ptr<float>();
+    a_.cnt = reinterpret_cast<unsigned*>(cnt_.data_ptr<int>());
+    a_.head = 1;
     a_.dC2 = dC2_.data_ptr<float>();
     a_.part2 = part2_.data_ptr<float>();
     a_.part1 = part1_.data_ptr<float>();
@@ -83,11 +86,11 @@ class MnistStep {
     a_.idx = idx_.data_ptr<int>() + off;
   }
 
-  // Individual stages (tests / profiling): 4 head, 5 dense1 bwd, 6 conv bwd, 8 fwd conv (+dense1), 9 finalize.
+  // Individual stages (tests / profiling): 5 dense1 bwd, 6 conv bwd, 8 fwd conv (+dense1, +head),
+  // 9 finalize.
   void stage(int64_t k, bool apply_sgd) {
     hipStream_t s = cur_stream();
     switch (k) {
-      case 4: tdl::mnist_head(a_, s); break;
       case 5: tdl::mnist_dense1_bwd(a_, s); break;
       case 6: tdl::mnist_conv_bwd(a_, s); break;
       case 8: tdl::mnist_fwd_conv(a_, s); break;
@@ -101,7 +104,6 @@ class MnistStep {
     set_idx_offset(idx_off);
     hipStream_t s = cur_stream();
     tdl::mnist_fwd_conv(a_, s);
-    tdl::mnist_head(a_, s);
     tdl::mnist_dense1_bwd(a_, s);
     tdl::mnist_conv_bwd(a_, s);
   }
@@ -112,18 +114,18 @@ class MnistStep {
     set_idx_offset(idx_off);
     hipStream_t s = cur_stream();
     tdl::mnist_fwd_conv(a_, s);
-    tdl::mnist_head(a_, s);
     tdl::mnist_dense1_bwd(a_, s);
   }
   void backward_conv() { tdl::mnist_conv_bwd(a_, cur_stream()); }
 
   void finalize(bool apply_sgd) { tdl::mnist_finalize(a_, apply_sgd, cur_stream()); }
 
-  // forward only (evaluation): K1..K3 + logits via head is training-only, so eval uses K1-K3.
+  // forward features only (dense1 partials, no loss head / metrics)
   void forward_features(int64_t idx_off) {
     set_idx_offset(idx_off);
-    hipStream_t s = cur_stream();
-    tdl::mnist_fwd_conv(a_, s);
+    tdl::MnistArgs f = a_;
+    f.head = 0;
+    tdl::mnist_fwd_conv(f, cur_stream());
   }
 
   // diagnostics: per-workgroup phase timestamps of the next launches (None to disable)
@@ -137,11 +139,11 @@ class MnistStep {
     }
   }
 
-  std::vector<at::Tensor> buffers() { return {P1_, A1_, P2_, A2_, H_, dH_, dC2_, part2_, part1_, part3_}; }
+  std::vector<at::Tensor> buffers() { return {P1_, A1_, P2_, A2_, H_, dH_, dC2_, part2_, part1_, part3_, dL_}; }
 
  private:
   at::Tensor X_, Y_, idx_, W_, G_, lr_, metrics_;
-  at::Tensor P1_, A1_, P2_, A2_, H_, dH_, dC2_, part2_, part1_, part3_, part4_;
+  at::Tensor P1_, A1_, P2_, A2_, H_, dH_, dC2_, part2_, part1_, part3_, dL_, cnt_;
   at::Tensor stamps_;
   tdl::MnistArgs a_;
 };

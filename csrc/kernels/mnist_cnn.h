@@ -31,13 +31,15 @@ struct MnistArgs {
   float* part2;       // [b][289][64] per-image partials of conv2 wgrad (row 288 = bias)
   float* part1;       // [2b][320] per-(image, pixel-half) partials of conv1 wgrad (+ bias)
   float* part3;       // [4][b][128] dense1 partials, one per conv2 channel quarter
-  float* part4;       // [ceil(b/4)][1290] per-workgroup partials of dense2 wgrad (+ bias)
+  float* dL;          // [b][10] dlogits (already scaled by 1/(b*R))
+  unsigned* cnt;      // [b] per-image arrival counters of the 4 quarter workgroups (monotonic)
   float* metrics;     // [0] loss sum, [1] correct, [2] count
   const float* lr;    // device scalar learning rate
   unsigned long long* stamps;  // optional [grid][8] phase timestamps (s_memrealtime), diagnostics
   int b;              // per-replica batch
   float scale;        // 1 / (b * R)
   int nslab;          // slab length (floats)
+  int head;           // 1: the forward kernel also runs the loss head (training); 0: features only
 };
 
 constexpr int kMnistPart2Rows = 289;
@@ -45,12 +47,11 @@ constexpr int kDense1Chunks = 4;  // dense1 partials: one per conv2 channel quar
 constexpr int kMnistPart1Cols = 320;
 __host__ __device__ inline int mnist_part1_rows(int b) { return 2 * b; }
 
-__host__ __device__ inline int mnist_head_blocks(int b) { return (b + 3) / 4; }
-
-void mnist_head(const MnistArgs& a, hipStream_t s);
 void mnist_dense1_bwd(const MnistArgs& a, hipStream_t s);
 void mnist_conv_bwd(const MnistArgs& a, hipStream_t s);
-void mnist_fwd_conv(const MnistArgs& a, hipStream_t s);  // conv1 + conv2 + dense1 partials per image
+// conv1 + conv2 + dense1 partials per (image, quarter); with a.head the image's last quarter
+// workgroup also runs the loss head (dense1 sum + ReLU, dense2, softmax-xent, dlogits, metrics)
+void mnist_fwd_conv(const MnistArgs& a, hipStream_t s);
 void mnist_finalize(const MnistArgs& a, bool apply_sgd, hipStream_t s);
 
 // Plain SGD over a flat slab: w -= lr * g  (lr read from device memory).

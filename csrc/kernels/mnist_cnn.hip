@@ -1,15 +1,17 @@
 // Fused MNIST-CNN training step for gfx950 (MI355X), f32 end to end.
 //
 // Replaces, for the reference model of tf_dist_example.py:40-52, the ~35 TF/cuDNN/Eigen kernels
-// of one replica step by five launches:
+// of one replica step by four launches:
 //
 //   KA fwd_conv     : per (image, channel quarter), LDS-staged: gather(idx) + conv1 3x3 (1->32)
 //                     and conv2 3x3 (32->64) on v_mfma_f32_16x16x4_f32 with bias + ReLU + maxpool2
 //                     in registers (a 16-row MFMA tile = 4 pool windows), then this quarter's
-//                     dense1 partial [1600/4 features] x W3 (W3 slice prefetched in registers)
-//   K4 head         : dense1 partial sum + bias + ReLU, dense2 + softmax-xent + dlogits*(1/(b*R))
-//                     + loss/accuracy accumulators + dW4/db4 partials + dH (ReLU mask)
-//   K5 dense1_bwd   : dW3 = P2^T dH, db3, dP2 = dH W3^T -> pool2/ReLU backward scatter to dC2
+//                     dense1 partial [1600/4 features] x W3 (W3 slice prefetched in registers);
+//                     the LAST of an image's 4 quarter workgroups (arrival counter) then runs the
+//                     head for that image: dense1 partial sum + bias + ReLU, dense2 + softmax-xent
+//                     + dlogits*(1/(b*R)) + loss/accuracy accumulators + dH (ReLU mask)
+//   K5 dense1_bwd   : dW3 = P2^T dH, db3, dP2 = dH W3^T -> pool2/ReLU backward scatter to dC2,
+//                     dW4 = H^T dL, db4
 //   KC conv_bwd     : per image (x4 parts), LDS-staged: dW2 (+db2 as an extra "ones" row) and
 //                     dP1 = dC2 (*) W2^T on MFMA with pool1/ReLU backward AND conv1 wgrad in
 //                     the epilogue (dC1 is never materialised); per-image partial slabs
@@ -24,38 +26,59 @@
 namespace tdl {
 
 // --------------------------------------------------------------------------------------------
-// K4: dense2 + sparse softmax cross-entropy + metrics + dense2 grads + dH.  ceil(b/4) workgroups.
+// Loss head of ONE batch row r, run by one wave (lane l owns hidden features l and l + 64):
+// H = relu(b3 + sum of the 4 dense1 quarter partials), logits = dense2 (wave reductions),
+// softmax / loss / dlogits computed redundantly by every lane, dH (ReLU-masked) and dL stored,
+// loss / accuracy / count accumulated.  The partials come from the other quarter workgroups of
+// the same launch: sc1 loads (L2, never a stale L1 line), see k_fwd_conv's hand-off.
 // --------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_head(MnistArgs a) {
-  // One wave per batch row: lane l owns hidden features l and l+64.  Logits are wave
-  // reductions; softmax / loss / dlogits are computed redundantly by every lane; dH is written
-  // per lane; dW4/db4 per-workgroup partials (4 rows) go to part4, reduced by K5's tail blocks.
-  __shared__ float sP[4][1290 + 2];
-  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const int r = blockIdx.x * 4 + wave;
-  const bool live = r < a.b;
-  const int rr = live ? r : 0;
-  const int y = a.Y[a.idx[rr]];  // dependent pair of loads: issued first
+struct HeadWeights {  // dense2 kernel rows l and l + 64, dense2 bias, dense1 bias of features l, l + 64
+  float wa[10], wb[10], b4[10], b3a, b3b;
+};
+
+__device__ __forceinline__ HeadWeights load_head_weights(const MnistArgs& a, int l) {
+  HeadWeights hw;
   const float* w4 = a.W + a.ow4;
-  float wa[10], wb[10];
 #pragma unroll
-  for (int c = 0; c < 10; ++c) { wa[c] = w4[l * 10 + c]; wb[c] = w4[(l + 64) * 10 + c]; }
-  // H = relu(b3 + sum of dense1's 25 split-K partials), 50 independent loads per lane
+  for (int c = 0; c < 10; ++c) {
+    hw.wa[c] = w4[l * 10 + c];
+    hw.wb[c] = w4[(l + 64) * 10 + c];
+    hw.b4[c] = a.W[a.ob4 + c];
+  }
+  hw.b3a = a.W[a.ob3 + l];
+  hw.b3b = a.W[a.ob3 + l + 64];
+  return hw;
+}
+
+// phase stamp k of the head, after the per-wave stamps: buf[grid*64 + workgroup*8 + k]
+// (diagnostics, stamps != null; the buffer then holds grid * 72 words)
+__device__ __forceinline__ void head_stamp(unsigned long long* buf, int k) {
+  if (buf != nullptr && (threadIdx.x & 63) == 0)
+    buf[(size_t)gridDim.x * 64 + blockIdx.x * 8 + k] = __builtin_amdgcn_s_memrealtime();
+}
+
+__device__ __forceinline__ void head_row(const MnistArgs& a, int r, int l, int y, const HeadWeights& hw) {
+  const float* wa = hw.wa;
+  const float* wb = hw.wb;
+  head_stamp(a.stamps, 0);
   float hp0[kDense1Chunks], hp1[kDense1Chunks];
 #pragma unroll
   for (int c = 0; c < kDense1Chunks; ++c) {
-    hp0[c] = a.part3[((size_t)c * a.b + rr) * 128 + l];
-    hp1[c] = a.part3[((size_t)c * a.b + rr) * 128 + l + 64];
+    hp0[c] = __hip_atomic_load(a.part3 + ((size_t)c * a.b + r) * 128 + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    hp1[c] = __hip_atomic_load(a.part3 + ((size_t)c * a.b + r) * 128 + l + 64, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
   }
-  float h0 = a.W[a.ob3 + l], h1 = a.W[a.ob3 + l + 64];
+  float h0 = hw.b3a, h1 = hw.b3b;
 #pragma unroll
   for (int c = 0; c < kDense1Chunks; ++c) { h0 += hp0[c]; h1 += hp1[c]; }
   h0 = fmaxf(h0, 0.f);
   h1 = fmaxf(h1, 0.f);
-  if (live) { a.H[r * 128 + l] = h0; a.H[r * 128 + l + 64] = h1; }
+  head_stamp(a.stamps, 1);
+  a.H[r * 128 + l] = h0;
+  a.H[r * 128 + l + 64] = h1;
   float lg[10];
 #pragma unroll
-  for (int c = 0; c < 10; ++c) lg[c] = wave_sum(fmaf(h0, wa[c], h1 * wb[c])) + a.W[a.ob4 + c];
+  for (int c = 0; c < 10; ++c) lg[c] = wave_sum(fmaf(h0, wa[c], h1 * wb[c])) + hw.b4[c];
   float m = lg[0];
   int am = 0;
 #pragma unroll
@@ -65,34 +88,29 @@ __global__ __launch_bounds__(256) void k_head(MnistArgs a) {
 #pragma unroll
   for (int c = 0; c < 10; ++c) se += expf(lg[c] - m);
   const float lse = m + logf(se);
+  head_stamp(a.stamps, 2);
   float ly = lg[0];
 #pragma unroll
   for (int c = 1; c < 10; ++c) ly = (c == y) ? lg[c] : ly;
   float dl[10];
-  const float sc = live ? a.scale : 0.f;
 #pragma unroll
-  for (int c = 0; c < 10; ++c) dl[c] = (expf(lg[c] - lse) - (c == y ? 1.f : 0.f)) * sc;
-  float d0 = 0.f, d1 = 0.f;
-#pragma unroll
-  for (int c = 0; c < 10; ++c) { d0 = fmaf(dl[c], wa[c], d0); d1 = fmaf(dl[c], wb[c], d1); }
-  if (live) {
-    a.dH[r * 128 + l] = h0 > 0.f ? d0 : 0.f;
-    a.dH[r * 128 + l + 64] = h1 > 0.f ? d1 : 0.f;
-  }
+  for (int c = 0; c < 10; ++c) dl[c] = (expf(lg[c] - lse) - (c == y ? 1.f : 0.f)) * a.scale;
+  float d0 = 0.f, d1 = 0.f, mine = 0.f;
 #pragma unroll
   for (int c = 0; c < 10; ++c) {
-    sP[wave][l * 10 + c] = h0 * dl[c];
-    sP[wave][(l + 64) * 10 + c] = h1 * dl[c];
+    d0 = fmaf(dl[c], wa[c], d0);
+    d1 = fmaf(dl[c], wb[c], d1);
+    mine = (l == c) ? dl[c] : mine;
   }
-  if (l < 10) sP[wave][1280 + l] = dl[l];
-  __syncthreads();
-  for (int o = threadIdx.x; o < 1290; o += 256)
-    a.part4[(size_t)blockIdx.x * 1290 + o] = (sP[0][o] + sP[1][o]) + (sP[2][o] + sP[3][o]);
-  if (l == 0 && live) {
+  a.dH[r * 128 + l] = h0 > 0.f ? d0 : 0.f;
+  a.dH[r * 128 + l + 64] = h1 > 0.f ? d1 : 0.f;
+  if (l < 10) a.dL[r * 10 + l] = mine;
+  if (l == 0) {
     atomicAdd(&a.metrics[0], lse - ly);
     atomicAdd(&a.metrics[1], am == y ? 1.f : 0.f);
     atomicAdd(&a.metrics[2], 1.f);
   }
+  head_stamp(a.stamps, 3);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -189,12 +207,23 @@ __global__ __launch_bounds__(256) void k_dense1_bwd(MnistArgs a) {
       a.G[a.ob3 + threadIdx.x] = s;
     }
   } else {
-    // dW4 / db4 = sum of the head's per-workgroup partials
+    // dW4[k][c] = sum_r H[r][k] dL[r][c], db4[c] = sum_r dL[r][c]; 16 rows' loads in flight
     const int o = (blk - 201 - nP) * 256 + threadIdx.x;
     if (o < 1290) {
-      const int nh = mnist_head_blocks(b);
+      const int k = o < 1280 ? o / 10 : 0, c = o < 1280 ? o % 10 : o - 1280;
+      const bool bias = o >= 1280;
       float s = 0.f;
-      for (int j = 0; j < nh; ++j) s += a.part4[(size_t)j * 1290 + o];
+      for (int r0 = 0; r0 < b; r0 += 16) {
+        float hv[16], lv[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int r = min(r0 + j, b - 1);
+          hv[j] = bias ? 1.f : a.H[r * 128 + k];
+          lv[j] = a.dL[r * 10 + c];
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) s = (r0 + j < b) ? fmaf(hv[j], lv[j], s) : s;
+      }
       a.G[o < 1280 ? a.ow4 + o : a.ob4 + (o - 1280)] = s;
     }
   }
@@ -419,7 +448,7 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
 //   with the 205 KB W3 slice loaded into registers at kernel start (its latency hides behind the
 //   convolutions); the head sums the 4 quarter partials + bias + ReLU.
 // --------------------------------------------------------------------------------------------
-constexpr int kLdsFwd = 784 + 320 + 169 * kP1Stride + 72 * 16 * 4 + 400;
+constexpr int kLdsFwd = 784 + 320 + 169 * kP1Stride + 72 * 16 * 4 + 400 + 4;
 
 __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -428,12 +457,15 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   float* P1s = w1s + 320;
   float* w2s = P1s + 169 * kP1Stride;  // [kc=72][j=16][t=4]: B[k=4kc+t][16cq+j]
   float* p2s = w2s + 72 * 16 * 4;      // [25 windows][16 channels] pooled conv2 output
+  int* s_last = reinterpret_cast<int*>(p2s + 400);  // head hand-off flag (one word)
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int i = lane & 15, g = lane >> 4;
   const int bi = blockIdx.x >> 2, cq = blockIdx.x & 3;
   stamp(a.stamps, 0);
   // ---- staging: all global loads first ----
-  const f4 vx = ld4(a.X + (size_t)a.idx[bi] * 784 + min(tid, 195) * 4);
+  const int sample = a.idx[bi];
+  const f4 vx = ld4(a.X + (size_t)sample * 784 + min(tid, 195) * 4);
+  const int label = a.Y[sample];  // for the head (this image's last quarter workgroup)
   const float vw1 = tid < 288 ? a.W[a.ow1 + tid] : a.W[a.ob1 + min(tid - 288, 31)];
   f4 vw2[3];
 #pragma unroll
@@ -592,9 +624,27 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
     float hsum = 0.f;
 #pragma unroll
     for (int k = 0; k < 16; ++k) hsum += P1s[k * 128 + tid];
-    a.part3[((size_t)cq * a.b + bi) * 128 + tid] = hsum;
+    // sc1 store: the image's head may run on another XCD (hand-off below)
+    __hip_atomic_store(a.part3 + ((size_t)cq * a.b + bi) * 128 + tid, hsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   stamp(a.stamps, 6);
+  if (!a.head) return;
+  // the head's weights, loaded by wave 0 of every workgroup now: their latency hides behind the
+  // hand-off (only the image's last workgroup uses them; 5 KB, L2-resident)
+  HeadWeights hw;
+  if (wave == 0) hw = load_head_weights(a, lane);
+  // ---- hand-off to the image's last quarter workgroup (MI355X_MICROARCH.md, inter-workgroup
+  // visibility, first table row): every storing wave waits for its sc1 stores, a workgroup
+  // barrier, ONE agent-scope add per workgroup on the image's counter; the workgroup whose add
+  // returns 3 (mod 4) is last and reads the 4 partials with sc1 loads.  Counters are never reset:
+  // each step adds exactly 4 per image, and the kernel boundary orders consecutive steps.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) *s_last = (__hip_atomic_fetch_add(a.cnt + bi, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 3u) == 3u;
+  __syncthreads();
+  if (!*s_last || wave != 0) return;
+  head_row(a, bi, lane, label, hw);
+  stamp(a.stamps, 7);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -700,9 +750,6 @@ __global__ __launch_bounds__(256) void k_sgd_momentum(float* __restrict__ w, con
 // --------------------------------------------------------------------------------------------
 // launchers
 // --------------------------------------------------------------------------------------------
-void mnist_head(const MnistArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_head, dim3(mnist_head_blocks(a.b)), dim3(256), 0, s, a);
-}
 void mnist_dense1_bwd(const MnistArgs& a, hipStream_t s) {
   const int MT = (a.b + 15) / 16;
   const int nP = (MT * 100 + 3) / 4;

@@ -13,7 +13,7 @@ from tensorflow_distributed_learning_amd.models import mnist_cnn as M  # noqa: E
 
 KERNELS = {
     "fwd_conv": (8, 8, {0: "start", 1: "stage-issued", 2: "stage-barrier", 3: "conv1-done", 4: "barrier2",
-                        5: "conv2-mfma", 6: "end"}, 256),
+                        5: "conv2-mfma", 6: "dense1-partial", 7: "head-end"}, 256),
     "conv_bwd": (6, 8, {0: "start", 1: "stage-issued", 2: "stage-barrier", 3: "wgrad-done", 6: "dgrad-mfma",
                         4: "dgrad-epi", 5: "final-barrier"}, 256),
 }
@@ -36,14 +36,15 @@ def main():
     for name, (k, waves, slots, grid) in KERNELS.items():
         if grid is None:  # dense_bwd: 4 row tiles x 13 dP2 blocks + 25 dW3 blocks
             grid = 4 * 13 + 25
-        buf = torch.zeros(grid * 64, dtype=torch.int64, device=dev)
+        buf = torch.zeros(grid * 72, dtype=torch.int64, device=dev)
         st.forward_backward(0)
         st.finalize(True)
         st._impl.set_stamps(buf)
         st.stage(k)
         st._impl.set_stamps(None)
         torch.cuda.synchronize()
-        r = buf.view(grid, 8, 8).cpu().numpy().astype(np.int64)
+        r = buf[:grid * 64].view(grid, 8, 8).cpu().numpy().astype(np.int64)
+        hs = buf[grid * 64:].view(grid, 8).cpu().numpy().astype(np.int64)
         t0 = r[:, :waves, 0].min(axis=1, keepdims=True)
         rel = (r - t0[:, :, None]) * 10 / 1000.0  # us since the workgroup's first wave started
         span = (r[:, :waves][r[:, :waves] > 0].max() - r[:, :waves, 0].min()) * 10 / 1000.0
@@ -56,6 +57,17 @@ def main():
                 print(f"  {lab:4s} blocks (median us): loads+H {ph[0]:.2f}  logits {ph[1]:.2f}  softmax {ph[2]:.2f}  "
                       f"dH/head {ph[3]:.2f}  end {ph[4]:.2f}")
             continue
+        if name == "fwd_conv":
+            # the loss head ran in the last quarter workgroup of each image: its phases
+            # (0 hand-off won, 1 partials loaded, 2 logits/softmax, 3 end) follow the wave stamps
+            last = hs[:, 0] > 0
+            g0 = r[:, :waves, 0][r[:, :waves, 0] > 0].min()
+            h = (hs[last][:, :4] - g0) / 100.0
+            p6 = (r[:, 0, 6] - g0) / 100.0
+            print(f"  head in {last.sum()} workgroups; us since kernel start (median / max): dense1 partial stored "
+                  f"{np.median(p6):.2f}/{p6.max():.2f}; head won {np.median(h[:, 0]):.2f}/{h[:, 0].max():.2f}; "
+                  f"partials loaded {np.median(h[:, 1]):.2f}/{h[:, 1].max():.2f}; softmax {np.median(h[:, 2]):.2f}/"
+                  f"{h[:, 2].max():.2f}; end {np.median(h[:, 3]):.2f}/{h[:, 3].max():.2f}")
         print("  slot/wave " + " ".join(f"{w:>6d}" for w in range(waves)))
         for s, label in sorted(slots.items(), key=lambda kv: np.median(rel[:, 0, kv[0]])):
             vals = [np.median(rel[:, w, s]) if (r[:, w, s] > 0).all() else float("nan") for w in range(waves)]
