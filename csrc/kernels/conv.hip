@@ -1,0 +1,207 @@
+// Implicit-GEMM NHWC bf16 convolution for gfx950 (see conv.h).
+//
+// GEMM view: rows = output pixels (n, oh, ow), columns = output channels, reduction =
+// (kh, kw, c) in chunks of 64 channels (C % 64 == 0, so a chunk never straddles a filter tap).
+// Workgroup tile 128 x BN (BN = 128 or 64) x 64, four waves as 2 x 2, each wave 64 x BN/2 built from
+// 16x16x32 MFMAs (4 x BN/32 accumulators).  Operands are register-staged through a double-buffered
+// LDS image with 144-byte rows (64 bf16 + 16 B pad: the 16 rows an MFMA fragment read touches land
+// on 16 distinct 4-bank slots).  Global loads of tile t+1 are in flight while the MFMAs of tile t
+// run; one barrier per tile.  Out-of-image taps and rows past M load zeros (padding is implicit:
+// no padded copy of the activations is ever made).  Epilogue: the f32 tile is rounded to bf16 into
+// LDS and written back as full 16-byte row segments.
+//
+// The same kernel computes the stride-1 input gradient: dy is the "image", the filter taps are
+// mirrored (kh -> KH-1-kh) and the weight rows are HWIO rows (K contiguous for fixed (kh, kw, c)).
+//
+// blockIdx -> tile mapping is XCD-aware: the 8 XCDs take workgroups round-robin, so the bijective
+// remap below hands each XCD a contiguous run of logical tiles (the column tiles of a row block
+// are adjacent), and the row block's activations are read into one L2 instead of eight.
+#include "kernels/conv.h"
+
+namespace tdl {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BM = 128;
+constexpr int BK = 64;
+constexpr int LDS_ROW = BK + 8;  // bf16 elements per LDS row (144 B)
+
+struct Igemm {
+  const uint16_t* x;  // NHWC image [N][H][W][C]
+  const uint16_t* w;  // weight rows
+  uint16_t* y;        // NHWC output [N][OH][OW][K] == row-major [M][K]
+  int N, H, W, C;
+  int OH, OW, K;
+  int KH, KW, SH, SW, PT, PL;
+  int flip;                 // 1: mirrored taps (input gradient)
+  long long w_col, w_kh, w_kw;  // weight element strides: per output column, per tap row, per tap column
+  int M;
+};
+
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7fffu + ((u >> 16) & 1u);  // round to nearest even (activations are finite)
+  return (uint16_t)(u >> 16);
+}
+
+template <int BN>
+__global__ __launch_bounds__(256, 2) void k_conv_igemm(Igemm a) {
+  constexpr int WN = BN / 2;         // columns per wave
+  constexpr int NS = WN / 16;        // 16-wide column subtiles per wave
+  constexpr int A_LD = BM * BK / 8 / 256;  // 16-B A chunks per thread per tile (4)
+  constexpr int B_LD = BN * BK / 8 / 256;  // 16-B B chunks per thread per tile (4 or 2)
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * (BM + BN) * LDS_ROW];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // XCD-aware bijective remap of the 1-D grid
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int ntn = a.K / BN;
+  const int tn = wg % ntn, tm = wg / ntn;
+
+  // per-thread A rows: chunk j = tid + 256 i -> row j >> 3, 16-B column j & 7
+  const int col8 = (tid & 7) * 8;
+  long long a_base[A_LD];
+  int a_ih[A_LD], a_iw[A_LD];
+#pragma unroll
+  for (int i = 0; i < A_LD; ++i) {
+    const int m = tm * BM + (tid >> 3) + 32 * i;
+    if (m < a.M) {
+      const int ow = m % a.OW, t = m / a.OW, oh = t % a.OH, n = t / a.OH;
+      a_ih[i] = oh * a.SH - a.PT;
+      a_iw[i] = ow * a.SW - a.PL;
+      a_base[i] = (((long long)n * a.H + a_ih[i]) * a.W + a_iw[i]) * a.C + col8;
+    } else {
+      a_ih[i] = -(1 << 28);
+      a_iw[i] = 0;
+      a_base[i] = 0;
+    }
+  }
+  long long b_base[B_LD];
+#pragma unroll
+  for (int i = 0; i < B_LD; ++i) b_base[i] = (long long)(tn * BN + (tid >> 3) + 32 * i) * a.w_col + col8;
+
+  u32x4 ra[A_LD], rb[B_LD];
+  const int ctiles = a.C / BK;
+  const int ntiles = a.KH * a.KW * ctiles;
+
+  auto gload = [&](int t) {
+    const int c0 = (t % ctiles) * BK, tap = t / ctiles;
+    const int kw = tap % a.KW, kh = tap / a.KW;
+    const long long aoff = ((long long)kh * a.W + kw) * a.C + c0;
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+      const int ih = a_ih[i] + kh, iw = a_iw[i] + kw;
+      if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+        ra[i] = *reinterpret_cast<const u32x4*>(a.x + a_base[i] + aoff);
+      else
+        ra[i] = u32x4{0u, 0u, 0u, 0u};
+    }
+    const int wkh = a.flip ? a.KH - 1 - kh : kh, wkw = a.flip ? a.KW - 1 - kw : kw;
+    const long long boff = wkh * a.w_kh + wkw * a.w_kw + c0;
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i) rb[i] = *reinterpret_cast<const u32x4*>(a.w + b_base[i] + boff);
+  };
+  auto sstore = [&](int buf) {
+    uint16_t* la = lds + buf * (BM + BN) * LDS_ROW;
+    uint16_t* lb = la + BM * LDS_ROW;
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i)
+      *reinterpret_cast<u32x4*>(la + ((tid >> 3) + 32 * i) * LDS_ROW + col8) = ra[i];
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i)
+      *reinterpret_cast<u32x4*>(lb + ((tid >> 3) + 32 * i) * LDS_ROW + col8) = rb[i];
+  };
+
+  f4v acc[4][NS];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NS; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  const int frow = lane & 15, fk = (lane >> 4) * 8;
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) gload(t + 1);
+    const uint16_t* la = lds + buf * (BM + BN) * LDS_ROW + (wm * 64 + frow) * LDS_ROW + fk;
+    const uint16_t* lb = lds + buf * (BM + BN) * LDS_ROW + BM * LDS_ROW + (wn * WN + frow) * LDS_ROW + fk;
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      bf16x8 fa[4], fb[NS];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(la + i * 16 * LDS_ROW + kk);
+#pragma unroll
+      for (int j = 0; j < NS; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(lb + j * 16 * LDS_ROW + kk);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NS; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    if (t + 1 < ntiles) sstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: bf16 tile into LDS ([BM][BN + 8]), then 16-B row segments to global
+  constexpr int OUT_LD = BN + 8;
+  static_assert(BM * OUT_LD <= 2 * (BM + BN) * LDS_ROW, "epilogue tile must fit the operand LDS");
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NS; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        lds[(wm * 64 + i * 16 + (lane >> 4) * 4 + rr) * OUT_LD + wn * WN + j * 16 + (lane & 15)] = f2bf(acc[i][j][rr]);
+  __syncthreads();
+  constexpr int SEG = BN / 8;  // 16-B segments per row
+#pragma unroll
+  for (int s = tid; s < BM * SEG; s += 256) {
+    const int row = s / SEG, seg = s % SEG;
+    const int m = tm * BM + row;
+    if (m < a.M)
+      *reinterpret_cast<u32x4*>(a.y + (long long)m * a.K + tn * BN + seg * 8) =
+          *reinterpret_cast<const u32x4*>(lds + row * OUT_LD + seg * 8);
+  }
+}
+
+void launch(const Igemm& a, hipStream_t s) {
+  const int mt = (a.M + BM - 1) / BM;
+  if (a.K % 128 == 0 && (long long)mt * (a.K / 128) >= 512) {
+    hipLaunchKernelGGL(k_conv_igemm<128>, dim3(mt * (a.K / 128)), dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL(k_conv_igemm<64>, dim3(mt * (a.K / 64)), dim3(256), 0, s, a);
+  }
+}
+
+}  // namespace
+
+bool conv_bf16_supported(const ConvGeom& g) {
+  return g.C % 64 == 0 && g.K % 64 == 0 && g.N > 0 && g.OH > 0 && g.OW > 0 &&
+         (long long)g.N * g.OH * g.OW < (1ll << 31) && (long long)g.N * g.H * g.W * g.C < (1ll << 40);
+}
+
+void conv_fwd_bf16(const void* x, const void* w_ohwi, void* y, const ConvGeom& g, hipStream_t s) {
+  Igemm a{static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w_ohwi), static_cast<uint16_t*>(y),
+          g.N, g.H, g.W, g.C, g.OH, g.OW, g.K, g.KH, g.KW, g.SH, g.SW, g.PT, g.PL, 0,
+          (long long)g.KH * g.KW * g.C, (long long)g.KW * g.C, (long long)g.C, g.N * g.OH * g.OW};
+  launch(a, s);
+}
+
+void conv_dgrad_bf16(const void* dy, const void* w_hwio, void* dx, const ConvGeom& g, hipStream_t s) {
+  // image = dy [N][OH][OW][K] (reduction channels K), output = dx [N][H][W][C] (columns C), stride 1,
+  // mirrored taps with padding KH-1-PT / KW-1-PL
+  Igemm a{static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w_hwio), static_cast<uint16_t*>(dx),
+          g.N, g.OH, g.OW, g.K, g.H, g.W, g.C, g.KH, g.KW, 1, 1, g.KH - 1 - g.PT, g.KW - 1 - g.PL, 1,
+          (long long)g.K, (long long)g.KW * g.C * g.K, (long long)g.C * g.K, g.N * g.H * g.W};
+  launch(a, s);
+}
+
+}  // namespace tdl

@@ -3,6 +3,7 @@
 #include <c10/hip/HIPStream.h>
 
 #include "kernels/bn.h"
+#include "kernels/conv.h"
 #include "kernels/ops.h"
 #include "kernels/pool.h"
 
@@ -145,9 +146,51 @@ at::Tensor maxpool_bwd(at::Tensor dy, at::Tensor arg, std::vector<int64_t> in_sh
                         cur_stream());
   return dx;
 }
+
+tdl::ConvGeom conv_geom(const at::Tensor& x, int64_t oh, int64_t ow, int64_t k, int64_t kh, int64_t kw, int64_t sh,
+                        int64_t sw, int64_t pt, int64_t pl) {
+  TORCH_CHECK(x.dim() == 4, "conv: NHWC activations expected");
+  tdl::ConvGeom g{(int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3), (int)oh, (int)ow, (int)k,
+                  (int)kh, (int)kw, (int)sh, (int)sw, (int)pt, (int)pl};
+  TORCH_CHECK(tdl::conv_bf16_supported(g), "conv: unsupported geometry (C and K must be multiples of 64)");
+  return g;
+}
+
+void conv_check(const at::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == at::kBFloat16, "conv: ", what,
+              " must be a contiguous bf16 GPU tensor");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "conv: ", what, " must be 16-byte aligned");
+}
+
+// y[N,OH,OW,K] = conv(x[N,H,W,C], w_ohwi[K,KH,KW,C]); top/left padding pt/pl, bottom/right implied by OH/OW
+at::Tensor conv_fwd(at::Tensor x, at::Tensor w_ohwi, int64_t oh, int64_t ow, int64_t sh, int64_t sw, int64_t pt,
+                    int64_t pl) {
+  conv_check(x, "x");
+  conv_check(w_ohwi, "w");
+  TORCH_CHECK(w_ohwi.dim() == 4 && w_ohwi.size(3) == x.size(3), "conv_fwd: weights must be OHWI [K,KH,KW,C]");
+  auto g = conv_geom(x, oh, ow, w_ohwi.size(0), w_ohwi.size(1), w_ohwi.size(2), sh, sw, pt, pl);
+  auto y = at::empty({x.size(0), oh, ow, w_ohwi.size(0)}, x.options());
+  tdl::conv_fwd_bf16(x.data_ptr(), w_ohwi.data_ptr(), y.data_ptr(), g, cur_stream());
+  return y;
+}
+
+// stride-1 input gradient: dx[N,H,W,C] from dy[N,OH,OW,K] and w_hwio[KH,KW,C,K]
+at::Tensor conv_dgrad(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w, int64_t pt, int64_t pl) {
+  conv_check(dy, "dy");
+  conv_check(w_hwio, "w");
+  TORCH_CHECK(w_hwio.dim() == 4 && w_hwio.size(3) == dy.size(3), "conv_dgrad: weights must be HWIO [KH,KW,C,K]");
+  tdl::ConvGeom g{(int)dy.size(0), (int)h, (int)w, (int)w_hwio.size(2), (int)dy.size(1), (int)dy.size(2),
+                  (int)dy.size(3), (int)w_hwio.size(0), (int)w_hwio.size(1), 1, 1, (int)pt, (int)pl};
+  TORCH_CHECK(tdl::conv_bf16_supported(g), "conv_dgrad: unsupported geometry (C and K must be multiples of 64)");
+  auto dx = at::empty({dy.size(0), h, w, w_hwio.size(2)}, dy.options());
+  tdl::conv_dgrad_bf16(dy.data_ptr(), w_hwio.data_ptr(), dx.data_ptr(), g, cur_stream());
+  return dx;
+}
 }  // namespace
 
 void register_ops(pybind11::module& m) {
+  m.def("conv_fwd", &conv_fwd, "NHWC bf16 implicit-GEMM convolution forward (MFMA)");
+  m.def("conv_dgrad", &conv_dgrad, "NHWC bf16 implicit-GEMM stride-1 convolution input gradient (MFMA)");
   m.def("gather_rows", &gather_rows, "row gather (+u8->f32 scale) of a device-resident dataset");
   m.def("gather_labels", &gather_labels);
   m.def("bn_forward_train", &bn_forward_train, "NHWC batch-norm training forward (+relu)", pybind11::arg("x"),

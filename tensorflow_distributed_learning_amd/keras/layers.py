@@ -19,6 +19,7 @@ import torch
 import torch.nn.functional as F
 
 from ..parallel.values import Variable, VariableAggregation, VariableSynchronization, create_variable
+from ..ops import conv as _conv
 from . import activations as _act
 from . import initializers as _init
 
@@ -313,17 +314,26 @@ class Conv2D(Layer):
         BatchNormalization (keras/fusion.py), so the convolution runs without it."""
         # (1x1 convs stay on MIOpen: routing them through hipBLASLt GEMMs measured slower on MI355X,
         #  scripts/probe_1x1_gemm.py)
-        w = self.kernel.value.to(x.dtype).permute(3, 2, 0, 1)  # HWIO -> OIHW
+        k_hwio = self.kernel.value.to(x.dtype)
+        w = k_hwio.permute(3, 2, 0, 1)  # HWIO -> OIHW
         h = x.permute(0, 3, 1, 2)  # NHWC data viewed as NCHW (channels_last memory format)
         pad = 0
+        symmetric = True
         if self.padding == "same":
             ph = _same_pads(h.shape[2], self.kernel_size[0], self.strides[0], self.dilation_rate[0])
             pw = _same_pads(h.shape[3], self.kernel_size[1], self.strides[1], self.dilation_rate[1])
             if ph[0] == ph[1] and pw[0] == pw[1]:
                 pad = (ph[0], pw[0])
             else:
+                symmetric = False
                 h = F.pad(h, (pw[0], pw[1], ph[0], ph[1]))
         b = self.bias.value.to(x.dtype) if (self.bias is not None and not _fold_bias) else None
+        if symmetric and _conv.supported(x, k_hwio, self.groups, self.dilation_rate):
+            # hand-written implicit-GEMM MFMA kernels (csrc/kernels/conv.hip), autotuned against MIOpen
+            y = _conv.conv2d_nhwc(x, k_hwio, self.strides, pad if pad else (0, 0))
+            if b is not None:
+                y = y + b
+            return self.activation(y)
         y = F.conv2d(h, w, b, stride=self.strides, padding=pad, dilation=self.dilation_rate, groups=self.groups)
         return self.activation(y.permute(0, 2, 3, 1))
 
