@@ -8,7 +8,8 @@
 // on 16 distinct 4-bank slots).  Global loads of tile t+1 are in flight while the MFMAs of tile t
 // run; one barrier per tile.  Out-of-image taps and rows past M load zeros (padding is implicit:
 // no padded copy of the activations is ever made).  Epilogue: the f32 tile is rounded to bf16 into
-// LDS and written back as full 16-byte row segments.
+// LDS (8-byte writes: the MFMA takes the weight fragment as its A operand, so each lane's four
+// accumulators are four adjacent channels of one pixel) and written back as 16-byte row segments.
 //
 // The same kernel computes the stride-1 input gradient: dy is the "image", the filter taps are
 // mirrored (kh -> KH-1-kh) and the weight rows are HWIO rows (K contiguous for fixed (kh, kw, c)).
@@ -144,7 +145,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_igemm(Igemm a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < NS; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < NS; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
     }
     if (t + 1 < ntiles) sstore(buf ^ 1);
     __syncthreads();
@@ -153,13 +154,16 @@ __global__ __launch_bounds__(256, 2) void k_conv_igemm(Igemm a) {
   // epilogue: bf16 tile into LDS ([BM][BN + 8]), then 16-B row segments to global
   constexpr int OUT_LD = BN + 8;
   static_assert(BM * OUT_LD <= 2 * (BM + BN) * LDS_ROW, "epilogue tile must fit the operand LDS");
+  // (operands are swapped in the MFMA, so a lane holds 4 consecutive channels of one pixel: one 8-B write)
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < NS; ++j)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr)
-        lds[(wm * 64 + i * 16 + (lane >> 4) * 4 + rr) * OUT_LD + wn * WN + j * 16 + (lane & 15)] = f2bf(acc[i][j][rr]);
+    for (int j = 0; j < NS; ++j) {
+      const uint32_t lo = f2bf(acc[i][j][0]) | ((uint32_t)f2bf(acc[i][j][1]) << 16);
+      const uint32_t hi = f2bf(acc[i][j][2]) | ((uint32_t)f2bf(acc[i][j][3]) << 16);
+      *reinterpret_cast<uint2*>(lds + (wm * 64 + i * 16 + (lane & 15)) * OUT_LD + wn * WN + j * 16 + (lane >> 4) * 4) =
+          make_uint2(lo, hi);
+    }
   __syncthreads();
   constexpr int SEG = BN / 8;  // 16-B segments per row
 #pragma unroll

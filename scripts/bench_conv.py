@@ -46,19 +46,25 @@ def main():
         w_ohwi = k.permute(3, 0, 1, 2).contiguous()
         xc = x.permute(0, 3, 1, 2)
         flop = 2.0 * B * OH * OW * K * KH * KH * Ci
+        y_h, y_m = C.conv_fwd(x, w_ohwi, OH, OW, s, s, p, p), F.conv2d(xc, w_oihw, None, s, p).permute(0, 2, 3, 1)
+        err = float((y_h.float() - y_m.float()).abs().max() / y_m.float().abs().max())
         t_h = t(lambda: C.conv_fwd(x, w_ohwi, OH, OW, s, s, p, p))
         t_m = t(lambda: F.conv2d(xc, w_oihw, None, s, p))
-        print(json.dumps({"dir": "fwd", "shape": [B, H, W, Ci, K, KH, s, p], "hip_us": round(t_h, 1),
+        print(json.dumps({"dir": "fwd", "shape": [B, H, W, Ci, K, KH, s, p], "rel_err": round(err, 5), "hip_us": round(t_h, 1),
                           "miopen_us": round(t_m, 1), "hip_tflops": round(flop / t_h / 1e6, 1),
                           "speedup": round(t_m / t_h, 3)}), flush=True)
         if s == 1:
             dy = torch.randn(B, OH, OW, K, device=dev).bfloat16()
             kc = k.contiguous()
             dyc = dy.permute(0, 3, 1, 2)
+            d_h = C.conv_dgrad(dy, kc, H, W, p, p)
+            d_m = torch.ops.aten.convolution_backward(dyc, xc, w_oihw, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
+                                                      [True, False, False])[0].permute(0, 2, 3, 1)
+            err = float((d_h.float() - d_m.float()).abs().max() / d_m.float().abs().max())
             t_h = t(lambda: C.conv_dgrad(dy, kc, H, W, p, p))
             t_m = t(lambda: torch.ops.aten.convolution_backward(dyc, xc, w_oihw, None, [s, s], [p, p], [1, 1], False,
                                                                 [0, 0], 1, [True, False, False]))
-            print(json.dumps({"dir": "dgrad", "shape": [B, H, W, Ci, K, KH, s, p], "hip_us": round(t_h, 1),
+            print(json.dumps({"dir": "dgrad", "shape": [B, H, W, Ci, K, KH, s, p], "rel_err": round(err, 5), "hip_us": round(t_h, 1),
                               "miopen_us": round(t_m, 1), "hip_tflops": round(flop / t_h / 1e6, 1),
                               "speedup": round(t_m / t_h, 3)}), flush=True)
 

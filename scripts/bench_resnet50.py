@@ -114,6 +114,13 @@ def main():
                        "engine": trainer.kind,
                        "communicator": comm.name, "final_loss": round(logs["loss"], 4)},
         }), flush=True)
+    if strategy.extended.rank == 0:
+        from tensorflow_distributed_learning_amd.ops import conv as _conv
+
+        ch = _conv.choices()
+        print(f"conv autotune: {sum(v == 'hip' for v in ch.values())}/{len(ch)} (shape, direction) pairs on the "
+              f"hand-written kernels: {sorted(k[0] + str(k[1][1:]) + str(k[2]) for k, v in ch.items() if v == 'hip')}",
+              file=sys.stderr, flush=True)
     strategy.shutdown()
 
 

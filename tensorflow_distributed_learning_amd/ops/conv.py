@@ -21,6 +21,7 @@ import torch.nn.functional as F
 from . import hip
 
 _choice: dict = {}  # (direction, shape key) -> True (hand-written kernel) / False (MIOpen)
+_times: dict = {}  # (direction, shape key) -> (hand-written ms, MIOpen ms) as measured by the autotuner
 
 
 def mode() -> str:
@@ -32,15 +33,20 @@ def supported(x: torch.Tensor, kernel_hwio: torch.Tensor, groups=1, dilation=(1,
             and x.shape[-1] % 64 == 0 and kernel_hwio.shape[-1] % 64 == 0 and mode() != "miopen")
 
 
-def _time(fn, reps=3) -> float:
+def _time(fn, reps=5) -> float:
+    """Median of ``reps`` individually timed calls after two untimed ones (the first MIOpen call of a
+    shape runs its find-mode solver search)."""
     fn()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
+    fn()
+    ts = []
     for _ in range(reps):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
         fn()
-    e.record()
-    e.synchronize()
-    return s.elapsed_time(e) / reps
+        e.record()
+        e.synchronize()
+        ts.append(s.elapsed_time(e))
+    return sorted(ts)[reps // 2]
 
 
 def _pick(key, hip_fn, ref_fn) -> bool:
@@ -52,8 +58,11 @@ def _pick(key, hip_fn, ref_fn) -> bool:
         return got
     if torch.cuda.is_current_stream_capturing():
         return False
-    got = _time(hip_fn) < _time(ref_fn)
+    t_ref = _time(ref_fn)
+    t_hip = _time(hip_fn)
+    got = t_hip < t_ref
     _choice[key] = got
+    _times[key] = (t_hip, t_ref)
     return got
 
 

@@ -77,3 +77,11 @@ def test_conv2d_layer_on_hip_kernels(monkeypatch):
     torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=2e-2)
     torch.testing.assert_close(x.grad.float(), xr.grad, atol=4e-2, rtol=2e-2)
     torch.testing.assert_close(kk.grad, kr.grad, atol=0.5, rtol=3e-2)
+
+
+@pytest.mark.parametrize("shape", [(64, 16, 16, 64, 512, 1, 1, 1, 0), (64, 16, 16, 128, 512, 3, 3, 1, 1),
+                                   (32, 56, 56, 64, 64, 3, 3, 1, 1)])
+def test_conv_fwd_dgrad_wide_tiles(shape):
+    """Grids of >= 512 workgroups take the 128-column tile variant."""
+    test_conv_fwd_matches_fp32(shape)
+    test_conv_dgrad_matches_fp32(shape)
