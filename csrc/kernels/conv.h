@@ -26,4 +26,7 @@ void conv_fwd_bf16(const void* x, const void* w_ohwi, void* y, const ConvGeom& g
 // Keras layout: for a fixed (kh, kw, c) the K reduction values are contiguous)
 void conv_dgrad_bf16(const void* dy, const void* w_hwio, void* dx, const ConvGeom& g, hipStream_t s);
 
+// Tile-sweep hook: 0 = per-shape heuristic (default), 1 = 128x64, 2 = 128x128, 3 = 256x128.
+void conv_force_tile(int tile);
+
 }  // namespace tdl

@@ -2,8 +2,8 @@
 //
 // GEMM view: rows = output pixels (n, oh, ow), columns = output channels, reduction =
 // (kh, kw, c) in chunks of 64 channels (C % 64 == 0, so a chunk never straddles a filter tap).
-// Workgroup tile 128 x BN (BN = 128 or 64) x 64, four waves as 2 x 2, each wave 64 x BN/2 built from
-// 16x16x32 MFMAs (4 x BN/32 accumulators).  Operands are register-staged through a double-buffered
+// Workgroup tile BM x BN x 64 (128 x 128; 128 x 64 when K % 128 != 0; 256 x 128 for sweeps), BM/64 x 2 waves, each
+// wave 64 x BN/2 built from 16x16x32 MFMAs (4 x BN/32 accumulators).  Operands are register-staged through a double-buffered
 // LDS image with 144-byte rows (64 bf16 + 16 B pad: the 16 rows an MFMA fragment read touches land
 // on 16 distinct 4-bank slots).  Global loads of tile t+1 are in flight while the MFMAs of tile t
 // run; one barrier per tile.  Out-of-image taps and rows past M load zeros (padding is implicit:
@@ -26,7 +26,6 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int BM = 128;
 constexpr int BK = 64;
 constexpr int LDS_ROW = BK + 8;  // bf16 elements per LDS row (144 B)
 
@@ -48,12 +47,14 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return (uint16_t)(u >> 16);
 }
 
-template <int BN>
-__global__ __launch_bounds__(256, 2) void k_conv_igemm(Igemm a) {
+template <int BM, int BN>
+__global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
+  constexpr int NT = BM * 2;         // threads: (BM / 64) x 2 waves, each 64 x BN/2
+  constexpr int RP = NT / 8;         // tile rows per staging pass (8 x 16-B chunks per 128-B row)
   constexpr int WN = BN / 2;         // columns per wave
   constexpr int NS = WN / 16;        // 16-wide column subtiles per wave
-  constexpr int A_LD = BM * BK / 8 / 256;  // 16-B A chunks per thread per tile (4)
-  constexpr int B_LD = BN * BK / 8 / 256;  // 16-B B chunks per thread per tile (4 or 2)
+  constexpr int A_LD = BM * BK / 8 / NT;  // 16-B A chunks per thread per tile (4)
+  constexpr int B_LD = BN * BK / 8 / NT;  // 16-B B chunks per thread per tile
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * (BM + BN) * LDS_ROW];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -72,7 +73,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_igemm(Igemm a) {
   int a_ih[A_LD], a_iw[A_LD];
 #pragma unroll
   for (int i = 0; i < A_LD; ++i) {
-    const int m = tm * BM + (tid >> 3) + 32 * i;
+    const int m = tm * BM + (tid >> 3) + RP * i;
     if (m < a.M) {
       const int ow = m % a.OW, t = m / a.OW, oh = t % a.OH, n = t / a.OH;
       a_ih[i] = oh * a.SH - a.PT;
@@ -86,7 +87,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_igemm(Igemm a) {
   }
   long long b_base[B_LD];
 #pragma unroll
-  for (int i = 0; i < B_LD; ++i) b_base[i] = (long long)(tn * BN + (tid >> 3) + 32 * i) * a.w_col + col8;
+  for (int i = 0; i < B_LD; ++i) b_base[i] = (long long)(tn * BN + (tid >> 3) + RP * i) * a.w_col + col8;
 
   u32x4 ra[A_LD], rb[B_LD];
   const int ctiles = a.C / BK;
@@ -114,10 +115,10 @@ __global__ __launch_bounds__(256, 2) void k_conv_igemm(Igemm a) {
     uint16_t* lb = la + BM * LDS_ROW;
 #pragma unroll
     for (int i = 0; i < A_LD; ++i)
-      *reinterpret_cast<u32x4*>(la + ((tid >> 3) + 32 * i) * LDS_ROW + col8) = ra[i];
+      *reinterpret_cast<u32x4*>(la + ((tid >> 3) + RP * i) * LDS_ROW + col8) = ra[i];
 #pragma unroll
     for (int i = 0; i < B_LD; ++i)
-      *reinterpret_cast<u32x4*>(lb + ((tid >> 3) + 32 * i) * LDS_ROW + col8) = rb[i];
+      *reinterpret_cast<u32x4*>(lb + ((tid >> 3) + RP * i) * LDS_ROW + col8) = rb[i];
   };
 
   f4v acc[4][NS];
@@ -167,7 +168,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_igemm(Igemm a) {
   __syncthreads();
   constexpr int SEG = BN / 8;  // 16-B segments per row
 #pragma unroll
-  for (int s = tid; s < BM * SEG; s += 256) {
+  for (int s = tid; s < BM * SEG; s += NT) {
     const int row = s / SEG, seg = s % SEG;
     const int m = tm * BM + row;
     if (m < a.M)
@@ -176,16 +177,27 @@ __global__ __launch_bounds__(256, 2) void k_conv_igemm(Igemm a) {
   }
 }
 
-void launch(const Igemm& a, hipStream_t s) {
+template <int BM, int BN>
+void launch_tile(const Igemm& a, hipStream_t s) {
   const int mt = (a.M + BM - 1) / BM;
-  if (a.K % 128 == 0 && (long long)mt * (a.K / 128) >= 512) {
-    hipLaunchKernelGGL(k_conv_igemm<128>, dim3(mt * (a.K / 128)), dim3(256), 0, s, a);
-  } else {
-    hipLaunchKernelGGL(k_conv_igemm<64>, dim3(mt * (a.K / 64)), dim3(256), 0, s, a);
-  }
+  hipLaunchKernelGGL((k_conv_igemm<BM, BN>), dim3(mt * (a.K / BN)), dim3(BM * 2), 0, s, a);
+}
+
+int g_forced_tile = 0;  // 0: heuristic below; 1: 128 x 64, 2: 128 x 128, 3: 256 x 128 (tile sweeps)
+
+// Tile choice, from the sweep over the ResNet-50 b=256 convolutions (profiles/conv_tile_sweep_r1.jsonl):
+// 128 x 128 wins every shape with K % 128 == 0, including the 7x7 ones whose grid is under two
+// workgroups per CU (the 64-column tile's extra LDS traffic per MFMA costs more than the idle CUs);
+// 256 x 128 loses 5-20 % everywhere.  The 64-column tile only serves K == 64 * odd.
+void launch(const Igemm& a, hipStream_t s) {
+  if (g_forced_tile == 3 && a.K % 128 == 0) return launch_tile<256, 128>(a, s);
+  if (g_forced_tile == 1 || a.K % 128 != 0) return launch_tile<128, 64>(a, s);
+  launch_tile<128, 128>(a, s);
 }
 
 }  // namespace
+
+void conv_force_tile(int tile) { g_forced_tile = tile; }
 
 bool conv_bf16_supported(const ConvGeom& g) {
   return g.C % 64 == 0 && g.K % 64 == 0 && g.N > 0 && g.OH > 0 && g.OW > 0 &&

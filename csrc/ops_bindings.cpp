@@ -189,6 +189,7 @@ at::Tensor conv_dgrad(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w, in
 }  // namespace
 
 void register_ops(pybind11::module& m) {
+  m.def("conv_force_tile", &tdl::conv_force_tile, "conv tile sweep hook (0 = heuristic)");
   m.def("conv_fwd", &conv_fwd, "NHWC bf16 implicit-GEMM convolution forward (MFMA)");
   m.def("conv_dgrad", &conv_dgrad, "NHWC bf16 implicit-GEMM stride-1 convolution input gradient (MFMA)");
   m.def("gather_rows", &gather_rows, "row gather (+u8->f32 scale) of a device-resident dataset");

@@ -34,6 +34,15 @@ def t(fn, reps=20):
     return s.elapsed_time(e) / reps * 1e3
 
 
+def sweep(C, fn):
+    out = []
+    for tile in (1, 2, 3):
+        C.conv_force_tile(tile)
+        out.append(round(t(fn), 1))
+    C.conv_force_tile(0)
+    return out
+
+
 def main():
     C = hip()
     dev = "cuda:0"
@@ -49,8 +58,9 @@ def main():
         y_h, y_m = C.conv_fwd(x, w_ohwi, OH, OW, s, s, p, p), F.conv2d(xc, w_oihw, None, s, p).permute(0, 2, 3, 1)
         err = float((y_h.float() - y_m.float()).abs().max() / y_m.float().abs().max())
         t_h = t(lambda: C.conv_fwd(x, w_ohwi, OH, OW, s, s, p, p))
+        tiles = sweep(C, lambda: C.conv_fwd(x, w_ohwi, OH, OW, s, s, p, p))
         t_m = t(lambda: F.conv2d(xc, w_oihw, None, s, p))
-        print(json.dumps({"dir": "fwd", "shape": [B, H, W, Ci, K, KH, s, p], "rel_err": round(err, 5), "hip_us": round(t_h, 1),
+        print(json.dumps({"dir": "fwd", "shape": [B, H, W, Ci, K, KH, s, p], "rel_err": round(err, 5), "hip_us": round(t_h, 1), "tiles_us": tiles,
                           "miopen_us": round(t_m, 1), "hip_tflops": round(flop / t_h / 1e6, 1),
                           "speedup": round(t_m / t_h, 3)}), flush=True)
         if s == 1:
@@ -62,9 +72,10 @@ def main():
                                                       [True, False, False])[0].permute(0, 2, 3, 1)
             err = float((d_h.float() - d_m.float()).abs().max() / d_m.float().abs().max())
             t_h = t(lambda: C.conv_dgrad(dy, kc, H, W, p, p))
+            tiles = sweep(C, lambda: C.conv_dgrad(dy, kc, H, W, p, p))
             t_m = t(lambda: torch.ops.aten.convolution_backward(dyc, xc, w_oihw, None, [s, s], [p, p], [1, 1], False,
                                                                 [0, 0], 1, [True, False, False]))
-            print(json.dumps({"dir": "dgrad", "shape": [B, H, W, Ci, K, KH, s, p], "rel_err": round(err, 5), "hip_us": round(t_h, 1),
+            print(json.dumps({"dir": "dgrad", "shape": [B, H, W, Ci, K, KH, s, p], "rel_err": round(err, 5), "hip_us": round(t_h, 1), "tiles_us": tiles,
                               "miopen_us": round(t_m, 1), "hip_tflops": round(flop / t_h / 1e6, 1),
                               "speedup": round(t_m / t_h, 3)}), flush=True)
 

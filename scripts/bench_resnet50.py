@@ -68,7 +68,7 @@ def main():
         model = tdl.keras.applications.ResNet50(weights=None, classes=args.classes, classifier_activation=None,
                                                 input_shape=(args.image, args.image, 3))
         model.compile(loss=tdl.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
-                      optimizer=tdl.keras.optimizers.SGD(learning_rate=0.1, momentum=0.9),
+                      optimizer=tdl.keras.optimizers.SGD(learning_rate=0.01, momentum=0.9),
                       metrics=["sparse_categorical_accuracy"])
     trainer = model._get_trainer()
     handler = trainer.prepare(ds) if hasattr(trainer, "prepare") else None

@@ -80,8 +80,9 @@ def test_conv2d_layer_on_hip_kernels(monkeypatch):
 
 
 @pytest.mark.parametrize("shape", [(64, 16, 16, 64, 512, 1, 1, 1, 0), (64, 16, 16, 128, 512, 3, 3, 1, 1),
-                                   (32, 56, 56, 64, 64, 3, 3, 1, 1)])
+                                   (32, 56, 56, 64, 64, 3, 3, 1, 1), (32, 56, 56, 128, 512, 1, 1, 1, 0),
+                                   (64, 32, 32, 64, 512, 3, 3, 1, 1)])
 def test_conv_fwd_dgrad_wide_tiles(shape):
-    """Grids of >= 512 workgroups take the 128-column tile variant."""
+    """Large grids take the 128 x 128 and 256 x 128 tile variants."""
     test_conv_fwd_matches_fp32(shape)
     test_conv_dgrad_matches_fp32(shape)
