@@ -4,8 +4,9 @@
 // (kh, kw, c) in chunks of 64 channels (C % 64 == 0, so a chunk never straddles a filter tap).
 // Workgroup tile BM x BN x 64 (128 x 128; 128 x 64 when K % 128 != 0; 256 x 128 for sweeps), BM/64 x 2 waves, each
 // wave 64 x BN/2 built from 16x16x32 MFMAs (4 x BN/32 accumulators).  Operands are register-staged through a double-buffered
-// LDS image with 144-byte rows (64 bf16 + 16 B pad: the 16 rows an MFMA fragment read touches land
-// on 16 distinct 4-bank slots).  Global loads of tile t+1 are in flight while the MFMAs of tile t
+// LDS image with 128-byte rows whose 16-byte chunks are XOR-swizzled by row (swz() below: conflict-free
+// fragment reads and staging writes; a 16-B row pad instead measured 34 % of LDS cycles in bank
+// conflicts, profiles/conv_pmc_r1_padded_rows.txt vs _swizzled.txt).  Global loads of tile t+1 are in flight while the MFMAs of tile t
 // run; one barrier per tile.  Out-of-image taps and rows past M load zeros (padding is implicit:
 // no padded copy of the activations is ever made).  Epilogue: the f32 tile is rounded to bf16 into
 // LDS (8-byte writes: the MFMA takes the weight fragment as its A operand, so each lane's four
@@ -27,7 +28,12 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BK = 64;
-constexpr int LDS_ROW = BK + 8;  // bf16 elements per LDS row (144 B)
+constexpr int LDS_ROW = BK;  // bf16 elements per LDS row (128 B, 16-B chunks XOR-swizzled by row)
+
+// 16-B chunk c of tile row r lives at chunk c ^ swz(r): every 16-lane group of a ds_read_b128 fragment
+// read (lanes {0-3,12-15,20-27}, {4-11,16-19,28-31}, ... on gfx950) and every 8-lane group of a
+// ds_write_b128 staging write then touches 16 (8) distinct 4-bank slots.
+__device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
 
 struct Igemm {
   const uint16_t* x;  // NHWC image [N][H][W][C]
@@ -93,9 +99,17 @@ __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
   const int ctiles = a.C / BK;
   const int ntiles = a.KH * a.KW * ctiles;
 
-  auto gload = [&](int t) {
-    const int c0 = (t % ctiles) * BK, tap = t / ctiles;
-    const int kw = tap % a.KW, kh = tap / a.KW;
+  // reduction position of the next tile to load (advanced incrementally: no per-tile div/mod)
+  int n_c = 0, n_kw = 0, n_kh = 0;
+  auto gload = [&](int) {
+    const int c0 = n_c * BK, kw = n_kw, kh = n_kh;
+    if (++n_c == ctiles) {
+      n_c = 0;
+      if (++n_kw == a.KW) {
+        n_kw = 0;
+        ++n_kh;
+      }
+    }
     const long long aoff = ((long long)kh * a.W + kw) * a.C + c0;
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
@@ -110,15 +124,16 @@ __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
 #pragma unroll
     for (int i = 0; i < B_LD; ++i) rb[i] = *reinterpret_cast<const u32x4*>(a.w + b_base[i] + boff);
   };
+  const int scol = ((tid & 7) ^ swz(tid >> 3)) * 8;  // swizzled LDS column of this thread's chunk (RP % 16 == 0)
   auto sstore = [&](int buf) {
     uint16_t* la = lds + buf * (BM + BN) * LDS_ROW;
     uint16_t* lb = la + BM * LDS_ROW;
 #pragma unroll
     for (int i = 0; i < A_LD; ++i)
-      *reinterpret_cast<u32x4*>(la + ((tid >> 3) + RP * i) * LDS_ROW + col8) = ra[i];
+      *reinterpret_cast<u32x4*>(la + ((tid >> 3) + RP * i) * LDS_ROW + scol) = ra[i];
 #pragma unroll
     for (int i = 0; i < B_LD; ++i)
-      *reinterpret_cast<u32x4*>(lb + ((tid >> 3) + RP * i) * LDS_ROW + col8) = rb[i];
+      *reinterpret_cast<u32x4*>(lb + ((tid >> 3) + RP * i) * LDS_ROW + scol) = rb[i];
   };
 
   f4v acc[4][NS];
@@ -130,19 +145,21 @@ __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
   gload(0);
   sstore(0);
   __syncthreads();
-  const int frow = lane & 15, fk = (lane >> 4) * 8;
+  const int frow = lane & 15;
+  const int fk0 = (((lane >> 4)) ^ swz(frow)) * 8, fk1 = (((lane >> 4) | 4) ^ swz(frow)) * 8;  // k 0-31, 32-63
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
     if (t + 1 < ntiles) gload(t + 1);
-    const uint16_t* la = lds + buf * (BM + BN) * LDS_ROW + (wm * 64 + frow) * LDS_ROW + fk;
-    const uint16_t* lb = lds + buf * (BM + BN) * LDS_ROW + BM * LDS_ROW + (wn * WN + frow) * LDS_ROW + fk;
+    const uint16_t* la = lds + buf * (BM + BN) * LDS_ROW + (wm * 64 + frow) * LDS_ROW;
+    const uint16_t* lb = lds + buf * (BM + BN) * LDS_ROW + BM * LDS_ROW + (wn * WN + frow) * LDS_ROW;
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 32) {
+      const int fk = kk ? fk1 : fk0;
       bf16x8 fa[4], fb[NS];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(la + i * 16 * LDS_ROW + kk);
+      for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(la + i * 16 * LDS_ROW + fk);
 #pragma unroll
-      for (int j = 0; j < NS; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(lb + j * 16 * LDS_ROW + kk);
+      for (int j = 0; j < NS; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(lb + j * 16 * LDS_ROW + fk);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
