@@ -140,6 +140,7 @@ class GenericTrainer:
         self.metrics = model.compiled_metrics
         self._policy = model._dtype_policy()
         self._buckets = self._make_buckets()
+        self._bind_cast_accumulate()
         # whole-step hipGraphs (forward + backward + all-reduce + optimizer + metrics), keyed by
         # the batch signature; the first two steps of a signature run eagerly (solver search,
         # allocator warm-up), the third is captured and every later one is a single replay
@@ -159,6 +160,15 @@ class GenericTrainer:
             leaf.grad = gview
             v._leaf = leaf
         self._leaves = [v._leaf for v in self.model._trainable_vars]
+        if hasattr(self, "_buckets"):
+            self._bind_cast_accumulate()
+
+    def _bind_cast_accumulate(self):
+        if self._buckets is None and os.environ.get("TDL_CAST_ACCUMULATE", "1") == "1":
+            # no bucket hooks to fire: compute-dtype weight copies accumulate their gradient
+            # straight into the slab view (Variable.cast)
+            for leaf in self._leaves:
+                leaf._tdl_gview = leaf.grad
 
     def _make_buckets(self):
         """Overlap of the gradient all-reduce with backward: contiguous slab buckets (reverse

@@ -253,7 +253,7 @@ class Dense(Layer):
         self.built = True
 
     def call(self, x, training=None):
-        y = torch.matmul(x, self.kernel.value.to(x.dtype))
+        y = torch.matmul(x, self.kernel.cast(x.dtype))
         if self.bias is not None:
             y = y + self.bias.value.to(y.dtype)
         return self.activation(y)
@@ -314,7 +314,7 @@ class Conv2D(Layer):
         BatchNormalization (keras/fusion.py), so the convolution runs without it."""
         # (1x1 convs stay on MIOpen: routing them through hipBLASLt GEMMs measured slower on MI355X,
         #  scripts/probe_1x1_gemm.py)
-        k_hwio = self.kernel.value.to(x.dtype)
+        k_hwio = self.kernel.cast(x.dtype)
         w = k_hwio.permute(3, 2, 0, 1)  # HWIO -> OIHW
         h = x.permute(0, 3, 1, 2)  # NHWC data viewed as NCHW (channels_last memory format)
         pad = 0

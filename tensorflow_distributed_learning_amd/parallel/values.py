@@ -32,6 +32,18 @@ class VariableAggregation(enum.Enum):
     ONLY_FIRST_REPLICA = 3
 
 
+class _CastAccumulate(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, leaf, gview, dtype):
+        ctx.gview = gview
+        return leaf.detach().to(dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        ctx.gview.add_(g.reshape(ctx.gview.shape))
+        return None, None, None
+
+
 class Variable:
     """A named tensor whose storage may be a view into a replica slab."""
 
@@ -62,6 +74,19 @@ class Variable:
             # inside a GradientTape: expose an autograd leaf sharing this variable's storage
             self._leaf = self._value.detach().requires_grad_(True)
         return self._leaf if self._leaf is not None else self._value
+
+    def cast(self, dtype: torch.dtype) -> torch.Tensor:
+        """``value.to(dtype)`` for a compute-dtype copy (mixed_bfloat16). When the generic trainer
+        bound the leaf's gradient to a slab view (``_tdl_gview``), the backward adds the bf16
+        gradient straight into that f32 view in one mixed-dtype kernel, instead of a bf16->f32
+        cast kernel followed by AccumulateGrad's f32 add (ResNet-50: 53 conv kernels per step)."""
+        t = self.value
+        if t.dtype == dtype:
+            return t
+        g = getattr(t, "_tdl_gview", None)
+        if g is not None and t.requires_grad and torch.is_grad_enabled():
+            return _CastAccumulate.apply(t, g, dtype)
+        return t.to(dtype)
 
     def read_value(self) -> torch.Tensor:
         return self._value

@@ -1,0 +1,34 @@
+"""Variable.cast: the bf16 compute copy's gradient lands in the slab view (engine/trainer.py)."""
+import torch
+
+from tensorflow_distributed_learning_amd.parallel.values import Variable
+
+
+def _grad_via(fused: bool):
+    torch.manual_seed(0)
+    v = Variable(torch.randn(3, 3, 4, 8), name="k")
+    G = torch.full((3 * 3 * 4 * 8 + 5,), 0.25)  # slab with a neighbour and non-zero start
+    gview = G[5:].view(3, 3, 4, 8)
+    leaf = v.read_value().detach().requires_grad_(True)
+    leaf.grad = gview
+    if fused:
+        leaf._tdl_gview = gview
+    v._leaf = leaf
+    x = torch.randn(16, 3 * 3 * 4, dtype=torch.bfloat16)
+    for _ in range(2):  # used twice in one step: both contributions accumulate
+        k = v.cast(torch.bfloat16)
+        assert k.dtype == torch.bfloat16
+        y = x @ k.reshape(-1, 8)
+        (y.float() ** 2).sum().backward()
+    return G
+
+
+def test_cast_accumulate_matches_autograd_accumulation():
+    a, b = _grad_via(True), _grad_via(False)
+    assert torch.equal(a[:5], torch.full((5,), 0.25))
+    torch.testing.assert_close(a, b, rtol=1e-2, atol=1e-2)
+
+
+def test_cast_same_dtype_is_identity():
+    v = Variable(torch.ones(4), name="b")
+    assert v.cast(torch.float32) is v.value
