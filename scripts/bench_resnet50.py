@@ -84,7 +84,14 @@ def main():
 
     if hasattr(trainer, "warm_graphs"):
         trainer.warm_graphs(args.steps)
-    trainer.run_train(handler, args.warmup)
+    if os.environ.get("TDL_TRACE_LOSS") == "1":  # per-step loss of the warm-up steps (diagnostic)
+        for i in range(args.warmup):
+            trainer.reset_metrics()
+            trainer.run_train(handler, 1)
+            print(f"warmup step {i}: loss {trainer.logs()['loss']:.4f}", flush=True)
+    else:
+        trainer.run_train(handler, args.warmup)
+    trainer.reset_metrics()  # the reported loss covers the timed steps only
     sync()
     comm.barrier()
     sync()

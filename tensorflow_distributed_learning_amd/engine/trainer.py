@@ -147,6 +147,9 @@ class GenericTrainer:
         self._graphs: Dict[tuple, tuple] = {}
         self._seen: Dict[tuple, int] = {}
         self._graph_ok: Optional[bool] = None
+        # metric accumulators start from zero for callers that drive run_train() directly
+        # (fit() resets them per epoch; scripts/bench_resnet50.py did not, and reported stale state)
+        self.reset_metrics()
         if self.device.type == "cuda" and os.environ.get("TDL_CONV_AUTOTUNE", "1") == "1":
             # like TF's cuDNN autotuning (TF_CUDNN_USE_AUTOTUNE=1): MIOpen find-mode search of the
             # conv solvers per shape on first use (+12% ResNet-50 step rate on MI355X)
