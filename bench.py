@@ -2,17 +2,25 @@
 """Headline benchmark: whole-node images/sec of the reference MNIST CNN (tf_dist_example.py)
 with global batch 64*N on N MI355X GPUs (BASELINE.json metric/config).
 
-    python bench.py                                   # N=1
+    python bench.py                                   # N=1 (exactly one replica, cuda:0)
+    python bench.py --gpus 8                          # self-launches 8 replica processes
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Runs the framework's real training path: MirroredStrategy (one process per GPU, RCCL over xGMI)
--> Keras Sequential exactly as the reference builds it -> compile(SCCE from_logits, SGD 1e-3,
-SparseCategoricalAccuracy) -> the fused MI355X engine (hand-written gfx950 kernels, device-resident
-synthetic MNIST-shaped dataset with map(scale).cache().shuffle(10000).batch(64*N).repeat(),
-hipGraph-captured executions incl. the gradient all-reduce and the SGD update).
+Runs the framework's training engine: MirroredStrategy over exactly N devices (one process per
+GPU; RCCL / the xGMI all-reduce kernel between them) -> Keras Sequential exactly as the reference
+builds it -> compile(SCCE from_logits, SGD 1e-3, SparseCategoricalAccuracy) -> the fused MI355X
+engine's executions (hand-written gfx950 kernels, device-resident synthetic MNIST-shaped dataset
+with map(scale).cache().shuffle(10000).batch(64*N).repeat(), hipGraph-captured executions incl.
+the gradient all-reduce and the SGD update).  The timed loop drives the trainer's execution loop
+(``run_train``, the loop ``Model.fit`` runs between callbacks) without progress-bar/log reads.
 W untimed warm-up steps, then EXACTLY K timed steps bracketed by barrier + device sync; the MAX
-time over ranks is reported by rank 0 as one JSON line.
+time over ranks is reported by rank 0 as one JSON line, together with a post-run check that the
+parameters are bit-identical on every replica.
+
+Without a launcher and N > 1 the script starts N-1 extra replica processes of itself before any
+GPU call (MirroredStrategy(devices=[/gpu:0 .. /gpu:N-1])).  With TDL_SHARE_GPU=1 the N replicas
+may share fewer physical GPUs (testing on a one-GPU box).
 """
 import argparse
 import json
@@ -25,6 +33,15 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 
+def _spe(K: int, cap: int = 200) -> int:
+    """Steps per execution: the largest divisor of K that is <= cap (one graph launch per
+    execution; the timed region replays K / spe graphs)."""
+    for d in range(min(K, cap), 0, -1):
+        if K % d == 0:
+            return d
+    return 1
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -32,30 +49,34 @@ def main():
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--per-replica-batch", type=int, default=64)
     ap.add_argument("--steps-per-execution", type=int, default=0, help="0 = auto")
+    ap.add_argument("--comm", choices=["auto", "nccl", "ring"], default="auto",
+                    help="CollectiveCommunication: AUTO (xGMI kernel + RCCL), NCCL (RCCL only), RING (TCP)")
     ap.add_argument("--take", type=int, default=0, help="diagnostics: train on the first N images only")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
 
     import torch
 
     import tensorflow_distributed_learning_amd as tdl
     from tensorflow_distributed_learning_amd.data import tfds
     from tensorflow_distributed_learning_amd.models.mnist_cnn import build_mnist_cnn
+    from tensorflow_distributed_learning_amd.parallel import consistency
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            print(f"bench.py: --gpus {args.gpus} needs a launcher (torch.distributed.run) with {args.gpus} ranks",
-                  file=sys.stderr)
-            sys.exit(2)
-    if world > 1 and "LOCAL_RANK" in os.environ:
-        torch.cuda.set_device(int(os.environ["LOCAL_RANK"]))
-
-    strategy = tdl.distribute.MirroredStrategy()
+    world = int(os.environ.get("WORLD_SIZE", "0") or 0)
+    if world and world != args.gpus:
+        raise SystemExit(f"bench.py: launched with WORLD_SIZE={world} but --gpus {args.gpus}")
+    # exactly N devices: on an 8-GPU node `--gpus 1` is ONE replica, `--gpus N` without a launcher
+    # spawns the other N-1 replica processes here (no GPU has been touched yet)
+    devices = [f"/gpu:{i}" for i in range(args.gpus)]
+    strategy = tdl.distribute.MirroredStrategy(devices=devices, communication=args.comm.upper())
     R = strategy.num_replicas_in_sync
+    if R != args.gpus:
+        raise SystemExit(f"bench.py: strategy has {R} replicas, expected {args.gpus}")
     rank = strategy.extended.rank
     B = args.per_replica_batch * R
     K, W = args.steps, args.warmup
-    spe = args.steps_per_execution or math.gcd(K, 50) or 1
+    spe = args.steps_per_execution or _spe(K)
 
     # synthetic MNIST-shaped data (no network): the reference's input pipeline
     (ds_all, info) = tfds.load("mnist", as_supervised=True, with_info=True)
@@ -85,8 +106,9 @@ def main():
     dev = strategy.extended.device
 
     trainer.warm_graphs(K)
-    trainer.warm_graphs(W)
-    trainer.run_train(handler, W)
+    if W:
+        trainer.warm_graphs(W)
+        trainer.run_train(handler, W)
     torch.cuda.synchronize(dev)
     comm.barrier()
     torch.cuda.synchronize(dev)
@@ -101,13 +123,14 @@ def main():
     t = torch.tensor([dt], dtype=torch.float64, device=dev if comm.name == "rccl" else "cpu")
     comm.all_reduce(t, "max")
     dt = float(t.item())
-    logs = trainer.logs()
+    logs = trainer.logs()  # also raises if an xGMI all-reduce timed out on this rank
+    identical = consistency.replicas_identical(comm, trainer.W)
     ips = K * B / dt
     ht = getattr(trainer, "_host_times", None)
     if ht:
         import numpy as np
 
-        a = np.array(ht[-(K // max(1, spe)):]) * 1e6
+        a = np.array(ht[-max(1, K // max(1, spe)):]) * 1e6
         print(f"host us per execution (take, upload, launch): median {np.median(a, 0).round(1).tolist()} "
               f"max {a.max(0).round(1).tolist()}", file=sys.stderr)
     if rank == 0:
@@ -130,9 +153,12 @@ def main():
                        "allreduce": getattr(comm, "algorithm", comm.name),
                        "steps_per_execution": spe, "graph_captured": bool(trainer.capture),
                        "allreduce_in_graph": bool(trainer.capture_comm and R > 1),
+                       "replicas_identical": identical,
                        "final_loss": round(logs["loss"], 4)},
         }), flush=True)
     strategy.shutdown()
+    if not identical:
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -6,8 +6,13 @@ Keras ResNet50 built with this framework, mixed_bfloat16 policy, SGD momentum 0.
     python scripts/bench_resnet50.py [--batch 256] [--steps 20] [--warmup 5]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 scripts/bench_resnet50.py
 
-Prints one JSON line (rank 0) in the bench.py format.  ``--engine`` picks the generic autograd
-engine ("generic") or the MI355X ResNet engine ("resnet", whole-step hipGraph + fused HIP kernels).
+    python scripts/bench_resnet50.py --gpus 8                      # config 4, self-launched replicas
+    python scripts/bench_resnet50.py --strategy mwms --workers 2 --gpus 8   # config 5 (2 tasks x 4 GPUs)
+
+Prints one JSON line (rank 0) in the bench.py format.  ``--strategy mwms`` without a TF_CONFIG in
+the environment starts ``--workers`` TF_CONFIG tasks on this node through the launcher
+(``launch_local_workers``: every task sees every GPU and pins its replicas to disjoint devices,
+so the xGMI all-reduce kernel and RCCL peer-to-peer work across tasks).
 """
 import argparse
 import json
@@ -26,30 +31,38 @@ def main():
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--classes", type=int, default=1000)
     ap.add_argument("--dtype", default="mixed_bfloat16", choices=["mixed_bfloat16", "float32"])
-    ap.add_argument("--engine", default="auto")
+    ap.add_argument("--gpus", type=int, default=1, help="replicas (GPUs) in the whole job")
+    ap.add_argument("--workers", type=int, default=2, help="--strategy mwms: TF_CONFIG tasks on this node")
+    ap.add_argument("--comm", choices=["auto", "nccl", "ring"], default="auto")
     ap.add_argument("--conv-search", type=int, default=1,
                     help="1: MIOpen find-mode solver search per conv shape (torch.backends.cudnn.benchmark)")
     ap.add_argument("--strategy", default="mirrored", choices=["mirrored", "mwms"],
                     help="mwms: MultiWorkerMirroredStrategy over TF_CONFIG workers (BASELINE config 5)")
     args = ap.parse_args()
 
+    if args.strategy == "mwms" and not os.environ.get("TF_CONFIG") and "WORLD_SIZE" not in os.environ:
+        # BASELINE config 5 on one node: K TF_CONFIG tasks x G GPUs each, started here (no GPU
+        # has been touched in this process)
+        from tensorflow_distributed_learning_amd.parallel.launch import launch_local_workers
+
+        if args.gpus % args.workers:
+            ap.error("--gpus must be a multiple of --workers")
+        sys.exit(launch_local_workers([sys.executable] + sys.argv, args.workers, args.gpus // args.workers))
+
     import torch
 
     import tensorflow_distributed_learning_amd as tdl
 
     torch.backends.cudnn.benchmark = bool(args.conv_search)
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1 and "LOCAL_RANK" in os.environ and torch.cuda.device_count() > 0:
-        torch.cuda.set_device(int(os.environ["LOCAL_RANK"]) % torch.cuda.device_count())
-    if args.engine != "auto":
-        os.environ["TDL_ENGINE"] = args.engine
     tdl.keras.mixed_precision.set_global_policy(args.dtype)
     if args.strategy == "mwms":
-        strategy = tdl.distribute.MultiWorkerMirroredStrategy()
+        strategy = tdl.distribute.MultiWorkerMirroredStrategy(communication=args.comm.upper())
     else:
-        strategy = tdl.distribute.MirroredStrategy()
+        strategy = tdl.distribute.MirroredStrategy(devices=[f"/gpu:{i}" for i in range(args.gpus)],
+                                                   communication=args.comm.upper())
     R = strategy.num_replicas_in_sync
+    if R != args.gpus:
+        raise SystemExit(f"bench_resnet50: strategy has {R} replicas, expected --gpus {args.gpus}")
     dev = strategy.extended.device
     b = args.batch
     B = b * R
@@ -106,6 +119,9 @@ def main():
     comm.all_reduce(t, "max")
     dt = float(t.item())
     logs = trainer.logs()
+    from tensorflow_distributed_learning_amd.parallel import consistency
+
+    identical = consistency.replicas_identical(comm, trainer.W)
     if strategy.extended.rank == 0:
         print(json.dumps({
             "metric": "images/sec (whole node) ResNet-50 synthetic ImageNet-shaped",
@@ -118,8 +134,10 @@ def main():
                        "image": args.image, "parallelism": f"dp{R}", "strategy": type(strategy).__name__,
                        "workers": (len(strategy.extended.tf_config.cluster.training_tasks())
                                    if getattr(strategy.extended, "tf_config", None) else 1),
-                       "engine": trainer.kind,
-                       "communicator": comm.name, "final_loss": round(logs["loss"], 4)},
+                       "engine": trainer.kind, "communicator": comm.name,
+                       "allreduce": getattr(comm, "algorithm", comm.name),
+                       "bucket_plan": getattr(trainer, "bucket_plan", None),
+                       "replicas_identical": identical, "final_loss": round(logs["loss"], 4)},
         }), flush=True)
     if strategy.extended.rank == 0:
         from tensorflow_distributed_learning_amd.ops import conv as _conv

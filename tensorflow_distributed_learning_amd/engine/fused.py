@@ -6,7 +6,7 @@ SparseCategoricalAccuracy) on a GPU replica is compiled into:
 
 * the model's flat parameter/gradient slabs (the same storage its MirroredVariables view);
 * a device-resident dataset (data/device.py) with per-step index vectors;
-* :class:`~..models.mnist_cnn.FusedMnistTrainStep` (8 hand-written gfx950 kernels);
+* :class:`~..models.mnist_cnn.FusedMnistTrainStep` (hand-written gfx950 kernels);
 * the cross-replica gradient all-reduce on RCCL (``world > 1``) followed by the SGD kernel;
 * ONE hipGraph per execution of ``steps_per_execution`` steps, replayed with a new index vector;
   with R > 1 the RCCL all-reduce is captured inside it as two buckets on a side stream, the dense
@@ -419,6 +419,16 @@ class FusedMnistTrainer:
 
     def finish(self):
         torch.cuda.synchronize(self.device)
+
+    def on_replica_divergence(self):
+        """The replicas' parameters differed after the custom xGMI all-reduce path (detected by
+        keras/models.py _check_replicas and already repaired from rank 0): drop that path and the
+        graphs that captured it; later executions all-reduce over RCCL / the ring."""
+        if getattr(self.comm, "xgmi", None) is not None:
+            self.comm.xgmi = None
+            self.comm.algorithm = "rccl" if self.comm.name == "rccl" else self.comm.name
+        self._graphs = {}
+        self._capture_comm = None
 
 
 class _IndexProducer:

@@ -163,6 +163,9 @@ class GenericTrainer:
             leaf.grad = gview
             v._leaf = leaf
         self._leaves = [v._leaf for v in self.model._trainable_vars]
+        if getattr(self, "_buckets", None) is not None:
+            # new leaves (after evaluate/predict): the bucket all-reduce hooks move with them
+            self._register_bucket_hooks()
         if hasattr(self, "_buckets"):
             self._bind_cast_accumulate()
 
@@ -192,8 +195,16 @@ class GenericTrainer:
                     var_bucket[i] = bi
         self._pending = [sum(1 for i in var_bucket if var_bucket[i] == b) for b in range(len(ranges))]
         self._bucket_ranges = ranges
+        self._var_bucket = var_bucket
         self._works = []
         self._counts = list(self._pending)
+        self._register_bucket_hooks()
+        return ranges
+
+    def _register_bucket_hooks(self):
+        """Post-accumulate hooks on the CURRENT leaves: the last gradient of a bucket launches that
+        bucket's asynchronous all-reduce."""
+        var_bucket = self._var_bucket
 
         def hook_for(i):
             b = var_bucket[i]
@@ -207,7 +218,6 @@ class GenericTrainer:
 
         for i, leaf in enumerate(self._leaves):
             leaf.register_post_accumulate_grad_hook(hook_for(i))
-        return ranges
 
     # ------------------------------------------------------------------ steps
     def _forward_loss(self, x, y, sw, global_n):
@@ -236,8 +246,14 @@ class GenericTrainer:
         if self._buckets is not None:
             self._counts = list(self._pending)
             self._works = []
-        with trace_range("tdl.forward"):
-            loss, per_ex, y_pred = self._forward_loss(x, y, sw, global_n)
+        from ..parallel import values as V
+
+        V.CAST_ACCUMULATE[0] += 1  # Variable.cast may add straight into the slab only in here
+        try:
+            with trace_range("tdl.forward"):
+                loss, per_ex, y_pred = self._forward_loss(x, y, sw, global_n)
+        finally:
+            V.CAST_ACCUMULATE[0] -= 1
         with trace_range("tdl.backward"):
             loss.backward()
         if self.comm.world_size > 1:

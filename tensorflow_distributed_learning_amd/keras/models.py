@@ -10,6 +10,7 @@ autograd engine otherwise (engine/trainer.py).
 from __future__ import annotations
 
 import math
+import os
 import sys
 import time
 import warnings
@@ -402,6 +403,9 @@ class Model(Layer):
                 logs.update({f"val_{k}": v for k, v in val.items()})
                 trainer = self._get_trainer()
             cb_list.on_epoch_end(epoch, logs)
+            every = int(os.environ.get("TDL_CHECK_REPLICAS_EVERY", "0") or 0)
+            if every > 0 and (epoch + 1) % every == 0:
+                self._check_replicas(trainer)
             if exhausted:
                 if self._is_chief():
                     warnings.warn("Your input ran out of data; interrupting training. Make sure that your dataset "
@@ -412,9 +416,24 @@ class Model(Layer):
         trainer.finish()
         if hasattr(handler, "close"):  # stop an index producer, commit the epochs it consumed
             handler.close()
+        if os.environ.get("TDL_CHECK_REPLICAS", "1") == "1":
+            self._check_replicas(trainer)
         cb_list.on_train_end(logs)
         self.history = history
         return history
+
+    def _check_replicas(self, trainer):
+        """Collective: the mirrored parameters must be bit-identical on every replica
+        (README.md:15-17).  On a mismatch rank 0's copy is broadcast and the trainer drops its
+        custom all-reduce path (parallel/consistency.py)."""
+        from ..parallel import consistency
+
+        comm = self._get_strategy().extended.communicator
+        if comm.world_size == 1 or self._W is None:
+            return
+        if not consistency.check_and_repair(comm, self._W):
+            if hasattr(trainer, "on_replica_divergence"):
+                trainer.on_replica_divergence()
 
     # ------------------------------------------------------------------ evaluate / predict
     def evaluate(self, x=None, y=None, batch_size=None, verbose="auto", sample_weight=None, steps=None,

@@ -12,7 +12,8 @@
         python -m tensorflow_distributed_learning_amd.launch --nproc-per-node 4 train.py
 
 Children get RANK / WORLD_SIZE / LOCAL_RANK / LOCAL_WORLD_SIZE (+ MASTER_ADDR/PORT when no
-TF_CONFIG is used, + TF_CONFIG and HIP_VISIBLE_DEVICES for --local-workers).  If any child fails
+TF_CONFIG is used, + TF_CONFIG and TDL_DEVICE_INDEX -- the node-global GPU of the replica -- for
+--local-workers).  If any child fails
 the others are terminated and the launcher exits with the failing code.
 """
 from __future__ import annotations
@@ -134,9 +135,16 @@ def launch_local_workers(cmd: List[str], workers: int, gpus_per_worker: int, bas
                        LOCAL_RANK=str(lr), LOCAL_WORLD_SIZE=str(gpus_per_worker), TDL_LAUNCHED="1")
             env.pop("MASTER_ADDR", None)
             env.pop("MASTER_PORT", None)
-            if gpus_per_worker > 0 and os.environ.get("TDL_NO_GPU_PARTITION") != "1":
+            if gpus_per_worker > 0:
                 first = t_rank * gpus_per_worker
-                env["HIP_VISIBLE_DEVICES"] = ",".join(str(first + i) for i in range(gpus_per_worker))
+                if os.environ.get("TDL_GPU_PARTITION") == "1":
+                    # opt-in: each task sees only its own GPUs (as on separate hosts); the xGMI
+                    # kernel's IPC mapping then fails its self-test and AUTO falls back to RCCL
+                    env["HIP_VISIBLE_DEVICES"] = ",".join(str(first + i) for i in range(gpus_per_worker))
+                else:
+                    # default: every task sees every GPU of the node and pins its replica to a
+                    # disjoint device, so peer IPC (xGMI kernel, RCCL P2P) works across tasks
+                    env["TDL_DEVICE_INDEX"] = str(first + lr)
             g.start(cmd, env)
     return g.wait()
 

@@ -385,9 +385,17 @@ class MirroredStrategy(Strategy):
 
             launched = maybe_spawn_local_replicas(len(devs), spawn=spawn)
             if launched is None:
+                import warnings
+
+                warnings.warn(
+                    f"MirroredStrategy: {len(devs)} devices requested but replica processes cannot be spawned "
+                    "from this entry point (interactive / `python -c` / `-m` / pytest, or TDL_AUTO_SPAWN=0); "
+                    f"running ONE replica on {devs[0]}. Start the script with "
+                    "`python -m tensorflow_distributed_learning_amd.launch --nproc-per-node N` for N replicas.",
+                    RuntimeWarning, stacklevel=2)
                 devs = devs[:1]
         if launched is None:
-            dev = devs[0]
+            dev = _shared_gpu(devs[0])
             comm = LocalCommunicator(dev)
             ext = StrategyExtended(self, dev, 0, 1, 0, comm, opts)
         else:
@@ -395,7 +403,7 @@ class MirroredStrategy(Strategy):
             if devices is not None:
                 if lr >= len(devs):
                     raise ValueError(f"local rank {lr} has no device in {devices}")
-                dev = devs[lr]
+                dev = _shared_gpu(devs[lr])
             else:
                 dev = _replica_device(lr)
             if dev.type == "cuda":
@@ -516,6 +524,16 @@ class experimental:  # noqa: N801 - tf.distribute.experimental namespace
     CommunicationOptions = CommunicationOptions
 
 
+def _shared_gpu(dev: torch.device) -> torch.device:
+    """TDL_SHARE_GPU=1: an explicit '/gpu:i' maps onto the visible GPUs round-robin (N replicas
+    on a one-GPU box for tests); otherwise the device is used as given."""
+    if dev.type == "cuda" and os.environ.get("TDL_SHARE_GPU") == "1":
+        n = torch.cuda.device_count()
+        if n > 0:
+            return torch.device("cuda", (dev.index or 0) % n)
+    return dev
+
+
 def _replica_device(local_rank: int) -> torch.device:
     """GPU of a replica process: cuda:<local_rank> (one process per GPU).  TDL_SHARE_GPU=1 maps
     several replica processes onto the visible GPUs round-robin (tests with the RING communicator on
@@ -523,6 +541,10 @@ def _replica_device(local_rank: int) -> torch.device:
     n = torch.cuda.device_count()
     if n == 0:
         return torch.device("cpu")
+    pinned = os.environ.get("TDL_DEVICE_INDEX")
+    if pinned:  # set by launch_local_workers: the node-global device of this replica
+        i = int(pinned)
+        return torch.device("cuda", i % n if os.environ.get("TDL_SHARE_GPU") == "1" else i)
     if os.environ.get("TDL_SHARE_GPU") == "1":
         return torch.device("cuda", local_rank % n)
     return torch.device("cuda", local_rank) if n > local_rank else torch.device("cpu")

@@ -16,6 +16,7 @@ import torch
 
 
 TAPE_DEPTH = [0]  # > 0 while a compat GradientTape is recording
+CAST_ACCUMULATE = [0]  # > 0 while GenericTrainer.train_step runs its forward (Variable.cast fast path)
 
 
 class VariableSynchronization(enum.Enum):
@@ -84,7 +85,10 @@ class Variable:
         if t.dtype == dtype:
             return t
         g = getattr(t, "_tdl_gview", None)
-        if g is not None and t.requires_grad and torch.is_grad_enabled():
+        # only inside the trainer's own step: a GradientTape loop (or any other autograd user) on
+        # the same leaves must see an ordinary differentiable cast, not a gradient routed into G
+        if (g is not None and CAST_ACCUMULATE[0] > 0 and TAPE_DEPTH[0] == 0 and t.requires_grad and
+                torch.is_grad_enabled()):
             return _CastAccumulate.apply(t, g, dtype)
         return t.to(dtype)
 

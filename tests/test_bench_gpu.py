@@ -1,0 +1,38 @@
+"""bench.py as the driver runs it: exactly N replicas for --gpus N, self-launched without a
+launcher, with the all-reduce algorithm and the replica-consistency check in the JSON line."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def _bench(args, **env_extra):
+    env = dict(os.environ, PYTHONPATH=ROOT, **env_extra)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "TF_CONFIG", "TDL_LAUNCHED"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
+                       text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_one_gpu_is_one_replica():
+    d = _bench(["--gpus", "1", "--steps", "20", "--warmup", "5"], HIP_VISIBLE_DEVICES="0")
+    assert d["n_gpus"] == 1 and d["config"]["global_batch"] == 64
+    assert d["config"]["engine"] == "fused" and d["config"]["replicas_identical"] is True
+    assert d["value"] > 0 and d["steps"] == 20
+
+
+def test_bench_two_replicas_self_launched_shared_gpu():
+    d = _bench(["--gpus", "2", "--steps", "20", "--warmup", "5"], TDL_SHARE_GPU="1")
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 128
+    assert d["config"]["allreduce"] == "xgmi-oneshot+gloo"
+    assert d["config"]["allreduce_in_graph"] is True
+    assert d["config"]["replicas_identical"] is True

@@ -1,6 +1,7 @@
 """Variable.cast: the bf16 compute copy's gradient lands in the slab view (engine/trainer.py)."""
 import torch
 
+from tensorflow_distributed_learning_amd.parallel import values as V
 from tensorflow_distributed_learning_amd.parallel.values import Variable
 
 
@@ -15,11 +16,15 @@ def _grad_via(fused: bool):
         leaf._tdl_gview = gview
     v._leaf = leaf
     x = torch.randn(16, 3 * 3 * 4, dtype=torch.bfloat16)
-    for _ in range(2):  # used twice in one step: both contributions accumulate
-        k = v.cast(torch.bfloat16)
-        assert k.dtype == torch.bfloat16
-        y = x @ k.reshape(-1, 8)
-        (y.float() ** 2).sum().backward()
+    V.CAST_ACCUMULATE[0] += 1  # as inside GenericTrainer.train_step
+    try:
+        for _ in range(2):  # used twice in one step: both contributions accumulate
+            k = v.cast(torch.bfloat16)
+            assert k.dtype == torch.bfloat16
+            y = x @ k.reshape(-1, 8)
+            (y.float() ** 2).sum().backward()
+    finally:
+        V.CAST_ACCUMULATE[0] -= 1
     return G
 
 
@@ -32,3 +37,17 @@ def test_cast_accumulate_matches_autograd_accumulation():
 def test_cast_same_dtype_is_identity():
     v = Variable(torch.ones(4), name="b")
     assert v.cast(torch.float32) is v.value
+
+
+def test_cast_outside_trainer_step_is_plain_autograd():
+    """A leaf left bound to a slab view by a trainer (after fit) must still get ordinary autograd
+    gradients in a custom loop (GradientTape under mixed_bfloat16), not have them routed into G."""
+    v = Variable(torch.randn(4, 8), name="k")
+    G = torch.zeros(32)
+    leaf = v.read_value().detach().requires_grad_(True)
+    leaf._tdl_gview = G.view(4, 8)
+    v._leaf = leaf
+    k = v.cast(torch.bfloat16)
+    assert k.grad_fn is not None and "CastAccumulate" not in type(k.grad_fn).__name__
+    g, = torch.autograd.grad(k.float().sum(), leaf)
+    assert torch.equal(g, torch.ones(4, 8)) and torch.count_nonzero(G) == 0

@@ -202,3 +202,36 @@ def test_optimizers_match_torch():
     s = keras.optimizers.schedules.ExponentialDecay(1.0, 10, 0.5)
     assert s(10) == pytest.approx(0.5)
     assert keras.optimizers.schedules.PiecewiseConstantDecay([5], [1.0, 0.1])(6) == 0.1
+
+
+def test_bucket_hooks_survive_evaluate_and_predict():
+    """evaluate()/predict() rebuild the autograd leaves; the bucketed all-reduce
+    hooks must follow them, or the next eager step finds no launched buckets."""
+    from tensorflow_distributed_learning_amd.parallel.communicator import LocalCommunicator, _Done
+
+    class FakeRccl(LocalCommunicator):
+        name = "rccl"
+
+        def __init__(self):
+            super().__init__(torch.device("cpu"))
+            self.world_size = 2
+            self.launched = 0
+
+        def all_reduce_async(self, t, op="sum"):
+            self.launched += 1
+            return _Done()
+
+    strategy = tdl.distribute.OneDeviceStrategy("/cpu:0")
+    fake = FakeRccl()
+    strategy.extended.communicator = fake
+    with strategy.scope():
+        m = build_mnist_cnn()
+        m.compile(loss=keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+                  optimizer=keras.optimizers.SGD(0.05), bucket_bytes=64 << 10)
+    m.fit(_ds(), epochs=1, steps_per_epoch=2, verbose=0)
+    nb = len(m._trainer._bucket_ranges)
+    assert nb > 1 and fake.launched == 2 * nb
+    m.evaluate(_ds(n=128, repeat=False), verbose=0)
+    m.predict(np.random.rand(3, 28, 28, 1).astype(np.float32))
+    m.fit(_ds(), epochs=1, steps_per_epoch=2, verbose=0)
+    assert fake.launched == 4 * nb
