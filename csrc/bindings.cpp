@@ -49,7 +49,7 @@ class MnistStep {
     dH_ = at::empty({b * 128}, f);
     dL_ = at::zeros({b * 10}, f);
     cnt_ = at::zeros({b}, f.dtype(at::kInt));
-    dC2_ = at::empty({b * 100 * 64}, f);
+    dP2_ = at::empty({b * 1600}, f);
     part2_ = at::zeros({b * tdl::kMnistPart2Rows * 64}, f);
     part1_ = at::zeros({(int64_t)tdl::mnist_part1_rows((int)b) * tdl::kMnistPart1Cols}, f);
     part3_ = at::zeros({(int64_t)tdl::kDense1Chunks * b * 128}, f);
@@ -70,7 +70,7 @@ class MnistStep {
     a_.dL = dL_.data_ptr<float>();
     a_.cnt = reinterpret_cast<unsigned*>(cnt_.data_ptr<int>());
     a_.head = 1;
-    a_.dC2 = dC2_.data_ptr<float>();
+    a_.dP2 = dP2_.data_ptr<float>();
     a_.part2 = part2_.data_ptr<float>();
     a_.part1 = part1_.data_ptr<float>();
     a_.part3 = part3_.data_ptr<float>();
@@ -86,26 +86,28 @@ class MnistStep {
     a_.idx = idx_.data_ptr<int>() + off;
   }
 
-  // Individual stages (tests / profiling): 5 dense1 bwd, 6 conv bwd, 8 fwd conv (+dense1, +head),
-  // 9 finalize.
+  // Individual stages (tests / profiling): 5 dP2 (+ dense weight grads if pending), 6 conv bwd,
+  // 8 fwd conv (+dense1, +head), 9 finalize.
   void stage(int64_t k, bool apply_sgd) {
     hipStream_t s = cur_stream();
     switch (k) {
-      case 5: tdl::mnist_dense1_bwd(a_, s); break;
+      case 5: tdl::mnist_dense1_bwd(a_, !dense_pending_, s); break;
       case 6: tdl::mnist_conv_bwd(a_, s); break;
       case 8: tdl::mnist_fwd_conv(a_, s); break;
-      case 9: tdl::mnist_finalize(a_, apply_sgd, s); break;
+      case 9: tdl::mnist_finalize(a_, apply_sgd, dense_pending_, s); break;
       default: TORCH_CHECK(false, "unknown stage");
     }
   }
 
-  // forward + loss + backward: leaves the complete gradient in G (after finalize).
+  // forward + loss + backward: leaves the complete gradient in G after finalize(), which also
+  // computes the dense weight gradients.
   void forward_backward(int64_t idx_off) {
     set_idx_offset(idx_off);
     hipStream_t s = cur_stream();
     tdl::mnist_fwd_conv(a_, s);
-    tdl::mnist_dense1_bwd(a_, s);
+    tdl::mnist_dense1_bwd(a_, false, s);
     tdl::mnist_conv_bwd(a_, s);
+    dense_pending_ = true;
   }
 
   // the same step split at the point where the dense-layer gradients are final in G (after K5):
@@ -114,11 +116,12 @@ class MnistStep {
     set_idx_offset(idx_off);
     hipStream_t s = cur_stream();
     tdl::mnist_fwd_conv(a_, s);
-    tdl::mnist_dense1_bwd(a_, s);
+    tdl::mnist_dense1_bwd(a_, true, s);
+    dense_pending_ = false;
   }
   void backward_conv() { tdl::mnist_conv_bwd(a_, cur_stream()); }
 
-  void finalize(bool apply_sgd) { tdl::mnist_finalize(a_, apply_sgd, cur_stream()); }
+  void finalize(bool apply_sgd) { tdl::mnist_finalize(a_, apply_sgd, dense_pending_, cur_stream()); }
 
   // forward features only (dense1 partials, no loss head / metrics)
   void forward_features(int64_t idx_off) {
@@ -139,11 +142,12 @@ class MnistStep {
     }
   }
 
-  std::vector<at::Tensor> buffers() { return {P1_, A1_, P2_, A2_, H_, dH_, dC2_, part2_, part1_, part3_, dL_}; }
+  std::vector<at::Tensor> buffers() { return {P1_, A1_, P2_, A2_, H_, dH_, dP2_, part2_, part1_, part3_, dL_}; }
 
  private:
   at::Tensor X_, Y_, idx_, W_, G_, lr_, metrics_;
-  at::Tensor P1_, A1_, P2_, A2_, H_, dH_, dC2_, part2_, part1_, part3_, dL_, cnt_;
+  at::Tensor P1_, A1_, P2_, A2_, H_, dH_, dP2_, part2_, part1_, part3_, dL_, cnt_;
+  bool dense_pending_ = true;
   at::Tensor stamps_;
   tdl::MnistArgs a_;
 };

@@ -25,6 +25,19 @@ __device__ __forceinline__ f4 zero4() { return f4{0.f, 0.f, 0.f, 0.f}; }
 __device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 __device__ __forceinline__ void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
 
+// Raw buffer resource over [base, base + bytes) (gfx9-family dword3 0x00020000).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+
+// 16-byte WRITE-THROUGH (sc1, aux 16) store: the bytes reach memory past this XCD's L2, so a
+// consumer workgroup on any XCD reads them with sc1 loads after the producer's vmcnt(0) drain and
+// an agent-scope counter/flag (MI355X_MICROARCH.md, inter-workgroup visibility).
+__device__ __forceinline__ void st4_sc1(__amdgpu_buffer_rsrc_t r, int byte_off, f4 v) {
+  typedef unsigned u4 __attribute__((ext_vector_type(4)));
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), r, byte_off, 0, 16);
+}
+
 // Sum across the four 16-lane groups of a wave (lanes l, l^16, l^32, l^48).
 __device__ __forceinline__ float sum_lane_groups(float v) {
   v += __shfl_xor(v, 16, 64);

@@ -10,13 +10,15 @@
 //                     the LAST of an image's 4 quarter workgroups (arrival counter) then runs the
 //                     head for that image: dense1 partial sum + bias + ReLU, dense2 + softmax-xent
 //                     + dlogits*(1/(b*R)) + loss/accuracy accumulators + dH (ReLU mask)
-//   K5 dense1_bwd   : dW3 = P2^T dH, db3, dP2 = dH W3^T -> pool2/ReLU backward scatter to dC2,
-//                     dW4 = H^T dL, db4
-//   KC conv_bwd     : per image (x4 parts), LDS-staged: dW2 (+db2 as an extra "ones" row) and
+//   K5 dense1_bwd   : dP2 = (dH W3^T) * relu-mask, one 16x16 MFMA tile per wave task (+ the
+//                     dense weight gradients dW3/db3/dW4/db4 when their bucket is all-reduced early)
+//   KC conv_bwd     : per image (x4 parts), LDS-staged (dC2 expanded from dP2 + pool-2 argmax):
+//                     dW2 (+db2 as an extra "ones" row) and
 //                     dP1 = dC2 (*) W2^T on MFMA with pool1/ReLU backward AND conv1 wgrad in
 //                     the epilogue (dC1 is never materialised); per-image partial slabs
-//   KF finalize     : deterministic reduction of the partial slabs into the flat gradient slab,
-//                     optionally fused with the SGD update (single replica)
+//   KF finalize     : deterministic reduction of the partial slabs into the flat gradient slab and
+//                     (unless K5 did) the dense weight gradients dW3 = P2^T dH (+db3), dW4 = H^T dL
+//                     (+db4), optionally fused with the SGD update (single replica)
 //
 // All reductions are slab-based (no float atomics) so every replica computes bit-identical
 // updates from identical inputs.
@@ -57,6 +59,43 @@ __device__ __forceinline__ void head_stamp(unsigned long long* buf, int k) {
     buf[(size_t)gridDim.x * 64 + blockIdx.x * 8 + k] = __builtin_amdgcn_s_memrealtime();
 }
 
+// Sums of 10 per-lane values over the wave, returned in every lane: a reduce-scatter butterfly
+// (lane halves keep 5 / 3 / 2 / 1 of the classes: 13 cross-lane moves instead of 10 x 6) whose
+// class sums end in lane groups, then broadcast by v_readlane.
+__device__ __forceinline__ void wave_sum10(const float (&v)[10], int l, float (&out)[10]) {
+  const bool b32 = l & 32, b16 = l & 16, b8 = l & 8, b4 = l & 4;
+  float u[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const float send = b32 ? v[j] : v[j + 5];
+    u[j] = (b32 ? v[j + 5] : v[j]) + __shfl_xor(send, 32, 64);
+  }
+  float w[3];  // b16 = 0 keeps u[0..2], b16 = 1 keeps u[3..4] (+0)
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const float hi = j + 3 < 5 ? u[j + 3] : 0.f;
+    const float send = b16 ? u[j] : hi;
+    w[j] = (b16 ? hi : u[j]) + __shfl_xor(send, 16, 64);
+  }
+  float x[2];  // b8 = 0 keeps w[0..1], b8 = 1 keeps w[2] (+0)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const float hi = j + 2 < 3 ? w[j + 2] : 0.f;
+    const float send = b8 ? w[j] : hi;
+    x[j] = (b8 ? hi : w[j]) + __shfl_xor(send, 8, 64);
+  }
+  float y = (b4 ? x[1] : x[0]) + __shfl_xor(b4 ? x[0] : x[1], 4, 64);
+  y += __shfl_xor(y, 2, 64);
+  y += __shfl_xor(y, 1, 64);
+  // class c sits in lane 32*hi + 16*b + 8*c8 + 4*d: c = 5*hi + (b ? 3 : 0) + (2*c8 + d)
+#pragma unroll
+  for (int c = 0; c < 10; ++c) {
+    const int hi = c / 5, kk = c % 5, bb = kk >= 3, wi = bb ? kk - 3 : kk;
+    const int lane = 32 * hi + 16 * bb + 8 * (wi >> 1) + 4 * (wi & 1);
+    out[c] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, y), lane));
+  }
+}
+
 __device__ __forceinline__ void head_row(const MnistArgs& a, int r, int l, int y, const HeadWeights& hw) {
   const float* wa = hw.wa;
   const float* wb = hw.wb;
@@ -74,27 +113,37 @@ __device__ __forceinline__ void head_row(const MnistArgs& a, int r, int l, int y
   h0 = fmaxf(h0, 0.f);
   h1 = fmaxf(h1, 0.f);
   head_stamp(a.stamps, 1);
-  a.H[r * 128 + l] = h0;
-  a.H[r * 128 + l + 64] = h1;
   float lg[10];
+  {
+    float v[10];
 #pragma unroll
-  for (int c = 0; c < 10; ++c) lg[c] = wave_sum(fmaf(h0, wa[c], h1 * wb[c])) + hw.b4[c];
+    for (int c = 0; c < 10; ++c) v[c] = fmaf(h0, wa[c], h1 * wb[c]);
+    wave_sum10(v, l, lg);
+  }
+#pragma unroll
+  for (int c = 0; c < 10; ++c) lg[c] += hw.b4[c];
   float m = lg[0];
   int am = 0;
 #pragma unroll
   for (int c = 1; c < 10; ++c)
     if (lg[c] > m) { m = lg[c]; am = c; }
-  float se = 0.f;
+  // softmax on the hardware exp2/log2 (v_exp_f32 / v_log_f32): |logit - max| is small here, so
+  // the log2(e) pre-scale costs ~1e-7 relative, far inside the f32 oracle tolerance
+  float e[10], se = 0.f;
 #pragma unroll
-  for (int c = 0; c < 10; ++c) se += expf(lg[c] - m);
-  const float lse = m + logf(se);
+  for (int c = 0; c < 10; ++c) {
+    e[c] = __expf(lg[c] - m);
+    se += e[c];
+  }
+  const float lse = m + __logf(se);
+  const float inv = 1.f / se;
   head_stamp(a.stamps, 2);
   float ly = lg[0];
 #pragma unroll
   for (int c = 1; c < 10; ++c) ly = (c == y) ? lg[c] : ly;
   float dl[10];
 #pragma unroll
-  for (int c = 0; c < 10; ++c) dl[c] = (expf(lg[c] - lse) - (c == y ? 1.f : 0.f)) * a.scale;
+  for (int c = 0; c < 10; ++c) dl[c] = (e[c] * inv - (c == y ? 1.f : 0.f)) * a.scale;
   float d0 = 0.f, d1 = 0.f, mine = 0.f;
 #pragma unroll
   for (int c = 0; c < 10; ++c) {
@@ -104,6 +153,8 @@ __device__ __forceinline__ void head_row(const MnistArgs& a, int r, int l, int y
   }
   a.dH[r * 128 + l] = h0 > 0.f ? d0 : 0.f;
   a.dH[r * 128 + l + 64] = h1 > 0.f ? d1 : 0.f;
+  a.H[r * 128 + l] = h0;
+  a.H[r * 128 + l + 64] = h1;
   if (l < 10) a.dL[r * 10 + l] = mine;
   if (l == 0) {
     atomicAdd(&a.metrics[0], lse - ly);
@@ -114,118 +165,140 @@ __device__ __forceinline__ void head_row(const MnistArgs& a, int r, int l, int y
 }
 
 // --------------------------------------------------------------------------------------------
-// K5: dense1 backward.  blocks [0,200): dW3 tiles; [200, 200+nP): dP2 tiles with the pool2 /
-// relu backward scatter into dC2; last block: db3.
+// K5: dense-layer backward, one 16x16 MFMA output tile per wave task (every task's loads issued
+// in one round trip; biases are an extra "ones" row of the weight-gradient GEMMs):
+//   tasks [0, 808)        dW3 = P2^T dH (M = 1600 features + db3 row, N = 128, K = b)
+//   tasks [808, +100 MT)  dP2 = (dH W3^T) * 1[P2 > 0]  (M = b, N = 1600, K = 128): the pool-2 /
+//                         ReLU mask; k_conv_bwd expands it to the conv2-output gradient itself
+//   tasks [.., + 9)       dW4 = H^T dL (+ db4 row) (M = 128 + 1, N = 10, K = b)
+// Block 0 also re-arms the per-image head counters of k_fwd_conv for the next step.
 // --------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_dense1_bwd(MnistArgs a) {
+constexpr int kD1TasksW3 = 101 * 8;
+
+// acc += A^T B over K = b rows, A rows a_row(r)[m], B rows b_row(r)[n]: lane (i, g) supplies
+// A[r = 4s + g][m0 + i] and B[r][n0 + i]; 64 rows' loads in flight per batch.
+template <typename FA, typename FB>
+__device__ __forceinline__ f4 gemm_tn_rows(int b, int g, FA fa, FB fb) {
+  f4 acc0 = zero4(), acc1 = zero4();
+  for (int r0 = 0; r0 < b; r0 += 64) {
+    float av[16], bv[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int rr = min(r0 + 4 * s + g, b - 1);
+      av[s] = fa(rr);
+      bv[s] = fb(rr);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const float x = (r0 + 4 * s + g < b) ? av[s] : 0.f;
+      if (s & 1) acc1 = mfma16x16x4(x, bv[s], acc1);
+      else acc0 = mfma16x16x4(x, bv[s], acc0);
+    }
+  }
+  return acc0 + acc1;
+}
+
+// One dense weight-gradient task T in [0, kDenseTasks) for the wave (optionally fused with plain
+// SGD of its outputs: nothing else in the launch reads W3 / W4 then).
+constexpr int kDenseTasks = kD1TasksW3 + 9;
+
+__device__ __forceinline__ void dense_w_task(const MnistArgs& a, int T, int lane, bool sgd, float lr) {
+  const int i = lane & 15, g = lane >> 4;
+  const int b = a.b;
+  if (T < kD1TasksW3) {
+    const int mt = T >> 3, nt = T & 7, n = nt * 16 + i;
+    if (mt < 100) {
+      const int kf = mt * 16 + i;
+      const f4 acc = gemm_tn_rows(
+          b, g, [&](int r) { return a.P2[(size_t)r * 1600 + kf]; }, [&](int r) { return a.dH[r * 128 + n]; });
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int e = a.ow3 + (mt * 16 + 4 * g + r) * 128 + n;
+        a.G[e] = acc[r];
+        if (sgd) a.W[e] -= lr * acc[r];
+      }
+    } else {  // db3: A = e_0 (row 0 of the tile = column sums of dH)
+      const f4 acc = gemm_tn_rows(
+          b, g, [&](int) { return i == 0 ? 1.f : 0.f; }, [&](int r) { return a.dH[r * 128 + n]; });
+      if (g == 0) {
+        a.G[a.ob3 + n] = acc[0];
+        if (sgd) a.W[a.ob3 + n] -= lr * acc[0];
+      }
+    }
+    return;
+  }
+  const int T3 = T - kD1TasksW3;
+  if (T3 < 9) {
+    // dW4[k][c] = sum_r H[r][k] dL[r][c] (tiles 0..7), db4 (tile 8, A = e_0); N = 10 of 16
+    const int c = min(i, 9);
+    const float cm = i < 10 ? 1.f : 0.f;
+    const f4 acc = gemm_tn_rows(
+        b, g, [&](int r) { return T3 < 8 ? a.H[r * 128 + T3 * 16 + i] : (i == 0 ? 1.f : 0.f); },
+        [&](int r) { return a.dL[r * 10 + c] * cm; });
+    if (i < 10) {
+      if (T3 < 8) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int e = a.ow4 + (T3 * 16 + 4 * g + r) * 10 + i;
+          a.G[e] = acc[r];
+          if (sgd) a.W[e] -= lr * acc[r];
+        }
+      } else if (g == 0) {
+        a.G[a.ob4 + i] = acc[0];
+        if (sgd) a.W[a.ob4 + i] -= lr * acc[0];
+      }
+    }
+  }
+}
+
+// K5: dP2 = (dH W3^T) * 1[P2 > 0] (M = b, N = 1600, K = 128), one 16x16 tile per wave task, the
+// pool-2 / ReLU mask in the epilogue (k_conv_bwd expands it to the conv2-output gradient); with
+// `with_dense` also the dense weight-gradient tasks (R > 1: that bucket's all-reduce then overlaps
+// the conv backward; at R = 1 k_finalize runs them).  Block 0 re-arms the forward's per-image
+// head counters for the next step.
+__global__ __launch_bounds__(256) void k_dense1_bwd(MnistArgs a, int with_dense) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int i = lane & 15, g = lane >> 4;
   const int b = a.b;
   const int MT = (b + 15) >> 4;
-  const int nP = (MT * 100 + 3) >> 2;
-  const int blk = blockIdx.x;
-  if (blk < 200) {
-    // dW3[k][n] = sum_r P2[r][k] dH[r][n]   (M = 1600 features, N = 128, K = b)
-    const int T = blk * 4 + wave, mt = T >> 3, nt = T & 7;
-    const int kf = mt * 16 + i, n = nt * 16 + i;
-    // rows in batches of 64 (16 MFMA k-steps); all 32 loads of a batch in flight together.
-    f4 acc0 = zero4(), acc1 = zero4();
-    for (int r0 = 0; r0 < b; r0 += 64) {
-      float av[16], bv[16];
+  if (blockIdx.x == 0)
+    for (int r = threadIdx.x; r < b; r += 256) a.cnt[r] = 0u;
+  const int T = blockIdx.x * 4 + wave;
+  if (T >= MT * 100) {
+    if (with_dense && T - MT * 100 < kDenseTasks) dense_w_task(a, T - MT * 100, lane, false, 0.f);
+    return;
+  }
+  const int mt = T % MT, nt = T / MT;
+  const int row = mt * 16 + i;
+  const bool valid = row < b;
+  const float* ap = a.dH + (valid ? row : 0) * 128 + 4 * g;
+  const float* bp = a.W + a.ow3 + (size_t)(nt * 16 + i) * 128 + 4 * g;
+  f4 av[8], bv[8];
 #pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const int rr = min(r0 + 4 * s + g, b - 1);
-        av[s] = a.P2[(size_t)rr * 1600 + kf];
-        bv[s] = a.dH[rr * 128 + n];
-      }
-      __builtin_amdgcn_sched_barrier(0);
+  for (int s = 0; s < 8; ++s) {
+    av[s] = ld4(ap + s * 16);
+    bv[s] = ld4(bp + s * 16);
+  }
+  float p2v[4];  // the epilogue's ReLU-mask operands in the same round trip
 #pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const float x = (r0 + 4 * s + g < b) ? av[s] : 0.f;
-        if (s & 1) acc1 = mfma16x16x4(x, bv[s], acc1);
-        else acc0 = mfma16x16x4(x, bv[s], acc0);
-      }
-    }
-    const f4 acc = acc0 + acc1;
+  for (int r = 0; r < 4; ++r) p2v[r] = a.P2[(size_t)min(mt * 16 + 4 * g + r, b - 1) * 1600 + nt * 16 + i];
+  __builtin_amdgcn_sched_barrier(0);
+  const float vm = valid ? 1.f : 0.f;
+  f4 acc0 = zero4(), acc1 = zero4();
 #pragma unroll
-    for (int r = 0; r < 4; ++r) a.G[a.ow3 + (mt * 16 + 4 * g + r) * 128 + nt * 16 + i] = acc[r];
-  } else if (blk < 200 + nP) {
-    // dP2[r][k] = sum_n dH[r][n] W3[k][n]  (M = b, N = 1600, K = 128)
-    const int T = (blk - 200) * 4 + wave;
-    if (T >= MT * 100) return;
-    const int mt = T % MT, nt = T / MT;
-    const int row = mt * 16 + i;
-    const bool valid = row < b;
-    const float* ap = a.dH + (valid ? row : 0) * 128 + 4 * g;
-    const float* bp = a.W + a.ow3 + (size_t)(nt * 16 + i) * 128 + 4 * g;
-    f4 av[8], bv[8];
+  for (int s = 0; s < 8; ++s) {
+    const f4 x = av[s] * vm;
+    acc0 = mfma16x16x4(x.x, bv[s].x, acc0);
+    acc1 = mfma16x16x4(x.y, bv[s].y, acc1);
+    acc0 = mfma16x16x4(x.z, bv[s].z, acc0);
+    acc1 = mfma16x16x4(x.w, bv[s].w, acc1);
+  }
+  const f4 acc = acc0 + acc1;
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      av[s] = ld4(ap + s * 16);
-      bv[s] = ld4(bp + s * 16);
-    }
-    // epilogue operands (pool2 output and argmax of the tile's 4 rows) in the same round trip
-    float p2v[4];
-    unsigned a2v[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const size_t e = (size_t)min(mt * 16 + 4 * g + r, b - 1) * 1600 + nt * 16 + i;
-      p2v[r] = a.P2[e];
-      a2v[r] = a.A2[e];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    const float vm = valid ? 1.f : 0.f;
-    f4 acc0 = zero4(), acc1 = zero4();
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const f4 x = av[s] * vm;
-      acc0 = mfma16x16x4(x.x, bv[s].x, acc0);
-      acc1 = mfma16x16x4(x.y, bv[s].y, acc1);
-      acc0 = mfma16x16x4(x.z, bv[s].z, acc0);
-      acc1 = mfma16x16x4(x.w, bv[s].w, acc1);
-    }
-    const f4 acc = acc0 + acc1;
-    const int k = nt * 16 + i, pp = k >> 6, co = k & 63;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int rr = mt * 16 + 4 * g + r;
-      if (rr < b) {
-        const float v = p2v[r] > 0.f ? acc[r] : 0.f;
-        const unsigned qa = a2v[r];
-        const int ph = pp / 5, pw = pp - ph * 5;
-        float* d = a.dC2 + ((size_t)(rr * 10 + 2 * ph) * 10 + 2 * pw) * 64 + co;  // [b][10][10][64]
-        d[0] = qa == 0 ? v : 0.f;
-        d[64] = qa == 1 ? v : 0.f;
-        d[640] = qa == 2 ? v : 0.f;
-        d[704] = qa == 3 ? v : 0.f;
-      }
-    }
-  } else if (blk == 200 + nP) {
-    if (threadIdx.x < 128) {
-      float s = 0.f;
-      for (int r = 0; r < b; ++r) s += a.dH[r * 128 + threadIdx.x];
-      a.G[a.ob3 + threadIdx.x] = s;
-    }
-  } else {
-    // dW4[k][c] = sum_r H[r][k] dL[r][c], db4[c] = sum_r dL[r][c]; 16 rows' loads in flight
-    const int o = (blk - 201 - nP) * 256 + threadIdx.x;
-    if (o < 1290) {
-      const int k = o < 1280 ? o / 10 : 0, c = o < 1280 ? o % 10 : o - 1280;
-      const bool bias = o >= 1280;
-      float s = 0.f;
-      for (int r0 = 0; r0 < b; r0 += 16) {
-        float hv[16], lv[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const int r = min(r0 + j, b - 1);
-          hv[j] = bias ? 1.f : a.H[r * 128 + k];
-          lv[j] = a.dL[r * 10 + c];
-        }
-#pragma unroll
-        for (int j = 0; j < 16; ++j) s = (r0 + j < b) ? fmaf(hv[j], lv[j], s) : s;
-      }
-      a.G[o < 1280 ? a.ow4 + o : a.ob4 + (o - 1280)] = s;
-    }
+  for (int r = 0; r < 4; ++r) {
+    const int rr = mt * 16 + 4 * g + r;
+    if (rr < b) a.dP2[(size_t)rr * 1600 + nt * 16 + i] = p2v[r] > 0.f ? acc[r] : 0.f;
   }
 }
 
@@ -270,17 +343,24 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
   // round trip for the whole staging), then all LDS stores.  Out-of-range slots load a valid
   // address and are zeroed by a multiply (no per-element branch around a load). ----
   constexpr int kIdc = (kLdsDc / 4 + 511) / 512, kIp1 = (169 * 8 + 511) / 512, kIwd = (kLdsWd / 4 + 511) / 512;
+  // the conv2-output gradient is expanded here from the pooled gradient dP2 (ReLU-masked by
+  // k_dense1_bwd) and the pool-2 argmax bytes: cell (y, x) of window (y/2, x/2) gets the
+  // window's value where the argmax is (y&1)*2 + (x&1), else 0 (4x fewer bytes than a dC2 read)
   f4 vdc[kIdc], vp1[kIp1], vwd[kIwd], vx;
-  float mdc[kIdc];
-  const float* dcb = a.dC2 + (size_t)bi * 6400;
+  unsigned qdc[kIdc];
+  int sel[kIdc];
+  const float* dpb = a.dP2 + (size_t)bi * 1600;
+  const unsigned* a2b = reinterpret_cast<const unsigned*>(a.A2 + (size_t)bi * 1600);
 #pragma unroll
   for (int j = 0; j < kIdc; ++j) {
     const int e4 = tid + j * 512;
     const int cell = e4 / 17, c4 = e4 - cell * 17;
     const int y = cell / kDcDim - 2, x = cell - (cell / kDcDim) * kDcDim - 2;
     const bool in = e4 < kLdsDc / 4 && c4 < 16 && y >= 0 && y < 10 && x >= 0 && x < 10;
-    mdc[j] = in ? 1.f : 0.f;
-    vdc[j] = ld4(dcb + (in ? (y * 10 + x) * 64 + c4 * 4 : 0));
+    const int o = in ? ((y >> 1) * 5 + (x >> 1)) * 64 + c4 * 4 : 0;
+    sel[j] = in ? (y & 1) * 2 + (x & 1) : 4;  // 4 = border / pad: no byte matches
+    vdc[j] = ld4(dpb + o);
+    qdc[j] = a2b[o >> 2];
   }
   const float* p1b = a.P1 + (size_t)bi * 169 * 32;
 #pragma unroll
@@ -299,7 +379,13 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
 #pragma unroll
   for (int j = 0; j < kIdc; ++j) {
     const int e4 = tid + j * 512;
-    if (e4 < kLdsDc / 4) st4(dCs + e4 * 4, vdc[j] * mdc[j]);
+    if (e4 < kLdsDc / 4) {
+      const unsigned q = qdc[j];
+      const unsigned s = (unsigned)sel[j];
+      const f4 v = vdc[j];
+      st4(dCs + e4 * 4, f4{(q & 0xffu) == s ? v.x : 0.f, ((q >> 8) & 0xffu) == s ? v.y : 0.f,
+                           ((q >> 16) & 0xffu) == s ? v.z : 0.f, (q >> 24) == s ? v.w : 0.f});
+    }
   }
 #pragma unroll
   for (int j = 0; j < kIp1; ++j) {
@@ -448,7 +534,32 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
 //   with the 205 KB W3 slice loaded into registers at kernel start (its latency hides behind the
 //   convolutions); the head sums the 4 quarter partials + bias + ReLU.
 // --------------------------------------------------------------------------------------------
-constexpr int kLdsFwd = 784 + 320 + 169 * kP1Stride + 72 * 16 * 4 + 400 + 4;
+constexpr int kLdsFwd = 784 + 320 + 169 * kP1Stride + 72 * 16 * 4 + 400 + 169 * 32 / 4 + 400 / 4 + 16 * 128 + 4;
+
+// Saved-for-backward activations of one (image, quarter) workgroup, written from LDS AFTER the
+// head hand-off (no global store sits in the conv phases, where it would queue behind the W3
+// prefetch in the CU's vector-memory pipe): this quarter's share of P1 / A1 (whole image,
+// 338 16-B chunks / 338 words) and its 16 channels of P2 / A2 (25 windows).
+__device__ __forceinline__ void store_saved_fwd(const MnistArgs& a, int bi, int cq, const float* P1s,
+                                                const uint8_t* a1s, const float* p2s, const uint8_t* a2s,
+                                                int t, int nt) {
+  for (int e = t; e < 2 * 338 + 200; e += nt) {
+    if (e < 338) {
+      const int e4 = cq * 338 + e, pos = e4 >> 3, c4 = (e4 & 7) * 4;
+      st4(a.P1 + (size_t)bi * 5408 + e4 * 4, ld4(P1s + pos * kP1Stride + c4));
+    } else if (e < 676) {
+      const int w = cq * 338 + (e - 338);
+      reinterpret_cast<unsigned*>(a.A1 + (size_t)bi * 5408)[w] = reinterpret_cast<const unsigned*>(a1s)[w];
+    } else if (e < 776) {
+      const int u = e - 676, wo = u >> 2, q = u & 3;
+      st4(a.P2 + (size_t)bi * 1600 + wo * 64 + 16 * cq + 4 * q, ld4(p2s + wo * 16 + 4 * q));
+    } else {
+      const int u = e - 776, wo = u >> 2, q = u & 3;
+      *reinterpret_cast<unsigned*>(a.A2 + (size_t)bi * 1600 + wo * 64 + 16 * cq + 4 * q) =
+          reinterpret_cast<const unsigned*>(a2s)[wo * 4 + q];
+    }
+  }
+}
 
 __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -457,7 +568,10 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   float* P1s = w1s + 320;
   float* w2s = P1s + 169 * kP1Stride;  // [kc=72][j=16][t=4]: B[k=4kc+t][16cq+j]
   float* p2s = w2s + 72 * 16 * 4;      // [25 windows][16 channels] pooled conv2 output
-  int* s_last = reinterpret_cast<int*>(p2s + 400);  // head hand-off flag (one word)
+  uint8_t* a1s = reinterpret_cast<uint8_t*>(p2s + 400);       // [169][32] pool-1 argmax
+  uint8_t* a2s = a1s + 169 * 32;                               // [25][16] pool-2 argmax
+  float* red = reinterpret_cast<float*>(a2s + 400);            // [16][128] dense1 row-group partials
+  int* s_last = reinterpret_cast<int*>(red + 16 * 128);        // head hand-off flag (one word)
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int i = lane & 15, g = lane >> 4;
   const int bi = blockIdx.x >> 2, cq = blockIdx.x & 3;
@@ -491,16 +605,21 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   stamp(a.stamps, 1);
   __syncthreads();
   stamp(a.stamps, 2);
-  // ---- dense1 operand prefetch (after the staging loads, overlapping the convolutions): thread
-  // (row group rg, 4 columns n4) needs W3 rows of features kk = 25 rg .. 25 rg + 24 of this quarter
-  // (feature kk = window (kk >> 4), channel 16cq + (kk & 15))
+  // ---- dense1 operand prefetch, overlapping the convolutions: thread (row group rg, 4 columns n4)
+  // needs W3 rows of features kk = 25 rg .. 25 rg + 24 of this quarter (feature kk = window
+  // (kk >> 4), channel 16cq + (kk & 15)).  The 25 16-B loads per thread (205 KB per workgroup,
+  // ~1.3 us of the CU's texture-address rate) are spread over the conv phases in small groups:
+  // issued back to back they fill the CU's vector-memory queue and every wave stalls behind them
+  // (measured: conv1 3.4-4.4 us instead of ~1 us).
   const int n4 = (tid & 31) * 4, rg = tid >> 5;
   f4 w3v[25];
-#pragma unroll
-  for (int j = 0; j < 25; ++j) {
+  const float* w3b = a.W + a.ow3 + n4;
+  auto ldw3 = [&](int j) {
     const int kk = rg * 25 + j;
-    w3v[j] = ld4(a.W + a.ow3 + (size_t)((kk >> 4) * 64 + 16 * cq + (kk & 15)) * 128 + n4);
-  }
+    w3v[j] = ld4(w3b + (size_t)((kk >> 4) * 64 + 16 * cq + (kk & 15)) * 128);
+  };
+#pragma unroll
+  for (int j = 0; j < 6; ++j) ldw3(j);
   // ---- conv1 on MFMA (K = 9 taps padded to 12): rows = 676 conv1 positions in pool-window-major
   // order, so a 16-row tile holds 4 whole 2x2 windows and the maxpool happens in registers.
   // 43 row tiles x 2 channel tiles; bias + relu after the max (they commute with it). ----
@@ -521,7 +640,9 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
     }
     // row tiles mt0 and mt0 + 8 per iteration, both channel tiles each: 4 independent MFMA
     // chains sharing 6 LDS loads (the two channel tiles read the same image values)
-    for (int mt0 = wave; mt0 < 43; mt0 += 16) {
+#pragma unroll
+    for (int it = 0; it < 3; ++it) {
+      const int mt0 = wave + 16 * it;
       float xa[2][3];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -544,6 +665,12 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
         for (int u = 0; u < 2; ++u)
 #pragma unroll
           for (int nt = 0; nt < 2; ++nt) acc[u][nt] = mfma16x16x4(xa[u][s3], bw[nt][s3], acc[u][nt]);
+      if (it < 2) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 6 + 5 * it; j < 11 + 5 * it; ++j) ldw3(j);
+        __builtin_amdgcn_sched_barrier(0);
+      }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int wo = (mt0 + 8 * u) * 4 + g;
@@ -559,11 +686,7 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
           const int co = nt * 16 + i;
           const float v = fmaxf(m + w1s[288 + co], 0.f);
           P1s[wo * kP1Stride + co] = v;
-          if (((mt0 + 8 * u) & 3) == cq) {  // each quarter stores a quarter of P1 / A1 for backward
-            const size_t gi = ((size_t)bi * 169 + wo) * 32 + co;
-            a.P1[gi] = v;
-            a.A1[gi] = (uint8_t)am;
-          }
+          a1s[wo * 32 + co] = (uint8_t)am;
         }
       }
     }
@@ -571,7 +694,8 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   stamp(a.stamps, 3);
   __syncthreads();
   stamp(a.stamps, 4);
-  // ---- conv2 on MFMA: wave w < 7 takes row tile w (windows 4w .. 4w+3) ----
+  // ---- conv2 on MFMA: wave w < 7 takes row tile w (windows 4w .. 4w+3); the last 9 W3 loads
+  // ride along, one per tap ----
   if (wave < 7) {
     const int wi = wave * 4 + (i >> 2), q = i & 3;
     const bool valid = wi < 25;
@@ -593,6 +717,9 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
         acc0 = mfma16x16x4(av.z, bv.z, acc0);
         acc1 = mfma16x16x4(av.w, bv.w, acc1);
       }
+      __builtin_amdgcn_sched_barrier(0);
+      ldw3(16 + kk);
+      __builtin_amdgcn_sched_barrier(0);
     }
     const f4 acc = acc0 + acc1;
     stamp(a.stamps, 5);
@@ -604,12 +731,13 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
       if (acc.z > m) { m = acc.z; am = 2; }
       if (acc.w > m) { m = acc.w; am = 3; }
       const int co = 16 * cq + i;
-      const size_t e = (size_t)bi * 1600 + wo * 64 + co;
       const float v = fmaxf(m + a.W[a.ob2 + co], 0.f);
-      a.P2[e] = v;
-      a.A2[e] = (uint8_t)am;
       p2s[wo * 16 + i] = v;
+      a2s[wo * 16 + i] = (uint8_t)am;
     }
+  } else {
+#pragma unroll
+    for (int j = 16; j < 25; ++j) ldw3(j);
   }
   __syncthreads();
   // ---- dense1 quarter partial: 25 features x 4 columns per thread, 16 row groups reduced in LDS
@@ -617,52 +745,66 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
     f4 hs = zero4();
 #pragma unroll
     for (int j = 0; j < 25; ++j) hs += p2s[rg * 25 + j] * w3v[j];
-    st4(P1s + rg * 128 + n4, hs);  // P1s is free after conv2
+    st4(red + rg * 128 + n4, hs);
   }
   __syncthreads();
-  if (tid < 128) {
-    float hsum = 0.f;
+  if (tid < 32) {
+    f4 hsum = zero4();
 #pragma unroll
-    for (int k = 0; k < 16; ++k) hsum += P1s[k * 128 + tid];
-    // sc1 store: the image's head may run on another XCD (hand-off below)
-    __hip_atomic_store(a.part3 + ((size_t)cq * a.b + bi) * 128 + tid, hsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int k = 0; k < 16; ++k) hsum += ld4(red + k * 128 + 4 * tid);
+    // 16-B sc1 store: the image's head may run on another XCD (hand-off below)
+    st4_sc1(buf_rsrc(a.part3 + ((size_t)cq * a.b + bi) * 128, 512), tid * 16, hsum);
   }
   stamp(a.stamps, 6);
-  if (!a.head) return;
+  if (!a.head) {
+    store_saved_fwd(a, bi, cq, P1s, a1s, p2s, a2s, tid, 512);
+    return;
+  }
   // the head's weights, loaded by wave 0 of every workgroup now: their latency hides behind the
   // hand-off (only the image's last workgroup uses them; 5 KB, L2-resident)
   HeadWeights hw;
   if (wave == 0) hw = load_head_weights(a, lane);
   // ---- hand-off to the image's last quarter workgroup (MI355X_MICROARCH.md, inter-workgroup
-  // visibility, first table row): every storing wave waits for its sc1 stores, a workgroup
-  // barrier, ONE agent-scope add per workgroup on the image's counter; the workgroup whose add
-  // returns 3 (mod 4) is last and reads the 4 partials with sc1 loads.  Counters are never reset:
-  // each step adds exactly 4 per image, and the kernel boundary orders consecutive steps.
+  // visibility, first table row): the storing wave drains its sc1 stores, a workgroup barrier,
+  // ONE agent-scope add per workgroup on the image's counter; the workgroup whose add returns
+  // 3 (mod 4) is last and reads the 4 partials with sc1 loads.  No workgroup ever waits for
+  // another (placement-independent).  k_dense1_bwd (the next launch of every training step)
+  // zeroes the counters, so a launch that did not add exactly 4 per image cannot shift the
+  // election of later steps.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) *s_last = (__hip_atomic_fetch_add(a.cnt + bi, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 3u) == 3u;
   __syncthreads();
-  if (!*s_last || wave != 0) return;
-  head_row(a, bi, lane, label, hw);
-  stamp(a.stamps, 7);
+  if (*s_last && wave == 0) {
+    head_row(a, bi, lane, label, hw);
+    stamp(a.stamps, 7);
+    return;
+  }
+  // saved activations leave LDS only now (off the head's critical path)
+  if (*s_last) store_saved_fwd(a, bi, cq, P1s, a1s, p2s, a2s, tid - 64, 448);
+  else store_saved_fwd(a, bi, cq, P1s, a1s, p2s, a2s, tid, 512);
 }
 
 // --------------------------------------------------------------------------------------------
 // KF: reduce the per-image partial slabs into G (+ optional fused SGD).
-//   blocks [0, nbs)          : slab sweep (SGD of the parameters whose gradient is already in G)
-//   blocks [nbs, nbs + nb2)  : conv2 kernel/bias, 4 threads per output (16 images each)
-//   blocks [.., + 20)        : conv1 kernel/bias, 16 threads per output
+//   blocks [0, ndb)               : dense weight-gradient tasks (when the step's forward did not
+//                                   run them as K5), each fused with SGD of its outputs
+//   blocks [ndb, ndb + nbs)       : SGD sweep of the dense range (dense gradients from K5)
+//   blocks [.., + nb2)            : conv2 kernel/bias, 4 threads per output (16 images each)
+//   blocks [.., + nb1)            : conv1 kernel/bias, 16 threads per output
 // --------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_finalize(MnistArgs a, int apply_sgd, int nbs, int nb2, int nb1) {
+__global__ __launch_bounds__(256) void k_finalize(MnistArgs a, int apply_sgd, int ndb, int nbs, int nb2, int nb1) {
   const float lr = *a.lr;
-  const int blk = blockIdx.x;
+  int blk = blockIdx.x;
+  if (blk < ndb) {
+    const int T = blk * 4 + (threadIdx.x >> 6);
+    if (T < kDenseTasks) dense_w_task(a, T, threadIdx.x & 63, apply_sgd != 0, lr);
+    return;
+  }
+  blk -= ndb;
   if (blk < nbs) {
-    const int e = blk * 256 + threadIdx.x;
-    if (e >= a.nslab) return;
-    const bool conv = (e >= a.ow1 && e < a.ow1 + 288) || (e >= a.ob1 && e < a.ob1 + 32) ||
-                      (e >= a.ow2 && e < a.ow2 + 18432) || (e >= a.ob2 && e < a.ob2 + 64);
-    if (conv || !apply_sgd) return;
-    a.W[e] -= lr * a.G[e];
+    const int e = a.ow3 + blk * 256 + threadIdx.x;
+    if (e < a.nslab) a.W[e] -= lr * a.G[e];
     return;
   }
   if (blk < nbs + nb2) {
@@ -750,10 +892,9 @@ __global__ __launch_bounds__(256) void k_sgd_momentum(float* __restrict__ w, con
 // --------------------------------------------------------------------------------------------
 // launchers
 // --------------------------------------------------------------------------------------------
-void mnist_dense1_bwd(const MnistArgs& a, hipStream_t s) {
-  const int MT = (a.b + 15) / 16;
-  const int nP = (MT * 100 + 3) / 4;
-  hipLaunchKernelGGL(k_dense1_bwd, dim3(200 + nP + 1 + 6), dim3(256), 0, s, a);
+void mnist_dense1_bwd(const MnistArgs& a, bool with_dense, hipStream_t s) {
+  const int tasks = ((a.b + 15) / 16) * 100 + (with_dense ? kDenseTasks : 0);
+  hipLaunchKernelGGL(k_dense1_bwd, dim3((tasks + 3) / 4), dim3(256), 0, s, a, with_dense ? 1 : 0);
 }
 void mnist_conv_bwd(const MnistArgs& a, hipStream_t s) {
   static bool attr = false;
@@ -771,11 +912,13 @@ void mnist_fwd_conv(const MnistArgs& a, hipStream_t s) {
   }
   hipLaunchKernelGGL(k_fwd_conv, dim3(a.b * 4), dim3(512), kLdsFwd * sizeof(float), s, a);
 }
-void mnist_finalize(const MnistArgs& a, bool apply_sgd, hipStream_t s) {
-  const int nbs = apply_sgd ? (a.nslab + 255) / 256 : 0;
+void mnist_finalize(const MnistArgs& a, bool apply_sgd, bool with_dense, hipStream_t s) {
+  const int ndb = with_dense ? (kDenseTasks + 3) / 4 : 0;
+  const int nbs = (apply_sgd && !with_dense) ? (a.nslab - a.ow3 + 255) / 256 : 0;
   const int nb2 = (kMnistPart2Rows * 64 * 4 + 255) / 256;
   const int nb1 = (kMnistPart1Cols * 16 + 255) / 256;
-  hipLaunchKernelGGL(k_finalize, dim3(nbs + nb2 + nb1), dim3(256), 0, s, a, apply_sgd ? 1 : 0, nbs, nb2, nb1);
+  hipLaunchKernelGGL(k_finalize, dim3(ndb + nbs + nb2 + nb1), dim3(256), 0, s, a, apply_sgd ? 1 : 0, ndb, nbs, nb2,
+                     nb1);
 }
 void sgd_apply(float* w, const float* g, const float* lr, int64_t n, hipStream_t s) {
   const int64_t nt = (n + 3) / 4;

@@ -13,7 +13,7 @@ from tensorflow_distributed_learning_amd.models import mnist_cnn as M  # noqa: E
 
 KERNELS = {
     "fwd_conv": (8, 8, {0: "start", 1: "stage-issued", 2: "stage-barrier", 3: "conv1-done", 4: "barrier2",
-                        5: "conv2-mfma", 6: "dense1-partial", 7: "head-end"}, 256),
+                        5: "conv2-mfma", 6: "dense1-partial", 7: "dP2-done"}, 256),
     "conv_bwd": (6, 8, {0: "start", 1: "stage-issued", 2: "stage-barrier", 3: "wgrad-done", 6: "dgrad-mfma",
                         4: "dgrad-epi", 5: "final-barrier"}, 256),
 }
@@ -67,7 +67,7 @@ def main():
             print(f"  head in {last.sum()} workgroups; us since kernel start (median / max): dense1 partial stored "
                   f"{np.median(p6):.2f}/{p6.max():.2f}; head won {np.median(h[:, 0]):.2f}/{h[:, 0].max():.2f}; "
                   f"partials loaded {np.median(h[:, 1]):.2f}/{h[:, 1].max():.2f}; softmax {np.median(h[:, 2]):.2f}/"
-                  f"{h[:, 2].max():.2f}; end {np.median(h[:, 3]):.2f}/{h[:, 3].max():.2f}")
+                  f"{h[:, 2].max():.2f}; dH published {np.median(h[:, 3]):.2f}/{h[:, 3].max():.2f}")
         print("  slot/wave " + " ".join(f"{w:>6d}" for w in range(waves)))
         for s, label in sorted(slots.items(), key=lambda kv: np.median(rel[:, 0, kv[0]])):
             vals = [np.median(rel[:, w, s]) if (r[:, w, s] > 0).all() else float("nan") for w in range(waves)]

@@ -126,6 +126,8 @@ class FusedMnistTrainer:
         self._ragged_bufs, self._ragged_stage, self._ragged_ev = {}, None, None
         # diagnostics: host seconds per execution (index take, upload, graph launch)
         self._host_times = [] if os.environ.get("TDL_HOST_TIMING") == "1" else None
+        # one execution's indices taken and uploaded ahead of its launch (prefetch())
+        self._ready = None
 
     @property
     def capture_comm(self) -> bool:
@@ -342,6 +344,30 @@ class FusedMnistTrainer:
         ev.record(torch.cuda.current_stream(self.device))
         self._stage_ev[slot] = ev
 
+    def _take_upload(self, handler: "DeviceHandler", K: int):
+        """Take the next K full batches' indices and start their upload into the next index slot
+        (None at a ragged tail / the end of finite data)."""
+        idx = handler.take(K)
+        if idx is None:
+            return None
+        if not hasattr(self, "_stage"):
+            self._stage, self._stage_ev, self._slot = [None] * self._nslots, [None] * self._nslots, 0
+        slot = self._slot
+        self._slot = (slot + 1) % self._nslots
+        graph, idx_buf, st = self._graph_for(K, handler.b, slot)
+        self._upload(idx, idx_buf, slot)
+        return (handler, K, idx.size // handler.b, graph, st)
+
+    def prefetch(self, handler: "DeviceHandler", K: int) -> bool:
+        """Input prefetch of depth one execution (tf.data ``prefetch`` semantics): take and upload
+        the indices of the next K-step execution now, so the next ``run_train`` launches its first
+        graph without waiting for the host's batch assembly.  Returns False at a ragged tail."""
+        K = min(int(K), self.K)
+        if self._ready is not None:
+            return self._ready[1] == K
+        self._ready = self._take_upload(handler, K)
+        return self._ready is not None
+
     def run_train(self, handler: "DeviceHandler", steps: int) -> int:
         done = 0
         b = handler.b
@@ -352,8 +378,13 @@ class FusedMnistTrainer:
         while done < steps:
             K = min(self.K, steps - done)
             t0 = time.perf_counter() if timing else 0.0
-            idx = handler.take(K)
-            if idx is None:
+            r, self._ready = self._ready, None
+            if r is not None and (r[0] is not handler or r[1] != K):
+                raise RuntimeError("fused trainer: prefetched execution does not match the requested steps")
+            if r is None:
+                r = self._take_upload(handler, K)
+            t1 = t2 = time.perf_counter() if timing else 0.0
+            if r is None:
                 # ragged tail (end of finite data) -> eager steps of their own sizes
                 one = handler.next_ragged()
                 if one is None:
@@ -363,13 +394,7 @@ class FusedMnistTrainer:
                 done += 1
                 continue
             opt._sync_lr()
-            slot = self._slot
-            self._slot = (slot + 1) % self._nslots
-            graph, idx_buf, st = self._graph_for(K, b, slot)
-            t1 = time.perf_counter() if timing else 0.0
-            self._upload(idx, idx_buf, slot)
-            t2 = time.perf_counter() if timing else 0.0
-            Kr = idx.size // b
+            _, _, Kr, graph, st = r
             if Kr < K:
                 # the full batches in front of an epoch's partial batch: same slot buffers and
                 # step object, launched eagerly (no per-step host sync, no new graph size)

@@ -5,7 +5,8 @@
 * :func:`reference_logits`  – plain-PyTorch functional forward (NHWC semantics); the fp32/fp64
   oracle for the fused HIP kernels.
 * :class:`FusedMnistTrainStep` – one replica's fused train step on the gfx950 kernels of
-  ``csrc/kernels/mnist_cnn.hip`` (4 launches: fwd + loss head, dense bwd, conv bwd, finalize[/SGD]).
+  ``csrc/kernels/mnist_cnn.hip`` (4 launches: fwd + loss head, dP2, conv bwd, finalize = partial
+  reductions + dense weight gradients [+ SGD]).
 """
 from __future__ import annotations
 
@@ -143,5 +144,5 @@ class FusedMnistTrainStep:
         self._impl.set_idx_offset(int(off))
 
     def buffers(self) -> Dict[str, torch.Tensor]:
-        names = ["P1", "A1", "P2", "A2", "H", "dH", "dC2", "part2", "part1", "part3", "dL"]
+        names = ["P1", "A1", "P2", "A2", "H", "dH", "dP2", "part2", "part1", "part3", "dL"]
         return dict(zip(names, self._impl.buffers()))
