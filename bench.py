@@ -146,7 +146,7 @@ def main():
         import numpy as np
 
         a = np.array(ht[-max(1, K // max(1, spe)):]) * 1e6
-        print(f"host us per execution (take, upload, launch): median {np.median(a, 0).round(1).tolist()} "
+        print(f"host us per execution (take, graph+upload, launch): median {np.median(a, 0).round(1).tolist()} "
               f"max {a.max(0).round(1).tolist()}", file=sys.stderr)
     if rank == 0:
         print(json.dumps({

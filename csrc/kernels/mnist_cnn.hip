@@ -22,6 +22,8 @@
 //
 // All reductions are slab-based (no float atomics) so every replica computes bit-identical
 // updates from identical inputs.
+#include <type_traits>
+
 #include "common.h"
 #include "mnist_cnn.h"
 
@@ -210,20 +212,24 @@ __device__ __forceinline__ void dense_w_task(const MnistArgs& a, int T, int lane
     const int mt = T >> 3, nt = T & 7, n = nt * 16 + i;
     if (mt < 100) {
       const int kf = mt * 16 + i;
+      float wold[4];  // the SGD operands ride in the operand loads' round trip
+#pragma unroll
+      for (int r = 0; r < 4; ++r) wold[r] = sgd ? a.W[a.ow3 + (mt * 16 + 4 * g + r) * 128 + n] : 0.f;
       const f4 acc = gemm_tn_rows(
           b, g, [&](int r) { return a.P2[(size_t)r * 1600 + kf]; }, [&](int r) { return a.dH[r * 128 + n]; });
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int e = a.ow3 + (mt * 16 + 4 * g + r) * 128 + n;
         a.G[e] = acc[r];
-        if (sgd) a.W[e] -= lr * acc[r];
+        if (sgd) a.W[e] = wold[r] - lr * acc[r];
       }
     } else {  // db3: A = e_0 (row 0 of the tile = column sums of dH)
+      const float wold = sgd ? a.W[a.ob3 + n] : 0.f;
       const f4 acc = gemm_tn_rows(
           b, g, [&](int) { return i == 0 ? 1.f : 0.f; }, [&](int r) { return a.dH[r * 128 + n]; });
       if (g == 0) {
         a.G[a.ob3 + n] = acc[0];
-        if (sgd) a.W[a.ob3 + n] -= lr * acc[0];
+        if (sgd) a.W[a.ob3 + n] = wold - lr * acc[0];
       }
     }
     return;
@@ -233,6 +239,10 @@ __device__ __forceinline__ void dense_w_task(const MnistArgs& a, int T, int lane
     // dW4[k][c] = sum_r H[r][k] dL[r][c] (tiles 0..7), db4 (tile 8, A = e_0); N = 10 of 16
     const int c = min(i, 9);
     const float cm = i < 10 ? 1.f : 0.f;
+    float wold[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      wold[r] = sgd ? a.W[T3 < 8 ? a.ow4 + (T3 * 16 + 4 * g + r) * 10 + c : a.ob4 + c] : 0.f;
     const f4 acc = gemm_tn_rows(
         b, g, [&](int r) { return T3 < 8 ? a.H[r * 128 + T3 * 16 + i] : (i == 0 ? 1.f : 0.f); },
         [&](int r) { return a.dL[r * 10 + c] * cm; });
@@ -242,11 +252,11 @@ __device__ __forceinline__ void dense_w_task(const MnistArgs& a, int T, int lane
         for (int r = 0; r < 4; ++r) {
           const int e = a.ow4 + (T3 * 16 + 4 * g + r) * 10 + i;
           a.G[e] = acc[r];
-          if (sgd) a.W[e] -= lr * acc[r];
+          if (sgd) a.W[e] = wold[r] - lr * acc[r];
         }
       } else if (g == 0) {
         a.G[a.ob4 + i] = acc[0];
-        if (sgd) a.W[a.ob4 + i] -= lr * acc[0];
+        if (sgd) a.W[a.ob4 + i] = wold[0] - lr * acc[0];
       }
     }
   }
@@ -315,16 +325,19 @@ __global__ __launch_bounds__(256) void k_dense1_bwd(MnistArgs a, int with_dense)
 // the zero border of dC2 for every pixel of a tile are skipped (exact).  Outputs are per-image
 // partial slabs, reduced deterministically by KF.
 // --------------------------------------------------------------------------------------------
-constexpr int kDcStride = 68, kDcDim = 15, kP1Stride = 36;
+constexpr int kP1Stride = 36;  // forward P1 rows: conflict-free ds_read_b128 in conv2
+// conv backward LDS row strides = 16 (mod 64) floats: the wgrad operand reads (16 consecutive
+// floats per lane group, lane groups one row apart) hit 4 disjoint 16-bank groups
+constexpr int kDcStride = 80, kDcDim = 15, kP1StrideB = 48;
 constexpr int kDgSplit = 80;  // pixel split of the dgrad parts: balances their MFMA work after tap skipping
 // conv2 wgrad tiles (first, count) per (pixel part, wave): waves w and w+4 share a SIMD, so each
 // SIMD's wgrad + dgrad MFMAs come to <= 294 (part 0) / 292 (part 1)
 __constant__ int kWgradTiles[2][8][2] = {{{0, 6}, {6, 5}, {11, 6}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {17, 2}},
                                          {{0, 5}, {5, 5}, {10, 5}, {15, 4}, {0, 0}, {0, 0}, {0, 0}, {0, 0}}};
-constexpr int kLdsDc = kDcDim * kDcDim * kDcStride;   // 15300
-constexpr int kLdsP1 = 169 * kP1Stride;              // 6084
+constexpr int kLdsDc = kDcDim * kDcDim * kDcStride;   // 18000
+constexpr int kLdsP1 = 169 * kP1StrideB;             // 8112
 constexpr int kLdsWd = 9 * 16 * 16 * 4;              // 9216
-constexpr int kLdsConvBwd = kLdsDc + kLdsP1 + 784 + kLdsWd + 8 * 10 * 16 + 16;
+constexpr int kLdsConvBwd = kLdsDc + kLdsP1 + 784 + kLdsWd + 8 * 10 * 16;
 
 __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -333,8 +346,7 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
   float* Xs = P1s + kLdsP1;
   float* Wd = Xs + 784;
   float* red = Wd + kLdsWd;  // [8 waves][10][16]
-  float* unit = red + 8 * 10 * 16;  // [16] = e_0 (A operand of the bias row)
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int i = lane & 15, g = lane >> 4;
   const int bi = blockIdx.x >> 2, p = blockIdx.x & 3;
   const int h = p & 1, half = p >> 1;
@@ -354,7 +366,7 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
 #pragma unroll
   for (int j = 0; j < kIdc; ++j) {
     const int e4 = tid + j * 512;
-    const int cell = e4 / 17, c4 = e4 - cell * 17;
+    const int cell = e4 / (kDcStride / 4), c4 = e4 - cell * (kDcStride / 4);
     const int y = cell / kDcDim - 2, x = cell - (cell / kDcDim) * kDcDim - 2;
     const bool in = e4 < kLdsDc / 4 && c4 < 16 && y >= 0 && y < 10 && x >= 0 && x < 10;
     const int o = in ? ((y >> 1) * 5 + (x >> 1)) * 64 + c4 * 4 : 0;
@@ -390,7 +402,7 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
 #pragma unroll
   for (int j = 0; j < kIp1; ++j) {
     const int e4 = tid + j * 512;
-    if (e4 < 169 * 8) st4(P1s + (e4 >> 3) * kP1Stride + (e4 & 7) * 4, vp1[j]);
+    if (e4 < 169 * 8) st4(P1s + (e4 >> 3) * kP1StrideB + (e4 & 7) * 4, vp1[j]);
   }
 #pragma unroll
   for (int j = 0; j < kIwd; ++j) {
@@ -398,7 +410,6 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
     if (e4 < kLdsWd / 4) st4(Wd + e4 * 4, vwd[j]);
   }
   if (tid < 196) st4(Xs + tid * 4, vx);
-  if (tid < 16) unit[tid] = tid == 0 ? 1.f : 0.f;
   stamp(a.stamps, 1);
   __syncthreads();
   stamp(a.stamps, 2);
@@ -413,33 +424,37 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
       const int k = mt * 16 + i;
       const int tap = bias_tile ? 0 : k >> 5, ci = k & 31;
       const int kh = tap / 3, kw = tap - kh * 3;
-      // the bias row reads the LDS unit vector (1 for i == 0) at every position: stride 0
-      const float* pa = bias_tile ? unit + i : P1s + (kh * 13 + kw) * kP1Stride + ci;
-      const int sa = bias_tile ? 0 : 1;
-      const float* pb = dCs + (2 * kDcDim + 2) * kDcStride + 16 * p + i;
-      // this lane's k-step s covers position 4s + g of the 10x10 grid: advance incrementally
-      int ow = g, offA = sa * g * kP1Stride, offB = g * kDcStride;
-      f4 acc0 = zero4(), acc1 = zero4();
+      // k-step s covers positions p = 4s + g of the 10x10 grid.  Every operand address is a
+      // per-lane base plus a compile-time offset: the 4 positions of a k-step sit in one grid row
+      // except for s = 2 mod 5 (p = 10q+8 .. 10q+11), where lanes g >= 2 wrap to the next row and
+      // use a second base (+3 P1 cells, +5 dC cells).  The bias row multiplies by the unit vector.
+      const float* pa0 = P1s + (kh * 13 + kw + g) * kP1StrideB + ci;
+      const float* paS = pa0 + (g >= 2 ? 3 * kP1StrideB : 0);
+      const float* pb0 = dCs + (2 * kDcDim + 2 + g) * kDcStride + 16 * p + i;
+      const float* pbS = pb0 + (g >= 2 ? 5 * kDcStride : 0);
+      const float unit_a = (i == 0) ? 1.f : 0.f;
+      auto kloop = [&](auto bias) {
+        f4 c0 = zero4(), c1 = zero4();
 #pragma unroll
-      for (int s0 = 0; s0 < 25; s0 += 5) {
-        float av[5], bv[5];
+        for (int s0 = 0; s0 < 25; s0 += 5) {
+          float av[5], bv[5];
 #pragma unroll
-        for (int u = 0; u < 5; ++u) {
-          av[u] = pa[offA];
-          bv[u] = pb[offB];
-          const int ow2 = ow + 4;
-          const bool wrap = ow2 >= 10;
-          ow = wrap ? ow2 - 10 : ow2;
-          offA += sa * (wrap ? 7 * kP1Stride : 4 * kP1Stride);
-          offB += wrap ? 9 * kDcStride : 4 * kDcStride;
+          for (int u = 0; u < 5; ++u) {
+            const int st = s0 + u, q = (4 * st) / 10, r = (4 * st) % 10;
+            const bool strad = r == 8;
+            if constexpr (decltype(bias)::value) av[u] = unit_a;
+            else av[u] = (strad ? paS : pa0)[(q * 13 + r) * kP1StrideB];
+            bv[u] = (strad ? pbS : pb0)[(q * kDcDim + r) * kDcStride];
+          }
+#pragma unroll
+          for (int u = 0; u < 5; ++u) {
+            if ((s0 + u) & 1) c1 = mfma16x16x4(av[u], bv[u], c1);
+            else c0 = mfma16x16x4(av[u], bv[u], c0);
+          }
         }
-#pragma unroll
-        for (int u = 0; u < 5; ++u) {
-          if ((s0 + u) & 1) acc1 = mfma16x16x4(av[u], bv[u], acc1);
-          else acc0 = mfma16x16x4(av[u], bv[u], acc0);
-        }
-      }
-      const f4 acc = acc0 + acc1;
+        return c0 + c1;
+      };
+      const f4 acc = bias_tile ? kloop(std::true_type{}) : kloop(std::false_type{});
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = mt * 16 + 4 * g + r;
@@ -495,7 +510,7 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
     for (int r = 0; r < 4; ++r) {
       const int Pr = pix0 + d * 16 + 4 * g + r;
       if (Pr < pix1) {
-        const float v = P1s[Pr * kP1Stride + c] > 0.f ? acc[r] : 0.f;
+        const float v = P1s[Pr * kP1StrideB + c] > 0.f ? acc[r] : 0.f;
         const unsigned q1 = q1v[r];
         const int ph = Pr / 13, pw = Pr - ph * 13;
         const float* img = Xs + (2 * ph + (q1 >> 1)) * 28 + 2 * pw + (q1 & 1);
@@ -813,6 +828,8 @@ __global__ __launch_bounds__(256) void k_finalize(MnistArgs a, int apply_sgd, in
     const int n = kMnistPart2Rows * 64;
     float s = 0.f;
     const int oc = min(o, n - 1);
+    const int e = (oc >> 6) < 288 ? a.ow2 + oc : a.ob2 + (oc & 63);
+    const float wold = apply_sgd ? a.W[e] : 0.f;  // in the same round trip as the partials
     for (int base = 0; base < a.b; base += 64) {  // 16 independent loads in flight per thread
       float v[16];
 #pragma unroll
@@ -823,10 +840,8 @@ __global__ __launch_bounds__(256) void k_finalize(MnistArgs a, int apply_sgd, in
     s += __shfl_xor(s, 1, 64);
     s += __shfl_xor(s, 2, 64);
     if (sub == 0 && o < n) {
-      const int row = o >> 6, col = o & 63;
-      const int e = row < 288 ? a.ow2 + o : a.ob2 + col;
       a.G[e] = s;
-      if (apply_sgd) a.W[e] -= lr * s;
+      if (apply_sgd) a.W[e] = wold - lr * s;
     }
     return;
   }
@@ -835,6 +850,8 @@ __global__ __launch_bounds__(256) void k_finalize(MnistArgs a, int apply_sgd, in
   const int rows = mnist_part1_rows(a.b);
   float s = 0.f;
   const int oc = min(o, kMnistPart1Cols - 1);
+  const int e = oc < 288 ? a.ow1 + oc : a.ob1 + (oc - 288);
+  const float wold = apply_sgd ? a.W[e] : 0.f;
   for (int base = 0; base < rows; base += 128) {
     float v[8];
 #pragma unroll
@@ -845,9 +862,8 @@ __global__ __launch_bounds__(256) void k_finalize(MnistArgs a, int apply_sgd, in
 #pragma unroll
   for (int m = 1; m < 16; m <<= 1) s += __shfl_xor(s, m, 64);
   if (sub == 0 && o < kMnistPart1Cols) {
-    const int e = o < 288 ? a.ow1 + o : a.ob1 + (o - 288);
     a.G[e] = s;
-    if (apply_sgd) a.W[e] -= lr * s;
+    if (apply_sgd) a.W[e] = wold - lr * s;
   }
 }
 

@@ -37,10 +37,13 @@ __device__ __forceinline__ bool reached(uint32_t v, uint32_t e) { return (int32_
 
 // All stores of this workgroup done -> system-scope release -> epoch e into word [blk][rank] of
 // every peer's signal array `round` -> wait for every peer's word [blk][q] in our own array ->
-// system-scope acquire.  Returns with the whole workgroup past a barrier.
+// system-scope acquire.  Returns with the whole workgroup past a barrier: true when every peer
+// arrived, false when a bounded wait timed out (error word set; the caller then writes nothing,
+// so a dead or lagging peer can never leave a half-reduced gradient or weight behind).
 template <int R>
-__device__ __forceinline__ void xgmi_exchange(const XgmiArgs& a, int round, int blk, uint32_t e) {
+__device__ __forceinline__ bool xgmi_exchange(const XgmiArgs& a, int round, int blk, uint32_t e) {
   const int tid = threadIdx.x;
+  int timed_out = 0;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid < kWave) {
@@ -57,6 +60,7 @@ __device__ __forceinline__ void xgmi_exchange(const XgmiArgs& a, int round, int 
         __builtin_amdgcn_s_sleep(1);
         if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout) {
           __hip_atomic_fetch_or(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          timed_out = 1;
           break;
         }
       }
@@ -64,7 +68,7 @@ __device__ __forceinline__ void xgmi_exchange(const XgmiArgs& a, int round, int 
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  __syncthreads();
+  return __syncthreads_or(timed_out) == 0;
 }
 
 // rank-order sum of element i (float4) over the R input halves
@@ -122,7 +126,10 @@ __global__ __launch_bounds__(256) void k_xgmi_oneshot(XgmiArgs a) {
     for (int64_t j = i; j < a.n && j < i + 4; ++j) mine[j] = a.src[j];
   }
   // 2-3. signal the peers, wait for them
-  xgmi_exchange<R>(a, 0, blk, e);
+  if (!xgmi_exchange<R>(a, 0, blk, e)) {
+    if (tid == 0) a.epoch[blk] = e;
+    return;
+  }
   // 4-5. reduce in rank order (all loads in flight before the adds), epilogue
   if (full) {
     st4(out + i, finish4<MODE>(a, i, sum_ranks<R>(a, half + i)));
@@ -153,23 +160,35 @@ __global__ __launch_bounds__(256) void k_xgmi_twoshot(XgmiArgs a) {
       for (int64_t j = i; j < a.n && j < i + 4; ++j) mine[half + j] = a.src[j];
     }
   }
-  xgmi_exchange<R>(a, 0, c, e);
-  // 2. reduce-scatter: chunk c of this rank's shard, from every rank, in rank order
+  if (!xgmi_exchange<R>(a, 0, c, e)) {
+    if (tid == 0) a.epoch[c] = e;
+    return;
+  }
+  // 2. reduce-scatter: chunk c of this rank's shard, from every rank, in rank order.  In SGD mode
+  // the updated owner shard is staged in the result region only; out (= W) is written after the
+  // second exchange, so a timeout leaves W untouched on this rank.
+  f4 own4 = zero4();
   {
     const int64_t i = a.rank * a.shard + within;
     if (i + 3 < a.n) {
-      const f4 v = finish4<MODE>(a, i, sum_ranks<R>(a, half + i));
-      st4(mine + res + i, v);
-      st4(out + i, v);
+      own4 = finish4<MODE>(a, i, sum_ranks<R>(a, half + i));
+      st4(mine + res + i, own4);
     } else {
-      for (int64_t j = i; j < a.n && j < i + 4; ++j) {
-        const float v = finish1<MODE>(a, j, sum_ranks1<R>(a, half + j));
-        mine[res + j] = v;
-        out[j] = v;
-      }
+      for (int64_t j = i; j < a.n && j < i + 4; ++j) mine[res + j] = finish1<MODE>(a, j, sum_ranks1<R>(a, half + j));
     }
   }
-  xgmi_exchange<R>(a, 1, c, e);
+  if (!xgmi_exchange<R>(a, 1, c, e)) {
+    if (tid == 0) a.epoch[c] = e;
+    return;
+  }
+  {
+    const int64_t i = a.rank * a.shard + within;
+    if (i + 3 < a.n) {
+      st4(out + i, own4);
+    } else {
+      for (int64_t j = i; j < a.n && j < i + 4; ++j) out[j] = mine[res + j];
+    }
+  }
   // 3. all-gather: chunk c of every other shard, from its owner's result region
 #pragma unroll
   for (int q = 0; q < R; ++q) {

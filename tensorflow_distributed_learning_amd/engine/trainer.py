@@ -376,6 +376,9 @@ class GenericTrainer:
     def logs(self) -> Dict[str, float]:
         from ..parallel.strategy import _cross_replica
 
+        if self.comm.world_size > 1:
+            # raises if a custom (xGMI) all-reduce of the executions since the last read timed out
+            self.comm.check_health()
         with _cross_replica():
             out = {"loss": float(self.loss_tracker.result())}
             for m in self.metrics:

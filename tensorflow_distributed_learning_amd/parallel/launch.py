@@ -26,6 +26,7 @@ import signal
 import socket
 import subprocess
 import sys
+import warnings
 import time
 from typing import Dict, List, Optional
 
@@ -153,16 +154,43 @@ def launch_local_workers(cmd: List[str], workers: int, gpus_per_worker: int, bas
 _SPAWNED: Optional[_Group] = None
 
 
+def _relaunch_argv() -> Optional[list]:
+    """Command line that re-runs this program: ``python script.py args`` or, for a program started
+    with ``python -m pkg.mod``, ``python -m pkg.mod args``; None for ``python -c`` / interactive."""
+    main = sys.argv[0] if sys.argv else ""
+    if not main or main == "-c" or not os.path.isfile(main):
+        return None
+    spec = getattr(sys.modules.get("__main__"), "__spec__", None)
+    if spec is not None and spec.name and spec.name != "__main__":
+        name = spec.name[:-len(".__main__")] if spec.name.endswith(".__main__") else spec.name
+        return [sys.executable, "-m", name] + sys.argv[1:]
+    return [sys.executable] + sys.argv
+
+
 def maybe_spawn_local_replicas(n: int, spawn: Optional[bool] = None) -> Optional[dict]:
     """MirroredStrategy started as a plain script with n > 1 devices: re-run the script once per
     extra device (children are replicas 1..n-1, this process is replica 0).  Must run before this
     process touches the GPU.  Returns the placement dict, or None to stay single-replica."""
     global _SPAWNED
+    if os.environ.get("TDL_LAUNCHED") == "1":
+        return None  # this process already is one of a launched group
     if spawn is None:
         spawn = os.environ.get("TDL_AUTO_SPAWN", "1") == "1"
     main = sys.argv[0] if sys.argv else ""
-    if not spawn or not main or not os.path.isfile(main) or "pytest" in os.path.basename(main) or \
-            os.environ.get("TDL_LAUNCHED") == "1":
+    argv = _relaunch_argv()
+    why = None
+    if not spawn:
+        why = "TDL_AUTO_SPAWN=0"
+    elif argv is None:
+        why = "the program is not a script or module file that can be re-run (python -c / interactive)"
+    elif "pytest" in sys.modules or os.path.basename(main).startswith("pytest") or \
+            os.path.basename(os.path.dirname(main)) in ("pytest", "_pytest"):
+        why = "running under pytest"
+    if why is not None:
+        warnings.warn(f"MirroredStrategy asked for {n} devices but runs as ONE replica: {why}; launch "
+                      f"with `python -m tensorflow_distributed_learning_amd.launch --nproc-per-node {n} ...` "
+                      f"for {n} replicas", RuntimeWarning, stacklevel=3)
+        sys.stderr.write(f"[tdl] WARNING: {n} devices requested, running 1 replica ({why})\n")
         return None
     port = free_port()
     env0 = _base_env(n)
@@ -171,7 +199,7 @@ def maybe_spawn_local_replicas(n: int, spawn: Optional[bool] = None) -> Optional
         env = dict(env0)
         env.update(RANK=str(lr), WORLD_SIZE=str(n), LOCAL_RANK=str(lr), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TDL_LAUNCHED="1")
-        g.start([sys.executable] + sys.argv, env)
+        g.start(argv, env)
     os.environ.update(RANK="0", WORLD_SIZE=str(n), LOCAL_RANK="0", LOCAL_WORLD_SIZE=str(n),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TDL_LAUNCHED="1")
     _SPAWNED = g

@@ -1,0 +1,57 @@
+"""Local replica self-launch (MirroredStrategy(devices=[...]) from a plain script): never degrade
+to one replica silently, and re-run ``python -m`` programs as modules."""
+import os
+import subprocess
+import sys
+import textwrap
+
+import pytest
+
+from tensorflow_distributed_learning_amd.parallel import launch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_degrade_to_one_replica_warns(monkeypatch):
+    monkeypatch.delenv("TDL_LAUNCHED", raising=False)
+    with pytest.warns(RuntimeWarning, match="runs as ONE replica"):
+        assert launch.maybe_spawn_local_replicas(2) is None
+
+
+def test_launched_child_does_not_warn(monkeypatch, recwarn):
+    monkeypatch.setenv("TDL_LAUNCHED", "1")
+    assert launch.maybe_spawn_local_replicas(4) is None
+    assert not [w for w in recwarn if issubclass(w.category, RuntimeWarning)]
+
+
+def test_relaunch_argv_script_and_c(monkeypatch, tmp_path):
+    script = tmp_path / "train.py"
+    script.write_text("pass\n")
+    monkeypatch.setattr(sys, "argv", [str(script), "--epochs", "2"])
+    main = sys.modules["__main__"]
+    monkeypatch.setattr(main, "__spec__", None, raising=False)
+    assert launch._relaunch_argv() == [sys.executable, str(script), "--epochs", "2"]
+    monkeypatch.setattr(sys, "argv", ["-c"])
+    assert launch._relaunch_argv() is None
+
+
+def test_python_dash_m_program_relaunches_as_module(tmp_path):
+    """A `python -m pkg.train` program asking for 2 CPU replicas spawns its peer as a module too."""
+    pkg = tmp_path / "mypkg"
+    pkg.mkdir()
+    (pkg / "__init__.py").write_text("")
+    (pkg / "train.py").write_text(textwrap.dedent("""
+        import os
+        from . import __name__ as _pkg  # relative import: fails if re-run as a plain script
+        import tensorflow_distributed_learning_amd as tdl
+        s = tdl.distribute.MirroredStrategy(devices=["/cpu:0", "/cpu:1"])
+        print("replicas", s.num_replicas_in_sync, "rank", s.extended.rank, flush=True)
+        s.shutdown()
+    """))
+    env = dict(os.environ, PYTHONPATH=f"{tmp_path}:{ROOT}", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "TF_CONFIG", "TDL_LAUNCHED"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-m", "mypkg.train"], env=env, capture_output=True, text=True,
+                       timeout=180, cwd=tmp_path)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "replicas 2 rank 0" in r.stdout, r.stdout + r.stderr
