@@ -130,14 +130,44 @@ def build_native_ext(nproc):
     return out
 
 
+def build_selftest(sanitize: str) -> str:
+    """Standalone C++ self-test of the runtime (csrc/native/tests/native_selftest.cpp + store.cpp +
+    ring.cpp) under a sanitizer: ``address`` = ASan + UBSan, ``thread`` = TSan (race detection).
+    Host code only (GPU sanitizers are not used on this pool)."""
+    odir = os.path.join(BUILD, "selftest")
+    os.makedirs(odir, exist_ok=True)
+    srcs = [os.path.join(CSRC, "native", "tests", "native_selftest.cpp"),
+            os.path.join(CSRC, "native", "store.cpp"), os.path.join(CSRC, "native", "ring.cpp")]
+    out = os.path.join(odir, f"native_selftest_{sanitize}")
+    newest = max([os.path.getmtime(x) for x in srcs] + [_newest_header()])
+    if os.path.exists(out) and os.path.getmtime(out) >= newest:
+        return out
+    san = ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"] if sanitize == "address" \
+        else ["-fsanitize=thread"]
+    # ROCm's clang: its TSan runtime intercepts pthread_cond_clockwait (what libstdc++'s
+    # condition_variable::wait_for calls); GCC 11's does not and reports false double locks
+    cxx = os.path.join(ROCM, "llvm", "bin", "clang++")
+    if not os.path.exists(cxx):
+        cxx = "c++"
+    _run([cxx, "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-pthread", *san, f"-I{CSRC}", *srcs,
+          "-o", out])
+    print(f"  built {os.path.relpath(out, HERE)}", flush=True)
+    return out
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--clean", action="store_true")
+    ap.add_argument("--sanitize", choices=["address", "thread"], default=None,
+                    help="build only the sanitizer self-test binary of the C++ runtime")
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 4))
     ap.add_argument("--only", choices=["hip", "native"], default=None)
     args = ap.parse_args(argv)
     if args.clean and os.path.isdir(BUILD):
         shutil.rmtree(BUILD)
+    if args.sanitize:
+        print(build_selftest(args.sanitize))
+        return 0
     if args.only in (None, "native"):
         build_native_ext(args.j)
     if args.only in (None, "hip"):
