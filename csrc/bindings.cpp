@@ -81,6 +81,14 @@ class MnistStep {
     a_.nslab = (int)W.numel();
   }
 
+  // accumulate metrics into another [>= 3] f32 tensor from now on (evaluation reuses step objects)
+  void set_metrics(at::Tensor m) {
+    check_cuda_f32(m, "metrics");
+    TORCH_CHECK(m.numel() >= 3, "metrics needs >= 3 elements");
+    metrics_ = m;
+    a_.metrics = metrics_.data_ptr<float>();
+  }
+
   void set_idx_offset(int64_t off) {
     TORCH_CHECK(off >= 0 && off + a_.b <= idx_.numel(), "idx offset out of range");
     a_.idx = idx_.data_ptr<int>() + off;
@@ -122,6 +130,21 @@ class MnistStep {
   void backward_conv() { tdl::mnist_conv_bwd(a_, cur_stream()); }
 
   void finalize(bool apply_sgd) { tdl::mnist_finalize(a_, apply_sgd, dense_pending_, cur_stream()); }
+
+  // forward-only evaluation / inference of the b rows at idx_off: loss, correct count and sample
+  // count accumulate into the metrics tensor; logits ([>= b*10] f32, optional) receive the logits
+  void forward_eval(int64_t idx_off, c10::optional<at::Tensor> logits) {
+    set_idx_offset(idx_off);
+    tdl::MnistArgs f = a_;
+    f.head = 2;
+    f.logits = nullptr;
+    if (logits.has_value()) {
+      check_cuda_f32(*logits, "logits");
+      TORCH_CHECK(logits->numel() >= (int64_t)a_.b * 10, "logits buffer too small");
+      f.logits = logits->data_ptr<float>();
+    }
+    tdl::mnist_fwd_conv(f, cur_stream());
+  }
 
   // forward features only (dense1 partials, no loss head / metrics)
   void forward_features(int64_t idx_off) {
@@ -181,9 +204,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def(pybind11::init<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, std::vector<int64_t>, int64_t,
                           double, at::Tensor, at::Tensor>())
       .def("set_idx_offset", &MnistStep::set_idx_offset)
+      .def("set_metrics", &MnistStep::set_metrics)
       .def("stage", &MnistStep::stage, pybind11::arg("k"), pybind11::arg("apply_sgd") = false)
       .def("forward_backward", &MnistStep::forward_backward)
       .def("forward_features", &MnistStep::forward_features)
+      .def("forward_eval", &MnistStep::forward_eval, pybind11::arg("idx_off"), pybind11::arg("logits") = pybind11::none())
       .def("forward_dense", &MnistStep::forward_dense)
       .def("backward_conv", &MnistStep::backward_conv)
       .def("finalize", &MnistStep::finalize)

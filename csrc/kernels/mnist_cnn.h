@@ -39,7 +39,9 @@ struct MnistArgs {
   int b;              // per-replica batch
   float scale;        // 1 / (b * R)
   int nslab;          // slab length (floats)
-  int head;           // 1: the forward kernel also runs the loss head (training); 0: features only
+  float* logits;      // [b][10] logits output of head mode 2 (null: metrics only)
+  int head;           // 1: training loss head (dH, dL, saved activations); 2: evaluation head
+                      // (logits, loss / accuracy accumulators, nothing saved); 0: features only
 };
 
 constexpr int kMnistPart2Rows = 289;

@@ -166,6 +166,49 @@ __device__ __forceinline__ void head_row(const MnistArgs& a, int r, int l, int y
   head_stamp(a.stamps, 3);
 }
 
+// Evaluation / inference head of ONE batch row (head mode 2): logits (optionally stored), loss and
+// top-1 accuracy into the metric accumulators; no gradient state.
+__device__ __forceinline__ void head_eval(const MnistArgs& a, int r, int l, int y, const HeadWeights& hw) {
+  float hp0[kDense1Chunks], hp1[kDense1Chunks];
+#pragma unroll
+  for (int c = 0; c < kDense1Chunks; ++c) {
+    hp0[c] = __hip_atomic_load(a.part3 + ((size_t)c * a.b + r) * 128 + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    hp1[c] = __hip_atomic_load(a.part3 + ((size_t)c * a.b + r) * 128 + l + 64, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+  }
+  float h0 = hw.b3a, h1 = hw.b3b;
+#pragma unroll
+  for (int c = 0; c < kDense1Chunks; ++c) { h0 += hp0[c]; h1 += hp1[c]; }
+  h0 = fmaxf(h0, 0.f);
+  h1 = fmaxf(h1, 0.f);
+  float lg[10];
+  {
+    float v[10];
+#pragma unroll
+    for (int c = 0; c < 10; ++c) v[c] = fmaf(h0, hw.wa[c], h1 * hw.wb[c]);
+    wave_sum10(v, l, lg);
+  }
+#pragma unroll
+  for (int c = 0; c < 10; ++c) lg[c] += hw.b4[c];
+  float m = lg[0], ly = lg[0], mine = lg[0];
+  int am = 0;
+#pragma unroll
+  for (int c = 1; c < 10; ++c) {
+    if (lg[c] > m) { m = lg[c]; am = c; }
+    ly = (c == y) ? lg[c] : ly;
+    mine = (c == l) ? lg[c] : mine;
+  }
+  float se = 0.f;
+#pragma unroll
+  for (int c = 0; c < 10; ++c) se += __expf(lg[c] - m);
+  if (a.logits != nullptr && l < 10) a.logits[(size_t)r * 10 + l] = mine;
+  if (l == 0) {
+    atomicAdd(&a.metrics[0], m + __logf(se) - ly);
+    atomicAdd(&a.metrics[1], am == y ? 1.f : 0.f);
+    atomicAdd(&a.metrics[2], 1.f);
+  }
+}
+
 // --------------------------------------------------------------------------------------------
 // K5: dense-layer backward, one 16x16 MFMA output tile per wave task (every task's loads issued
 // in one round trip; biases are an extra "ones" row of the weight-gradient GEMMs):
@@ -771,7 +814,7 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
     st4_sc1(buf_rsrc(a.part3 + ((size_t)cq * a.b + bi) * 128, 512), tid * 16, hsum);
   }
   stamp(a.stamps, 6);
-  if (!a.head) {
+  if (a.head == 0) {
     store_saved_fwd(a, bi, cq, P1s, a1s, p2s, a2s, tid, 512);
     return;
   }
@@ -791,10 +834,12 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   if (tid == 0) *s_last = (__hip_atomic_fetch_add(a.cnt + bi, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 3u) == 3u;
   __syncthreads();
   if (*s_last && wave == 0) {
-    head_row(a, bi, lane, label, hw);
+    if (a.head == 1) head_row(a, bi, lane, label, hw);
+    else head_eval(a, bi, lane, label, hw);
     stamp(a.stamps, 7);
     return;
   }
+  if (a.head != 1) return;  // evaluation: nothing is saved for a backward pass
   // saved activations leave LDS only now (off the head's critical path)
   if (*s_last) store_saved_fwd(a, bi, cq, P1s, a1s, p2s, a2s, tid - 64, 448);
   else store_saved_fwd(a, bi, cq, P1s, a1s, p2s, a2s, tid, 512);

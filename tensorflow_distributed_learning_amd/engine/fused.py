@@ -439,6 +439,121 @@ class FusedMnistTrainer:
             done += K
         return done
 
+    # ------------------------------------------------------------------ evaluate / predict
+    def _eval_columns(self, lp, labels: bool):
+        """Device copies of an evaluation pipeline's columns (the last one is cached), or None
+        when they are not the reference model's input."""
+        cols = lp.columns if isinstance(lp.columns, (tuple, list)) else (lp.columns,)
+        x = cols[0]
+        y = cols[1] if len(cols) > 1 else None
+        if not isinstance(x, torch.Tensor) or tuple(x.shape[1:]) not in ((28, 28, 1), (28, 28)) or \
+                x.dtype != torch.float32:
+            return None
+        if labels and (not isinstance(y, torch.Tensor) or y.dim() != 1):
+            return None
+        key = (id(x), id(y) if labels else None)
+        cached = getattr(self, "_eval_cache", None)
+        if cached is None or cached[0] != key:
+            X = x.reshape(len(x), 28, 28, 1).to(self.device, torch.float32).contiguous()
+            Y = (y.to(self.device, torch.int32) if labels else torch.zeros(len(x), dtype=torch.int32, device=self.device)).contiguous()
+            self._eval_cache = cached = (key, X, Y, {})
+        return cached[1], cached[2], cached[3]
+
+    def _eval_step(self, steps: dict, X, Y, b: int, cap: int, metrics):
+        st = steps.get(b)
+        if st is None or st.idx_buf.numel() < cap * b:
+            idx_buf = torch.zeros(max(cap, 1) * b, dtype=torch.int32, device=self.device)
+            st = M.FusedMnistTrainStep(X, Y, idx_buf, self.W, self.G, self.layout, b, self.R, self.optimizer.lr_dev,
+                                       metrics)
+            steps[b] = st
+        st.metrics = metrics
+        st._impl.set_metrics(metrics)
+        return st
+
+    def _forward_batches(self, handler: "DeviceHandler", X, Y, cache, steps, metrics, logits_out=None):
+        """Forward-only passes over the handler's batches on the hand-written kernels."""
+        K = 64
+        done = 0
+        while steps is None or done < steps:
+            n = K if steps is None else min(K, steps - done)
+            idx = handler.take(n)
+            if idx is None:
+                one = handler.next_ragged()
+                if one is None:
+                    break
+                ids, nb, _ = one
+                if nb > 0:
+                    st = self._eval_step(cache, X, Y, nb, 1, metrics)
+                    st.idx_buf[:nb].copy_(torch.from_numpy(np.ascontiguousarray(ids, dtype=np.int32)))
+                    lg = None if logits_out is None else torch.empty(nb * 10, device=self.device)
+                    st.forward_eval(0, lg)
+                    if lg is not None:
+                        logits_out.append(lg.view(nb, 10))
+                done += 1
+                continue
+            b = handler.b
+            kb = idx.size // b
+            st = self._eval_step(cache, X, Y, b, K, metrics)
+            st.idx_buf[:idx.size].copy_(torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int32)))
+            lg = None if logits_out is None else torch.empty(kb * b * 10, device=self.device)
+            for k in range(kb):
+                st.forward_eval(k * b, None if lg is None else lg[k * b * 10:])
+            if lg is not None:
+                logits_out.append(lg.view(kb * b, 10))
+            done += kb
+        return done
+
+    def evaluate(self, dataset, steps: Optional[int] = None) -> Optional[Dict[str, float]]:
+        """``Model.evaluate`` on the gfx950 forward kernel (head mode 2): each replica evaluates its
+        slice of every global batch of the device-resident pipeline; loss / accuracy sums are
+        all-reduced once at the end.  None when the pipeline does not lower to the device."""
+        lp = DD.lower(dataset)
+        if lp is None:
+            return None
+        cols = self._eval_columns(lp, labels=True)
+        if cols is None:
+            return None
+        X, Y, cache = cols
+        if lp.batch_size % self.R:
+            return None
+        h = DeviceHandler(lp, None, self.rank, self.R)
+        h._async = False
+        metrics = torch.zeros(4, dtype=torch.float32, device=self.device)
+        try:
+            self._forward_batches(h, X, Y, cache, steps, metrics)
+        finally:
+            h.close()
+        if self.R > 1:
+            self.comm.check_health()
+            self.comm.all_reduce(metrics, "sum")
+        loss_sum, correct, count = (float(v) for v in metrics[:3].cpu())
+        out = {"loss": loss_sum / max(count, 1.0)}
+        for m in self.model.compiled_metrics:
+            out[m.name] = correct / max(count, 1.0)
+        return out
+
+    def predict(self, dataset, steps: Optional[int] = None) -> Optional[np.ndarray]:
+        """``Model.predict`` on the gfx950 forward kernel: logits of every sample in order.  Every
+        replica computes all of them (inference is replica-independent; no collective)."""
+        lp = DD.lower(dataset)
+        if lp is None:
+            return None
+        cols = self._eval_columns(lp, labels=False)
+        if cols is None:
+            return None
+        X, Y, cache = cols
+        h = DeviceHandler(lp, None, 0, 1)
+        h._async = False
+        metrics = torch.zeros(4, dtype=torch.float32, device=self.device)
+        out = []
+        try:
+            self._forward_batches(h, X, Y, cache, steps, metrics, logits_out=out)
+        finally:
+            h.close()
+        if not out:
+            return np.zeros((0, 10), dtype=np.float32)
+        return torch.cat(out).cpu().numpy()
+
     def reset_metrics(self):
         self.metrics_dev.zero_()
         self.model._loss_tracker.reset_state()

@@ -444,6 +444,18 @@ class Model(Layer):
         self._peek_build(ds)
         if self.optimizer is None:
             raise RuntimeError("compile() the model before evaluate()")
+        if sample_weight is None and os.environ.get("TDL_FUSED_EVAL", "1") == "1":
+            tr = self._get_trainer()
+            out = tr.evaluate(ds, steps) if tr.kind == "fused" else None
+            if out is not None:  # forward-only pass on the MI355X kernels (engine/fused.py)
+                if verbose and verbose != "auto" and self._is_chief() and not _internal:
+                    from ..utils.progbar import format_logs
+
+                    print(format_logs(out))
+                if return_dict:
+                    return out
+                vals = [out[k] for k in ["loss"] + [m.name for m in self.compiled_metrics]]
+                return vals if len(vals) > 1 else vals[0]
         prev = self._trainer
         self._ensure_slabs()
         ev = GenericTrainer.__new__(GenericTrainer)
@@ -484,6 +496,13 @@ class Model(Layer):
         else:
             ds = D.Dataset.from_tensor_slices(x).batch(batch_size or 32)
         self._peek_build(ds)
+        tr = self._trainer
+        if tr is None and self.optimizer is not None and self.loss is not None:
+            tr = self._get_trainer()
+        if tr is not None and tr.kind == "fused" and os.environ.get("TDL_FUSED_EVAL", "1") == "1":
+            out = tr.predict(ds, steps)
+            if out is not None:  # forward-only pass on the MI355X kernels (engine/fused.py)
+                return out
         if self._W is not None:
             for v in self._trainable_vars:
                 v._leaf = None

@@ -126,6 +126,11 @@ class FusedMnistTrainStep:
     def forward_backward(self, idx_offset: int) -> None:
         self._impl.forward_backward(int(idx_offset))
 
+    def forward_eval(self, idx_offset: int, logits: Optional[torch.Tensor] = None) -> None:
+        """Forward only (evaluate / predict): loss, correct and sample counts of the b rows at
+        ``idx_offset`` accumulate into ``metrics``; ``logits`` [>= b*10] receives their logits."""
+        self._impl.forward_eval(int(idx_offset), logits)
+
     def forward_dense(self, idx_offset: int) -> None:
         """Forward, loss and the dense-layer backward (their gradients land in G)."""
         self._impl.forward_dense(int(idx_offset))
