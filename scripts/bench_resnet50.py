@@ -34,6 +34,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1, help="replicas (GPUs) in the whole job")
     ap.add_argument("--workers", type=int, default=2, help="--strategy mwms: TF_CONFIG tasks on this node")
     ap.add_argument("--comm", choices=["auto", "nccl", "ring"], default="auto")
+    ap.add_argument("--allreduce-dtype", choices=["float32", "bfloat16"], default="float32",
+                    help="gradient dtype on the wire (CommunicationOptions.all_reduce_dtype)")
+    ap.add_argument("--bytes-per-pack", type=int, default=0,
+                    help="all-reduce bucket bytes (CommunicationOptions.bytes_per_pack; 0 = size/topology plan)")
     ap.add_argument("--conv-search", type=int, default=1,
                     help="1: MIOpen find-mode solver search per conv shape (torch.backends.cudnn.benchmark)")
     ap.add_argument("--strategy", default="mirrored", choices=["mirrored", "mwms"],
@@ -55,11 +59,14 @@ def main():
 
     torch.backends.cudnn.benchmark = bool(args.conv_search)
     tdl.keras.mixed_precision.set_global_policy(args.dtype)
+    copts = tdl.distribute.experimental.CommunicationOptions(
+        implementation=args.comm.upper(), bytes_per_pack=args.bytes_per_pack,
+        all_reduce_dtype=None if args.allreduce_dtype == "float32" else args.allreduce_dtype)
     if args.strategy == "mwms":
-        strategy = tdl.distribute.MultiWorkerMirroredStrategy(communication=args.comm.upper())
+        strategy = tdl.distribute.MultiWorkerMirroredStrategy(communication_options=copts)
     else:
         strategy = tdl.distribute.MirroredStrategy(devices=[f"/gpu:{i}" for i in range(args.gpus)],
-                                                   communication=args.comm.upper())
+                                                   communication_options=copts)
     R = strategy.num_replicas_in_sync
     if R != args.gpus:
         raise SystemExit(f"bench_resnet50: strategy has {R} replicas, expected --gpus {args.gpus}")
@@ -136,7 +143,7 @@ def main():
                                    if getattr(strategy.extended, "tf_config", None) else 1),
                        "engine": trainer.kind, "communicator": comm.name,
                        "allreduce": getattr(comm, "algorithm", comm.name),
-                       "bucket_plan": getattr(trainer, "bucket_plan", None),
+                       "bucket_plan": (trainer.plan.as_dict() if getattr(trainer, "plan", None) else None),
                        "replicas_identical": identical, "final_loss": round(logs["loss"], 4)},
         }), flush=True)
     if strategy.extended.rank == 0:

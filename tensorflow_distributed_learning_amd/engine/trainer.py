@@ -178,14 +178,29 @@ class GenericTrainer:
 
     def _make_buckets(self):
         """Overlap of the gradient all-reduce with backward: contiguous slab buckets (reverse
-        layer order) are launched asynchronously as soon as every gradient inside is final."""
+        layer order) are launched asynchronously as soon as every gradient inside is final.  The
+        bucket size comes from compile(bucket_bytes=...), else CommunicationOptions.bytes_per_pack,
+        else the size/topology plan of parallel/bucketing.py; CommunicationOptions.all_reduce_dtype
+        sets the dtype on the wire."""
+        from ..parallel import bucketing
+
+        opts = getattr(self.strategy.extended, "communication_options", None)
+        self._wire = (getattr(opts, "all_reduce_dtype", None) or "float32") if self.device.type == "cuda" else "float32"
+        wb = bucketing.DTYPE_BYTES[self._wire]
+        explicit = self.model._bucket_bytes
+        per_pack = explicit if explicit is not None else int(getattr(opts, "bytes_per_pack", 0) or 0)
+        lw = int(os.environ.get("LOCAL_WORLD_SIZE", self.comm.world_size) or self.comm.world_size)
+        self.plan = bucketing.plan(self.G.numel(), self.comm.world_size, lw, self._wire, per_pack,
+                                   algorithm=getattr(self.comm, "algorithm", self.comm.name))
+        self._wire_full = None
         if self.comm.world_size == 1 or self.comm.name != "rccl":
             return None
-        bucket_bytes = self.model._bucket_bytes
-        if not bucket_bytes:
+        if explicit == 0:
+            self.plan.n_buckets, self.plan.bucket_bytes = 1, self.plan.wire_bytes
             return None
         layout = self.model._layout
-        ranges = layout.buckets(bucket_bytes)
+        ranges = layout.buckets(self.plan.bucket_bytes, elem_bytes=wb)
+        self.plan.n_buckets = len(ranges)
         if len(ranges) <= 1:
             return None
         var_bucket = {}
@@ -195,6 +210,9 @@ class GenericTrainer:
                     var_bucket[i] = bi
         self._pending = [sum(1 for i in var_bucket if var_bucket[i] == b) for b in range(len(ranges))]
         self._bucket_ranges = ranges
+        # low-precision wire copies of every bucket, allocated once (graph-capture safe)
+        self._wire_bufs = None if self._wire == "float32" else [
+            torch.empty(e - s, dtype=getattr(torch, self._wire), device=self.device) for s, e in ranges]
         self._var_bucket = var_bucket
         self._works = []
         self._counts = list(self._pending)
@@ -213,7 +231,12 @@ class GenericTrainer:
                 self._counts[b] -= 1
                 if self._counts[b] == 0:
                     s, e = self._bucket_ranges[b]
-                    self._works.append(self.comm.all_reduce_async(self.G[s:e], "sum"))
+                    if self._wire_bufs is None:
+                        self._works.append(self.comm.all_reduce_async(self.G[s:e], "sum"))
+                    else:
+                        buf = self._wire_bufs[b]
+                        buf.copy_(self.G[s:e])
+                        self._works.append((self.comm.all_reduce_async(buf, "sum"), b))
             return hook
 
         for i, leaf in enumerate(self._leaves):
@@ -260,9 +283,20 @@ class GenericTrainer:
             with trace_range("tdl.allreduce"):
                 if self._buckets is not None:
                     for w in self._works:
-                        w.wait()
+                        if isinstance(w, tuple):  # low-precision wire copy: cast back into G
+                            w[0].wait()
+                            s, e = self._bucket_ranges[w[1]]
+                            G[s:e].copy_(self._wire_bufs[w[1]])
+                        else:
+                            w.wait()
                     if len(self._works) != len(self._bucket_ranges):
                         raise RuntimeError("gradient bucket hooks did not fire for every bucket (unused parameters?)")
+                elif self._wire != "float32":
+                    if self._wire_full is None:
+                        self._wire_full = torch.empty(G.numel(), dtype=getattr(torch, self._wire), device=G.device)
+                    self._wire_full.copy_(G)
+                    self.comm.all_reduce(self._wire_full, "sum")
+                    G.copy_(self._wire_full)
                 else:
                     self.comm.all_reduce(G, "sum")
         with torch.no_grad(), trace_range("tdl.optimizer"):

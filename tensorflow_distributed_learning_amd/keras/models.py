@@ -251,8 +251,10 @@ class Model(Layer):
             self.compiled_metrics = [_metrics.get(m, self.loss) for m in ms]
             self._loss_tracker = _metrics.Mean(name="loss")
         self._steps_per_execution = int(steps_per_execution or 1)
-        # RCCL all-reduce bucket size for overlap with backward (0 = one all-reduce per step)
-        self._bucket_bytes = int(bucket_bytes if bucket_bytes is not None else (25 << 20))
+        # RCCL all-reduce bucket size for overlap with backward (0 = one all-reduce per step,
+        # None = the strategy's CommunicationOptions.bytes_per_pack, else the size/topology plan
+        # of parallel/bucketing.py)
+        self._bucket_bytes = None if bucket_bytes is None else int(bucket_bytes)
         self._run_eagerly = bool(run_eagerly)
         self._trainer = None
         self._compile_config = {

@@ -33,12 +33,17 @@ class CommunicationOptions:
     bytes_per_pack: int = 0
     timeout_seconds: Optional[float] = None
     implementation: CommunicationImplementation = CommunicationImplementation.AUTO
+    # extension (not in TF): dtype of the gradient on the wire; "bfloat16" halves the all-reduce
+    # bytes of an f32 gradient (cast before, cast back after; summation error of bf16)
+    all_reduce_dtype: Optional[str] = None
 
     def __post_init__(self):
         if isinstance(self.implementation, str):
             self.implementation = CommunicationImplementation(self.implementation.upper())
         if self.bytes_per_pack < 0:
             raise ValueError("bytes_per_pack must be >= 0")
+        if self.all_reduce_dtype not in (None, "float32", "bfloat16", "float16"):
+            raise ValueError(f"all_reduce_dtype must be float32, bfloat16 or float16, got {self.all_reduce_dtype!r}")
 
 
 def normalize_options(communication=None, communication_options=None) -> CommunicationOptions:

@@ -370,8 +370,9 @@ class MirroredStrategy(Strategy):
     """tf.distribute.MirroredStrategy(devices=None, cross_device_ops=None)."""
 
     def __init__(self, devices: Optional[Sequence] = None, cross_device_ops=None, *, communication=None,
-                 spawn: Optional[bool] = None):
-        opts = normalize_options(communication if communication is not None else _cdo_to_impl(cross_device_ops))
+                 communication_options=None, spawn: Optional[bool] = None):
+        opts = normalize_options(communication if communication is not None or communication_options is not None
+                                 else _cdo_to_impl(cross_device_ops), communication_options)
         launched = _launched()
         if devices is not None:
             devs = [parse_device(d) for d in devices]

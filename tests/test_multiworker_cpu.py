@@ -160,3 +160,53 @@ def test_launcher_propagates_failure(tmp_path):
     """
     r = _launch(tmp_path, body, ["--nproc-per-node", "2"], timeout=60)
     assert r.returncode == 7
+
+
+def test_corrupted_replica_detected_and_repaired(tmp_path):
+    """A replica whose weights are silently corrupted mid-training (as a broken fabric hand-off
+    would) is detected by fit's periodic fingerprint check, re-synchronised from rank 0, and
+    raises instead under TDL_REPLICA_MISMATCH=raise."""
+    body = """
+    import json, os, sys, warnings, numpy as np, torch
+    import tensorflow_distributed_learning_amd as tdl
+    from tensorflow_distributed_learning_amd.models.mnist_cnn import build_mnist_cnn
+    from tensorflow_distributed_learning_amd.parallel import consistency
+    out = sys.argv[1]
+    strategy = tdl.distribute.MirroredStrategy(communication="RING")
+    rank = strategy.extended.rank
+    from tensorflow_distributed_learning_amd.data.tfds import synthetic_mnist
+    x, y = synthetic_mnist(512, 2)
+    ds = tdl.data.Dataset.from_tensor_slices((x.reshape(-1, 28, 28, 1).astype(np.float32) / 255, y)).batch(64).repeat()
+    with strategy.scope():
+        m = build_mnist_cnn()
+        m.compile(loss=tdl.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+                  optimizer=tdl.keras.optimizers.SGD(0.05))
+
+    class Corrupt(tdl.keras.callbacks.Callback):
+        def on_epoch_end(self, epoch, logs=None):
+            if epoch == 0 and rank == 1:
+                with torch.no_grad():
+                    m._W.view(-1)[12345] += 1e-3   # one parameter of one replica drifts
+    comm = strategy.extended.communicator
+    status = {}
+    with warnings.catch_warnings(record=True) as rec:
+        warnings.simplefilter("always")
+        m.fit(ds, epochs=3, steps_per_epoch=2, verbose=0, callbacks=[Corrupt()])
+    status["warned"] = any("replica divergence" in str(w.message) for w in rec)
+    status["identical_after"] = consistency.replicas_identical(comm, m._W)
+    # strict mode: the same drift raises on every rank
+    if rank == 1:
+        with torch.no_grad():
+            m._W.view(-1)[7] -= 1e-3
+    os.environ["TDL_REPLICA_MISMATCH"] = "raise"
+    try:
+        consistency.check_and_repair(comm, m._W)
+        status["raised"] = False
+    except consistency.ReplicaDivergenceError:
+        status["raised"] = True
+    json.dump(status, open(os.path.join(out, f"out{rank}.json"), "w"))
+    """
+    r = _launch(tmp_path, body, ["--nproc-per-node", "2"], env={"TDL_CHECK_REPLICAS_EVERY": "1"})
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    for s in _results(tmp_path, 2):
+        assert s["warned"] and s["identical_after"] and s["raised"], s
