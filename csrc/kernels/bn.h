@@ -27,12 +27,12 @@ void bn_forward_stats(const void* x, BnDType dt, int64_t M, int C, float* part, 
 // y = act(x*scale + shift [+ residual])  (relu when relu != 0; residual nullable)
 void bn_apply(const void* x, const void* residual, void* y, BnDType dt, int64_t M, int C, const float* scale,
               const float* shift, int relu, hipStream_t s);
-// backward; dgamma/dbeta [C] out, coef [3][C] scratch, dx = A*dz + B*x + D where
+// backward; dgamma/dbeta [C] out (acc bit 0/1: added into them), coef [3][C] scratch, dx = A*dz + B*x + D where
 //   mode 0: dz = dy                         (plain BN)
 //   mode 1: dz = dy * (x*scale+shift > 0)   (BN + ReLU, mask recomputed from x)
 //   mode 2: dz = dy * (y > 0), written to dz (BN + Add + ReLU: dz is also the residual's gradient)
 void bn_backward(const void* dy, const void* x, const void* y, void* dz, void* dx, BnDType dt, int64_t M, int C,
                  float* part, const float* gamma, const float* mean, const float* invstd, const float* scale,
-                 const float* shift, float* dgamma, float* dbeta, float* coef, int mode, hipStream_t s);
+                 const float* shift, float* dgamma, float* dbeta, float* coef, int mode, int acc, hipStream_t s);
 
 }  // namespace tdl

@@ -195,7 +195,7 @@ __global__ __launch_bounds__(1024) void k_bn_bwd_finalize(const float* __restric
                                                          const float* __restrict__ gamma,
                                                          const float* __restrict__ mean,
                                                          const float* __restrict__ invstd, float* __restrict__ dgamma,
-                                                         float* __restrict__ dbeta, float* __restrict__ coef) {
+                                                         float* __restrict__ dbeta, float* __restrict__ coef, int acc) {
   double S, Q;
   if (!reduce_parts(part, P, C, S, Q)) return;
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
@@ -203,8 +203,9 @@ __global__ __launch_bounds__(1024) void k_bn_bwd_finalize(const float* __restric
   const double g = gamma ? gamma[c] : 1.0;
   const double dg = (Q - mu * S) * inv;  // sum dy * xhat
   const double db = S;                   // sum dy
-  if (dgamma) dgamma[c] = (float)dg;
-  if (dbeta) dbeta[c] = (float)db;
+  // acc bit 0 / 1: add into dgamma / dbeta (a trainer's gradient slab) instead of overwriting
+  if (dgamma) dgamma[c] = (acc & 1) ? dgamma[c] + (float)dg : (float)dg;
+  if (dbeta) dbeta[c] = (acc & 2) ? dbeta[c] + (float)db : (float)db;
   // dx = g*inv/M * (M*dy - db - xhat*dg) = A*dy + B*x + D
   const double A = g * inv, B = -g * inv * inv * dg / (double)M;
   coef[c] = (float)A;
@@ -224,8 +225,10 @@ __global__ __launch_bounds__(256) void k_bn_apply(const void* __restrict__ x, co
   }
   __syncthreads();
   const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < n8; v += stride) {
-    const int c0 = (int)((v * 8) % C);
+  const int64_t v0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int cstep = (int)((stride * 8) % C);  // channel advance per grid stride (no 64-bit modulo per vector)
+  int c0 = (int)((v0 * 8) % C);
+  for (int64_t v = v0; v < n8; v += stride, c0 = (c0 + cstep >= C) ? c0 + cstep - C : c0 + cstep) {
     float xv[8], rv[8];
     Io<D>::load(x, v * 8, xv);
     if (res != nullptr) Io<D>::load(res, v * 8, rv);
@@ -257,8 +260,10 @@ __global__ __launch_bounds__(256) void k_bn_dx(const void* __restrict__ dy, cons
   }
   __syncthreads();
   const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < n8; v += stride) {
-    const int c0 = (int)((v * 8) % C);
+  const int64_t v0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int cstep = (int)((stride * 8) % C);
+  int c0 = (int)((v0 * 8) % C);
+  for (int64_t v = v0; v < n8; v += stride, c0 = (c0 + cstep >= C) ? c0 + cstep - C : c0 + cstep) {
     float g[8], xv[8];
     Io<D>::load(dy, v * 8, g);
     Io<D>::load(x, v * 8, xv);
@@ -318,7 +323,8 @@ void bn_apply(const void* x, const void* residual, void* y, BnDType dt, int64_t 
 template <BnDType D>
 static void bn_backward_t(const void* dy, const void* x, const void* y, void* dz, void* dx, int64_t M, int C,
                           float* part, const float* gamma, const float* mean, const float* invstd, const float* scale,
-                          const float* shift, float* dgamma, float* dbeta, float* coef, int mode, hipStream_t s) {
+                          const float* shift, float* dgamma, float* dbeta, float* coef, int mode, int acc,
+                          hipStream_t s) {
   const BnPlan p = bn_plan(M, C);
   const dim3 gp(p.parts), blk(256);
   if (mode == 0)
@@ -330,7 +336,7 @@ static void bn_backward_t(const void* dy, const void* x, const void* y, void* dz
   else
     hipLaunchKernelGGL((k_bn_partial<D, 3>), gp, blk, 0, s, dy, x, y, nullptr, nullptr, dz, M, C, p.rows_wg, part);
   hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), dim3(64 * kFinPhases), 0, s, part, p.parts, M, C, gamma, mean, invstd,
-                     dgamma, dbeta, coef);
+                     dgamma, dbeta, coef, acc);
   const int64_t n8 = M * C / 8;
   const dim3 ge(elementwise_grid(n8));
   if (mode == 1)
@@ -341,13 +347,13 @@ static void bn_backward_t(const void* dy, const void* x, const void* y, void* dz
 
 void bn_backward(const void* dy, const void* x, const void* y, void* dz, void* dx, BnDType dt, int64_t M, int C,
                  float* part, const float* gamma, const float* mean, const float* invstd, const float* scale,
-                 const float* shift, float* dgamma, float* dbeta, float* coef, int mode, hipStream_t s) {
+                 const float* shift, float* dgamma, float* dbeta, float* coef, int mode, int acc, hipStream_t s) {
   if (dt == BnDType::kBF16)
     bn_backward_t<BnDType::kBF16>(dy, x, y, dz, dx, M, C, part, gamma, mean, invstd, scale, shift, dgamma, dbeta,
-                                   coef, mode, s);
+                                   coef, mode, acc, s);
   else
     bn_backward_t<BnDType::kF32>(dy, x, y, dz, dx, M, C, part, gamma, mean, invstd, scale, shift, dgamma, dbeta, coef,
-                                  mode, s);
+                                  mode, acc, s);
 }
 
 }  // namespace tdl

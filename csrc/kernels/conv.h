@@ -8,6 +8,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <vector>
+
 namespace tdl {
 
 struct ConvGeom {
@@ -25,6 +27,26 @@ void conv_fwd_bf16(const void* x, const void* w_ohwi, void* y, const ConvGeom& g
 // stride-1 input gradient: dx[N,H,W,C] = conv_transpose(dy[N,OH,OW,K], w[KH][KW][C][K]) (HWIO, the
 // Keras layout: for a fixed (kh, kw, c) the K reduction values are contiguous)
 void conv_dgrad_bf16(const void* dy, const void* w_hwio, void* dx, const ConvGeom& g, hipStream_t s);
+
+// Input gradient of a 1x1, stride-2, unpadded convolution (the strided shortcut / first 1x1 of a
+// ResNet-50 stage): dx[n][2i][2j] = dy[n][i][j] . w^T, the other three pixels of every 2x2 block are
+// zero (written by the same kernel's epilogue; H <= 2*OH, W <= 2*OW).
+void conv_dgrad_s2_1x1_bf16(const void* dy, const void* w_hwio, void* dx, const ConvGeom& g, hipStream_t s);
+
+// Weight gradient, split-K over output pixels with a deterministic partial-slab reduction.
+struct WgradPlan {
+  int wmw, wnw;        // workgroup tile: (64 wmw) output channels x (64 wnw) (kh, kw, c) columns
+  int chunk, nsplit;   // pixels per slice, slices
+  long long ws_elems;  // f32 partial slab elements (nsplit x KH*KW*C x K)
+};
+bool conv_wgrad_supported(const ConvGeom& g);
+// the model's best `max_plans` candidates, best first
+std::vector<WgradPlan> conv_wgrad_plans(const ConvGeom& g, int max_plans);
+WgradPlan conv_wgrad_make_plan(const ConvGeom& g, int wmw, int wnw, int nsplit);
+// dW (HWIO [KH][KW][C][K]) from x[N,H,W,C] and dy[N,OH,OW,K]: into dw_bf16, or (dw_bf16 == nullptr)
+// into the f32 dw_f32 (added to it when accumulate).  ws: plan.ws_elems f32.
+void conv_wgrad_bf16(const void* x, const void* dy, float* ws, const WgradPlan& p, void* dw_bf16, float* dw_f32,
+                     bool accumulate, const ConvGeom& g, hipStream_t s);
 
 // Tile-sweep hook: 0 = per-shape heuristic (default), 1 = 128x64, 2 = 128x128, 3 = 256x128.
 void conv_force_tile(int tile);

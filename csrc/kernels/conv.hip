@@ -45,6 +45,9 @@ struct Igemm {
   int flip;                 // 1: mirrored taps (input gradient)
   long long w_col, w_kh, w_kw;  // weight element strides: per output column, per tap row, per tap column
   int M;
+  int scatter;  // 2: output row (n, oh, ow) goes to pixel (2oh, 2ow) of a [N][XH][XW][K] tensor whose
+                // other three pixels of each 2x2 block are written as zeros (1x1 stride-2 input gradient)
+  int XH, XW;
 };
 
 __device__ __forceinline__ uint16_t f2bf(float f) {
@@ -184,13 +187,32 @@ __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
     }
   __syncthreads();
   constexpr int SEG = BN / 8;  // 16-B segments per row
+  if (!a.scatter) {
 #pragma unroll
-  for (int s = tid; s < BM * SEG; s += NT) {
-    const int row = s / SEG, seg = s % SEG;
-    const int m = tm * BM + row;
-    if (m < a.M)
-      *reinterpret_cast<u32x4*>(a.y + (long long)m * a.K + tn * BN + seg * 8) =
-          *reinterpret_cast<const u32x4*>(lds + row * OUT_LD + seg * 8);
+    for (int s = tid; s < BM * SEG; s += NT) {
+      const int row = s / SEG, seg = s % SEG;
+      const int m = tm * BM + row;
+      if (m < a.M)
+        *reinterpret_cast<u32x4*>(a.y + (long long)m * a.K + tn * BN + seg * 8) =
+            *reinterpret_cast<const u32x4*>(lds + row * OUT_LD + seg * 8);
+    }
+  } else {
+    for (int s = tid; s < BM * SEG; s += NT) {
+      const int row = s / SEG, seg = s % SEG;
+      const int m = tm * BM + row;
+      if (m >= a.M) continue;
+      const int ow = m % a.OW, t = m / a.OW, oh = t % a.OH, n = t / a.OH;
+      const int h = 2 * oh, w = 2 * ow;
+      uint16_t* o = a.y + (((long long)n * a.XH + h) * a.XW + w) * a.K + tn * BN + seg * 8;
+      const long long rs = (long long)a.XW * a.K;
+      const u32x4 z{0u, 0u, 0u, 0u};
+      *reinterpret_cast<u32x4*>(o) = *reinterpret_cast<const u32x4*>(lds + row * OUT_LD + seg * 8);
+      if (w + 1 < a.XW) *reinterpret_cast<u32x4*>(o + a.K) = z;
+      if (h + 1 < a.XH) {
+        *reinterpret_cast<u32x4*>(o + rs) = z;
+        if (w + 1 < a.XW) *reinterpret_cast<u32x4*>(o + rs + a.K) = z;
+      }
+    }
   }
 }
 
@@ -234,6 +256,15 @@ void conv_dgrad_bf16(const void* dy, const void* w_hwio, void* dx, const ConvGeo
   Igemm a{static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w_hwio), static_cast<uint16_t*>(dx),
           g.N, g.OH, g.OW, g.K, g.H, g.W, g.C, g.KH, g.KW, 1, 1, g.KH - 1 - g.PT, g.KW - 1 - g.PL, 1,
           (long long)g.K, (long long)g.KW * g.C * g.K, (long long)g.C * g.K, g.N * g.H * g.W};
+  launch(a, s);
+}
+
+void conv_dgrad_s2_1x1_bf16(const void* dy, const void* w_hwio, void* dx, const ConvGeom& g, hipStream_t s) {
+  // a 1x1 stride-1 "convolution" of dy [N][OH][OW][K] with the HWIO rows [C][K] (columns C, reduction K),
+  // scattered to the even pixels of dx [N][H][W][C]
+  Igemm a{static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w_hwio), static_cast<uint16_t*>(dx),
+          g.N, g.OH, g.OW, g.K, g.OH, g.OW, g.C, 1, 1, 1, 1, 0, 0, 0,
+          (long long)g.K, 0, 0, g.N * g.OH * g.OW, 2, g.H, g.W};
   launch(a, s);
 }
 

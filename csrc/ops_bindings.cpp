@@ -89,8 +89,11 @@ std::vector<at::Tensor> bn_forward_train(at::Tensor x, c10::optional<at::Tensor>
 }
 
 // backward (mode 0 plain, 1 relu, 2 add+relu using y); returns (dx, dgamma, dbeta[, dz])
+// dgamma_out / dbeta_out: f32 [C] tensors the parameter gradients are ADDED into (a trainer's slab
+// views); the returned dgamma / dbeta are then those tensors
 std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> y,
-                                    c10::optional<at::Tensor> gamma, at::Tensor st, int64_t mode) {
+                                    c10::optional<at::Tensor> gamma, at::Tensor st, int64_t mode,
+                                    c10::optional<at::Tensor> dgamma_out, c10::optional<at::Tensor> dbeta_out) {
   bn_check(x);
   bn_check(dy);
   TORCH_CHECK(dy.scalar_type() == x.scalar_type() && dy.numel() == x.numel(), "batch_norm backward: dy/x mismatch");
@@ -112,11 +115,21 @@ std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, c10::optional<a
   auto dx = at::empty_like(x);
   float* o = out.data_ptr<float>();
   const float* sp = st.data_ptr<float>();
+  auto check_out = [&](const c10::optional<at::Tensor>& t) {
+    if (!t.has_value() || !t->defined()) return (float*)nullptr;
+    TORCH_CHECK(t->is_cuda() && t->is_contiguous() && t->scalar_type() == at::kFloat && t->numel() == C,
+                "batch_norm backward: gradient outputs must be contiguous f32 [C]");
+    return t->data_ptr<float>();
+  };
+  float* pg = check_out(dgamma_out);
+  float* pb = check_out(dbeta_out);
+  const int acc = (pg ? 1 : 0) | (pb ? 2 : 0);
   tdl::bn_backward(dy.data_ptr(), x.data_ptr(), yp, mode == 2 ? dz.data_ptr() : nullptr, dx.data_ptr(), bn_dtype(x), M,
-                   (int)C, part.data_ptr<float>(), opt_f32(gamma), sp, sp + C, sp + 2 * C, sp + 3 * C, o, o + C,
-                   o + 2 * C, (int)mode, cur_stream());
-  if (mode == 2) return {dx, out[0], out[1], dz};
-  return {dx, out[0], out[1]};
+                   (int)C, part.data_ptr<float>(), opt_f32(gamma), sp, sp + C, sp + 2 * C, sp + 3 * C, pg ? pg : o,
+                   pb ? pb : o + C, o + 2 * C, (int)mode, acc, cur_stream());
+  at::Tensor g = pg ? *dgamma_out : out[0], b = pb ? *dbeta_out : out[1];
+  if (mode == 2) return {dx, g, b, dz};
+  return {dx, g, b};
 }
 // max pool NHWC: returns (y, argmax bytes); pads = (top, left), output size given
 std::vector<at::Tensor> maxpool_fwd(at::Tensor x, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t pt,
@@ -186,9 +199,78 @@ at::Tensor conv_dgrad(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w, in
   tdl::conv_dgrad_bf16(dy.data_ptr(), w_hwio.data_ptr(), dx.data_ptr(), g, cur_stream());
   return dx;
 }
+// input gradient of a 1x1 stride-2 unpadded conv: dx[N,H,W,C] from dy[N,OH,OW,K] and w_hwio[1,1,C,K]
+at::Tensor conv_dgrad_s2(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w) {
+  conv_check(dy, "dy");
+  conv_check(w_hwio, "w");
+  TORCH_CHECK(w_hwio.dim() == 4 && w_hwio.size(0) == 1 && w_hwio.size(1) == 1 && w_hwio.size(3) == dy.size(3),
+              "conv_dgrad_s2: weights must be HWIO [1,1,C,K]");
+  TORCH_CHECK(h <= 2 * dy.size(1) && w <= 2 * dy.size(2) && h > 2 * (dy.size(1) - 1) && w > 2 * (dy.size(2) - 1),
+              "conv_dgrad_s2: (h, w) inconsistent with a stride-2 1x1 conv");
+  tdl::ConvGeom g{(int)dy.size(0), (int)h, (int)w, (int)w_hwio.size(2), (int)dy.size(1), (int)dy.size(2),
+                  (int)dy.size(3), 1, 1, 2, 2, 0, 0};
+  TORCH_CHECK(tdl::conv_bf16_supported(g), "conv_dgrad_s2: unsupported geometry (C and K must be multiples of 64)");
+  auto dx = at::empty({dy.size(0), h, w, w_hwio.size(2)}, dy.options());
+  tdl::conv_dgrad_s2_1x1_bf16(dy.data_ptr(), w_hwio.data_ptr(), dx.data_ptr(), g, cur_stream());
+  return dx;
+}
+
+// weight gradient: dw[KH,KW,C,K] (bf16, or added into the f32 `out` when given) from x[N,H,W,C] and
+// dy[N,OH,OW,K]; deterministic split-K.  plan = [wmw, wnw, nsplit] (empty: the model's first choice)
+at::Tensor conv_wgrad(at::Tensor x, at::Tensor dy, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t pt,
+                      int64_t pl, c10::optional<at::Tensor> out, bool accumulate, std::vector<int64_t> plan) {
+  conv_check(x, "x");
+  conv_check(dy, "dy");
+  TORCH_CHECK(dy.dim() == 4 && dy.size(0) == x.size(0), "conv_wgrad: dy must be NHWC [N,OH,OW,K]");
+  auto g = conv_geom(x, dy.size(1), dy.size(2), dy.size(3), kh, kw, sh, sw, pt, pl);
+  TORCH_CHECK(tdl::conv_wgrad_supported(g), "conv_wgrad: N*OH*OW must be < 2^24");
+  TORCH_CHECK(plan.empty() || plan.size() == 3, "conv_wgrad: plan = [wmw, wnw, nsplit]");
+  tdl::WgradPlan p;
+  if (plan.empty()) {
+    p = tdl::conv_wgrad_plans(g, 1).at(0);
+  } else {
+    const int wmw = (int)plan[0], wnw = (int)plan[1];
+    TORCH_CHECK((wmw == 1 || wmw == 2 || wmw == 4) && (wnw == 1 || wnw == 2 || wnw == 4) && wmw * wnw <= 4 &&
+                    g.K % (64 * wmw) == 0 && plan[2] >= 1,
+                "conv_wgrad: bad plan");
+    p = tdl::conv_wgrad_make_plan(g, wmw, wnw, (int)plan[2]);
+  }
+  auto ws = at::empty({p.ws_elems}, x.options().dtype(at::kFloat));
+  if (out.has_value()) {
+    auto& o = *out;
+    TORCH_CHECK(o.is_cuda() && o.is_contiguous() && o.scalar_type() == at::kFloat &&
+                    o.numel() == kh * kw * x.size(3) * dy.size(3),
+                "conv_wgrad: out must be a contiguous f32 tensor of KH*KW*C*K elements");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(o.data_ptr()) % 16 == 0, "conv_wgrad: out must be 16-byte aligned");
+    tdl::conv_wgrad_bf16(x.data_ptr(), dy.data_ptr(), ws.data_ptr<float>(), p, nullptr, o.data_ptr<float>(),
+                         accumulate, g, cur_stream());
+    return o;
+  }
+  auto dw = at::empty({kh, kw, x.size(3), dy.size(3)}, x.options());
+  tdl::conv_wgrad_bf16(x.data_ptr(), dy.data_ptr(), ws.data_ptr<float>(), p, dw.data_ptr(), nullptr, false, g,
+                       cur_stream());
+  return dw;
+}
+
+// the model's best candidate plans: [[wmw, wnw, chunk, nsplit], ...]
+std::vector<std::vector<int64_t>> conv_wgrad_plans(std::vector<int64_t> x_shape, std::vector<int64_t> dy_shape,
+                                                   int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t pt,
+                                                   int64_t pl, int64_t max_plans) {
+  tdl::ConvGeom g{(int)x_shape[0], (int)x_shape[1], (int)x_shape[2], (int)x_shape[3], (int)dy_shape[1],
+                  (int)dy_shape[2], (int)dy_shape[3], (int)kh, (int)kw, (int)sh, (int)sw, (int)pt, (int)pl};
+  std::vector<std::vector<int64_t>> out;
+  for (const auto& p : tdl::conv_wgrad_plans(g, (int)max_plans)) out.push_back({p.wmw, p.wnw, p.chunk, p.nsplit});
+  return out;
+}
 }  // namespace
 
 void register_ops(pybind11::module& m) {
+  m.def("conv_dgrad_s2", &conv_dgrad_s2, "NHWC bf16 1x1 stride-2 convolution input gradient (MFMA)");
+  m.def("conv_wgrad", &conv_wgrad, "NHWC bf16 convolution weight gradient (MFMA, transposed LDS reads, split-K)",
+        pybind11::arg("x"), pybind11::arg("dy"), pybind11::arg("kh"), pybind11::arg("kw"), pybind11::arg("sh"),
+        pybind11::arg("sw"), pybind11::arg("pt"), pybind11::arg("pl"), pybind11::arg("out") = pybind11::none(),
+        pybind11::arg("accumulate") = false, pybind11::arg("plan") = std::vector<int64_t>{});
+  m.def("conv_wgrad_plans", &conv_wgrad_plans, "weight-gradient candidate plans, best first: [[wmw, wnw, chunk, nsplit]]");
   m.def("conv_force_tile", &tdl::conv_force_tile, "conv tile sweep hook (0 = heuristic)");
   m.def("conv_fwd", &conv_fwd, "NHWC bf16 implicit-GEMM convolution forward (MFMA)");
   m.def("conv_dgrad", &conv_dgrad, "NHWC bf16 implicit-GEMM stride-1 convolution input gradient (MFMA)");
@@ -201,5 +283,6 @@ void register_ops(pybind11::module& m) {
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC max pool forward (+argmax)");
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC max pool backward (gather form)");
   m.def("bn_backward", &bn_backward, "NHWC batch-norm training backward", pybind11::arg("dy"), pybind11::arg("x"),
-        pybind11::arg("y"), pybind11::arg("gamma"), pybind11::arg("stats"), pybind11::arg("mode"));
+        pybind11::arg("y"), pybind11::arg("gamma"), pybind11::arg("stats"), pybind11::arg("mode"),
+        pybind11::arg("dgamma_out") = pybind11::none(), pybind11::arg("dbeta_out") = pybind11::none());
 }

@@ -14,7 +14,8 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    n = re.sub(r"\(.*", "", name)
+    n = name.replace("(anonymous namespace)::", "")
+    n = re.sub(r"\(.*", "", n)
     n = re.sub(r"^void ", "", n)
     return n[:90]
 

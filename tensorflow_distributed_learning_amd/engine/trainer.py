@@ -139,6 +139,13 @@ class GenericTrainer:
         self.loss_tracker = model._loss_tracker
         self.metrics = model.compiled_metrics
         self._policy = model._dtype_policy()
+        self._Wc = None
+        if self._policy == "mixed_bfloat16" and self.device.type == "cuda" and \
+                os.environ.get("TDL_CAST_ACCUMULATE", "1") == "1":
+            # bf16 compute copy of the whole weight slab: one cast kernel per step instead of one
+            # per layer; Variable.cast / compute_view hand out views of it inside the step
+            self._Wc = torch.empty(self.W.numel(), dtype=torch.bfloat16, device=self.device)
+            self._bind_compute_views()
         self._buckets = self._make_buckets()
         self._bind_cast_accumulate()
         # whole-step hipGraphs (forward + backward + all-reduce + optimizer + metrics), keyed by
@@ -168,6 +175,13 @@ class GenericTrainer:
             self._register_bucket_hooks()
         if hasattr(self, "_buckets"):
             self._bind_cast_accumulate()
+        self._bind_compute_views()
+
+    def _bind_compute_views(self):
+        if getattr(self, "_Wc", None) is None:
+            return
+        for leaf, cv in zip(self._leaves, self.model._layout.views(self._Wc)):
+            leaf._tdl_cview = cv
 
     def _bind_cast_accumulate(self):
         if self._buckets is None and os.environ.get("TDL_CAST_ACCUMULATE", "1") == "1":
@@ -271,6 +285,8 @@ class GenericTrainer:
             self._works = []
         from ..parallel import values as V
 
+        if self._Wc is not None:
+            self._Wc.copy_(self.W)  # the step's bf16 weights, one kernel
         V.CAST_ACCUMULATE[0] += 1  # Variable.cast may add straight into the slab only in here
         try:
             with trace_range("tdl.forward"):

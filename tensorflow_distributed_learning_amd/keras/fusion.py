@@ -118,8 +118,14 @@ def run_group(g: Group, vals, training):
     bn = g.bn_node.layer
     x = vals[id(g.bn_node.inputs)]
     r = vals[id(g.residual)] if g.residual is not None else None
-    cb = g.conv_layer.bias.value if g.conv_layer is not None else None
+    cb = None
+    if g.conv_layer is not None:
+        cbv = g.conv_layer.bias
+        # the folded bias's gradient is exactly zero: with a gradient slab bound, leave its (zeroed)
+        # slab entries alone instead of accumulating zeros
+        cb = cbv.value.detach() if cbv.grad_target() is not None else cbv.value
     y = batch_norm_train(x, bn.gamma.value if bn.gamma is not None else None,
                          bn.beta.value if bn.beta is not None else None, bn.moving_mean.value,
-                         bn.moving_variance.value, bn.momentum, bn.epsilon, relu=g.relu, residual=r, conv_bias=cb)
+                         bn.moving_variance.value, bn.momentum, bn.epsilon, relu=g.relu, residual=r, conv_bias=cb,
+                         grad_out=bn._grad_targets())
     vals[id(g.out)] = y

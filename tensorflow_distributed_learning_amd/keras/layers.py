@@ -314,7 +314,16 @@ class Conv2D(Layer):
         BatchNormalization (keras/fusion.py), so the convolution runs without it."""
         # (1x1 convs stay on MIOpen: routing them through hipBLASLt GEMMs measured slower on MI355X,
         #  scripts/probe_1x1_gemm.py)
-        k_hwio = self.kernel.cast(x.dtype)
+        gt = None
+        if _conv.supported(x, self.kernel.value, self.groups, self.dilation_rate):
+            gt = self.kernel.grad_target()
+        # with a slab target the weight gradient kernel adds dW straight into the f32 slab view
+        if gt is not None:
+            k_hwio = self.kernel.compute_view(x.dtype)
+            if k_hwio is None:
+                k_hwio = self.kernel.value.detach().to(x.dtype)
+        else:
+            k_hwio = self.kernel.cast(x.dtype)
         w = k_hwio.permute(3, 2, 0, 1)  # HWIO -> OIHW
         h = x.permute(0, 3, 1, 2)  # NHWC data viewed as NCHW (channels_last memory format)
         pad = 0
@@ -328,9 +337,12 @@ class Conv2D(Layer):
                 symmetric = False
                 h = F.pad(h, (pw[0], pw[1], ph[0], ph[1]))
         b = self.bias.value.to(x.dtype) if (self.bias is not None and not _fold_bias) else None
+        if gt is not None and not symmetric:  # (asymmetric "same" padding: undo the detached fast path)
+            gt, k_hwio = None, self.kernel.cast(x.dtype)
+            w = k_hwio.permute(3, 2, 0, 1)
         if symmetric and _conv.supported(x, k_hwio, self.groups, self.dilation_rate):
             # hand-written implicit-GEMM MFMA kernels (csrc/kernels/conv.hip), autotuned against MIOpen
-            y = _conv.conv2d_nhwc(x, k_hwio, self.strides, pad if pad else (0, 0))
+            y = _conv.conv2d_nhwc(x, k_hwio, self.strides, pad if pad else (0, 0), grad_out=gt)
             if b is not None:
                 y = y + b
             return self.activation(y)
@@ -598,7 +610,7 @@ class BatchNormalization(Layer):
                 return _bn.batch_norm_train(x, self.gamma.value if self.gamma is not None else None,
                                             self.beta.value if self.beta is not None else None,
                                             self.moving_mean.value, self.moving_variance.value, self.momentum,
-                                            self.epsilon)
+                                            self.epsilon, grad_out=self._grad_targets())
         perm = None
         if axis != 1:
             perm = [0, axis] + [i for i in range(1, x.dim()) if i != axis]
@@ -616,6 +628,13 @@ class BatchNormalization(Layer):
                 inv[p] = i
             y = y.permute(*inv)
         return y
+
+    def _grad_targets(self):
+        """(gamma, beta) slab views the BN backward kernel adds into directly, or None."""
+        t = tuple(v.grad_target() if v is not None else None for v in (self.gamma, self.beta))
+        if any(tt is None and v is not None for tt, v in zip(t, (self.gamma, self.beta))):
+            return None
+        return t
 
     def compute_output_shape(self, s):
         return s

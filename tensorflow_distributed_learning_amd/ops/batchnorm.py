@@ -36,7 +36,7 @@ def _aligned(t: torch.Tensor) -> torch.Tensor:
 
 class _BatchNormTrain(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, residual, conv_bias, moving_mean, moving_var, momentum, eps, relu):
+    def forward(ctx, x, gamma, beta, residual, conv_bias, moving_mean, moving_var, momentum, eps, relu, grad_out):
         C = hip()
         xc = _aligned(x)
         rc = _aligned(residual.to(xc.dtype)) if residual is not None else None
@@ -45,6 +45,7 @@ class _BatchNormTrain(torch.autograd.Function):
         ctx.mode = 2 if residual is not None else (1 if relu else 0)
         ctx.flags = (gamma is not None, beta is not None, residual is not None, conv_bias is not None)
         ctx.res_dtype = residual.dtype if residual is not None else None
+        ctx.grad_out = grad_out
         ctx.save_for_backward(xc, gamma if gamma is not None else st, st, y if ctx.mode == 2 else st,
                               conv_bias if conv_bias is not None else st)
         return y
@@ -55,22 +56,32 @@ class _BatchNormTrain(torch.autograd.Function):
         xc, gamma, st, y, conv_bias = ctx.saved_tensors
         has_g, has_b, has_r, has_cb = ctx.flags
         dy = _aligned(dy.to(xc.dtype))
-        out = C.bn_backward(dy, xc, y if ctx.mode == 2 else None, gamma if has_g else None, st, ctx.mode)
+        go = ctx.grad_out or (None, None)
+        out = C.bn_backward(dy, xc, y if ctx.mode == 2 else None, gamma if has_g else None, st, ctx.mode,
+                            go[0], go[1])
         dx, dgamma, dbeta = out[0], out[1], out[2]
         dres = out[3].to(ctx.res_dtype) if has_r else None
-        dcb = torch.zeros_like(conv_bias) if has_cb else None
-        return (dx, dgamma if has_g else None, dbeta if has_b else None, dres, dcb, None, None, None, None, None)
+        dcb = torch.zeros_like(conv_bias) if (has_cb and ctx.needs_input_grad[4]) else None
+        return (dx, dgamma if ctx.needs_input_grad[1] else None, dbeta if ctx.needs_input_grad[2] else None, dres,
+                dcb, None, None, None, None, None, None)
 
 
 def batch_norm_train(x: torch.Tensor, gamma: Optional[torch.Tensor], beta: Optional[torch.Tensor],
                      moving_mean: Optional[torch.Tensor], moving_var: Optional[torch.Tensor], momentum: float,
                      eps: float, relu: bool = False, residual: Optional[torch.Tensor] = None,
-                     conv_bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Keras-convention ``momentum`` (moving = moving*momentum + batch*(1-momentum))."""
+                     conv_bias: Optional[torch.Tensor] = None, grad_out=None) -> torch.Tensor:
+    """Keras-convention ``momentum`` (moving = moving*momentum + batch*(1-momentum)).
+
+    ``grad_out = (dgamma_target, dbeta_target)``: f32 slab views the GPU backward ADDS the gamma /
+    beta gradients into (Variable.grad_target); gamma / beta are then passed without autograd."""
     if residual is not None and not relu:
         raise ValueError("the fused residual form is BN -> Add -> ReLU")
     if supported(x) and (residual is None or tuple(residual.shape) == tuple(x.shape)):
-        return _BatchNormTrain.apply(x, gamma, beta, residual, conv_bias, moving_mean, moving_var, momentum, eps, relu)
+        if grad_out is not None:
+            gamma = gamma.detach() if gamma is not None else None
+            beta = beta.detach() if beta is not None else None
+        return _BatchNormTrain.apply(x, gamma, beta, residual, conv_bias, moving_mean, moving_var, momentum, eps, relu,
+                                     grad_out)
     h = x if conv_bias is None else x + conv_bias.to(x.dtype)
     perm = [0, h.dim() - 1] + list(range(1, h.dim() - 1))
     hp = h.permute(*perm)

@@ -3,8 +3,9 @@
 The reference's ``tf.keras.layers.Conv2D`` (tf_dist_example.py:41,43; ResNet-50 of BASELINE configs
 4/5) runs on cuDNN inside TensorFlow.  Here a Conv2D with bf16 NHWC activations, C and K multiples
 of 64 and symmetric padding has two implementations per direction: the hand-written kernels
-(forward; stride-1 input gradient) and MIOpen (through ``torch.nn.functional``).  The weight
-gradient, and the input gradient of strided convolutions, stay on MIOpen.
+(forward; stride-1 and 1x1 stride-2 input gradient, csrc/kernels/conv.hip; weight gradient,
+csrc/kernels/conv_wgrad.hip) and MIOpen (through ``torch.nn.functional``).  Other strided input
+gradients stay on MIOpen.
 
 ``TDL_CONV`` picks: ``auto`` (default) times both implementations on the first eager call of every
 (shape, direction) and keeps the faster one (decisions are cached per process and never measured
@@ -66,9 +67,35 @@ def _pick(key, hip_fn, ref_fn) -> bool:
     return got
 
 
+def _pick_wgrad(key, C, x, dy, kh, kw, stride, pad, ref_fn):
+    """Weight gradient: time the cost model's first ``TDL_WGRAD_CANDIDATES`` (default 6) tile/slice
+    plans and MIOpen on the first eager call of a shape; returns the winning plan
+    ``[wmw, wnw, nsplit]`` or None (MIOpen)."""
+    m = mode()
+    if key in _choice:
+        return _choice[key]
+    n = 1 if m == "hip" or torch.cuda.is_current_stream_capturing() else int(os.environ.get("TDL_WGRAD_CANDIDATES", 6))
+    plans = [[p[0], p[1], p[3]] for p in C.conv_wgrad_plans(list(x.shape), list(dy.shape), kh, kw, stride[0],
+                                                            stride[1], pad[0], pad[1], n)]
+    if m == "hip":
+        _choice[key] = plans[0]
+        return plans[0]
+    if torch.cuda.is_current_stream_capturing():
+        return None
+    t_ref = _time(ref_fn)
+    best, t_best = None, t_ref
+    for p in plans:
+        t = _time(lambda: C.conv_wgrad(x, dy, kh, kw, stride[0], stride[1], pad[0], pad[1], plan=p))
+        if t < t_best:
+            best, t_best = p, t
+    _choice[key] = best
+    _times[key] = (t_best, t_ref)
+    return best
+
+
 def choices() -> dict:
     """The autotuner's decisions so far: {(direction, shape key): 'hip' | 'miopen'}."""
-    return {k: ("hip" if v else "miopen") for k, v in _choice.items()}
+    return {k: ("hip" if (v is True or isinstance(v, list)) else "miopen") for k, v in _choice.items()}
 
 
 def _ref_fwd(x, w_oihw, stride, pad):
@@ -77,7 +104,7 @@ def _ref_fwd(x, w_oihw, stride, pad):
 
 class _Conv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, kernel, stride, pad):
+    def forward(ctx, x, kernel, stride, pad, grad_out):
         C = hip()
         x = x.contiguous()
         if x.data_ptr() % 16:
@@ -96,6 +123,7 @@ class _Conv(torch.autograd.Function):
             y = _ref_fwd(x, w_oihw, stride, pad).contiguous()
         ctx.save_for_backward(x, kernel)
         ctx.geo = (stride, pad)
+        ctx.grad_out = grad_out
         return y
 
     @staticmethod
@@ -108,27 +136,57 @@ class _Conv(torch.autograd.Function):
             dy = dy.clone()
         w_oihw = kernel.permute(3, 2, 0, 1)
         x_nchw, dy_nchw = x.permute(0, 3, 1, 2), dy.permute(0, 3, 1, 2)
-        dx = None
-        want_dx = ctx.needs_input_grad[0]
-        if want_dx and stride == (1, 1):
+        kh, kw = kernel.shape[0], kernel.shape[1]
+        gout = ctx.grad_out  # f32 HWIO slab view: dW is ADDED into it and not returned
+        want_dx, want_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1] or gout is not None
+        shape_key = (tuple(x.shape), tuple(kernel.shape), stride, pad)
+        dx = dw = None
+
+        def ref(mask):
+            return lambda: _miopen_bwd(dy_nchw, x_nchw, w_oihw, list(stride), list(pad), mask)
+
+        if want_dx:
             kc = kernel.contiguous()
-            key = ("dgrad", tuple(x.shape), tuple(kernel.shape), stride, pad)
-            hip_fn = lambda: C.conv_dgrad(dy, kc, x.shape[1], x.shape[2], pad[0], pad[1])  # noqa: E731
-            ref_fn = lambda: torch.ops.aten.convolution_backward(  # noqa: E731
-                dy_nchw, x_nchw, w_oihw, None, list(stride), list(pad), [1, 1], False, [0, 0], 1,
-                [True, False, False])[0]
-            if _pick(key, hip_fn, ref_fn):
+            hip_fn = None
+            if stride == (1, 1):
+                hip_fn = lambda: C.conv_dgrad(dy, kc, x.shape[1], x.shape[2], pad[0], pad[1])  # noqa: E731
+                key = ("dgrad",) + shape_key
+            elif stride == (2, 2) and (kh, kw) == (1, 1) and pad == (0, 0):
+                hip_fn = lambda: C.conv_dgrad_s2(dy, kc, x.shape[1], x.shape[2])  # noqa: E731
+                key = ("dgrad_s2",) + shape_key
+            if hip_fn is not None and _pick(key, hip_fn, lambda: ref([True, False, False])()[0]):
                 dx = hip_fn()
-        gx, gw, _ = torch.ops.aten.convolution_backward(
-            dy_nchw, x_nchw, w_oihw, None, list(stride), list(pad), [1, 1], False, [0, 0], 1,
-            [want_dx and dx is None, ctx.needs_input_grad[1], False])
-        if dx is None and gx is not None:
-            dx = gx.permute(0, 2, 3, 1)
-        dk = gw.permute(2, 3, 1, 0) if gw is not None else None
-        return dx, dk, None, None
+        if want_dw and x.shape[0] * dy.shape[1] * dy.shape[2] < (1 << 24):
+            plan = _pick_wgrad(("wgrad",) + shape_key, C, x, dy, kh, kw, stride, pad,
+                               lambda: ref([False, True, False])()[1])
+            if plan is not None:
+                if gout is not None:
+                    C.conv_wgrad(x, dy, kh, kw, stride[0], stride[1], pad[0], pad[1], out=gout, accumulate=True,
+                                 plan=plan)
+                    want_dw = False
+                else:
+                    dw = C.conv_wgrad(x, dy, kh, kw, stride[0], stride[1], pad[0], pad[1], plan=plan)
+        need_dx, need_dw = want_dx and dx is None, want_dw and dw is None
+        if need_dx or need_dw:
+            gx, gw, _ = ref([need_dx, need_dw, False])()
+            if need_dx:
+                dx = gx.permute(0, 2, 3, 1)
+            if need_dw:
+                dw = gw.permute(2, 3, 1, 0)
+                if gout is not None:
+                    gout.add_(dw)
+                    dw = None
+        return dx, dw, None, None, None
 
 
-def conv2d_nhwc(x, kernel_hwio, stride=(1, 1), pad=(0, 0)):
+def _miopen_bwd(dy_nchw, x_nchw, w_oihw, stride, pad, mask):
+    """MIOpen convolution backward (input / weight gradients as selected by ``mask``)."""
+    return torch.ops.aten.convolution_backward(dy_nchw, x_nchw, w_oihw, None, stride, pad, [1, 1], False, [0, 0], 1,
+                                               mask)
+
+
+def conv2d_nhwc(x, kernel_hwio, stride=(1, 1), pad=(0, 0), grad_out=None):
     """y[N,OH,OW,K] = conv(x[N,H,W,C], kernel[KH,KW,C,K]) with symmetric zero padding ``pad = (ph, pw)``,
-    bf16; the caller checked :func:`supported`."""
-    return _Conv.apply(x, kernel_hwio, tuple(stride), tuple(pad))
+    bf16; the caller checked :func:`supported`.  ``grad_out``: f32 [KH,KW,C,K] tensor the weight
+    gradient is added into (a trainer's gradient slab view; ``kernel_hwio`` then needs no autograd)."""
+    return _Conv.apply(x, kernel_hwio, tuple(stride), tuple(pad), grad_out)

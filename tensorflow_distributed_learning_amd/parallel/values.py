@@ -35,14 +35,15 @@ class VariableAggregation(enum.Enum):
 
 class _CastAccumulate(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, leaf, gview, dtype):
+    def forward(ctx, leaf, gview, dtype, cview=None):
         ctx.gview = gview
-        return leaf.detach().to(dtype)
+        # cview: this variable's view of the trainer's compute-dtype weight slab (cast once per step)
+        return cview.view_as(cview) if cview is not None else leaf.detach().to(dtype)
 
     @staticmethod
     def backward(ctx, g):
         ctx.gview.add_(g.reshape(ctx.gview.shape))
-        return None, None, None
+        return None, None, None, None
 
 
 class Variable:
@@ -89,8 +90,28 @@ class Variable:
         # the same leaves must see an ordinary differentiable cast, not a gradient routed into G
         if (g is not None and CAST_ACCUMULATE[0] > 0 and TAPE_DEPTH[0] == 0 and t.requires_grad and
                 torch.is_grad_enabled()):
-            return _CastAccumulate.apply(t, g, dtype)
+            return _CastAccumulate.apply(t, g, dtype, self.compute_view(dtype))
         return t.to(dtype)
+
+    def compute_view(self, dtype: torch.dtype) -> Optional[torch.Tensor]:
+        """This variable's view of the trainer's compute-dtype copy of the weight slab (refreshed by
+        ONE cast kernel at the start of every GenericTrainer step), or None outside such a step."""
+        cv = getattr(self.value, "_tdl_cview", None)
+        if cv is not None and cv.dtype == dtype and CAST_ACCUMULATE[0] > 0:
+            return cv
+        return None
+
+    def grad_target(self) -> Optional[torch.Tensor]:
+        """The f32 slab view a hand-written kernel may ADD this variable's gradient into directly
+        (skipping autograd's accumulate kernel), or None.  Same conditions as the :meth:`cast`
+        fast path: inside GenericTrainer.train_step, no GradientTape, gradient slab bound (no
+        bucket all-reduce hooks waiting on this leaf)."""
+        t = self.value
+        g = getattr(t, "_tdl_gview", None)
+        if (g is not None and CAST_ACCUMULATE[0] > 0 and TAPE_DEPTH[0] == 0 and t.requires_grad and
+                torch.is_grad_enabled()):
+            return g
+        return None
 
     def read_value(self) -> torch.Tensor:
         return self._value

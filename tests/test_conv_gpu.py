@@ -86,3 +86,104 @@ def test_conv_fwd_dgrad_wide_tiles(shape):
     """Large grids take the 128 x 128 and 256 x 128 tile variants."""
     test_conv_fwd_matches_fp32(shape)
     test_conv_dgrad_matches_fp32(shape)
+
+
+def _ref_grads(x, k, s, p, dy):
+    xr = x.float().requires_grad_(True)
+    kr = k.float().requires_grad_(True)
+    y = _ref_fwd(xr, kr, s, p)
+    y.backward(dy.float())
+    return xr.grad, kr.grad
+
+
+WGRAD_SHAPES = SHAPES + [
+    (32, 28, 28, 128, 128, 3, 3, 1, 1),  # 3 x 3, 128 x 128 tiles, many slices
+    (16, 56, 56, 64, 256, 1, 1, 1, 0),   # direct 1 x 1 path
+    (8, 28, 28, 256, 512, 1, 1, 2, 0),   # strided shortcut
+    (4, 7, 7, 512, 512, 3, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("shape", WGRAD_SHAPES)
+def test_conv_wgrad_matches_fp32(shape):
+    """Hand-written split-K weight gradient (transposed LDS reads) vs the fp32 autograd gradient;
+    also checks the f32 accumulate form and that the result is bitwise deterministic."""
+    from tensorflow_distributed_learning_amd.ops import hip
+
+    C = hip()
+    N, H, W, Ci, K, KH, KW, s, p = shape
+    x, k = _mk(shape, "cuda:0")
+    OH, OW = (H + 2 * p - KH) // s + 1, (W + 2 * p - KW) // s + 1
+    dy = torch.randn(N, OH, OW, K, device="cuda:0").bfloat16()
+    _, gw = _ref_grads(x, k, s, p, dy)
+    dw = C.conv_wgrad(x, dy, KH, KW, s, s, p, p)
+    assert dw.dtype == torch.bfloat16 and dw.shape == k.shape
+    scale = gw.abs().max().item()
+    torch.testing.assert_close(dw.float(), gw, atol=2e-2 * scale + 1e-3, rtol=2e-2)
+    base = torch.full(gw.shape, 0.5, device="cuda:0")
+    acc = base.clone()
+    C.conv_wgrad(x, dy, KH, KW, s, s, p, p, out=acc, accumulate=True)
+    torch.testing.assert_close(acc, base + gw, atol=1e-3 * scale + 1e-4, rtol=1e-3)
+    again = base.clone()
+    C.conv_wgrad(x, dy, KH, KW, s, s, p, p, out=again, accumulate=True)
+    assert torch.equal(acc, again), "weight gradient is not deterministic"
+    # a single slice (no split-K) agrees with the split result to f32 rounding
+    plan = C.conv_wgrad_plans(list(x.shape), list(dy.shape), KH, KW, s, s, p, p, 1)[0]
+    one = C.conv_wgrad(x, dy, KH, KW, s, s, p, p, out=torch.zeros_like(gw), plan=[plan[0], plan[1], 1])
+    torch.testing.assert_close(one, acc - base, atol=1e-3 * scale + 1e-4, rtol=1e-3)
+
+
+@pytest.mark.parametrize("tile", [(1, 1), (1, 2), (2, 1), (2, 2), (1, 4), (4, 1)])
+@pytest.mark.parametrize("shape", [(4, 14, 14, 256, 256, 3, 3, 1, 1), (8, 9, 9, 192, 256, 1, 1, 2, 0)])
+def test_conv_wgrad_every_tile_shape(shape, tile):
+    """Every workgroup tile shape (incl. partial last tc tiles: 192 columns) and a few slice counts."""
+    from tensorflow_distributed_learning_amd.ops import hip
+
+    C = hip()
+    N, H, W, Ci, K, KH, KW, s, p = shape
+    x, k = _mk(shape, "cuda:0")
+    OH, OW = (H + 2 * p - KH) // s + 1, (W + 2 * p - KW) // s + 1
+    dy = torch.randn(N, OH, OW, K, device="cuda:0").bfloat16()
+    _, gw = _ref_grads(x, k, s, p, dy)
+    scale = gw.abs().max().item()
+    for S in (1, 3, 40):
+        dw = C.conv_wgrad(x, dy, KH, KW, s, s, p, p, out=torch.empty_like(gw), plan=[tile[0], tile[1], S])
+        torch.testing.assert_close(dw, gw, atol=2e-3 * scale + 1e-4, rtol=2e-3)
+
+
+@pytest.mark.parametrize("shape", [(2, 14, 14, 64, 128, 1, 1, 2, 0), (4, 56, 56, 256, 512, 1, 1, 2, 0),
+                                   (3, 7, 9, 128, 64, 1, 1, 2, 0), (2, 28, 28, 512, 1024, 1, 1, 2, 0)])
+def test_conv_dgrad_stride2_1x1_matches_fp32(shape):
+    """1x1 stride-2 input gradient (scatter epilogue writes the zero pixels too, odd sizes included)."""
+    from tensorflow_distributed_learning_amd.ops import hip
+
+    C = hip()
+    N, H, W, Ci, K, KH, KW, s, p = shape
+    x, k = _mk(shape, "cuda:0")
+    OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    dy = torch.randn(N, OH, OW, K, device="cuda:0").bfloat16()
+    gx, _ = _ref_grads(x, k, s, p, dy)
+    dx = C.conv_dgrad_s2(dy, k.contiguous(), H, W)
+    assert dx.shape == x.shape
+    torch.testing.assert_close(dx.float(), gx, atol=4e-2, rtol=2e-2)
+
+
+def test_conv2d_layer_wgrad_and_strided_on_hip_kernels(monkeypatch):
+    """keras Conv2D backward with TDL_CONV=hip runs the weight gradient and the strided 1x1 input
+    gradient on the hand-written kernels (no MIOpen call)."""
+    monkeypatch.setenv("TDL_CONV", "hip")
+    from tensorflow_distributed_learning_amd.ops import conv as conv_ops
+
+    x, k = _mk((4, 16, 16, 128, 256, 1, 1, 2, 0), "cuda:0")
+    x.requires_grad_(True)
+    kk = k.float().requires_grad_(True)
+    calls = []
+    orig = torch.ops.aten.convolution_backward
+    monkeypatch.setattr(conv_ops, "_miopen_bwd", lambda *a: calls.append(1) or orig(*a))
+    y = conv_ops.conv2d_nhwc(x, kk.bfloat16(), (2, 2), (0, 0))
+    dy = torch.randn(y.shape, device="cuda:0").bfloat16()
+    y.backward(dy)
+    gx, gw = _ref_grads(x.detach(), k, 2, 0, dy)
+    assert not calls, "backward fell back to MIOpen"
+    torch.testing.assert_close(x.grad.float(), gx, atol=4e-2, rtol=2e-2)
+    torch.testing.assert_close(kk.grad, gw, atol=2e-2 * gw.abs().max().item(), rtol=3e-2)
