@@ -15,15 +15,21 @@ struct BnPlan {
   int rows_iter;    // rows per workgroup iteration = 256 / groups
   int64_t rows_wg;  // rows per workgroup
   int parts;        // workgroups (partial rows in the workspace)
+  int part_rows;    // workspace rows ([part_rows][2][C] f32): partials + their first-level reduction
 };
 BnPlan bn_plan(int64_t M, int C);
+// sweep hooks: partial-pass workgroup cap, elementwise-pass grid cap, vectors per thread (1 or 2)
+void bn_set_tuning(int max_parts, int elem_blocks, int elem_unroll);
 
 // forward: part [parts][2][C] scratch; mean/invstd [C] out; scale/shift [C] out (x*scale+shift);
 // moving stats updated in place (momentum m: moving = moving*m + batch*(1-m), variance unbiased);
 // mean_off (nullable): per-channel bias of a preceding conv folded into this BN (moving mean only).
+// given_parts > 0: `part` already holds that many partial rows ([rows][2][C]; space for
+// ceil(rows / 64) more behind them), the partial pass is skipped
 void bn_forward_stats(const void* x, BnDType dt, int64_t M, int C, float* part, const float* gamma,
                       const float* beta, const float* mean_off, float* mean, float* invstd, float* scale, float* shift,
-                      float* moving_mean, float* moving_var, float momentum, float eps, hipStream_t s);
+                      float* moving_mean, float* moving_var, float momentum, float eps, hipStream_t s,
+                      int given_parts = 0);
 // y = act(x*scale + shift [+ residual])  (relu when relu != 0; residual nullable)
 void bn_apply(const void* x, const void* residual, void* y, BnDType dt, int64_t M, int C, const float* scale,
               const float* shift, int relu, hipStream_t s);

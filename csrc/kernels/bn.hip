@@ -15,7 +15,12 @@ namespace tdl {
 namespace {
 
 constexpr int kUnroll = 4;
-constexpr int kMaxParts = 512;
+// workgroups of the partial-sum pass and of the elementwise passes, and vectors per thread in the
+// latter, tunable at run time (bn_set_tuning) for the sweep in scripts/bench_bn.py: the defaults
+// measured best (the large shapes run at 4.7-5.7 TB/s, the device copy at 5.3-6.7 TB/s)
+int g_max_parts = 512;
+int g_elem_blocks = 256 * 16;
+int g_elem_unroll = 1;  // 2 measured 1-4 % slower (scripts/bench_bn.py, profiles/bn_tuning_sweep_r2.jsonl)
 constexpr int kFinPhases = 16;  // partial-row phases per channel in the finalize kernels (1024 threads)
 
 __device__ __forceinline__ float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
@@ -164,6 +169,47 @@ __device__ __forceinline__ bool reduce_parts(const float* __restrict__ part, int
   return true;
 }
 
+// First level of the partial reduction when there are many partial rows: block (cb, pb) sums rows
+// [64 pb, 64 pb + 64) of channels [64 cb, 64 cb + 64) in a fixed order into out[pb][2][C] (the
+// finalize then reduces ceil(P / 64) rows: a single 1024-thread block per 64 channels reading
+// thousands of rows was latency-bound).
+__global__ __launch_bounds__(1024) void k_bn_prereduce(const float* __restrict__ part, int P, int C,
+                                                       float* __restrict__ out) {
+  __shared__ float rs[kFinPhases][64], rq[kFinPhases][64];
+  const int lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int p0 = blockIdx.y * 64, p1 = min(P, p0 + 64);
+  float s = 0.f, q = 0.f;
+  if (c < C)
+    for (int p = p0 + ph; p < p1; p += kFinPhases) {
+      s += part[((int64_t)p * 2) * C + c];
+      q += part[((int64_t)p * 2 + 1) * C + c];
+    }
+  rs[ph][lane] = s;
+  rq[ph][lane] = q;
+  __syncthreads();
+  if (ph != 0 || c >= C) return;
+  s = 0.f;
+  q = 0.f;
+#pragma unroll
+  for (int k = 0; k < kFinPhases; ++k) {
+    s += rs[k][lane];
+    q += rq[k][lane];
+  }
+  out[((int64_t)blockIdx.y * 2) * C + c] = s;
+  out[((int64_t)blockIdx.y * 2 + 1) * C + c] = q;
+}
+
+// P > 1024 partial rows in `part` -> ceil(P / 64) rows at part + P*2*C
+static const float* prereduce(const float* part, int& P, int C, hipStream_t s) {
+  if (P <= 1024) return part;
+  float* out = const_cast<float*>(part) + (int64_t)P * 2 * C;
+  const int P2 = (P + 63) / 64;
+  hipLaunchKernelGGL(k_bn_prereduce, dim3((C + 63) / 64, P2), dim3(64 * kFinPhases), 0, s, part, P, C, out);
+  P = P2;
+  return out;
+}
+
 __global__ __launch_bounds__(1024) void k_bn_fwd_finalize(const float* __restrict__ part, int P, int64_t M, int C,
                                                          const float* __restrict__ gamma,
                                                          const float* __restrict__ beta,
@@ -213,7 +259,7 @@ __global__ __launch_bounds__(1024) void k_bn_bwd_finalize(const float* __restric
   coef[2 * C + c] = (float)(-A * db / (double)M - B * mu);
 }
 
-template <BnDType D>
+template <BnDType D, int U>
 __global__ __launch_bounds__(256) void k_bn_apply(const void* __restrict__ x, const void* __restrict__ res,
                                                   void* __restrict__ y, int64_t n8, int C,
                                                   const float* __restrict__ scale, const float* __restrict__ shift,
@@ -224,27 +270,43 @@ __global__ __launch_bounds__(256) void k_bn_apply(const void* __restrict__ x, co
     sh[c] = shift[c];
   }
   __syncthreads();
+  // U vectors per thread per iteration (all loads issued before any math): U x 16 B in flight
   const int64_t stride = (int64_t)gridDim.x * 256;
   const int64_t v0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int cstep = (int)((stride * 8) % C);  // channel advance per grid stride (no 64-bit modulo per vector)
   int c0 = (int)((v0 * 8) % C);
-  for (int64_t v = v0; v < n8; v += stride, c0 = (c0 + cstep >= C) ? c0 + cstep - C : c0 + cstep) {
-    float xv[8], rv[8];
-    Io<D>::load(x, v * 8, xv);
-    if (res != nullptr) Io<D>::load(res, v * 8, rv);
+  auto adv = [&](int c) { return c + cstep >= C ? c + cstep - C : c + cstep; };
+  for (int64_t v = v0; v < n8; v += U * stride) {
+    float xv[U][8], rv[U][8];
+    int cu[U];
+    cu[0] = c0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float o = fmaf(xv[j], sc[c0 + j], sh[c0 + j]);
-      if (res != nullptr) o += rv[j];
-      xv[j] = relu ? fmaxf(o, 0.f) : o;
+    for (int u = 1; u < U; ++u) cu[u] = adv(cu[u - 1]);
+    c0 = adv(cu[U - 1]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (v + u * stride < n8) {
+        Io<D>::load(x, (v + u * stride) * 8, xv[u]);
+        if (res != nullptr) Io<D>::load(res, (v + u * stride) * 8, rv[u]);
+      }
     }
-    Io<D>::store(y, v * 8, xv);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (v + u * stride >= n8) break;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float o = fmaf(xv[u][j], sc[cu[u] + j], sh[cu[u] + j]);
+        if (res != nullptr) o += rv[u][j];
+        xv[u][j] = relu ? fmaxf(o, 0.f) : o;
+      }
+      Io<D>::store(y, (v + u * stride) * 8, xv[u]);
+    }
   }
 }
 
 // dx = A*dz + B*x + D with dz = dy (modes 1, 3: dy is the masked dz) or dy masked by the
 // recomputed relu condition x*scale + shift > 0 (mode 2)
-template <BnDType D, bool MASK>
+template <BnDType D, bool MASK, int U>
 __global__ __launch_bounds__(256) void k_bn_dx(const void* __restrict__ dy, const void* __restrict__ x,
                                                void* __restrict__ dx, int64_t n8, int C, const float* __restrict__ coef,
                                                const float* __restrict__ scale, const float* __restrict__ shift) {
@@ -263,25 +325,47 @@ __global__ __launch_bounds__(256) void k_bn_dx(const void* __restrict__ dy, cons
   const int64_t v0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int cstep = (int)((stride * 8) % C);
   int c0 = (int)((v0 * 8) % C);
-  for (int64_t v = v0; v < n8; v += stride, c0 = (c0 + cstep >= C) ? c0 + cstep - C : c0 + cstep) {
-    float g[8], xv[8];
-    Io<D>::load(dy, v * 8, g);
-    Io<D>::load(x, v * 8, xv);
+  auto adv = [&](int c) { return c + cstep >= C ? c + cstep - C : c + cstep; };
+  for (int64_t v = v0; v < n8; v += U * stride) {
+    float g[U][8], xv[U][8];
+    int cu[U];
+    cu[0] = c0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (MASK && !(fmaf(xv[j], cS[c0 + j], cT[c0 + j]) > 0.f)) g[j] = 0.f;
-      g[j] = fmaf(cA[c0 + j], g[j], fmaf(cB[c0 + j], xv[j], cD[c0 + j]));
+    for (int u = 1; u < U; ++u) cu[u] = adv(cu[u - 1]);
+    c0 = adv(cu[U - 1]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (v + u * stride < n8) {
+        Io<D>::load(dy, (v + u * stride) * 8, g[u]);
+        Io<D>::load(x, (v + u * stride) * 8, xv[u]);
+      }
     }
-    Io<D>::store(dx, v * 8, g);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (v + u * stride >= n8) break;
+      const int cc = cu[u];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (MASK && !(fmaf(xv[u][j], cS[cc + j], cT[cc + j]) > 0.f)) g[u][j] = 0.f;
+        g[u][j] = fmaf(cA[cc + j], g[u][j], fmaf(cB[cc + j], xv[u][j], cD[cc + j]));
+      }
+      Io<D>::store(dx, (v + u * stride) * 8, g[u]);
+    }
   }
 }
 
 int elementwise_grid(int64_t n8) {
   const int64_t b = (n8 + 255) / 256;
-  return (int)std::min<int64_t>(b, 256 * 16);
+  return (int)std::min<int64_t>(b, g_elem_blocks);
 }
 
 }  // namespace
+
+void bn_set_tuning(int max_parts, int elem_blocks, int elem_unroll) {
+  if (max_parts > 0) g_max_parts = max_parts;
+  if (elem_blocks > 0) g_elem_blocks = elem_blocks;
+  if (elem_unroll == 1 || elem_unroll == 2) g_elem_unroll = elem_unroll;
+}
 
 BnPlan bn_plan(int64_t M, int C) {
   BnPlan p;
@@ -289,35 +373,50 @@ BnPlan bn_plan(int64_t M, int C) {
   p.rows_iter = 256 / p.groups;
   const int64_t chunk = (int64_t)p.rows_iter * kUnroll;
   const int64_t nchunks = (M + chunk - 1) / chunk;
-  const int64_t parts = std::min<int64_t>(std::max<int64_t>(nchunks, 1), kMaxParts);
+  const int64_t parts = std::min<int64_t>(std::max<int64_t>(nchunks, 1), g_max_parts);
   p.rows_wg = ((nchunks + parts - 1) / parts) * chunk;
   p.parts = (int)std::max<int64_t>(1, (M + p.rows_wg - 1) / p.rows_wg);
+  // scratch rows: the partials, plus the pre-reduced rows when there are more than 256
+  p.part_rows = p.parts + (p.parts > 1024 ? (p.parts + 63) / 64 : 0);
   return p;
 }
 
 void bn_forward_stats(const void* x, BnDType dt, int64_t M, int C, float* part, const float* gamma, const float* beta,
                       const float* mean_off, float* mean, float* invstd, float* scale, float* shift,
-                      float* moving_mean, float* moving_var, float momentum, float eps, hipStream_t s) {
+                      float* moving_mean, float* moving_var, float momentum, float eps, hipStream_t s,
+                      int given_parts) {
   const BnPlan p = bn_plan(M, C);
+  if (given_parts > 0) {  // partial sums already produced (by the conv epilogue that wrote x)
+    int P = given_parts;
+    const float* pr = prereduce(part, P, C, s);
+    hipLaunchKernelGGL(k_bn_fwd_finalize, dim3((C + 63) / 64), dim3(64 * kFinPhases), 0, s, pr, P, M, C, gamma, beta,
+                       mean_off, mean, invstd, scale, shift, moving_mean, moving_var, momentum, eps);
+    return;
+  }
   if (dt == BnDType::kBF16)
     hipLaunchKernelGGL((k_bn_partial<BnDType::kBF16, 0>), dim3(p.parts), dim3(256), 0, s, x, nullptr, nullptr, nullptr,
                        nullptr, nullptr, M, C, p.rows_wg, part);
   else
     hipLaunchKernelGGL((k_bn_partial<BnDType::kF32, 0>), dim3(p.parts), dim3(256), 0, s, x, nullptr, nullptr, nullptr,
                        nullptr, nullptr, M, C, p.rows_wg, part);
-  hipLaunchKernelGGL(k_bn_fwd_finalize, dim3((C + 63) / 64), dim3(64 * kFinPhases), 0, s, part, p.parts, M, C, gamma, beta,
+  int P = p.parts;
+  const float* pr = prereduce(part, P, C, s);
+  hipLaunchKernelGGL(k_bn_fwd_finalize, dim3((C + 63) / 64), dim3(64 * kFinPhases), 0, s, pr, P, M, C, gamma, beta,
                      mean_off, mean, invstd, scale, shift, moving_mean, moving_var, momentum, eps);
 }
 
 void bn_apply(const void* x, const void* residual, void* y, BnDType dt, int64_t M, int C, const float* scale,
               const float* shift, int relu, hipStream_t s) {
   const int64_t n8 = M * C / 8;
-  if (dt == BnDType::kBF16)
-    hipLaunchKernelGGL(k_bn_apply<BnDType::kBF16>, dim3(elementwise_grid(n8)), dim3(256), 0, s, x, residual, y, n8, C,
-                       scale, shift, relu);
-  else
-    hipLaunchKernelGGL(k_bn_apply<BnDType::kF32>, dim3(elementwise_grid(n8)), dim3(256), 0, s, x, residual, y, n8, C,
-                       scale, shift, relu);
+  const dim3 g(elementwise_grid(n8)), b(256);
+  if (dt == BnDType::kBF16) {
+    if (g_elem_unroll == 2)
+      hipLaunchKernelGGL((k_bn_apply<BnDType::kBF16, 2>), g, b, 0, s, x, residual, y, n8, C, scale, shift, relu);
+    else
+      hipLaunchKernelGGL((k_bn_apply<BnDType::kBF16, 1>), g, b, 0, s, x, residual, y, n8, C, scale, shift, relu);
+  } else {
+    hipLaunchKernelGGL((k_bn_apply<BnDType::kF32, 1>), g, b, 0, s, x, residual, y, n8, C, scale, shift, relu);
+  }
 }
 
 template <BnDType D>
@@ -335,14 +434,26 @@ static void bn_backward_t(const void* dy, const void* x, const void* y, void* dz
                        part);
   else
     hipLaunchKernelGGL((k_bn_partial<D, 3>), gp, blk, 0, s, dy, x, y, nullptr, nullptr, dz, M, C, p.rows_wg, part);
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), dim3(64 * kFinPhases), 0, s, part, p.parts, M, C, gamma, mean, invstd,
+  int P = p.parts;
+  const float* pr = prereduce(part, P, C, s);
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), dim3(64 * kFinPhases), 0, s, pr, P, M, C, gamma, mean, invstd,
                      dgamma, dbeta, coef, acc);
   const int64_t n8 = M * C / 8;
   const dim3 ge(elementwise_grid(n8));
-  if (mode == 1)
-    hipLaunchKernelGGL((k_bn_dx<D, true>), ge, blk, 0, s, dy, x, dx, n8, C, coef, scale, shift);
-  else
-    hipLaunchKernelGGL((k_bn_dx<D, false>), ge, blk, 0, s, mode == 2 ? dz : dy, x, dx, n8, C, coef, nullptr, nullptr);
+  const bool u2 = g_elem_unroll == 2 && D == BnDType::kBF16;
+  if (mode == 1) {
+    if (u2)
+      hipLaunchKernelGGL((k_bn_dx<D, true, 2>), ge, blk, 0, s, dy, x, dx, n8, C, coef, scale, shift);
+    else
+      hipLaunchKernelGGL((k_bn_dx<D, true, 1>), ge, blk, 0, s, dy, x, dx, n8, C, coef, scale, shift);
+  } else {
+    if (u2)
+      hipLaunchKernelGGL((k_bn_dx<D, false, 2>), ge, blk, 0, s, mode == 2 ? dz : dy, x, dx, n8, C, coef, nullptr,
+                         nullptr);
+    else
+      hipLaunchKernelGGL((k_bn_dx<D, false, 1>), ge, blk, 0, s, mode == 2 ? dz : dy, x, dx, n8, C, coef, nullptr,
+                         nullptr);
+  }
 }
 
 void bn_backward(const void* dy, const void* x, const void* y, void* dz, void* dx, BnDType dt, int64_t M, int C,

@@ -23,15 +23,23 @@ struct ConvGeom {
 bool conv_bf16_supported(const ConvGeom& g);
 
 // y[N,OH,OW,K] = conv(x[N,H,W,C], w[K][KH][KW][C])           (weights OHWI: reduction-contiguous rows)
-void conv_fwd_bf16(const void* x, const void* w_ohwi, void* y, const ConvGeom& g, hipStream_t s);
+// stats (optional, [ceil(M / conv_fwd_row_tile) row tiles][2][K] f32, M = N*OH*OW): per-row-tile
+// channel sums of y and y^2 for a following batch norm (deterministic; bn_forward_train(part=...))
+void conv_fwd_bf16(const void* x, const void* w_ohwi, void* y, const ConvGeom& g, hipStream_t s,
+                   float* stats = nullptr);
+int conv_fwd_row_tile(const ConvGeom& g);
 // stride-1 input gradient: dx[N,H,W,C] = conv_transpose(dy[N,OH,OW,K], w[KH][KW][C][K]) (HWIO, the
 // Keras layout: for a fixed (kh, kw, c) the K reduction values are contiguous)
-void conv_dgrad_bf16(const void* dy, const void* w_hwio, void* dx, const ConvGeom& g, hipStream_t s);
+// residual (optional, shaped like dx): added in the epilogue, dx = dgrad + residual (the other
+// gradient contribution of a tensor with two consumers; saves a separate add pass)
+void conv_dgrad_bf16(const void* dy, const void* w_hwio, void* dx, const ConvGeom& g, hipStream_t s,
+                     const void* residual = nullptr);
 
 // Input gradient of a 1x1, stride-2, unpadded convolution (the strided shortcut / first 1x1 of a
 // ResNet-50 stage): dx[n][2i][2j] = dy[n][i][j] . w^T, the other three pixels of every 2x2 block are
 // zero (written by the same kernel's epilogue; H <= 2*OH, W <= 2*OW).
-void conv_dgrad_s2_1x1_bf16(const void* dy, const void* w_hwio, void* dx, const ConvGeom& g, hipStream_t s);
+void conv_dgrad_s2_1x1_bf16(const void* dy, const void* w_hwio, void* dx, const ConvGeom& g, hipStream_t s,
+                            const void* residual = nullptr);
 
 // Weight gradient, split-K over output pixels with a deterministic partial-slab reduction.
 struct WgradPlan {

@@ -48,7 +48,25 @@ struct Igemm {
   int scatter;  // 2: output row (n, oh, ow) goes to pixel (2oh, 2ow) of a [N][XH][XW][K] tensor whose
                 // other three pixels of each 2x2 block are written as zeros (1x1 stride-2 input gradient)
   int XH, XW;
+  const uint16_t* res;  // optional bf16 tensor shaped like y, added in the epilogue (gradient sums)
+  float* stats;         // optional [M / BM row tiles][2][K]: per-tile channel sums of y and y^2 (the
+                        // batch-norm statistics of the conv output, from the stored bf16 values)
 };
+
+// a + b for 8 packed bf16 values (f32 add, round to nearest even)
+__device__ __forceinline__ u32x4 add_bf16x8(u32x4 a, u32x4 b) {
+  u32x4 o;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float lo = __uint_as_float(a[i] << 16) + __uint_as_float(b[i] << 16);
+    const float hi = __uint_as_float(a[i] & 0xffff0000u) + __uint_as_float(b[i] & 0xffff0000u);
+    uint32_t ul = __float_as_uint(lo), uh = __float_as_uint(hi);
+    ul += 0x7fffu + ((ul >> 16) & 1u);
+    uh += 0x7fffu + ((uh >> 16) & 1u);
+    o[i] = (ul >> 16) | (uh & 0xffff0000u);
+  }
+  return o;
+}
 
 __device__ __forceinline__ uint16_t f2bf(float f) {
   uint32_t u = __float_as_uint(f);
@@ -174,6 +192,20 @@ __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
 
   // epilogue: bf16 tile into LDS ([BM][BN + 8]), then 16-B row segments to global
   constexpr int OUT_LD = BN + 8;
+  constexpr int SEG = BN / 8;              // 16-B segments per row
+  constexpr int EPI = BM * SEG / NT;       // segments per thread
+  static_assert(BM * SEG % NT == 0, "epilogue segments must divide evenly");
+  // residual (gradient sum): all of this thread's loads issued here, before the LDS round trip, so
+  // their latency overlaps it instead of serialising the store loop
+  u32x4 rv[EPI];
+  if (a.res && !a.scatter) {
+#pragma unroll
+    for (int e = 0; e < EPI; ++e) {
+      const int s = tid + e * NT, row = s / SEG, seg = s % SEG, m = tm * BM + row;
+      rv[e] = m < a.M ? *reinterpret_cast<const u32x4*>(a.res + (long long)m * a.K + tn * BN + seg * 8)
+                      : u32x4{0u, 0u, 0u, 0u};
+    }
+  }
   static_assert(BM * OUT_LD <= 2 * (BM + BN) * LDS_ROW, "epilogue tile must fit the operand LDS");
   // (operands are swapped in the MFMA, so a lane holds 4 consecutive channels of one pixel: one 8-B write)
 #pragma unroll
@@ -186,15 +218,54 @@ __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
           make_uint2(lo, hi);
     }
   __syncthreads();
-  constexpr int SEG = BN / 8;  // 16-B segments per row
   if (!a.scatter) {
+    static_assert(NT % SEG == 0, "a thread keeps one 8-channel segment across its rows");
+    float cs[8], cq[8];
 #pragma unroll
-    for (int s = tid; s < BM * SEG; s += NT) {
-      const int row = s / SEG, seg = s % SEG;
+    for (int j = 0; j < 8; ++j) cs[j] = cq[j] = 0.f;
+#pragma unroll
+    for (int e = 0; e < EPI; ++e) {
+      const int s = tid + e * NT, row = s / SEG, seg = s % SEG;
       const int m = tm * BM + row;
-      if (m < a.M)
-        *reinterpret_cast<u32x4*>(a.y + (long long)m * a.K + tn * BN + seg * 8) =
-            *reinterpret_cast<const u32x4*>(lds + row * OUT_LD + seg * 8);
+      if (m < a.M) {
+        const long long o = (long long)m * a.K + tn * BN + seg * 8;
+        u32x4 v = *reinterpret_cast<const u32x4*>(lds + row * OUT_LD + seg * 8);
+        if (a.res) v = add_bf16x8(v, rv[e]);
+        *reinterpret_cast<u32x4*>(a.y + o) = v;
+        if (a.stats) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float lo = __uint_as_float(v[j] << 16), hi = __uint_as_float(v[j] & 0xffff0000u);
+            cs[2 * j] += lo;
+            cq[2 * j] = fmaf(lo, lo, cq[2 * j]);
+            cs[2 * j + 1] += hi;
+            cq[2 * j + 1] = fmaf(hi, hi, cq[2 * j + 1]);
+          }
+        }
+      }
+    }
+    if (a.stats) {
+      // fixed-order reduction over the NT / SEG threads of each segment, through the (now free) LDS
+      constexpr int TPS = NT / SEG;  // threads per segment
+      static_assert(2 * TPS * BN * 4 <= 2 * (BM + BN) * LDS_ROW * 2, "stats scratch must fit the operand LDS");
+      __syncthreads();  // every thread has read its tile rows
+      float* red = reinterpret_cast<float*>(lds);
+      const int seg = tid % SEG, grp = tid / SEG;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[grp * BN + seg * 8 + j] = cs[j];
+        red[TPS * BN + grp * BN + seg * 8 + j] = cq[j];
+      }
+      __syncthreads();
+      for (int c = tid; c < BN; c += NT) {
+        float S = 0.f, Q = 0.f;
+        for (int g2 = 0; g2 < TPS; ++g2) {
+          S += red[g2 * BN + c];
+          Q += red[TPS * BN + g2 * BN + c];
+        }
+        a.stats[((long long)tm * 2) * a.K + tn * BN + c] = S;
+        a.stats[((long long)tm * 2 + 1) * a.K + tn * BN + c] = Q;
+      }
     }
   } else {
     for (int s = tid; s < BM * SEG; s += NT) {
@@ -203,10 +274,30 @@ __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
       if (m >= a.M) continue;
       const int ow = m % a.OW, t = m / a.OW, oh = t % a.OH, n = t / a.OH;
       const int h = 2 * oh, w = 2 * ow;
-      uint16_t* o = a.y + (((long long)n * a.XH + h) * a.XW + w) * a.K + tn * BN + seg * 8;
+      const long long off = (((long long)n * a.XH + h) * a.XW + w) * a.K + tn * BN + seg * 8;
+      uint16_t* o = a.y + off;
       const long long rs = (long long)a.XW * a.K;
+      u32x4 v = *reinterpret_cast<const u32x4*>(lds + row * OUT_LD + seg * 8);
+      if (a.res) {
+        // the other gradient contribution: added at the computed pixel, copied to the three others
+        // (the four loads issued together)
+        const uint16_t* rp = a.res + off;
+        const bool w1 = w + 1 < a.XW, h1 = h + 1 < a.XH;
+        const u32x4 z{0u, 0u, 0u, 0u};
+        const u32x4 r00 = *reinterpret_cast<const u32x4*>(rp);
+        const u32x4 r01 = w1 ? *reinterpret_cast<const u32x4*>(rp + a.K) : z;
+        const u32x4 r10 = h1 ? *reinterpret_cast<const u32x4*>(rp + rs) : z;
+        const u32x4 r11 = (w1 && h1) ? *reinterpret_cast<const u32x4*>(rp + rs + a.K) : z;
+        *reinterpret_cast<u32x4*>(o) = add_bf16x8(v, r00);
+        if (w1) *reinterpret_cast<u32x4*>(o + a.K) = r01;
+        if (h1) {
+          *reinterpret_cast<u32x4*>(o + rs) = r10;
+          if (w1) *reinterpret_cast<u32x4*>(o + rs + a.K) = r11;
+        }
+        continue;
+      }
       const u32x4 z{0u, 0u, 0u, 0u};
-      *reinterpret_cast<u32x4*>(o) = *reinterpret_cast<const u32x4*>(lds + row * OUT_LD + seg * 8);
+      *reinterpret_cast<u32x4*>(o) = v;
       if (w + 1 < a.XW) *reinterpret_cast<u32x4*>(o + a.K) = z;
       if (h + 1 < a.XH) {
         *reinterpret_cast<u32x4*>(o + rs) = z;
@@ -243,28 +334,37 @@ bool conv_bf16_supported(const ConvGeom& g) {
          (long long)g.N * g.OH * g.OW < (1ll << 31) && (long long)g.N * g.H * g.W * g.C < (1ll << 40);
 }
 
-void conv_fwd_bf16(const void* x, const void* w_ohwi, void* y, const ConvGeom& g, hipStream_t s) {
+int conv_fwd_row_tile(const ConvGeom& g) {
+  // the tile launch() picks for the forward (128 rows in every variant but the sweep-only 256)
+  return (g_forced_tile == 3 && g.K % 128 == 0) ? 256 : 128;
+}
+
+void conv_fwd_bf16(const void* x, const void* w_ohwi, void* y, const ConvGeom& g, hipStream_t s, float* stats) {
   Igemm a{static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w_ohwi), static_cast<uint16_t*>(y),
           g.N, g.H, g.W, g.C, g.OH, g.OW, g.K, g.KH, g.KW, g.SH, g.SW, g.PT, g.PL, 0,
-          (long long)g.KH * g.KW * g.C, (long long)g.KW * g.C, (long long)g.C, g.N * g.OH * g.OW};
+          (long long)g.KH * g.KW * g.C, (long long)g.KW * g.C, (long long)g.C, g.N * g.OH * g.OW, 0, 0, 0, nullptr,
+          stats};
   launch(a, s);
 }
 
-void conv_dgrad_bf16(const void* dy, const void* w_hwio, void* dx, const ConvGeom& g, hipStream_t s) {
+void conv_dgrad_bf16(const void* dy, const void* w_hwio, void* dx, const ConvGeom& g, hipStream_t s,
+                     const void* residual) {
   // image = dy [N][OH][OW][K] (reduction channels K), output = dx [N][H][W][C] (columns C), stride 1,
   // mirrored taps with padding KH-1-PT / KW-1-PL
   Igemm a{static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w_hwio), static_cast<uint16_t*>(dx),
           g.N, g.OH, g.OW, g.K, g.H, g.W, g.C, g.KH, g.KW, 1, 1, g.KH - 1 - g.PT, g.KW - 1 - g.PL, 1,
-          (long long)g.K, (long long)g.KW * g.C * g.K, (long long)g.C * g.K, g.N * g.H * g.W};
+          (long long)g.K, (long long)g.KW * g.C * g.K, (long long)g.C * g.K, g.N * g.H * g.W, 0, 0, 0,
+          static_cast<const uint16_t*>(residual)};
   launch(a, s);
 }
 
-void conv_dgrad_s2_1x1_bf16(const void* dy, const void* w_hwio, void* dx, const ConvGeom& g, hipStream_t s) {
+void conv_dgrad_s2_1x1_bf16(const void* dy, const void* w_hwio, void* dx, const ConvGeom& g, hipStream_t s,
+                            const void* residual) {
   // a 1x1 stride-1 "convolution" of dy [N][OH][OW][K] with the HWIO rows [C][K] (columns C, reduction K),
   // scattered to the even pixels of dx [N][H][W][C]
   Igemm a{static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w_hwio), static_cast<uint16_t*>(dx),
           g.N, g.OH, g.OW, g.K, g.OH, g.OW, g.C, 1, 1, 1, 1, 0, 0, 0,
-          (long long)g.K, 0, 0, g.N * g.OH * g.OW, 2, g.H, g.W};
+          (long long)g.K, 0, 0, g.N * g.OH * g.OW, 2, g.H, g.W, static_cast<const uint16_t*>(residual)};
   launch(a, s);
 }
 

@@ -14,4 +14,11 @@ void gather_rows_u8(const uint8_t* src, const int* idx, float* out, int64_t rows
 // out[r] = src[idx[r]]   (labels)
 void gather_i32(const int* src, const int* idx, int* out, int64_t rows, hipStream_t s);
 
+// Weight-slab cast with transposes: for every 64 x 64 tile listed in `tiles` (int4: entry, row
+// tile, column tile, unused) of every entry e (int4 in `entries`: src offset, dst offset, R, K),
+// dst[e.dst + k * R + r] = bf16(src[e.src + r * K + k]) -- HWIO [R = KH*KW*C][K] f32 conv kernels
+// into the OHWI bf16 rows the implicit-GEMM forward reads, for all convs of a model in one launch.
+void slab_transpose_bf16(const float* src, uint16_t* dst, const int* entries, const int* tiles, int ntiles,
+                         hipStream_t s);
+
 }  // namespace tdl

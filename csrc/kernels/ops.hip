@@ -53,4 +53,44 @@ void gather_i32(const int* src, const int* idx, int* out, int64_t rows, hipStrea
   hipLaunchKernelGGL(k_gather_i32, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, src, idx, out, rows);
 }
 
+namespace {
+
+__global__ __launch_bounds__(256) void k_slab_transpose_bf16(const float* __restrict__ src, uint16_t* __restrict__ dst,
+                                                            const int4* __restrict__ entries,
+                                                            const int4* __restrict__ tiles) {
+  __shared__ float t[64][65];
+  const int4 tl = tiles[blockIdx.x];
+  const int4 e = entries[tl.x];
+  const int R = e.z, K = e.w, r0 = tl.y * 64, k0 = tl.z * 64;
+  const int tid = threadIdx.x;
+  // read 64 rows (r) x 64 columns (k): thread -> column k0 + (tid & 63), rows (tid >> 6) + 4 i
+  const int kc = tid & 63;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int r = (tid >> 6) + 4 * i;
+    t[r][kc] = (r0 + r < R && k0 + kc < K) ? src[(long long)e.x + (long long)(r0 + r) * K + k0 + kc] : 0.f;
+  }
+  __syncthreads();
+  // write 64 rows (k) x 64 columns (r): thread -> r column r0 + (tid & 63), k rows (tid >> 6) + 4 i
+  const int rc = tid & 63;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int k = (tid >> 6) + 4 * i;
+    if (k0 + k < K && r0 + rc < R) {
+      uint32_t u = __float_as_uint(t[rc][k]);
+      u += 0x7fffu + ((u >> 16) & 1u);
+      dst[(long long)e.y + (long long)(k0 + k) * R + r0 + rc] = (uint16_t)(u >> 16);
+    }
+  }
+}
+
+}  // namespace
+
+void slab_transpose_bf16(const float* src, uint16_t* dst, const int* entries, const int* tiles, int ntiles,
+                         hipStream_t s) {
+  if (ntiles <= 0) return;
+  hipLaunchKernelGGL(k_slab_transpose_bf16, dim3(ntiles), dim3(256), 0, s, src, dst,
+                     reinterpret_cast<const int4*>(entries), reinterpret_cast<const int4*>(tiles));
+}
+
 }  // namespace tdl

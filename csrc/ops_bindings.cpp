@@ -62,7 +62,7 @@ const float* opt_f32(const c10::optional<at::Tensor>& t) {
 std::vector<at::Tensor> bn_forward_train(at::Tensor x, c10::optional<at::Tensor> gamma, c10::optional<at::Tensor> beta,
                                          c10::optional<at::Tensor> moving_mean, c10::optional<at::Tensor> moving_var,
                                          double momentum, double eps, bool relu, c10::optional<at::Tensor> residual,
-                                         c10::optional<at::Tensor> mean_off) {
+                                         c10::optional<at::Tensor> mean_off, c10::optional<at::Tensor> part_in) {
   bn_check(x);
   const int64_t C = x.size(-1), M = x.numel() / C;
   const void* res = nullptr;
@@ -74,7 +74,22 @@ std::vector<at::Tensor> bn_forward_train(at::Tensor x, c10::optional<at::Tensor>
   }
   const tdl::BnPlan plan = tdl::bn_plan(M, (int)C);
   auto f = x.options().dtype(at::kFloat);
-  auto part = at::empty({(int64_t)plan.parts * 2 * C}, f);
+  int given = 0;
+  at::Tensor part;
+  if (part_in.has_value() && part_in->defined()) {
+    // [rows + ceil(rows/64)][2][C] from conv_fwd_stats: the first `rows` rows are the partial sums
+    TORCH_CHECK(part_in->is_cuda() && part_in->is_contiguous() && part_in->scalar_type() == at::kFloat &&
+                    part_in->dim() == 3 && part_in->size(1) == 2 && part_in->size(2) == C,
+                "batch_norm: part must be f32 [rows][2][C]");
+    const int64_t rows = part_in->size(0);
+    int64_t p = 1;
+    while (p + (p + 63) / 64 < rows) ++p;  // invert rows = P + ceil(P / 64)
+    TORCH_CHECK(p + (p + 63) / 64 == rows, "batch_norm: part rows must be P + ceil(P/64)");
+    given = (int)p;
+    part = *part_in;
+  } else {
+    part = at::empty({(int64_t)plan.part_rows * 2 * C}, f);
+  }
   auto st = at::empty({4, C}, f);  // mean, invstd, scale, shift
   float* mm = const_cast<float*>(opt_f32(moving_mean));
   float* mv = const_cast<float*>(opt_f32(moving_var));
@@ -82,7 +97,8 @@ std::vector<at::Tensor> bn_forward_train(at::Tensor x, c10::optional<at::Tensor>
   hipStream_t s = cur_stream();
   float* sp = st.data_ptr<float>();
   tdl::bn_forward_stats(x.data_ptr(), bn_dtype(x), M, (int)C, part.data_ptr<float>(), opt_f32(gamma), opt_f32(beta),
-                        opt_f32(mean_off), sp, sp + C, sp + 2 * C, sp + 3 * C, mm, mv, (float)momentum, (float)eps, s);
+                        opt_f32(mean_off), sp, sp + C, sp + 2 * C, sp + 3 * C, mm, mv, (float)momentum, (float)eps, s,
+                        given);
   auto y = at::empty_like(x);
   tdl::bn_apply(x.data_ptr(), res, y.data_ptr(), bn_dtype(x), M, (int)C, sp + 2 * C, sp + 3 * C, relu ? 1 : 0, s);
   return {y, st};
@@ -110,7 +126,7 @@ std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, c10::optional<a
   }
   const tdl::BnPlan plan = tdl::bn_plan(M, (int)C);
   auto f = x.options().dtype(at::kFloat);
-  auto part = at::empty({(int64_t)plan.parts * 2 * C}, f);
+  auto part = at::empty({(int64_t)plan.part_rows * 2 * C}, f);
   auto out = at::empty({5, C}, f);  // dgamma, dbeta, coef[3]
   auto dx = at::empty_like(x);
   float* o = out.data_ptr<float>();
@@ -187,8 +203,34 @@ at::Tensor conv_fwd(at::Tensor x, at::Tensor w_ohwi, int64_t oh, int64_t ow, int
   return y;
 }
 
+// forward + batch-norm partial sums of y: returns (y, part[P + ceil(P/64)][2][K]) with P row tiles
+std::vector<at::Tensor> conv_fwd_stats(at::Tensor x, at::Tensor w_ohwi, int64_t oh, int64_t ow, int64_t sh,
+                                       int64_t sw, int64_t pt, int64_t pl) {
+  conv_check(x, "x");
+  conv_check(w_ohwi, "w");
+  TORCH_CHECK(w_ohwi.dim() == 4 && w_ohwi.size(3) == x.size(3), "conv_fwd: weights must be OHWI [K,KH,KW,C]");
+  auto g = conv_geom(x, oh, ow, w_ohwi.size(0), w_ohwi.size(1), w_ohwi.size(2), sh, sw, pt, pl);
+  auto y = at::empty({x.size(0), oh, ow, w_ohwi.size(0)}, x.options());
+  const int64_t M = (int64_t)g.N * g.OH * g.OW, bm = tdl::conv_fwd_row_tile(g);
+  const int64_t P = (M + bm - 1) / bm;
+  auto part = at::empty({P + (P + 63) / 64, 2, (int64_t)g.K}, x.options().dtype(at::kFloat));
+  tdl::conv_fwd_bf16(x.data_ptr(), w_ohwi.data_ptr(), y.data_ptr(), g, cur_stream(), part.data_ptr<float>());
+  return {y, part};
+}
+
 // stride-1 input gradient: dx[N,H,W,C] from dy[N,OH,OW,K] and w_hwio[KH,KW,C,K]
-at::Tensor conv_dgrad(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w, int64_t pt, int64_t pl) {
+const void* opt_residual(const c10::optional<at::Tensor>& r, const at::Tensor& like_dy, int64_t n, int64_t h,
+                         int64_t w, int64_t c) {
+  if (!r.has_value() || !r->defined()) return nullptr;
+  conv_check(*r, "residual");
+  TORCH_CHECK(r->dim() == 4 && r->size(0) == n && r->size(1) == h && r->size(2) == w && r->size(3) == c,
+              "conv dgrad: residual must be shaped like dx");
+  (void)like_dy;
+  return r->data_ptr();
+}
+
+at::Tensor conv_dgrad(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w, int64_t pt, int64_t pl,
+                      c10::optional<at::Tensor> residual) {
   conv_check(dy, "dy");
   conv_check(w_hwio, "w");
   TORCH_CHECK(w_hwio.dim() == 4 && w_hwio.size(3) == dy.size(3), "conv_dgrad: weights must be HWIO [KH,KW,C,K]");
@@ -196,11 +238,12 @@ at::Tensor conv_dgrad(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w, in
                   (int)dy.size(3), (int)w_hwio.size(0), (int)w_hwio.size(1), 1, 1, (int)pt, (int)pl};
   TORCH_CHECK(tdl::conv_bf16_supported(g), "conv_dgrad: unsupported geometry (C and K must be multiples of 64)");
   auto dx = at::empty({dy.size(0), h, w, w_hwio.size(2)}, dy.options());
-  tdl::conv_dgrad_bf16(dy.data_ptr(), w_hwio.data_ptr(), dx.data_ptr(), g, cur_stream());
+  tdl::conv_dgrad_bf16(dy.data_ptr(), w_hwio.data_ptr(), dx.data_ptr(), g, cur_stream(),
+                       opt_residual(residual, dy, dy.size(0), h, w, w_hwio.size(2)));
   return dx;
 }
 // input gradient of a 1x1 stride-2 unpadded conv: dx[N,H,W,C] from dy[N,OH,OW,K] and w_hwio[1,1,C,K]
-at::Tensor conv_dgrad_s2(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w) {
+at::Tensor conv_dgrad_s2(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w, c10::optional<at::Tensor> residual) {
   conv_check(dy, "dy");
   conv_check(w_hwio, "w");
   TORCH_CHECK(w_hwio.dim() == 4 && w_hwio.size(0) == 1 && w_hwio.size(1) == 1 && w_hwio.size(3) == dy.size(3),
@@ -211,7 +254,8 @@ at::Tensor conv_dgrad_s2(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w)
                   (int)dy.size(3), 1, 1, 2, 2, 0, 0};
   TORCH_CHECK(tdl::conv_bf16_supported(g), "conv_dgrad_s2: unsupported geometry (C and K must be multiples of 64)");
   auto dx = at::empty({dy.size(0), h, w, w_hwio.size(2)}, dy.options());
-  tdl::conv_dgrad_s2_1x1_bf16(dy.data_ptr(), w_hwio.data_ptr(), dx.data_ptr(), g, cur_stream());
+  tdl::conv_dgrad_s2_1x1_bf16(dy.data_ptr(), w_hwio.data_ptr(), dx.data_ptr(), g, cur_stream(),
+                              opt_residual(residual, dy, dy.size(0), h, w, w_hwio.size(2)));
   return dx;
 }
 
@@ -262,10 +306,26 @@ std::vector<std::vector<int64_t>> conv_wgrad_plans(std::vector<int64_t> x_shape,
   for (const auto& p : tdl::conv_wgrad_plans(g, (int)max_plans)) out.push_back({p.wmw, p.wnw, p.chunk, p.nsplit});
   return out;
 }
+// dst (bf16 slab) <- transposed copies of the HWIO f32 conv kernels in src (f32 slab); entries
+// [E][4] (src off, dst off, R, K) and tiles [T][4] (entry, row tile, col tile, 0) int32 on the GPU
+void slab_transpose_bf16(at::Tensor src, at::Tensor dst, at::Tensor entries, at::Tensor tiles) {
+  TORCH_CHECK(src.is_cuda() && src.is_contiguous() && src.scalar_type() == at::kFloat, "slab_transpose: f32 src");
+  TORCH_CHECK(dst.is_cuda() && dst.is_contiguous() && dst.scalar_type() == at::kBFloat16, "slab_transpose: bf16 dst");
+  TORCH_CHECK(entries.is_cuda() && entries.scalar_type() == at::kInt && entries.dim() == 2 && entries.size(1) == 4,
+              "slab_transpose: entries [E][4] int32");
+  TORCH_CHECK(tiles.is_cuda() && tiles.scalar_type() == at::kInt && tiles.dim() == 2 && tiles.size(1) == 4,
+              "slab_transpose: tiles [T][4] int32");
+  tdl::slab_transpose_bf16(src.data_ptr<float>(), reinterpret_cast<uint16_t*>(dst.data_ptr()),
+                           entries.data_ptr<int>(), tiles.data_ptr<int>(), (int)tiles.size(0), cur_stream());
+}
 }  // namespace
 
 void register_ops(pybind11::module& m) {
-  m.def("conv_dgrad_s2", &conv_dgrad_s2, "NHWC bf16 1x1 stride-2 convolution input gradient (MFMA)");
+  m.def("bn_set_tuning", &tdl::bn_set_tuning, "BN kernel sweep hooks (max_parts, elem_blocks, elem_unroll; 0 = keep)");
+  m.def("slab_transpose_bf16", &slab_transpose_bf16, "HWIO f32 conv kernels -> OHWI bf16, all in one launch");
+  m.def("conv_dgrad_s2", &conv_dgrad_s2, "NHWC bf16 1x1 stride-2 convolution input gradient (MFMA)",
+        pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("h"), pybind11::arg("wd"),
+        pybind11::arg("residual") = pybind11::none());
   m.def("conv_wgrad", &conv_wgrad, "NHWC bf16 convolution weight gradient (MFMA, transposed LDS reads, split-K)",
         pybind11::arg("x"), pybind11::arg("dy"), pybind11::arg("kh"), pybind11::arg("kw"), pybind11::arg("sh"),
         pybind11::arg("sw"), pybind11::arg("pt"), pybind11::arg("pl"), pybind11::arg("out") = pybind11::none(),
@@ -273,13 +333,17 @@ void register_ops(pybind11::module& m) {
   m.def("conv_wgrad_plans", &conv_wgrad_plans, "weight-gradient candidate plans, best first: [[wmw, wnw, chunk, nsplit]]");
   m.def("conv_force_tile", &tdl::conv_force_tile, "conv tile sweep hook (0 = heuristic)");
   m.def("conv_fwd", &conv_fwd, "NHWC bf16 implicit-GEMM convolution forward (MFMA)");
-  m.def("conv_dgrad", &conv_dgrad, "NHWC bf16 implicit-GEMM stride-1 convolution input gradient (MFMA)");
+  m.def("conv_fwd_stats", &conv_fwd_stats, "conv forward + batch-norm partial channel sums of its output");
+  m.def("conv_dgrad", &conv_dgrad, "NHWC bf16 implicit-GEMM stride-1 convolution input gradient (MFMA)",
+        pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("h"), pybind11::arg("wd"), pybind11::arg("pt"),
+        pybind11::arg("pl"), pybind11::arg("residual") = pybind11::none());
   m.def("gather_rows", &gather_rows, "row gather (+u8->f32 scale) of a device-resident dataset");
   m.def("gather_labels", &gather_labels);
   m.def("bn_forward_train", &bn_forward_train, "NHWC batch-norm training forward (+relu)", pybind11::arg("x"),
         pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("moving_mean"), pybind11::arg("moving_var"),
         pybind11::arg("momentum"), pybind11::arg("eps"), pybind11::arg("relu") = false,
-        pybind11::arg("residual") = pybind11::none(), pybind11::arg("mean_off") = pybind11::none());
+        pybind11::arg("residual") = pybind11::none(), pybind11::arg("mean_off") = pybind11::none(),
+        pybind11::arg("part") = pybind11::none());
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC max pool forward (+argmax)");
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC max pool backward (gather form)");
   m.def("bn_backward", &bn_backward, "NHWC batch-norm training backward", pybind11::arg("dy"), pybind11::arg("x"),

@@ -140,6 +140,7 @@ class GenericTrainer:
         self.metrics = model.compiled_metrics
         self._policy = model._dtype_policy()
         self._Wc = None
+        self._Wt = None
         if self._policy == "mixed_bfloat16" and self.device.type == "cuda" and \
                 os.environ.get("TDL_CAST_ACCUMULATE", "1") == "1":
             # bf16 compute copy of the whole weight slab: one cast kernel per step instead of one
@@ -180,8 +181,30 @@ class GenericTrainer:
     def _bind_compute_views(self):
         if getattr(self, "_Wc", None) is None:
             return
-        for leaf, cv in zip(self._leaves, self.model._layout.views(self._Wc)):
+        layout = self.model._layout
+        for leaf, cv in zip(self._leaves, layout.views(self._Wc)):
             leaf._tdl_cview = cv
+        # 4-D (conv) kernels also get an OHWI bf16 copy (the implicit-GEMM forward's weight rows),
+        # refreshed with the cast by one transpose kernel over the whole slab
+        if getattr(self, "_Wt", None) is None:
+            entries, tiles = [], []
+            for i, (spec, off) in enumerate(zip(layout.specs, layout.offsets)):
+                if len(spec.shape) != 4 or i >= len(self._leaves):
+                    continue
+                R, K = spec.shape[0] * spec.shape[1] * spec.shape[2], spec.shape[3]
+                e = len(entries)
+                entries.append([off, off, R, K])
+                tiles += [[e, a, b, 0] for a in range((R + 63) // 64) for b in range((K + 63) // 64)]
+            self._Wt = torch.empty_like(self._Wc) if entries else False
+            if entries:
+                assert max(o + r * k for o, _, r, k in entries) <= self.W.numel()
+                self._wt_tables = (torch.tensor(entries, dtype=torch.int32, device=self.device),
+                                   torch.tensor(tiles, dtype=torch.int32, device=self.device))
+        if self._Wt is not False:
+            for leaf, spec, off in zip(self._leaves, layout.specs, layout.offsets):
+                if len(spec.shape) == 4:
+                    kh, kw, c, k = spec.shape
+                    leaf._tdl_tview = self._Wt[off: off + spec.size].view(k, kh, kw, c)
 
     def _bind_cast_accumulate(self):
         if self._buckets is None and os.environ.get("TDL_CAST_ACCUMULATE", "1") == "1":
@@ -287,6 +310,10 @@ class GenericTrainer:
 
         if self._Wc is not None:
             self._Wc.copy_(self.W)  # the step's bf16 weights, one kernel
+            if self._Wt is not False:
+                from ..ops import hip
+
+                hip().slab_transpose_bf16(self.W, self._Wt, *self._wt_tables)  # OHWI conv rows, one kernel
         V.CAST_ACCUMULATE[0] += 1  # Variable.cast may add straight into the slab only in here
         try:
             with trace_range("tdl.forward"):
@@ -295,6 +322,9 @@ class GenericTrainer:
             V.CAST_ACCUMULATE[0] -= 1
         with trace_range("tdl.backward"):
             loss.backward()
+        for b in (self.model.__dict__.get("_grad_boxes") or {}).values():
+            if b.g is not None:  # a parked gradient contribution nobody collected
+                raise RuntimeError("fused gradient sum lost a contribution (keras/fusion.py grad boxes)")
         if self.comm.world_size > 1:
             with trace_range("tdl.allreduce"):
                 if self._buckets is not None:

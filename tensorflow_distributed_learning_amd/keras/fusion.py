@@ -5,11 +5,17 @@ list; the plan rewrites, at execution time only (the layer graph, variables, che
 ``model.summary()`` are untouched):
 
 * ``Conv2D(use_bias, linear) -> BatchNormalization``: the conv runs without its bias; the bias is
-  folded into the BN (only the moving mean sees it; its gradient is exactly zero in training mode).
+  folded into the BN (only the moving mean sees it; its gradient is exactly zero in training mode),
+  and the hand-written conv forward's epilogue computes the BN's batch statistics (per-tile
+  channel sums of its bf16 output), so the BN skips its statistics pass over the tensor.
 * ``BatchNormalization -> ReLU``: one fused kernel pass (ops/batchnorm.py).
 * ``BatchNormalization -> Add(other) -> ReLU``: the ResNet block tail, one fused pass that also
   produces the residual's gradient.
 * ``ZeroPadding2D -> MaxPooling2D('valid')``: one pooling pass with implicit zero padding.
+* a tensor read by a Conv2D and by one other node (the ResNet block input: the shortcut / the
+  residual of the block tail, and the first 1x1 conv): the two backward contributions meet in a
+  ``GradBox`` (ops/conv.py) and the conv's input-gradient kernel adds the other one in its
+  epilogue, instead of autograd's separate add pass over the tensor.
 
 Every intermediate tensor of a fused group must have exactly one consumer.  A group executes at
 the position of its last node, when all its external inputs exist.  Eval / CPU calls run the
@@ -38,6 +44,8 @@ class Plan:
         self.conv_nobias = set()  # conv node ids whose bias is folded into their BN
         self.groups: Dict[int, Group] = {}  # id(last node) -> group
         self.pool_pad: Dict[int, tuple] = {}  # id(max-pool node) -> (padding input, padding)
+        self.conv_box: Dict[int, int] = {}   # id(conv node) -> id(input tensor) of its GradBox
+        self.taps: Dict[int, set] = {}       # id(node or group last node) -> ids of inputs read through a tap
 
     def __len__(self):
         return len(self.groups)
@@ -109,15 +117,57 @@ def plan(nodes: List[L.Node], outputs) -> Plan:
         if last is not n:
             p.skip.add(id(n))
         p.groups[id(last)] = Group(n, relu, residual, conv_layer, out, last)
+    if os.environ.get("TDL_FUSE_GRAD_SUM", "1") == "1":
+        _plan_grad_sums(p, nodes, consumers, outs)
     return p
 
 
-def run_group(g: Group, vals, training):
+def _plan_grad_sums(p: Plan, nodes, consumers, outs):
+    """Tensors with exactly two consumers, at least one a Conv2D reading it as its only input."""
+    owner = {}  # id(node absorbed in a group) -> id(group's last node)
+    for last_id, g in p.groups.items():
+        if g.residual is not None:
+            for c in consumers.get(id(g.residual), []):
+                if isinstance(c.layer, L.Add) and id(c) in p.skip:
+                    owner[id(c)] = last_id
+
+    def is_conv_reader(c, t):
+        return isinstance(c.layer, L.Conv2D) and c.inputs is t and id(c) not in p.skip
+
+    seen = set()
+    for n in nodes:
+        for t in L._flat(n.inputs):
+            tid = id(t)
+            if tid in seen or tid in outs:
+                continue
+            seen.add(tid)
+            cs = consumers.get(tid, [])
+            if len(cs) != 2 or cs[0] is cs[1] or not any(is_conv_reader(c, t) for c in cs):
+                continue
+            for c in cs:
+                if is_conv_reader(c, t):
+                    p.conv_box[id(c)] = tid
+                elif id(c) in owner:  # the residual of a fused BN -> Add -> ReLU group
+                    p.taps.setdefault(owner[id(c)], set()).add(tid)
+                elif id(c) not in p.skip:
+                    p.taps.setdefault(id(c), set()).add(tid)
+                else:  # absorbed elsewhere: leave this tensor to autograd
+                    p.conv_box = {k: v for k, v in p.conv_box.items() if v != tid}
+                    for v in p.taps.values():
+                        v.discard(tid)
+                    break
+
+
+def run_group(g: Group, vals, training, taps=None, boxes=None):
     from ..ops.batchnorm import batch_norm_train
 
     bn = g.bn_node.layer
     x = vals[id(g.bn_node.inputs)]
     r = vals[id(g.residual)] if g.residual is not None else None
+    if r is not None and taps and id(g.residual) in taps:
+        from ..ops.conv import GradBox, grad_tap
+
+        r = grad_tap(r, boxes.setdefault(id(g.residual), GradBox()))
     cb = None
     if g.conv_layer is not None:
         cbv = g.conv_layer.bias
@@ -127,5 +177,5 @@ def run_group(g: Group, vals, training):
     y = batch_norm_train(x, bn.gamma.value if bn.gamma is not None else None,
                          bn.beta.value if bn.beta is not None else None, bn.moving_mean.value,
                          bn.moving_variance.value, bn.momentum, bn.epsilon, relu=g.relu, residual=r, conv_bias=cb,
-                         grad_out=bn._grad_targets())
+                         grad_out=bn._grad_targets(), part=getattr(x, "_tdl_bn_part", None))
     vals[id(g.out)] = y

@@ -309,9 +309,10 @@ class Conv2D(Layer):
                                     regularizer=self.bias_regularizer) if self.use_bias else None
         self.built = True
 
-    def call(self, x, training=None, _fold_bias=False):
+    def call(self, x, training=None, _fold_bias=False, _grad_box=None, _bn_stats=False):
         """``_fold_bias``: the functional executor folded this bias into the following training-mode
-        BatchNormalization (keras/fusion.py), so the convolution runs without it."""
+        BatchNormalization (keras/fusion.py), so the convolution runs without it.  ``_grad_box``:
+        the input's other consumer's gradient is summed into this conv's input gradient."""
         # (1x1 convs stay on MIOpen: routing them through hipBLASLt GEMMs measured slower on MI355X,
         #  scripts/probe_1x1_gemm.py)
         gt = None
@@ -342,7 +343,9 @@ class Conv2D(Layer):
             w = k_hwio.permute(3, 2, 0, 1)
         if symmetric and _conv.supported(x, k_hwio, self.groups, self.dilation_rate):
             # hand-written implicit-GEMM MFMA kernels (csrc/kernels/conv.hip), autotuned against MIOpen
-            y = _conv.conv2d_nhwc(x, k_hwio, self.strides, pad if pad else (0, 0), grad_out=gt)
+            y = _conv.conv2d_nhwc(x, k_hwio, self.strides, pad if pad else (0, 0), grad_out=gt,
+                                  w_ohwi=self.kernel.compute_view_ohwi(x.dtype) if gt is not None else None,
+                                  grad_box=_grad_box, bn_stats=_bn_stats)
             if b is not None:
                 y = y + b
             return self.activation(y)

@@ -31,6 +31,7 @@ from .layers import InputLayer, KerasTensor, Layer, Node, _flat, _map
 _GLOBAL_POLICY = ["float32"]
 
 
+_CONV_BN_STATS = os.environ.get("TDL_CONV_BN_STATS", "1") == "1"
 _FUSE_CPU = [False]  # tests: apply the training-graph fusion plan to CPU tensors too
 
 
@@ -123,8 +124,10 @@ class Model(Layer):
         fp = None
         if training and isinstance(xs[0], torch.Tensor) and (xs[0].is_cuda or _FUSE_CPU[0]):
             fp = self._fusion()  # keras/fusion.py: conv-bias/BN/ReLU/Add groups (training, GPU)
-            if not fp.groups and not fp.pool_pad:
+            if not fp.groups and not fp.pool_pad and not fp.conv_box:
                 fp = None
+        boxes = {}  # id(tensor) -> GradBox of its two consumers' backward contributions
+        self.__dict__["_grad_boxes"] = boxes
         for n in self._nodes:
             if fp is not None:
                 nid = id(n)
@@ -134,18 +137,29 @@ class Model(Layer):
                 if g is not None:
                     from .fusion import run_group
 
-                    run_group(g, vals, training)
+                    run_group(g, vals, training, fp.taps.get(nid), boxes)
                     continue
             kw = {k: v for k, v in n.kwargs.items() if k != "training"}
             src = n.inputs
             if fp is not None:
                 if id(n) in fp.conv_nobias:
                     kw["_fold_bias"] = True
+                    if _CONV_BN_STATS:
+                        kw["_bn_stats"] = True  # its BN's statistics come from the conv epilogue
                 pp = fp.pool_pad.get(id(n))
                 if pp is not None:  # fused ZeroPadding2D: read the padding layer's input
                     src = pp[0]
                     kw["_zero_pad"] = pp[1]
-            args = _map(lambda t: vals[id(t)], src)
+            if fp is not None and (id(n) in fp.conv_box or id(n) in fp.taps):
+                from ..ops.conv import GradBox, grad_tap
+
+                if id(n) in fp.conv_box:
+                    kw["_grad_box"] = boxes.setdefault(fp.conv_box[id(n)], GradBox())
+                tapped = fp.taps.get(id(n), ())
+                args = _map(lambda t: grad_tap(vals[id(t)], boxes.setdefault(id(t), GradBox()))
+                            if id(t) in tapped else vals[id(t)], src)
+            else:
+                args = _map(lambda t: vals[id(t)], src)
             out = n.layer(args, training=training, **kw)
             if isinstance(n.outputs, list):
                 for t, o in zip(n.outputs, out):

@@ -36,12 +36,13 @@ def _aligned(t: torch.Tensor) -> torch.Tensor:
 
 class _BatchNormTrain(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, residual, conv_bias, moving_mean, moving_var, momentum, eps, relu, grad_out):
+    def forward(ctx, x, gamma, beta, residual, conv_bias, moving_mean, moving_var, momentum, eps, relu, grad_out,
+                part=None):
         C = hip()
         xc = _aligned(x)
         rc = _aligned(residual.to(xc.dtype)) if residual is not None else None
         y, st = C.bn_forward_train(xc, gamma, beta, moving_mean, moving_var, float(momentum), float(eps), bool(relu),
-                                   rc, conv_bias.detach() if conv_bias is not None else None)
+                                   rc, conv_bias.detach() if conv_bias is not None else None, part)
         ctx.mode = 2 if residual is not None else (1 if relu else 0)
         ctx.flags = (gamma is not None, beta is not None, residual is not None, conv_bias is not None)
         ctx.res_dtype = residual.dtype if residual is not None else None
@@ -63,17 +64,19 @@ class _BatchNormTrain(torch.autograd.Function):
         dres = out[3].to(ctx.res_dtype) if has_r else None
         dcb = torch.zeros_like(conv_bias) if (has_cb and ctx.needs_input_grad[4]) else None
         return (dx, dgamma if ctx.needs_input_grad[1] else None, dbeta if ctx.needs_input_grad[2] else None, dres,
-                dcb, None, None, None, None, None, None)
+                dcb, None, None, None, None, None, None, None)
 
 
 def batch_norm_train(x: torch.Tensor, gamma: Optional[torch.Tensor], beta: Optional[torch.Tensor],
                      moving_mean: Optional[torch.Tensor], moving_var: Optional[torch.Tensor], momentum: float,
                      eps: float, relu: bool = False, residual: Optional[torch.Tensor] = None,
-                     conv_bias: Optional[torch.Tensor] = None, grad_out=None) -> torch.Tensor:
+                     conv_bias: Optional[torch.Tensor] = None, grad_out=None, part=None) -> torch.Tensor:
     """Keras-convention ``momentum`` (moving = moving*momentum + batch*(1-momentum)).
 
     ``grad_out = (dgamma_target, dbeta_target)``: f32 slab views the GPU backward ADDS the gamma /
-    beta gradients into (Variable.grad_target); gamma / beta are then passed without autograd."""
+    beta gradients into (Variable.grad_target); gamma / beta are then passed without autograd.
+    ``part``: the batch statistics' partial sums already computed by the conv that produced x
+    (ops/conv.py ``bn_stats``); the statistics pass over x is skipped."""
     if residual is not None and not relu:
         raise ValueError("the fused residual form is BN -> Add -> ReLU")
     if supported(x) and (residual is None or tuple(residual.shape) == tuple(x.shape)):
@@ -81,7 +84,7 @@ def batch_norm_train(x: torch.Tensor, gamma: Optional[torch.Tensor], beta: Optio
             gamma = gamma.detach() if gamma is not None else None
             beta = beta.detach() if beta is not None else None
         return _BatchNormTrain.apply(x, gamma, beta, residual, conv_bias, moving_mean, moving_var, momentum, eps, relu,
-                                     grad_out)
+                                     grad_out, part)
     h = x if conv_bias is None else x + conv_bias.to(x.dtype)
     perm = [0, h.dim() - 1] + list(range(1, h.dim() - 1))
     hp = h.permute(*perm)

@@ -34,6 +34,51 @@ def supported(x: torch.Tensor, kernel_hwio: torch.Tensor, groups=1, dilation=(1,
             and x.shape[-1] % 64 == 0 and kernel_hwio.shape[-1] % 64 == 0 and mode() != "miopen")
 
 
+class GradBox:
+    """Rendezvous of the two backward contributions to a tensor with two consumers, at least one of
+    them a hand-written conv (keras/fusion.py plans them).  Participants register in the forward
+    (``n``); in the backward the first participant parks its contribution in ``g`` and returns
+    nothing for the tensor, the second adds it in: a conv input gradient inside its epilogue (no
+    separate add pass), a :class:`_GradTap` with one add.  With fewer than two registered
+    participants (a conv that fell back to a library path) everybody returns gradients normally."""
+
+    __slots__ = ("n", "g")
+
+    def __init__(self):
+        self.n = 0
+        self.g = None
+
+    @property
+    def active(self) -> bool:
+        return self.n == 2
+
+
+class _GradTap(torch.autograd.Function):
+    """Identity in the forward; in the backward a :class:`GradBox` participant."""
+
+    @staticmethod
+    def forward(ctx, t, box):
+        box.n += 1
+        ctx.box = box
+        return t.view_as(t)
+
+    @staticmethod
+    def backward(ctx, g):
+        box = ctx.box
+        if not box.active:
+            return g, None
+        if box.g is None:
+            box.g = g
+            return None, None
+        s = g + box.g
+        box.g = None
+        return s, None
+
+
+def grad_tap(t: torch.Tensor, box: GradBox) -> torch.Tensor:
+    return _GradTap.apply(t, box)
+
+
 def _time(fn, reps=5) -> float:
     """Median of ``reps`` individually timed calls after two untimed ones (the first MIOpen call of a
     shape runs its find-mode solver search)."""
@@ -104,7 +149,7 @@ def _ref_fwd(x, w_oihw, stride, pad):
 
 class _Conv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, kernel, stride, pad, grad_out):
+    def forward(ctx, x, kernel, stride, pad, grad_out, w_ohwi=None, box=None, stats_out=None):
         C = hip()
         x = x.contiguous()
         if x.data_ptr() % 16:
@@ -115,15 +160,22 @@ class _Conv(torch.autograd.Function):
         oh, ow = (x.shape[1] + 2 * ph - kh) // sh + 1, (x.shape[2] + 2 * pw - kw) // sw + 1
         w_oihw = kernel.permute(3, 2, 0, 1)
         key = ("fwd", tuple(x.shape), tuple(kernel.shape), stride, pad)
-        w_ohwi = kernel.permute(3, 0, 1, 2).contiguous()
+        if w_ohwi is None:
+            w_ohwi = kernel.permute(3, 0, 1, 2).contiguous()
         hip_fn = lambda: C.conv_fwd(x, w_ohwi, oh, ow, sh, sw, ph, pw)  # noqa: E731
         if _pick(key, hip_fn, lambda: _ref_fwd(x, w_oihw, stride, pad)):
-            y = hip_fn()
+            if stats_out is not None:  # + the following batch norm's partial channel sums
+                y, stats_out[0] = C.conv_fwd_stats(x, w_ohwi, oh, ow, sh, sw, ph, pw)
+            else:
+                y = hip_fn()
         else:
             y = _ref_fwd(x, w_oihw, stride, pad).contiguous()
         ctx.save_for_backward(x, kernel)
         ctx.geo = (stride, pad)
         ctx.grad_out = grad_out
+        ctx.box = box
+        if box is not None:
+            box.n += 1
         return y
 
     @staticmethod
@@ -145,17 +197,28 @@ class _Conv(torch.autograd.Function):
         def ref(mask):
             return lambda: _miopen_bwd(dy_nchw, x_nchw, w_oihw, list(stride), list(pad), mask)
 
+        box = ctx.box if (ctx.box is not None and ctx.box.active and want_dx) else None
+        other = None  # the other consumer's gradient contribution, added into dx
+        first = False
+        if box is not None:
+            other, box.g = box.g, None
+            first = other is None
+            if other is not None:
+                other = other.contiguous()
+                if other.data_ptr() % 16:
+                    other = other.clone()
         if want_dx:
             kc = kernel.contiguous()
             hip_fn = None
             if stride == (1, 1):
-                hip_fn = lambda: C.conv_dgrad(dy, kc, x.shape[1], x.shape[2], pad[0], pad[1])  # noqa: E731
+                hip_fn = lambda r=None: C.conv_dgrad(dy, kc, x.shape[1], x.shape[2], pad[0], pad[1], r)  # noqa: E731
                 key = ("dgrad",) + shape_key
             elif stride == (2, 2) and (kh, kw) == (1, 1) and pad == (0, 0):
-                hip_fn = lambda: C.conv_dgrad_s2(dy, kc, x.shape[1], x.shape[2])  # noqa: E731
+                hip_fn = lambda r=None: C.conv_dgrad_s2(dy, kc, x.shape[1], x.shape[2], r)  # noqa: E731
                 key = ("dgrad_s2",) + shape_key
             if hip_fn is not None and _pick(key, hip_fn, lambda: ref([True, False, False])()[0]):
-                dx = hip_fn()
+                dx = hip_fn(other)
+                other = None
         if want_dw and x.shape[0] * dy.shape[1] * dy.shape[2] < (1 << 24):
             plan = _pick_wgrad(("wgrad",) + shape_key, C, x, dy, kh, kw, stride, pad,
                                lambda: ref([False, True, False])()[1])
@@ -171,12 +234,16 @@ class _Conv(torch.autograd.Function):
             gx, gw, _ = ref([need_dx, need_dw, False])()
             if need_dx:
                 dx = gx.permute(0, 2, 3, 1)
+        if other is not None:  # library input gradient: one add
+            dx = dx + other.view_as(dx)
+        if first:  # park this contribution for the other consumer's backward
+            box.g, dx = dx, None
             if need_dw:
                 dw = gw.permute(2, 3, 1, 0)
                 if gout is not None:
                     gout.add_(dw)
                     dw = None
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None, None, None
 
 
 def _miopen_bwd(dy_nchw, x_nchw, w_oihw, stride, pad, mask):
@@ -185,8 +252,17 @@ def _miopen_bwd(dy_nchw, x_nchw, w_oihw, stride, pad, mask):
                                                mask)
 
 
-def conv2d_nhwc(x, kernel_hwio, stride=(1, 1), pad=(0, 0), grad_out=None):
+def conv2d_nhwc(x, kernel_hwio, stride=(1, 1), pad=(0, 0), grad_out=None, w_ohwi=None, grad_box=None,
+                bn_stats=False):
     """y[N,OH,OW,K] = conv(x[N,H,W,C], kernel[KH,KW,C,K]) with symmetric zero padding ``pad = (ph, pw)``,
     bf16; the caller checked :func:`supported`.  ``grad_out``: f32 [KH,KW,C,K] tensor the weight
-    gradient is added into (a trainer's gradient slab view; ``kernel_hwio`` then needs no autograd)."""
-    return _Conv.apply(x, kernel_hwio, tuple(stride), tuple(pad), grad_out)
+    gradient is added into (a trainer's gradient slab view; ``kernel_hwio`` then needs no autograd);
+    ``w_ohwi``: the same kernel already in OHWI [K,KH,KW,C] layout (skips the per-call transpose);
+    ``grad_box``: a :class:`GradBox` shared with the other consumer of ``x``; ``bn_stats``: the
+    hand-written forward also writes the batch-norm partial channel sums of y, attached as
+    ``y._tdl_bn_part`` for the BN that consumes it (ops/batchnorm.py skips its statistics pass)."""
+    holder = [None] if bn_stats else None
+    y = _Conv.apply(x, kernel_hwio, tuple(stride), tuple(pad), grad_out, w_ohwi, grad_box, holder)
+    if holder is not None and holder[0] is not None:
+        y._tdl_bn_part = holder[0]
+    return y

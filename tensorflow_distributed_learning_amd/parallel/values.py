@@ -101,6 +101,13 @@ class Variable:
             return cv
         return None
 
+    def compute_view_ohwi(self, dtype: torch.dtype) -> Optional[torch.Tensor]:
+        """Conv kernels: the step's OHWI [K,KH,KW,C] compute-dtype copy (see :meth:`compute_view`)."""
+        tv = getattr(self.value, "_tdl_tview", None)
+        if tv is not None and tv.dtype == dtype and CAST_ACCUMULATE[0] > 0:
+            return tv
+        return None
+
     def grad_target(self) -> Optional[torch.Tensor]:
         """The f32 slab view a hand-written kernel may ADD this variable's gradient into directly
         (skipping autograd's accumulate kernel), or None.  Same conditions as the :meth:`cast`

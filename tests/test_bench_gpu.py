@@ -36,3 +36,25 @@ def test_bench_two_replicas_self_launched_shared_gpu():
     assert d["config"]["allreduce"] == "xgmi-oneshot+gloo"
     assert d["config"]["allreduce_in_graph"] is True
     assert d["config"]["replicas_identical"] is True
+
+
+def test_bench_two_replicas_under_torchrun_shared_gpu():
+    """The driver's launch form: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, PYTHONPATH=ROOT, TDL_SHARE_GPU="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "TF_CONFIG", "TDL_LAUNCHED"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "20", "--warmup", "5"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 128 and d["steps"] == 20
+    assert d["config"]["replicas_identical"] is True

@@ -187,3 +187,29 @@ def test_conv2d_layer_wgrad_and_strided_on_hip_kernels(monkeypatch):
     assert not calls, "backward fell back to MIOpen"
     torch.testing.assert_close(x.grad.float(), gx, atol=4e-2, rtol=2e-2)
     torch.testing.assert_close(kk.grad, gw, atol=2e-2 * gw.abs().max().item(), rtol=3e-2)
+
+
+@pytest.mark.parametrize("shape", [(4, 14, 14, 64, 128, 3, 3, 1, 1), (2, 9, 11, 128, 64, 1, 1, 2, 0),
+                                   (8, 28, 28, 256, 256, 1, 1, 1, 0)])
+def test_conv_fwd_bn_stats_epilogue(shape):
+    """conv_fwd_stats: same y as conv_fwd, and a batch norm fed its partial sums matches one that
+    computes its own statistics (moving stats, outputs)."""
+    from tensorflow_distributed_learning_amd.ops import hip
+
+    C = hip()
+    N, H, W, Ci, K, KH, KW, s, p = shape
+    x, k = _mk(shape, "cuda:0")
+    w = k.permute(3, 0, 1, 2).contiguous()
+    OH, OW = (H + 2 * p - KH) // s + 1, (W + 2 * p - KW) // s + 1
+    y0 = C.conv_fwd(x, w, OH, OW, s, s, p, p)
+    y1, part = C.conv_fwd_stats(x, w, OH, OW, s, s, p, p)
+    assert torch.equal(y0, y1)
+    g, b = torch.rand(K, device="cuda:0") + 0.5, torch.randn(K, device="cuda:0")
+    mm0, mv0 = torch.zeros(K, device="cuda:0"), torch.ones(K, device="cuda:0")
+    mm1, mv1 = mm0.clone(), mv0.clone()
+    ya, sa = C.bn_forward_train(y0, g, b, mm0, mv0, 0.9, 1e-3, True, None, None)
+    yb, sb = C.bn_forward_train(y1, g, b, mm1, mv1, 0.9, 1e-3, True, None, None, part)
+    torch.testing.assert_close(sb, sa, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(mm1, mm0, atol=1e-5, rtol=1e-4)
+    torch.testing.assert_close(mv1, mv0, atol=1e-5, rtol=1e-4)
+    torch.testing.assert_close(yb.float(), ya.float(), atol=2e-2, rtol=1e-2)

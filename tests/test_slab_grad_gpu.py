@@ -20,19 +20,28 @@ def _model():
     x = L.Conv2D(64, 3, padding="same")(inp)
     x = L.BatchNormalization()(x)
     x = L.Activation("relu")(x)
-    y = L.Conv2D(64, 1)(x)
+    y = L.Conv2D(64, 1)(x)  # identity block: x feeds this conv and the residual Add (grad tap)
     y = L.BatchNormalization()(y)
     x = L.Activation("relu")(L.Add()([x, y]))
-    x = L.Conv2D(128, 1, strides=2)(x)  # strided 1x1: hand-written stride-2 input gradient
-    x = L.BatchNormalization()(x)
-    x = L.Activation("relu")(x)
+    s = L.Conv2D(128, 1, strides=2)(x)  # projection block: x feeds two strided 1x1 convs (grad box)
+    s = L.BatchNormalization()(s)
+    m = L.Conv2D(128, 1, strides=2)(x)
+    m = L.BatchNormalization()(m)
+    m = L.Activation("relu")(m)
+    m = L.Conv2D(128, 3, padding="same")(m)
+    m = L.BatchNormalization()(m)
+    x = L.Activation("relu")(L.Add()([m, s]))
     x = L.GlobalAveragePooling2D()(x)
     out = L.Dense(10)(x)
     return tdl.keras.Model(inp, out)
 
 
-def _train(direct: bool, steps=2):
-    env = {"TDL_CAST_ACCUMULATE": "1" if direct else "0", "TDL_GRAPH_STEP": "0", "TDL_CONV": "hip"}
+def _train(direct: bool, steps=2, grad_sum=True, bn_stats=True):
+    env = {"TDL_CAST_ACCUMULATE": "1" if direct else "0", "TDL_GRAPH_STEP": "0", "TDL_CONV": "hip",
+           "TDL_FUSE_GRAD_SUM": "1" if grad_sum else "0"}
+    from tensorflow_distributed_learning_amd.keras import models as _models
+
+    _models._CONV_BN_STATS = bn_stats
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -50,6 +59,7 @@ def _train(direct: bool, steps=2):
         h = m.fit(ds, epochs=1, steps_per_epoch=steps, verbose=0)
         return m, h
     finally:
+        _models._CONV_BN_STATS = True
         tdl.keras.mixed_precision.set_global_policy("float32")
         for k, v in old.items():
             if v is None:
@@ -71,3 +81,45 @@ def test_direct_slab_gradients_match_autograd_accumulation():
     for v in md.weights:
         if "conv" in v.name and v.name.endswith("bias:0"):
             assert float(np.abs(v.numpy()).max()) == 0.0, v.name
+
+
+def test_fused_gradient_sums_match_autograd_adds():
+    """Tensors read by a conv and one other node: the conv's input-gradient epilogue adds the other
+    contribution (keras/fusion.py grad boxes) instead of autograd's separate add."""
+    mf, hf = _train(True, grad_sum=True)
+    boxes = mf.__dict__["_grad_boxes"]
+    assert len(boxes) == 2 and all(b.n == 2 and b.g is None for b in boxes.values())
+    mu, hu = _train(True, grad_sum=False)
+    assert not mu.__dict__["_grad_boxes"]
+    for v, a, b in zip(mf.weights, mf.get_weights(), mu.get_weights()):
+        scale = max(float(np.abs(b).max()), 1e-3)
+        np.testing.assert_allclose(a, b, atol=2e-2 * scale, rtol=2e-2, err_msg=v.name)
+    np.testing.assert_allclose(hf.history["loss"], hu.history["loss"], rtol=1e-2)
+
+
+@pytest.mark.parametrize("s2", [False, True])
+def test_conv_dgrad_residual_epilogue(s2):
+    from tensorflow_distributed_learning_amd.ops import hip
+
+    C = hip()
+    g = torch.Generator(device="cpu").manual_seed(1)
+    N, H, W, Ci, K = 4, 14, 14, 128, 256
+    k = (torch.randn(1 if s2 else 3, 1 if s2 else 3, Ci, K, generator=g) * 0.05).cuda().bfloat16()
+    OH = 7 if s2 else H
+    dy = torch.randn(N, OH, OH, K, generator=g).cuda().bfloat16()
+    r = torch.randn(N, H, W, Ci, generator=g).cuda().bfloat16()
+    if s2:
+        a, b = C.conv_dgrad_s2(dy, k, H, W), C.conv_dgrad_s2(dy, k, H, W, r)
+    else:
+        a, b = C.conv_dgrad(dy, k, H, W, 1, 1), C.conv_dgrad(dy, k, H, W, 1, 1, r)
+    assert torch.equal(b, (a.float() + r.float()).bfloat16())
+
+
+def test_conv_epilogue_bn_statistics_match_bn_pass():
+    """BN statistics from the conv forward epilogue vs the BN's own statistics pass."""
+    ma, ha = _train(True, bn_stats=True)
+    mb, hb = _train(True, bn_stats=False)
+    for v, a, b in zip(ma.weights, ma.get_weights(), mb.get_weights()):
+        scale = max(float(np.abs(b).max()), 1e-3)
+        np.testing.assert_allclose(a, b, atol=2e-2 * scale, rtol=2e-2, err_msg=v.name)
+    np.testing.assert_allclose(ha.history["loss"], hb.history["loss"], rtol=1e-2)
