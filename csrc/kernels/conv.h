@@ -58,5 +58,7 @@ void conv_wgrad_bf16(const void* x, const void* dy, float* ws, const WgradPlan& 
 
 // Tile-sweep hook: 0 = per-shape heuristic (default), 1 = 128x64, 2 = 128x128, 3 = 256x128.
 void conv_force_tile(int tile);
+// A/B hook: register prefetch depth of the implicit-GEMM main loop (1 or 2 tiles in flight)
+void conv_force_depth(int depth);
 
 }  // namespace tdl

@@ -74,7 +74,7 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return (uint16_t)(u >> 16);
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int DEPTH>
 __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
   constexpr int NT = BM * 2;         // threads: (BM / 64) x 2 waves, each 64 x BN/2
   constexpr int RP = NT / 8;         // tile rows per staging pass (8 x 16-B chunks per 128-B row)
@@ -116,13 +116,15 @@ __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
 #pragma unroll
   for (int i = 0; i < B_LD; ++i) b_base[i] = (long long)(tn * BN + (tid >> 3) + RP * i) * a.w_col + col8;
 
-  u32x4 ra[A_LD], rb[B_LD];
+  // register staging sets: DEPTH 2 keeps two tiles of global loads in flight (tile t+2 is issued
+  // while tile t computes and tile t+1's registers are written to LDS), DEPTH 1 one tile
+  u32x4 ra[2][A_LD], rb[2][B_LD];
   const int ctiles = a.C / BK;
   const int ntiles = a.KH * a.KW * ctiles;
 
   // reduction position of the next tile to load (advanced incrementally: no per-tile div/mod)
   int n_c = 0, n_kw = 0, n_kh = 0;
-  auto gload = [&](int) {
+  auto gload = [&](u32x4* pa, u32x4* pb) {
     const int c0 = n_c * BK, kw = n_kw, kh = n_kh;
     if (++n_c == ctiles) {
       n_c = 0;
@@ -136,25 +138,25 @@ __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
     for (int i = 0; i < A_LD; ++i) {
       const int ih = a_ih[i] + kh, iw = a_iw[i] + kw;
       if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
-        ra[i] = *reinterpret_cast<const u32x4*>(a.x + a_base[i] + aoff);
+        pa[i] = *reinterpret_cast<const u32x4*>(a.x + a_base[i] + aoff);
       else
-        ra[i] = u32x4{0u, 0u, 0u, 0u};
+        pa[i] = u32x4{0u, 0u, 0u, 0u};
     }
     const int wkh = a.flip ? a.KH - 1 - kh : kh, wkw = a.flip ? a.KW - 1 - kw : kw;
     const long long boff = wkh * a.w_kh + wkw * a.w_kw + c0;
 #pragma unroll
-    for (int i = 0; i < B_LD; ++i) rb[i] = *reinterpret_cast<const u32x4*>(a.w + b_base[i] + boff);
+    for (int i = 0; i < B_LD; ++i) pb[i] = *reinterpret_cast<const u32x4*>(a.w + b_base[i] + boff);
   };
   const int scol = ((tid & 7) ^ swz(tid >> 3)) * 8;  // swizzled LDS column of this thread's chunk (RP % 16 == 0)
-  auto sstore = [&](int buf) {
+  auto sstore = [&](int buf, const u32x4* pa, const u32x4* pb) {
     uint16_t* la = lds + buf * (BM + BN) * LDS_ROW;
     uint16_t* lb = la + BM * LDS_ROW;
 #pragma unroll
     for (int i = 0; i < A_LD; ++i)
-      *reinterpret_cast<u32x4*>(la + ((tid >> 3) + RP * i) * LDS_ROW + scol) = ra[i];
+      *reinterpret_cast<u32x4*>(la + ((tid >> 3) + RP * i) * LDS_ROW + scol) = pa[i];
 #pragma unroll
     for (int i = 0; i < B_LD; ++i)
-      *reinterpret_cast<u32x4*>(lb + ((tid >> 3) + RP * i) * LDS_ROW + scol) = rb[i];
+      *reinterpret_cast<u32x4*>(lb + ((tid >> 3) + RP * i) * LDS_ROW + scol) = pb[i];
   };
 
   f4v acc[4][NS];
@@ -163,14 +165,9 @@ __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
 #pragma unroll
     for (int j = 0; j < NS; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
 
-  gload(0);
-  sstore(0);
-  __syncthreads();
   const int frow = lane & 15;
   const int fk0 = (((lane >> 4)) ^ swz(frow)) * 8, fk1 = (((lane >> 4) | 4) ^ swz(frow)) * 8;  // k 0-31, 32-63
-  for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < ntiles) gload(t + 1);
+  auto compute = [&](int buf) {
     const uint16_t* la = lds + buf * (BM + BN) * LDS_ROW + (wm * 64 + frow) * LDS_ROW;
     const uint16_t* lb = lds + buf * (BM + BN) * LDS_ROW + BM * LDS_ROW + (wn * WN + frow) * LDS_ROW;
 #pragma unroll
@@ -186,8 +183,37 @@ __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
 #pragma unroll
         for (int j = 0; j < NS; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
     }
-    if (t + 1 < ntiles) sstore(buf ^ 1);
+  };
+
+  if (DEPTH == 1) {
+    gload(ra[0], rb[0]);
+    sstore(0, ra[0], rb[0]);
     __syncthreads();
+    for (int t = 0; t < ntiles; ++t) {
+      const int buf = t & 1;
+      if (t + 1 < ntiles) gload(ra[0], rb[0]);
+      compute(buf);
+      if (t + 1 < ntiles) sstore(buf ^ 1, ra[0], rb[0]);
+      __syncthreads();
+    }
+  } else {
+    gload(ra[0], rb[0]);
+    if (ntiles > 1) gload(ra[1], rb[1]);
+    sstore(0, ra[0], rb[0]);
+    __syncthreads();
+    for (int t = 0; t < ntiles; t += 2) {
+      // even tile t in LDS buffer 0; set 0 is free, set 1 holds tile t + 1
+      if (t + 2 < ntiles) gload(ra[0], rb[0]);
+      compute(0);
+      if (t + 1 < ntiles) sstore(1, ra[1], rb[1]);
+      __syncthreads();
+      if (t + 1 >= ntiles) break;
+      // odd tile t + 1 in LDS buffer 1; set 1 is free, set 0 holds tile t + 2
+      if (t + 3 < ntiles) gload(ra[1], rb[1]);
+      compute(1);
+      if (t + 2 < ntiles) sstore(0, ra[0], rb[0]);
+      __syncthreads();
+    }
   }
 
   // epilogue: bf16 tile into LDS ([BM][BN + 8]), then 16-B row segments to global
@@ -307,10 +333,15 @@ __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
   }
 }
 
+int g_depth = 2;  // register prefetch depth (tiles in flight); conv_force_depth for A/B sweeps
+
 template <int BM, int BN>
 void launch_tile(const Igemm& a, hipStream_t s) {
   const int mt = (a.M + BM - 1) / BM;
-  hipLaunchKernelGGL((k_conv_igemm<BM, BN>), dim3(mt * (a.K / BN)), dim3(BM * 2), 0, s, a);
+  if (g_depth == 1)
+    hipLaunchKernelGGL((k_conv_igemm<BM, BN, 1>), dim3(mt * (a.K / BN)), dim3(BM * 2), 0, s, a);
+  else
+    hipLaunchKernelGGL((k_conv_igemm<BM, BN, 2>), dim3(mt * (a.K / BN)), dim3(BM * 2), 0, s, a);
 }
 
 int g_forced_tile = 0;  // 0: heuristic below; 1: 128 x 64, 2: 128 x 128, 3: 256 x 128 (tile sweeps)
@@ -328,6 +359,7 @@ void launch(const Igemm& a, hipStream_t s) {
 }  // namespace
 
 void conv_force_tile(int tile) { g_forced_tile = tile; }
+void conv_force_depth(int depth) { g_depth = depth == 1 ? 1 : 2; }
 
 bool conv_bf16_supported(const ConvGeom& g) {
   return g.C % 64 == 0 && g.K % 64 == 0 && g.N > 0 && g.OH > 0 && g.OW > 0 &&

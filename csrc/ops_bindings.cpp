@@ -332,6 +332,7 @@ void register_ops(pybind11::module& m) {
         pybind11::arg("accumulate") = false, pybind11::arg("plan") = std::vector<int64_t>{});
   m.def("conv_wgrad_plans", &conv_wgrad_plans, "weight-gradient candidate plans, best first: [[wmw, wnw, chunk, nsplit]]");
   m.def("conv_force_tile", &tdl::conv_force_tile, "conv tile sweep hook (0 = heuristic)");
+  m.def("conv_force_depth", &tdl::conv_force_depth, "conv main-loop prefetch depth A/B hook (1 or 2)");
   m.def("conv_fwd", &conv_fwd, "NHWC bf16 implicit-GEMM convolution forward (MFMA)");
   m.def("conv_fwd_stats", &conv_fwd_stats, "conv forward + batch-norm partial channel sums of its output");
   m.def("conv_dgrad", &conv_dgrad, "NHWC bf16 implicit-GEMM stride-1 convolution input gradient (MFMA)",

@@ -11,8 +11,9 @@ sys.path.insert(0, ".")
 from tensorflow_distributed_learning_amd.ops import hip  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+KERAS = len(sys.argv) > 2 and sys.argv[2] == "keras"
 # (H, W, C, K, KH, stride, pad) of ResNet-50 v1.5 (C % 64 == 0 ones; the 7x7 stem stays on MIOpen)
-SHAPES = [
+SHAPES_V15 = [
     (56, 56, 64, 64, 1, 1, 0), (56, 56, 64, 64, 3, 1, 1), (56, 56, 64, 256, 1, 1, 0), (56, 56, 256, 64, 1, 1, 0),
     (56, 56, 256, 128, 1, 1, 0), (56, 56, 128, 128, 3, 2, 1), (28, 28, 128, 128, 3, 1, 1),
     (28, 28, 128, 512, 1, 1, 0), (28, 28, 512, 128, 1, 1, 0), (56, 56, 256, 512, 1, 2, 0),
@@ -20,6 +21,17 @@ SHAPES = [
     (14, 14, 1024, 256, 1, 1, 0), (14, 14, 1024, 512, 1, 1, 0), (7, 7, 512, 512, 3, 1, 1),
     (7, 7, 512, 2048, 1, 1, 0), (7, 7, 2048, 512, 1, 1, 0),
 ]
+# the Keras ResNet50 of models/resnet50.py (stride on the 1x1 convs), with the per-step call count
+SHAPES_KERAS = {
+    (56, 56, 64, 64, 1, 1, 0): 1, (56, 56, 64, 64, 3, 1, 1): 3, (56, 56, 64, 256, 1, 1, 0): 4,
+    (56, 56, 256, 64, 1, 1, 0): 2, (56, 56, 256, 128, 1, 2, 0): 1, (56, 56, 256, 512, 1, 2, 0): 1,
+    (28, 28, 128, 128, 3, 1, 1): 4, (28, 28, 128, 512, 1, 1, 0): 4, (28, 28, 512, 128, 1, 1, 0): 3,
+    (28, 28, 512, 256, 1, 2, 0): 1, (28, 28, 512, 1024, 1, 2, 0): 1, (14, 14, 256, 256, 3, 1, 1): 6,
+    (14, 14, 256, 1024, 1, 1, 0): 6, (14, 14, 1024, 256, 1, 1, 0): 5, (14, 14, 1024, 512, 1, 2, 0): 1,
+    (14, 14, 1024, 2048, 1, 2, 0): 1, (7, 7, 512, 512, 3, 1, 1): 3, (7, 7, 512, 2048, 1, 1, 0): 3,
+    (7, 7, 2048, 512, 1, 1, 0): 2,
+}
+SHAPES = list(SHAPES_KERAS) if KERAS else SHAPES_V15
 
 
 def t(fn, reps=20):
@@ -35,11 +47,12 @@ def t(fn, reps=20):
 
 
 def sweep(C, fn):
+    """Times at main-loop prefetch depth 1 and 2 (default tile heuristic)."""
     out = []
-    for tile in (1, 2, 3):
-        C.conv_force_tile(tile)
+    for d in (1, 2):
+        C.conv_force_depth(d)
         out.append(round(t(fn), 1))
-    C.conv_force_tile(0)
+    C.conv_force_depth(2)
     return out
 
 
@@ -60,9 +73,12 @@ def main():
         t_h = t(lambda: C.conv_fwd(x, w_ohwi, OH, OW, s, s, p, p))
         tiles = sweep(C, lambda: C.conv_fwd(x, w_ohwi, OH, OW, s, s, p, p))
         t_m = t(lambda: F.conv2d(xc, w_oihw, None, s, p))
-        print(json.dumps({"dir": "fwd", "shape": [B, H, W, Ci, K, KH, s, p], "rel_err": round(err, 5), "hip_us": round(t_h, 1), "tiles_us": tiles,
+        byt = 2.0 * B * (H * W * Ci + OH * OW * K)
+        floor = max(flop / 1.2e15, byt / 5e12) * 1e6
+        print(json.dumps({"dir": "fwd", "shape": [B, H, W, Ci, K, KH, s, p], "rel_err": round(err, 5), "hip_us": round(t_h, 1), "depth_us": tiles,
                           "miopen_us": round(t_m, 1), "hip_tflops": round(flop / t_h / 1e6, 1),
-                          "speedup": round(t_m / t_h, 3)}), flush=True)
+                          "speedup": round(t_m / t_h, 3), "floor_us": round(floor, 1),
+                          "calls": SHAPES_KERAS.get((H, W, Ci, K, KH, s, p), 0)}), flush=True)
         if s == 1:
             dy = torch.randn(B, OH, OW, K, device=dev).bfloat16()
             kc = k.contiguous()
@@ -75,9 +91,10 @@ def main():
             tiles = sweep(C, lambda: C.conv_dgrad(dy, kc, H, W, p, p))
             t_m = t(lambda: torch.ops.aten.convolution_backward(dyc, xc, w_oihw, None, [s, s], [p, p], [1, 1], False,
                                                                 [0, 0], 1, [True, False, False]))
-            print(json.dumps({"dir": "dgrad", "shape": [B, H, W, Ci, K, KH, s, p], "rel_err": round(err, 5), "hip_us": round(t_h, 1), "tiles_us": tiles,
+            print(json.dumps({"dir": "dgrad", "shape": [B, H, W, Ci, K, KH, s, p], "rel_err": round(err, 5), "hip_us": round(t_h, 1), "depth_us": tiles,
                               "miopen_us": round(t_m, 1), "hip_tflops": round(flop / t_h / 1e6, 1),
-                              "speedup": round(t_m / t_h, 3)}), flush=True)
+                              "speedup": round(t_m / t_h, 3), "floor_us": round(floor, 1),
+                              "calls": SHAPES_KERAS.get((H, W, Ci, K, KH, s, p), 0)}), flush=True)
 
 
 if __name__ == "__main__":
