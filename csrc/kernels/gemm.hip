@@ -1,0 +1,325 @@
+// General bf16 GEMM on the gfx950 matrix cores for Dense layers (see gemm.h).
+//
+// C[m][n] = alpha * sum_k A[m][k] B[k][n] (+ bias[n]), f32 accumulation, each operand in either
+// of its two row-major storages:
+//   T = 0 "reduction-contiguous": A[m][k] at a[m * lda + k]  /  B[k][n] at b[n * ldb + k]
+//   T = 1 "reduction-rows"      : A[m][k] at a[k * lda + m]  /  B[k][n] at b[k * ldb + n]
+// so the three products of a Dense layer need no transposed copies:
+//   forward  y  = x W       : A = x (T0), B = W[in][out] (T1)
+//   input gr dx = dy W^T    : A = dy (T0), B = W (T0: column n of B is row n of W)
+//   weight gr dW = x^T dy   : A = x (T1), B = dy (T1)
+// Tiles are staged into LDS exactly as they arrive (16-B chunks).  T0 tiles are [rows][64 k]
+// 128-B rows with the chunk XOR swizzle of the conv kernels (fragments by ds_read_b128); T1 tiles
+// are [64 k][64 cols] sub-images with the swizzle of the weight-gradient kernel (fragments by two
+// ds_read_b64_tr_b16 transposed reads).  Workgroup tile 128 (m) x 128 (n) x 64 (k), 4 waves as
+// 2 x 2, each 64 x 64 of v_mfma_f32_16x16x32_bf16 with B as the first operand, so a lane holds 4
+// consecutive n of one m (16-B f32 / 8-B bf16 stores).  Edges are zero-filled on load and masked
+// on store (M, N, K multiples of 8 for the 16-B loads; N multiple of 4 for the stores).
+#include "kernels/gemm.h"
+
+#include <algorithm>
+
+namespace tdl {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int TM = 128, TN = 128, BK = 64;
+constexpr int OP = TM * BK;  // bf16 elements of one operand tile (16 KiB)
+
+__device__ __forceinline__ int swz0(int r) { return (r >> 1) & 7; }                                  // T0 rows
+__device__ __forceinline__ int swz1(int r) { return (((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2); }  // T1 rows
+
+struct Gemm {
+  const uint16_t* a;
+  const uint16_t* b;
+  long long lda, ldb;
+  int M, N, K;
+  float* c32;        // f32 output (c16 == nullptr)
+  uint16_t* c16;     // bf16 output
+  long long ldc;
+  const float* bias;  // [N] or nullptr
+  float alpha;
+  int accumulate;  // f32 output: C += result
+};
+
+// One operand tile (rows x 64 k) into registers: 4 chunks of 16 B per thread.
+//   T0: row r = (tid >> 3) + 32 i, chunk tid & 7   -> src[(row0 + r) * ld + k0 + 8 chunk]
+//   T1: sub-image i >> 1 (64 columns each), k row (tid >> 3) + 32 (i & 1), chunk tid & 7
+//       -> src[(k0 + krow) * ld + row0 + 64 sub + 8 chunk]
+template <int T>
+__device__ __forceinline__ void load_tile(const uint16_t* src, long long ld, int rows, int K, int row0, int k0,
+                                          int tid, u32x4 (&r)[4]) {
+  const int ch = tid & 7;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    bool ok;
+    long long off;
+    if (T == 0) {
+      const int row = row0 + (tid >> 3) + 32 * i, k = k0 + ch * 8;
+      ok = row < rows && k < K;
+      off = (long long)row * ld + k;
+    } else {
+      const int krow = k0 + (tid >> 3) + 32 * (i & 1), col = row0 + 64 * (i >> 1) + ch * 8;
+      ok = krow < K && col < rows;
+      off = (long long)krow * ld + col;
+    }
+    r[i] = ok ? *reinterpret_cast<const u32x4*>(src + off) : u32x4{0u, 0u, 0u, 0u};
+  }
+}
+
+template <int T>
+__device__ __forceinline__ void store_tile(uint16_t* lds, int tid, const u32x4 (&r)[4]) {
+  const int ch = tid & 7;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (T == 0) {
+      const int row = (tid >> 3) + 32 * i;
+      *reinterpret_cast<u32x4*>(lds + row * BK + ((ch ^ swz0(row)) << 3)) = r[i];
+    } else {
+      const int krow = (tid >> 3) + 32 * (i & 1);
+      *reinterpret_cast<u32x4*>(lds + (i >> 1) * (BK * 64) + krow * 64 + ((ch ^ swz1(krow)) << 3)) = r[i];
+    }
+  }
+}
+
+// 16 x 32 fragment of rows [r0, r0 + 16) at k offset kk (0 or 32): lane l gets row r0 + (l & 15),
+// k = kk + 8 (l >> 4) .. + 7
+template <int T>
+__device__ __forceinline__ bf16x8 frag(const uint16_t* lds, int r0, int kk, int lane) {
+  if (T == 0) {
+    const int row = r0 + (lane & 15);
+    const int ch = (kk >> 3) + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(lds + row * BK + ((ch ^ swz0(row)) << 3));
+  } else {
+    // transposed read: group g = lane >> 4 covers k rows kk + 8g .. + 7 (two reads of 4 rows);
+    // lane 4q + p of the group addresses k row + q, columns col0 + 4p .. + 3
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int sub = r0 >> 6, col0 = r0 & 63;
+    const int krow = kk + 8 * g + q;
+    const uint16_t* base = lds + sub * (BK * 64);
+    const int off = krow * 64 + ((((col0 >> 3) + (p >> 1)) ^ swz1(krow)) << 3) + (p & 1) * 4;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + off));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + off + 4 * 64));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  }
+}
+
+template <int TA, int TB>
+__global__ __launch_bounds__(256, 2) void k_gemm_bf16(Gemm g) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * OP];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ntn = (g.N + TN - 1) / TN;
+  const int tm = blockIdx.x / ntn, tn = blockIdx.x % ntn;
+  const int m0 = tm * TM, n0 = tn * TN;
+  const int nk = (g.K + BK - 1) / BK;
+
+  u32x4 ra[4], rb[4];
+  f4v acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  load_tile<TA>(g.a, g.lda, g.M, g.K, m0, 0, tid, ra);
+  load_tile<TB>(g.b, g.ldb, g.N, g.K, n0, 0, tid, rb);
+  store_tile<TA>(lds, tid, ra);
+  store_tile<TB>(lds + OP, tid, rb);
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < nk) {
+      load_tile<TA>(g.a, g.lda, g.M, g.K, m0, (t + 1) * BK, tid, ra);
+      load_tile<TB>(g.b, g.ldb, g.N, g.K, n0, (t + 1) * BK, tid, rb);
+    }
+    const uint16_t* la = lds + buf * 2 * OP;
+    const uint16_t* lb = la + OP;
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      bf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = frag<TA>(la, wm * 64 + 16 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = frag<TB>(lb, wn * 64 + 16 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+    if (t + 1 < nk) {
+      store_tile<TA>(lds + (buf ^ 1) * 2 * OP, tid, ra);
+      store_tile<TB>(lds + (buf ^ 1) * 2 * OP + OP, tid, rb);
+    }
+    __syncthreads();
+  }
+
+  // lane holds n = n0 + wn*64 + 16 j + 4 (lane >> 4) .. + 3 of row m = m0 + wm*64 + 16 i + (lane & 15)
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = m0 + wm * 64 + 16 * i + (lane & 15);
+      const int n = n0 + wn * 64 + 16 * j + 4 * (lane >> 4);
+      if (m >= g.M || n >= g.N) continue;
+      f4v v = acc[i][j] * g.alpha;
+      if (g.bias) v += *reinterpret_cast<const f4v*>(g.bias + n);
+      const long long o = (long long)m * g.ldc + n;
+      if (g.c16) {
+        uint32_t u[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          u[e] = __float_as_uint(v[e]);
+          u[e] += 0x7fffu + ((u[e] >> 16) & 1u);
+        }
+        *reinterpret_cast<uint2*>(g.c16 + o) =
+            make_uint2((u[0] >> 16) | (u[1] & 0xffff0000u), (u[2] >> 16) | (u[3] & 0xffff0000u));
+      } else {
+        f4v* p = reinterpret_cast<f4v*>(g.c32 + o);
+        *p = g.accumulate ? *p + v : v;
+      }
+    }
+}
+
+}  // namespace
+
+bool gemm_bf16_supported(int M, int N, int K) { return M > 0 && N > 0 && K > 0 && M % 8 == 0 && N % 8 == 0 && K % 8 == 0; }
+
+void gemm_bf16(int ta, int tb, const void* a, long long lda, const void* b, long long ldb, int M, int N, int K,
+               float* c32, void* c16, long long ldc, const float* bias, float alpha, bool accumulate, hipStream_t s) {
+  Gemm g{static_cast<const uint16_t*>(a), static_cast<const uint16_t*>(b), lda, ldb, M, N, K, c32,
+         static_cast<uint16_t*>(c16), ldc, bias, alpha, accumulate ? 1 : 0};
+  const dim3 grid(((M + TM - 1) / TM) * ((N + TN - 1) / TN)), blk(256);
+  const int t = ta * 2 + tb;
+  if (t == 0)
+    hipLaunchKernelGGL((k_gemm_bf16<0, 0>), grid, blk, 0, s, g);
+  else if (t == 1)
+    hipLaunchKernelGGL((k_gemm_bf16<0, 1>), grid, blk, 0, s, g);
+  else if (t == 2)
+    hipLaunchKernelGGL((k_gemm_bf16<1, 0>), grid, blk, 0, s, g);
+  else
+    hipLaunchKernelGGL((k_gemm_bf16<1, 1>), grid, blk, 0, s, g);
+}
+
+namespace {
+
+// one thread per 8 channels of one image: HW 16-B loads, f32 sums
+__global__ __launch_bounds__(256) void k_gap_fwd(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int N,
+                                                int HW, int C) {
+  const int G = C >> 3;
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (long long)N * G) return;
+  const int n = (int)(t / G), cg = (int)(t % G);
+  const uint16_t* p = x + (long long)n * HW * C + cg * 8;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 7
+  for (int i = 0; i < HW; ++i) {
+    const u32x4 v = *reinterpret_cast<const u32x4*>(p + (long long)i * C);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s[2 * j] += __uint_as_float(v[j] << 16);
+      s[2 * j + 1] += __uint_as_float(v[j] & 0xffff0000u);
+    }
+  }
+  const float inv = 1.f / (float)HW;
+  uint32_t o[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    uint32_t lo = __float_as_uint(s[2 * j] * inv), hi = __float_as_uint(s[2 * j + 1] * inv);
+    lo += 0x7fffu + ((lo >> 16) & 1u);
+    hi += 0x7fffu + ((hi >> 16) & 1u);
+    o[j] = (lo >> 16) | (hi & 0xffff0000u);
+  }
+  *reinterpret_cast<u32x4*>(y + (long long)n * C + cg * 8) = u32x4{o[0], o[1], o[2], o[3]};
+}
+
+// dx[n][p][c] = dy[n][c] / HW: one 16-B store per thread per pixel
+__global__ __launch_bounds__(256) void k_gap_bwd(const uint16_t* __restrict__ dy, uint16_t* __restrict__ dx, int N,
+                                                int HW, int C) {
+  const int G = C >> 3;
+  const long long total = (long long)N * HW * G;
+  const float inv = 1.f / (float)HW;
+  for (long long t = (long long)blockIdx.x * 256 + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const int cg = (int)(t % G);
+    const long long np = t / G;
+    const int n = (int)(np / HW);
+    const u32x4 v = *reinterpret_cast<const u32x4*>(dy + (long long)n * C + cg * 8);
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint32_t lo = __float_as_uint(__uint_as_float(v[j] << 16) * inv);
+      uint32_t hi = __float_as_uint(__uint_as_float(v[j] & 0xffff0000u) * inv);
+      lo += 0x7fffu + ((lo >> 16) & 1u);
+      hi += 0x7fffu + ((hi >> 16) & 1u);
+      o[j] = (lo >> 16) | (hi & 0xffff0000u);
+    }
+    *reinterpret_cast<u32x4*>(dx + np * C + cg * 8) = u32x4{o[0], o[1], o[2], o[3]};
+  }
+}
+
+}  // namespace
+
+void gap_fwd_bf16(const void* x, void* y, int N, int HW, int C, hipStream_t s) {
+  const long long threads = (long long)N * (C / 8);
+  hipLaunchKernelGGL(k_gap_fwd, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
+                     static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), N, HW, C);
+}
+
+void gap_bwd_bf16(const void* dy, void* dx, int N, int HW, int C, hipStream_t s) {
+  const long long total = (long long)N * HW * (C / 8);
+  const long long blocks = std::min<long long>((total + 255) / 256, 256 * 16);
+  hipLaunchKernelGGL(k_gap_bwd, dim3((unsigned)blocks), dim3(256), 0, s, static_cast<const uint16_t*>(dy),
+                     static_cast<uint16_t*>(dx), N, HW, C);
+}
+
+namespace {
+
+// one wave per row: logsumexp over K logits (f32), loss = lse - z[label]; optional backward
+// dz = (softmax - onehot) * g[row] written as f32 (mode 1)
+__global__ __launch_bounds__(256) void k_softmax_xent(const float* __restrict__ z, const long long* __restrict__ lab,
+                                                      int N, int K, float* __restrict__ loss,
+                                                      float* __restrict__ lse_out, const float* __restrict__ g,
+                                                      float* __restrict__ dz) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= N) return;
+  const float* zr = z + (long long)row * K;
+  float mx = -INFINITY;
+  for (int k = lane; k < K; k += 64) mx = fmaxf(mx, zr[k]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  float se = 0.f;
+  for (int k = lane; k < K; k += 64) se += __expf(zr[k] - mx);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) se += __shfl_xor(se, o);
+  const float lse = mx + __logf(se);
+  const long long y = lab[row];
+  if (dz == nullptr) {
+    if (lane == 0) {
+      loss[row] = (y >= 0 && y < K) ? lse - zr[y] : 0.f;
+      lse_out[row] = lse;
+    }
+    return;
+  }
+  const float gr = g[row];
+  float* dr = dz + (long long)row * K;
+  for (int k = lane; k < K; k += 64) dr[k] = (__expf(zr[k] - lse) - (k == y ? 1.f : 0.f)) * gr;
+}
+
+}  // namespace
+
+void softmax_xent_fwd(const float* z, const long long* labels, int N, int K, float* loss, float* lse, hipStream_t s) {
+  hipLaunchKernelGGL(k_softmax_xent, dim3((N + 3) / 4), dim3(256), 0, s, z, labels, N, K, loss, lse, nullptr,
+                     nullptr);
+}
+
+void softmax_xent_bwd(const float* z, const long long* labels, int N, int K, const float* g, float* dz,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(k_softmax_xent, dim3((N + 3) / 4), dim3(256), 0, s, z, labels, N, K, nullptr, nullptr, g, dz);
+}
+
+}  // namespace tdl

@@ -21,4 +21,7 @@ void gather_i32(const int* src, const int* idx, int* out, int64_t rows, hipStrea
 void slab_transpose_bf16(const float* src, uint16_t* dst, const int* entries, const int* tiles, int ntiles,
                          hipStream_t s);
 
+// dst = bf16(src) (round to nearest even), n % 8 == 0 (the trainer's whole-slab compute copy)
+void cast_bf16(const float* src, uint16_t* dst, long long n, hipStream_t s);
+
 }  // namespace tdl

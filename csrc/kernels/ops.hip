@@ -3,6 +3,8 @@
 #include "common.h"
 #include "ops.h"
 
+#include <algorithm>
+
 namespace tdl {
 
 __global__ __launch_bounds__(256) void k_gather_rows_f32(const float* __restrict__ src, const int* __restrict__ idx,
@@ -91,6 +93,37 @@ void slab_transpose_bf16(const float* src, uint16_t* dst, const int* entries, co
   if (ntiles <= 0) return;
   hipLaunchKernelGGL(k_slab_transpose_bf16, dim3(ntiles), dim3(256), 0, s, src, dst,
                      reinterpret_cast<const int4*>(entries), reinterpret_cast<const int4*>(tiles));
+}
+
+namespace {
+
+// dst[i] = bf16(src[i]), 8 elements (two 16-B loads, one 16-B store) per thread per iteration
+__global__ __launch_bounds__(256) void k_cast_bf16(const float* __restrict__ src, uint16_t* __restrict__ dst,
+                                                  long long n8) {
+  const long long stride = (long long)gridDim.x * 256;
+  for (long long v = (long long)blockIdx.x * 256 + threadIdx.x; v < n8; v += stride) {
+    const f4 a = reinterpret_cast<const f4*>(src)[2 * v], b = reinterpret_cast<const f4*>(src)[2 * v + 1];
+    const float f[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint32_t lo = __float_as_uint(f[2 * j]), hi = __float_as_uint(f[2 * j + 1]);
+      lo += 0x7fffu + ((lo >> 16) & 1u);
+      hi += 0x7fffu + ((hi >> 16) & 1u);
+      o[j] = (lo >> 16) | (hi & 0xffff0000u);
+    }
+    reinterpret_cast<uint4*>(dst)[v] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+}  // namespace
+
+void cast_bf16(const float* src, uint16_t* dst, long long n, hipStream_t s) {
+  const long long n8 = n / 8;
+  if (n8 > 0) {
+    const long long blocks = std::min<long long>((n8 + 255) / 256, 256 * 8);
+    hipLaunchKernelGGL(k_cast_bf16, dim3((unsigned)blocks), dim3(256), 0, s, src, dst, n8);
+  }
 }
 
 }  // namespace tdl

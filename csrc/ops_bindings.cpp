@@ -4,6 +4,7 @@
 
 #include "kernels/bn.h"
 #include "kernels/conv.h"
+#include "kernels/gemm.h"
 #include "kernels/ops.h"
 #include "kernels/pool.h"
 
@@ -318,9 +319,102 @@ void slab_transpose_bf16(at::Tensor src, at::Tensor dst, at::Tensor entries, at:
   tdl::slab_transpose_bf16(src.data_ptr<float>(), reinterpret_cast<uint16_t*>(dst.data_ptr()),
                            entries.data_ptr<int>(), tiles.data_ptr<int>(), (int)tiles.size(0), cur_stream());
 }
+void slab_cast_bf16(at::Tensor src, at::Tensor dst) {
+  TORCH_CHECK(src.is_cuda() && src.is_contiguous() && src.scalar_type() == at::kFloat, "slab_cast: f32 src");
+  TORCH_CHECK(dst.is_cuda() && dst.is_contiguous() && dst.scalar_type() == at::kBFloat16, "slab_cast: bf16 dst");
+  TORCH_CHECK(src.numel() == dst.numel() && src.numel() % 8 == 0, "slab_cast: sizes (multiple of 8)");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(dst.data_ptr()) % 16 == 0,
+              "slab_cast: 16-byte aligned buffers");
+  tdl::cast_bf16(src.data_ptr<float>(), reinterpret_cast<uint16_t*>(dst.data_ptr()), src.numel(), cur_stream());
+}
+void bf16_check(const at::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 2 && t.stride(1) == 1, what,
+              " must be a 2-D row-major bf16 GPU tensor");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0 && t.stride(0) % 8 == 0, what,
+              " must be 16-byte aligned (rows too)");
+}
+
+// C = alpha * op(A) op(B) (+ bias), see kernels/gemm.h; A/B given in their STORED [rows][cols] form:
+// ta = 0: a is [M][K], ta = 1: a is [K][M]; tb = 0: b is [N][K], tb = 1: b is [K][N].
+// out: f32 [M][N] (+= when accumulate) or None -> a new bf16 [M][N]
+at::Tensor gemm_bf16(at::Tensor a, int64_t ta, at::Tensor b, int64_t tb, c10::optional<at::Tensor> bias,
+                     c10::optional<at::Tensor> out, bool accumulate, double alpha) {
+  bf16_check(a, "gemm: a");
+  bf16_check(b, "gemm: b");
+  const int64_t M = ta ? a.size(1) : a.size(0), K = ta ? a.size(0) : a.size(1);
+  const int64_t N = tb ? b.size(1) : b.size(0), Kb = tb ? b.size(0) : b.size(1);
+  TORCH_CHECK(K == Kb, "gemm: inner dimensions differ");
+  TORCH_CHECK(tdl::gemm_bf16_supported((int)M, (int)N, (int)K), "gemm: M, N, K must be multiples of 8");
+  const float* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == at::kFloat && bias->is_contiguous() && bias->numel() == N &&
+                    reinterpret_cast<uintptr_t>(bias->data_ptr()) % 16 == 0,
+                "gemm: bias must be a 16-byte aligned contiguous f32 [N]");
+    bp = bias->data_ptr<float>();
+  }
+  if (out.has_value() && out->defined()) {
+    auto& o = *out;
+    TORCH_CHECK(o.is_cuda() && o.scalar_type() == at::kFloat && o.dim() == 2 && o.size(0) == M && o.size(1) == N &&
+                    o.stride(1) == 1 && o.stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(o.data_ptr()) % 16 == 0,
+                "gemm: out must be a 16-byte aligned row-major f32 [M][N]");
+    tdl::gemm_bf16((int)ta, (int)tb, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), (int)M, (int)N, (int)K,
+                   o.data_ptr<float>(), nullptr, o.stride(0), bp, (float)alpha, accumulate, cur_stream());
+    return o;
+  }
+  auto c = at::empty({M, N}, a.options());
+  tdl::gemm_bf16((int)ta, (int)tb, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), (int)M, (int)N, (int)K,
+                 nullptr, c.data_ptr(), N, bp, (float)alpha, false, cur_stream());
+  return c;
+}
+
+at::Tensor gap_fwd(at::Tensor x) {
+  conv_check(x, "gap: x");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "gap: NHWC with C % 8 == 0");
+  auto y = at::empty({x.size(0), x.size(3)}, x.options());
+  tdl::gap_fwd_bf16(x.data_ptr(), y.data_ptr(), (int)x.size(0), (int)(x.size(1) * x.size(2)), (int)x.size(3),
+                    cur_stream());
+  return y;
+}
+
+at::Tensor gap_bwd(at::Tensor dy, int64_t h, int64_t w) {
+  conv_check(dy, "gap: dy");
+  TORCH_CHECK(dy.dim() == 2 && dy.size(1) % 8 == 0, "gap: dy [N][C], C % 8 == 0");
+  auto dx = at::empty({dy.size(0), h, w, dy.size(1)}, dy.options());
+  tdl::gap_bwd_bf16(dy.data_ptr(), dx.data_ptr(), (int)dy.size(0), (int)(h * w), (int)dy.size(1), cur_stream());
+  return dx;
+}
+std::vector<at::Tensor> xent_fwd(at::Tensor z, at::Tensor labels) {
+  TORCH_CHECK(z.is_cuda() && z.is_contiguous() && z.scalar_type() == at::kFloat && z.dim() == 2, "xent: f32 [N][K] logits");
+  TORCH_CHECK(labels.is_cuda() && labels.is_contiguous() && labels.scalar_type() == at::kLong &&
+                  labels.numel() == z.size(0), "xent: int64 [N] labels");
+  auto loss = at::empty({z.size(0)}, z.options());
+  auto lse = at::empty({z.size(0)}, z.options());
+  tdl::softmax_xent_fwd(z.data_ptr<float>(), reinterpret_cast<const long long*>(labels.data_ptr<int64_t>()), (int)z.size(0), (int)z.size(1),
+                        loss.data_ptr<float>(), lse.data_ptr<float>(), cur_stream());
+  return {loss, lse};
+}
+
+at::Tensor xent_bwd(at::Tensor z, at::Tensor labels, at::Tensor g) {
+  TORCH_CHECK(z.is_cuda() && z.is_contiguous() && z.scalar_type() == at::kFloat && z.dim() == 2, "xent: f32 [N][K] logits");
+  TORCH_CHECK(labels.is_contiguous() && labels.scalar_type() == at::kLong && labels.numel() == z.size(0), "xent: labels");
+  TORCH_CHECK(g.is_cuda() && g.is_contiguous() && g.scalar_type() == at::kFloat && g.numel() == z.size(0), "xent: g");
+  auto dz = at::empty_like(z);
+  tdl::softmax_xent_bwd(z.data_ptr<float>(), reinterpret_cast<const long long*>(labels.data_ptr<int64_t>()), (int)z.size(0), (int)z.size(1),
+                        g.data_ptr<float>(), dz.data_ptr<float>(), cur_stream());
+  return dz;
+}
 }  // namespace
 
 void register_ops(pybind11::module& m) {
+  m.def("xent_fwd", &xent_fwd, "sparse softmax cross-entropy forward: (loss, logsumexp)");
+  m.def("xent_bwd", &xent_bwd, "sparse softmax cross-entropy backward: (softmax - onehot) * g");
+  m.def("gemm_bf16", &gemm_bf16, "bf16 MFMA GEMM with either storage per operand (Dense fwd / dgrad / wgrad)",
+        pybind11::arg("a"), pybind11::arg("ta"), pybind11::arg("b"), pybind11::arg("tb"),
+        pybind11::arg("bias") = pybind11::none(), pybind11::arg("out") = pybind11::none(),
+        pybind11::arg("accumulate") = false, pybind11::arg("alpha") = 1.0);
+  m.def("gap_fwd", &gap_fwd, "NHWC bf16 global average pooling");
+  m.def("gap_bwd", &gap_bwd, "NHWC bf16 global average pooling backward");
+  m.def("slab_cast_bf16", &slab_cast_bf16, "f32 -> bf16 copy of a whole weight slab (one launch)");
   m.def("bn_set_tuning", &tdl::bn_set_tuning, "BN kernel sweep hooks (max_parts, elem_blocks, elem_unroll; 0 = keep)");
   m.def("slab_transpose_bf16", &slab_transpose_bf16, "HWIO f32 conv kernels -> OHWI bf16, all in one launch");
   m.def("conv_dgrad_s2", &conv_dgrad_s2, "NHWC bf16 1x1 stride-2 convolution input gradient (MFMA)",

@@ -309,10 +309,10 @@ class GenericTrainer:
         from ..parallel import values as V
 
         if self._Wc is not None:
-            self._Wc.copy_(self.W)  # the step's bf16 weights, one kernel
-            if self._Wt is not False:
-                from ..ops import hip
+            from ..ops import hip
 
+            hip().slab_cast_bf16(self.W, self._Wc)  # the step's bf16 weights, one kernel
+            if self._Wt is not False:
                 hip().slab_transpose_bf16(self.W, self._Wt, *self._wt_tables)  # OHWI conv rows, one kernel
         V.CAST_ACCUMULATE[0] += 1  # Variable.cast may add straight into the slab only in here
         try:

@@ -20,6 +20,7 @@ import torch.nn.functional as F
 
 from ..parallel.values import Variable, VariableAggregation, VariableSynchronization, create_variable
 from ..ops import conv as _conv
+from ..ops import dense as _dense
 from . import activations as _act
 from . import initializers as _init
 
@@ -253,6 +254,18 @@ class Dense(Layer):
         self.built = True
 
     def call(self, x, training=None):
+        if _dense.dense_supported(x, self.units):
+            # bf16 on the GPU: hand-written MFMA GEMMs (ops/dense.py), gradients straight into the
+            # trainer's slab when it is bound
+            gw = self.kernel.grad_target()
+            gb = self.bias.grad_target() if self.bias is not None else None
+            if gw is not None and (self.bias is None or gb is not None):
+                w = self.kernel.compute_view(x.dtype)
+                w = w if w is not None else self.kernel.value.detach().to(x.dtype)
+                b = self.bias.value.detach() if self.bias is not None else None
+                return self.activation(_dense.dense_bf16(x, w, b, (gw, gb)))
+            b = self.bias.value if self.bias is not None else None
+            return self.activation(_dense.dense_bf16(x, self.kernel.cast(x.dtype), b))
         y = torch.matmul(x, self.kernel.cast(x.dtype))
         if self.bias is not None:
             y = y + self.bias.value.to(y.dtype)
@@ -447,6 +460,8 @@ class GlobalAveragePooling2D(Layer):
         self.keepdims = keepdims
 
     def call(self, x, training=None):
+        if not self.keepdims and type(self) is GlobalAveragePooling2D and _dense.gap_supported(x):
+            return _dense.gap_nhwc(x)  # hand-written NHWC kernel (ops/dense.py)
         return x.mean(dim=(1, 2), keepdim=self.keepdims)
 
     def compute_output_shape(self, s):

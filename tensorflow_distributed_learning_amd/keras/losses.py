@@ -61,6 +61,11 @@ class SparseCategoricalCrossentropy(Loss):
         if logits.dim() > 2:
             logits = logits.reshape(-1, logits.shape[-1])
             y = y.reshape(-1)
+        if self.from_logits and self.ignore_class is None:
+            from ..ops import dense as _dense
+
+            if _dense.xent_supported(logits, y):
+                return _dense.softmax_xent(logits, y)  # hand-written kernel (csrc/kernels/gemm.hip)
         l = F.cross_entropy(logits, y, reduction="none")
         if self.ignore_class is not None:
             l = l * (y != self.ignore_class)
