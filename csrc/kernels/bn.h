@@ -39,6 +39,7 @@ void bn_apply(const void* x, const void* residual, void* y, BnDType dt, int64_t 
 //   mode 2: dz = dy * (y > 0), written to dz (BN + Add + ReLU: dz is also the residual's gradient)
 void bn_backward(const void* dy, const void* x, const void* y, void* dz, void* dx, BnDType dt, int64_t M, int C,
                  float* part, const float* gamma, const float* mean, const float* invstd, const float* scale,
-                 const float* shift, float* dgamma, float* dbeta, float* coef, int mode, int acc, hipStream_t s);
+                 const float* shift, float* dgamma, float* dbeta, float* coef, int mode, int acc, hipStream_t s,
+                 int given_parts = 0);  // > 0: dy is the masked dz and part holds its reduction
 
 }  // namespace tdl

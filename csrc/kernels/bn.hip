@@ -423,9 +423,20 @@ template <BnDType D>
 static void bn_backward_t(const void* dy, const void* x, const void* y, void* dz, void* dx, int64_t M, int C,
                           float* part, const float* gamma, const float* mean, const float* invstd, const float* scale,
                           const float* shift, float* dgamma, float* dbeta, float* coef, int mode, int acc,
-                          hipStream_t s) {
+                          hipStream_t s, int given_parts) {
   const BnPlan p = bn_plan(M, C);
   const dim3 gp(p.parts), blk(256);
+  if (given_parts > 0) {
+    // dy is already the group's dz and `part` its reduction (the producing conv's epilogue)
+    int P = given_parts;
+    const float* pr = prereduce(part, P, C, s);
+    hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), dim3(64 * kFinPhases), 0, s, pr, P, M, C, gamma, mean,
+                       invstd, dgamma, dbeta, coef, acc);
+    const int64_t n8 = M * C / 8;
+    hipLaunchKernelGGL((k_bn_dx<D, false, 1>), dim3(elementwise_grid(n8)), blk, 0, s, dy, x, dx, n8, C, coef, nullptr,
+                       nullptr);
+    return;
+  }
   if (mode == 0)
     hipLaunchKernelGGL((k_bn_partial<D, 1>), gp, blk, 0, s, dy, x, nullptr, nullptr, nullptr, nullptr, M, C, p.rows_wg,
                        part);
@@ -458,13 +469,14 @@ static void bn_backward_t(const void* dy, const void* x, const void* y, void* dz
 
 void bn_backward(const void* dy, const void* x, const void* y, void* dz, void* dx, BnDType dt, int64_t M, int C,
                  float* part, const float* gamma, const float* mean, const float* invstd, const float* scale,
-                 const float* shift, float* dgamma, float* dbeta, float* coef, int mode, int acc, hipStream_t s) {
+                 const float* shift, float* dgamma, float* dbeta, float* coef, int mode, int acc, hipStream_t s,
+                 int given_parts) {
   if (dt == BnDType::kBF16)
     bn_backward_t<BnDType::kBF16>(dy, x, y, dz, dx, M, C, part, gamma, mean, invstd, scale, shift, dgamma, dbeta,
-                                   coef, mode, acc, s);
+                                   coef, mode, acc, s, given_parts);
   else
     bn_backward_t<BnDType::kF32>(dy, x, y, dz, dx, M, C, part, gamma, mean, invstd, scale, shift, dgamma, dbeta, coef,
-                                  mode, acc, s);
+                                  mode, acc, s, given_parts);
 }
 
 }  // namespace tdl

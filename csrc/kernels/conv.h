@@ -32,8 +32,14 @@ int conv_fwd_row_tile(const ConvGeom& g);
 // Keras layout: for a fixed (kh, kw, c) the K reduction values are contiguous)
 // residual (optional, shaped like dx): added in the epilogue, dx = dgrad + residual (the other
 // gradient contribution of a tensor with two consumers; saves a separate add pass)
+// bn_part (with bn_y, bn_x: tensors shaped like dx): fused backward of a BN -> Add -> ReLU group
+// whose output is this conv's input bn_y and whose BN input is bn_x: dx := (dgrad + residual) *
+// [bn_y > 0] (the group's dz) and bn_part[ceil(M / conv_dgrad_row_tile)][2][C] := per-tile channel
+// sums of dz and dz * bn_x (bn_backward(part=...) then skips its reduction pass)
 void conv_dgrad_bf16(const void* dy, const void* w_hwio, void* dx, const ConvGeom& g, hipStream_t s,
-                     const void* residual = nullptr);
+                     const void* residual = nullptr, const void* bn_y = nullptr, const void* bn_x = nullptr,
+                     float* bn_part = nullptr);
+int conv_dgrad_row_tile(const ConvGeom& g);
 
 // Input gradient of a 1x1, stride-2, unpadded convolution (the strided shortcut / first 1x1 of a
 // ResNet-50 stage): dx[n][2i][2j] = dy[n][i][j] . w^T, the other three pixels of every 2x2 block are

@@ -51,7 +51,25 @@ struct Igemm {
   const uint16_t* res;  // optional bf16 tensor shaped like y, added in the epilogue (gradient sums)
   float* stats;         // optional [M / BM row tiles][2][K]: per-tile channel sums of y and y^2 (the
                         // batch-norm statistics of the conv output, from the stored bf16 values)
+  // optional batch-norm backward fusion (input gradient of a conv whose input is the output
+  // relu(bn(x) + r) of a BN -> Add -> ReLU group): the stored gradient is dz = (dgrad + res) * [yb > 0]
+  // and bn_part [row tiles][2][K] gets the per-tile channel sums of dz and dz * xb
+  const uint16_t* bn_y;  // the conv's input (the group output), for the ReLU mask
+  const uint16_t* bn_x;  // the group's BN input
+  float* bn_part;
 };
+
+// v * [y > 0] for 8 packed bf16 (y > 0: sign clear and not +0)
+__device__ __forceinline__ u32x4 relu_mask_bf16x8(u32x4 v, u32x4 y) {
+  u32x4 o;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t lo = ((y[i] & 0x8000u) == 0u && (y[i] & 0x7fffu) != 0u) ? 0x0000ffffu : 0u;
+    const uint32_t hi = ((y[i] & 0x80000000u) == 0u && (y[i] & 0x7fff0000u) != 0u) ? 0xffff0000u : 0u;
+    o[i] = v[i] & (lo | hi);
+  }
+  return o;
+}
 
 // a + b for 8 packed bf16 values (f32 add, round to nearest even)
 __device__ __forceinline__ u32x4 add_bf16x8(u32x4 a, u32x4 b) {
@@ -243,9 +261,21 @@ __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
       *reinterpret_cast<uint2*>(lds + (wm * 64 + i * 16 + (lane & 15)) * OUT_LD + wn * WN + j * 16 + (lane >> 4) * 4) =
           make_uint2(lo, hi);
     }
+  // BN-backward fusion operands (the accumulators are dead now: registers to spare)
+  u32x4 ry[EPI], rx[EPI];
+  if (a.bn_part && !a.scatter) {
+#pragma unroll
+    for (int e = 0; e < EPI; ++e) {
+      const int s = tid + e * NT, row = s / SEG, seg = s % SEG, m = tm * BM + row;
+      const long long o = (long long)m * a.K + tn * BN + seg * 8;
+      ry[e] = m < a.M ? *reinterpret_cast<const u32x4*>(a.bn_y + o) : u32x4{0u, 0u, 0u, 0u};
+      rx[e] = m < a.M ? *reinterpret_cast<const u32x4*>(a.bn_x + o) : u32x4{0u, 0u, 0u, 0u};
+    }
+  }
   __syncthreads();
   if (!a.scatter) {
     static_assert(NT % SEG == 0, "a thread keeps one 8-channel segment across its rows");
+    float* sums = a.stats ? a.stats : a.bn_part;  // per-tile channel sums: (y, y^2) or (dz, dz * xb)
     float cs[8], cq[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) cs[j] = cq[j] = 0.f;
@@ -257,20 +287,23 @@ __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
         const long long o = (long long)m * a.K + tn * BN + seg * 8;
         u32x4 v = *reinterpret_cast<const u32x4*>(lds + row * OUT_LD + seg * 8);
         if (a.res) v = add_bf16x8(v, rv[e]);
+        if (a.bn_part) v = relu_mask_bf16x8(v, ry[e]);
         *reinterpret_cast<u32x4*>(a.y + o) = v;
-        if (a.stats) {
+        if (sums) {
+          const u32x4 w = a.bn_part ? rx[e] : v;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const float lo = __uint_as_float(v[j] << 16), hi = __uint_as_float(v[j] & 0xffff0000u);
+            const float wl = __uint_as_float(w[j] << 16), wh = __uint_as_float(w[j] & 0xffff0000u);
             cs[2 * j] += lo;
-            cq[2 * j] = fmaf(lo, lo, cq[2 * j]);
+            cq[2 * j] = fmaf(lo, wl, cq[2 * j]);
             cs[2 * j + 1] += hi;
-            cq[2 * j + 1] = fmaf(hi, hi, cq[2 * j + 1]);
+            cq[2 * j + 1] = fmaf(hi, wh, cq[2 * j + 1]);
           }
         }
       }
     }
-    if (a.stats) {
+    if (sums) {
       // fixed-order reduction over the NT / SEG threads of each segment, through the (now free) LDS
       constexpr int TPS = NT / SEG;  // threads per segment
       static_assert(2 * TPS * BN * 4 <= 2 * (BM + BN) * LDS_ROW * 2, "stats scratch must fit the operand LDS");
@@ -289,8 +322,8 @@ __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
           S += red[g2 * BN + c];
           Q += red[TPS * BN + g2 * BN + c];
         }
-        a.stats[((long long)tm * 2) * a.K + tn * BN + c] = S;
-        a.stats[((long long)tm * 2 + 1) * a.K + tn * BN + c] = Q;
+        sums[((long long)tm * 2) * a.K + tn * BN + c] = S;
+        sums[((long long)tm * 2 + 1) * a.K + tn * BN + c] = Q;
       }
     }
   } else {
@@ -371,6 +404,8 @@ int conv_fwd_row_tile(const ConvGeom& g) {
   return (g_forced_tile == 3 && g.K % 128 == 0) ? 256 : 128;
 }
 
+int conv_dgrad_row_tile(const ConvGeom& g) { return (g_forced_tile == 3 && g.C % 128 == 0) ? 256 : 128; }
+
 void conv_fwd_bf16(const void* x, const void* w_ohwi, void* y, const ConvGeom& g, hipStream_t s, float* stats) {
   Igemm a{static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w_ohwi), static_cast<uint16_t*>(y),
           g.N, g.H, g.W, g.C, g.OH, g.OW, g.K, g.KH, g.KW, g.SH, g.SW, g.PT, g.PL, 0,
@@ -380,13 +415,14 @@ void conv_fwd_bf16(const void* x, const void* w_ohwi, void* y, const ConvGeom& g
 }
 
 void conv_dgrad_bf16(const void* dy, const void* w_hwio, void* dx, const ConvGeom& g, hipStream_t s,
-                     const void* residual) {
+                     const void* residual, const void* bn_y, const void* bn_x, float* bn_part) {
   // image = dy [N][OH][OW][K] (reduction channels K), output = dx [N][H][W][C] (columns C), stride 1,
   // mirrored taps with padding KH-1-PT / KW-1-PL
   Igemm a{static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w_hwio), static_cast<uint16_t*>(dx),
           g.N, g.OH, g.OW, g.K, g.H, g.W, g.C, g.KH, g.KW, 1, 1, g.KH - 1 - g.PT, g.KW - 1 - g.PL, 1,
           (long long)g.K, (long long)g.KW * g.C * g.K, (long long)g.C * g.K, g.N * g.H * g.W, 0, 0, 0,
-          static_cast<const uint16_t*>(residual)};
+          static_cast<const uint16_t*>(residual), nullptr, static_cast<const uint16_t*>(bn_y),
+          static_cast<const uint16_t*>(bn_x), bn_part};
   launch(a, s);
 }
 

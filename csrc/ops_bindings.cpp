@@ -58,6 +58,18 @@ const float* opt_f32(const c10::optional<at::Tensor>& t) {
   return t->data_ptr<float>();
 }
 
+// partial rows P of a [P + ceil(P/64)][2][C] f32 workspace produced by a conv epilogue
+int parts_rows(const at::Tensor& t, int64_t C) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == at::kFloat && t.dim() == 3 && t.size(1) == 2 &&
+                  t.size(2) == C,
+              "batch_norm: part must be f32 [rows][2][C]");
+  const int64_t rows = t.size(0);
+  int64_t p = 1;
+  while (p + (p + 63) / 64 < rows) ++p;  // invert rows = P + ceil(P / 64)
+  TORCH_CHECK(p + (p + 63) / 64 == rows, "batch_norm: part rows must be P + ceil(P/64)");
+  return (int)p;
+}
+
 // training forward: y = act(bn(x) [+ residual]); returns (y, stats[4][C] = mean, invstd, scale, shift);
 // moving statistics updated in place (mean_off: folded conv bias, moving mean only)
 std::vector<at::Tensor> bn_forward_train(at::Tensor x, c10::optional<at::Tensor> gamma, c10::optional<at::Tensor> beta,
@@ -82,11 +94,7 @@ std::vector<at::Tensor> bn_forward_train(at::Tensor x, c10::optional<at::Tensor>
     TORCH_CHECK(part_in->is_cuda() && part_in->is_contiguous() && part_in->scalar_type() == at::kFloat &&
                     part_in->dim() == 3 && part_in->size(1) == 2 && part_in->size(2) == C,
                 "batch_norm: part must be f32 [rows][2][C]");
-    const int64_t rows = part_in->size(0);
-    int64_t p = 1;
-    while (p + (p + 63) / 64 < rows) ++p;  // invert rows = P + ceil(P / 64)
-    TORCH_CHECK(p + (p + 63) / 64 == rows, "batch_norm: part rows must be P + ceil(P/64)");
-    given = (int)p;
+    given = parts_rows(*part_in, C);
     part = *part_in;
   } else {
     part = at::empty({(int64_t)plan.part_rows * 2 * C}, f);
@@ -110,7 +118,8 @@ std::vector<at::Tensor> bn_forward_train(at::Tensor x, c10::optional<at::Tensor>
 // views); the returned dgamma / dbeta are then those tensors
 std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> y,
                                     c10::optional<at::Tensor> gamma, at::Tensor st, int64_t mode,
-                                    c10::optional<at::Tensor> dgamma_out, c10::optional<at::Tensor> dbeta_out) {
+                                    c10::optional<at::Tensor> dgamma_out, c10::optional<at::Tensor> dbeta_out,
+                                    c10::optional<at::Tensor> part_in) {
   bn_check(x);
   bn_check(dy);
   TORCH_CHECK(dy.scalar_type() == x.scalar_type() && dy.numel() == x.numel(), "batch_norm backward: dy/x mismatch");
@@ -119,15 +128,26 @@ std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, c10::optional<a
   TORCH_CHECK(st.is_contiguous() && st.numel() == 4 * C && st.scalar_type() == at::kFloat, "batch_norm: stats [4][C]");
   const void* yp = nullptr;
   at::Tensor dz;
-  if (mode == 2) {
+  if (mode == 2 && !(part_in.has_value() && part_in->defined())) {
     TORCH_CHECK(y.has_value() && y->defined(), "batch_norm backward mode 2 needs y");
     bn_check(*y);
     yp = y->data_ptr();
     dz = at::empty_like(x);
+  } else if (mode == 2) {
+    dz = dy;
   }
   const tdl::BnPlan plan = tdl::bn_plan(M, (int)C);
   auto f = x.options().dtype(at::kFloat);
-  auto part = at::empty({(int64_t)plan.part_rows * 2 * C}, f);
+  int given = 0;
+  at::Tensor part;
+  if (part_in.has_value() && part_in->defined()) {
+    // (dz, part) from conv_dgrad_bn: dy IS the group's masked gradient dz (returned as the residual's)
+    TORCH_CHECK(mode == 2, "batch_norm backward: precomputed partials are for the add+relu group");
+    given = parts_rows(*part_in, C);
+    part = *part_in;
+  } else {
+    part = at::empty({(int64_t)plan.part_rows * 2 * C}, f);
+  }
   auto out = at::empty({5, C}, f);  // dgamma, dbeta, coef[3]
   auto dx = at::empty_like(x);
   float* o = out.data_ptr<float>();
@@ -143,7 +163,7 @@ std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, c10::optional<a
   const int acc = (pg ? 1 : 0) | (pb ? 2 : 0);
   tdl::bn_backward(dy.data_ptr(), x.data_ptr(), yp, mode == 2 ? dz.data_ptr() : nullptr, dx.data_ptr(), bn_dtype(x), M,
                    (int)C, part.data_ptr<float>(), opt_f32(gamma), sp, sp + C, sp + 2 * C, sp + 3 * C, pg ? pg : o,
-                   pb ? pb : o + C, o + 2 * C, (int)mode, acc, cur_stream());
+                   pb ? pb : o + C, o + 2 * C, (int)mode, acc, cur_stream(), given);
   at::Tensor g = pg ? *dgamma_out : out[0], b = pb ? *dbeta_out : out[1];
   if (mode == 2) return {dx, g, b, dz};
   return {dx, g, b};
@@ -230,8 +250,25 @@ const void* opt_residual(const c10::optional<at::Tensor>& r, const at::Tensor& l
   return r->data_ptr();
 }
 
+std::vector<at::Tensor> conv_dgrad_impl(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w, int64_t pt,
+                                        int64_t pl, c10::optional<at::Tensor> residual,
+                                        c10::optional<at::Tensor> bn_y, c10::optional<at::Tensor> bn_x);
+
 at::Tensor conv_dgrad(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w, int64_t pt, int64_t pl,
                       c10::optional<at::Tensor> residual) {
+  return conv_dgrad_impl(dy, w_hwio, h, w, pt, pl, residual, c10::nullopt, c10::nullopt)[0];
+}
+
+// input gradient with the fused backward of the BN -> Add -> ReLU group that produced the conv's
+// input bn_y from bn_x: returns (dz, part[P + ceil(P/64)][2][C])
+std::vector<at::Tensor> conv_dgrad_bn(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w, int64_t pt, int64_t pl,
+                                      c10::optional<at::Tensor> residual, at::Tensor bn_y, at::Tensor bn_x) {
+  return conv_dgrad_impl(dy, w_hwio, h, w, pt, pl, residual, bn_y, bn_x);
+}
+
+std::vector<at::Tensor> conv_dgrad_impl(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w, int64_t pt,
+                                        int64_t pl, c10::optional<at::Tensor> residual,
+                                        c10::optional<at::Tensor> bn_y, c10::optional<at::Tensor> bn_x) {
   conv_check(dy, "dy");
   conv_check(w_hwio, "w");
   TORCH_CHECK(w_hwio.dim() == 4 && w_hwio.size(3) == dy.size(3), "conv_dgrad: weights must be HWIO [KH,KW,C,K]");
@@ -239,9 +276,20 @@ at::Tensor conv_dgrad(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w, in
                   (int)dy.size(3), (int)w_hwio.size(0), (int)w_hwio.size(1), 1, 1, (int)pt, (int)pl};
   TORCH_CHECK(tdl::conv_bf16_supported(g), "conv_dgrad: unsupported geometry (C and K must be multiples of 64)");
   auto dx = at::empty({dy.size(0), h, w, w_hwio.size(2)}, dy.options());
+  const void* by = opt_residual(bn_y, dy, dy.size(0), h, w, w_hwio.size(2));
+  const void* bx = opt_residual(bn_x, dy, dy.size(0), h, w, w_hwio.size(2));
+  TORCH_CHECK((by == nullptr) == (bx == nullptr), "conv_dgrad: bn_y and bn_x go together");
+  at::Tensor part;
+  if (by) {
+    const int64_t M = (int64_t)g.N * g.H * g.W, bm = tdl::conv_dgrad_row_tile(g);
+    const int64_t P = (M + bm - 1) / bm;
+    part = at::empty({P + (P + 63) / 64, 2, (int64_t)g.C}, dy.options().dtype(at::kFloat));
+  }
   tdl::conv_dgrad_bf16(dy.data_ptr(), w_hwio.data_ptr(), dx.data_ptr(), g, cur_stream(),
-                       opt_residual(residual, dy, dy.size(0), h, w, w_hwio.size(2)));
-  return dx;
+                       opt_residual(residual, dy, dy.size(0), h, w, w_hwio.size(2)), by, bx,
+                       by ? part.data_ptr<float>() : nullptr);
+  if (by) return {dx, part};
+  return {dx};
 }
 // input gradient of a 1x1 stride-2 unpadded conv: dx[N,H,W,C] from dy[N,OH,OW,K] and w_hwio[1,1,C,K]
 at::Tensor conv_dgrad_s2(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w, c10::optional<at::Tensor> residual) {
@@ -417,6 +465,7 @@ void register_ops(pybind11::module& m) {
   m.def("slab_cast_bf16", &slab_cast_bf16, "f32 -> bf16 copy of a whole weight slab (one launch)");
   m.def("bn_set_tuning", &tdl::bn_set_tuning, "BN kernel sweep hooks (max_parts, elem_blocks, elem_unroll; 0 = keep)");
   m.def("slab_transpose_bf16", &slab_transpose_bf16, "HWIO f32 conv kernels -> OHWI bf16, all in one launch");
+  m.def("conv_dgrad_bn", &conv_dgrad_bn, "stride-1 conv input gradient + fused BN->Add->ReLU backward (dz, part)");
   m.def("conv_dgrad_s2", &conv_dgrad_s2, "NHWC bf16 1x1 stride-2 convolution input gradient (MFMA)",
         pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("h"), pybind11::arg("wd"),
         pybind11::arg("residual") = pybind11::none());
@@ -443,5 +492,6 @@ void register_ops(pybind11::module& m) {
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC max pool backward (gather form)");
   m.def("bn_backward", &bn_backward, "NHWC batch-norm training backward", pybind11::arg("dy"), pybind11::arg("x"),
         pybind11::arg("y"), pybind11::arg("gamma"), pybind11::arg("stats"), pybind11::arg("mode"),
-        pybind11::arg("dgamma_out") = pybind11::none(), pybind11::arg("dbeta_out") = pybind11::none());
+        pybind11::arg("dgamma_out") = pybind11::none(), pybind11::arg("dbeta_out") = pybind11::none(),
+        pybind11::arg("part") = pybind11::none());
 }

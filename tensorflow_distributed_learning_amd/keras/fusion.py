@@ -178,4 +178,8 @@ def run_group(g: Group, vals, training, taps=None, boxes=None):
                          bn.beta.value if bn.beta is not None else None, bn.moving_mean.value,
                          bn.moving_variance.value, bn.momentum, bn.epsilon, relu=g.relu, residual=r, conv_bias=cb,
                          grad_out=bn._grad_targets(), part=getattr(x, "_tdl_bn_part", None))
+    if r is not None and g.relu and y.is_cuda:
+        # a conv reading this group's output can fuse the group's backward reduction into its
+        # input-gradient epilogue (ops/conv.py): it needs the BN input
+        y._tdl_bn_src = x
     vals[id(g.out)] = y

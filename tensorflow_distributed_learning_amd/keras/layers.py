@@ -358,7 +358,7 @@ class Conv2D(Layer):
             # hand-written implicit-GEMM MFMA kernels (csrc/kernels/conv.hip), autotuned against MIOpen
             y = _conv.conv2d_nhwc(x, k_hwio, self.strides, pad if pad else (0, 0), grad_out=gt,
                                   w_ohwi=self.kernel.compute_view_ohwi(x.dtype) if gt is not None else None,
-                                  grad_box=_grad_box, bn_stats=_bn_stats)
+                                  grad_box=_grad_box, bn_stats=_bn_stats, bn_src=getattr(x, "_tdl_bn_src", None))
             if b is not None:
                 y = y + b
             return self.activation(y)

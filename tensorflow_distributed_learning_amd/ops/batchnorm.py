@@ -24,6 +24,9 @@ import torch.nn.functional as F
 from . import hip
 
 
+FUSED_BWD = [0]  # backward calls that took their reduction from a conv epilogue (tests)
+
+
 def supported(x: torch.Tensor) -> bool:
     C = x.shape[-1]
     return x.is_cuda and x.dim() >= 2 and C % 8 == 0 and C <= 2048 and x.dtype in (torch.float32, torch.bfloat16)
@@ -56,10 +59,16 @@ class _BatchNormTrain(torch.autograd.Function):
         C = hip()
         xc, gamma, st, y, conv_bias = ctx.saved_tensors
         has_g, has_b, has_r, has_cb = ctx.flags
+        part = getattr(dy, "_tdl_bn_bwd_part", None) if ctx.mode == 2 else None
         dy = _aligned(dy.to(xc.dtype))
         go = ctx.grad_out or (None, None)
-        out = C.bn_backward(dy, xc, y if ctx.mode == 2 else None, gamma if has_g else None, st, ctx.mode,
-                            go[0], go[1])
+        if part is not None and dy.dtype == xc.dtype and dy.is_contiguous() and dy.data_ptr() % 16 == 0:
+            # dy is already this group's masked dz, reduced by the consuming conv's dgrad epilogue
+            FUSED_BWD[0] += 1
+            out = C.bn_backward(dy, xc, None, gamma if has_g else None, st, ctx.mode, go[0], go[1], part)
+        else:
+            out = C.bn_backward(dy, xc, y if ctx.mode == 2 else None, gamma if has_g else None, st, ctx.mode,
+                                go[0], go[1])
         dx, dgamma, dbeta = out[0], out[1], out[2]
         dres = out[3].to(ctx.res_dtype) if has_r else None
         dcb = torch.zeros_like(conv_bias) if (has_cb and ctx.needs_input_grad[4]) else None

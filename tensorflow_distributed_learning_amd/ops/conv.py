@@ -21,6 +21,7 @@ import torch.nn.functional as F
 
 from . import hip
 
+_FUSE_BN_BWD = [os.environ.get("TDL_FUSE_BN_BWD", "1") == "1"]
 _choice: dict = {}  # (direction, shape key) -> True (hand-written kernel) / False (MIOpen)
 _times: dict = {}  # (direction, shape key) -> (hand-written ms, MIOpen ms) as measured by the autotuner
 
@@ -95,7 +96,12 @@ def _time(fn, reps=5) -> float:
     return sorted(ts)[reps // 2]
 
 
-def _pick(key, hip_fn, ref_fn) -> bool:
+_HBM_BYTES_PER_MS = 4.5e9  # streaming rate the BN/add kernels reach on MI355X (profiles/bn_tuning_sweep_r2.jsonl)
+
+
+def _pick(key, hip_fn, ref_fn, saved_bytes: int = 0) -> bool:
+    """``saved_bytes``: HBM traffic of the passes the hand-written kernel's fused epilogue removes
+    (BN statistics, gradient sums) that the library path would still run; credited to it."""
     m = mode()
     if m == "hip":
         return True
@@ -104,7 +110,7 @@ def _pick(key, hip_fn, ref_fn) -> bool:
         return got
     if torch.cuda.is_current_stream_capturing():
         return False
-    t_ref = _time(ref_fn)
+    t_ref = _time(ref_fn) + saved_bytes / _HBM_BYTES_PER_MS
     t_hip = _time(hip_fn)
     got = t_hip < t_ref
     _choice[key] = got
@@ -149,7 +155,7 @@ def _ref_fwd(x, w_oihw, stride, pad):
 
 class _Conv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, kernel, stride, pad, grad_out, w_ohwi=None, box=None, stats_out=None):
+    def forward(ctx, x, kernel, stride, pad, grad_out, w_ohwi=None, box=None, stats_out=None, bn_src=None):
         C = hip()
         x = x.contiguous()
         if x.data_ptr() % 16:
@@ -159,11 +165,13 @@ class _Conv(torch.autograd.Function):
         ph, pw = pad
         oh, ow = (x.shape[1] + 2 * ph - kh) // sh + 1, (x.shape[2] + 2 * pw - kw) // sw + 1
         w_oihw = kernel.permute(3, 2, 0, 1)
-        key = ("fwd", tuple(x.shape), tuple(kernel.shape), stride, pad)
+        # with BN statistics in the epilogue the library path would also pay a read of y
+        key = ("fwd", tuple(x.shape), tuple(kernel.shape), stride, pad, stats_out is not None)
+        y_bytes = x.shape[0] * oh * ow * cout * x.element_size()
         if w_ohwi is None:
             w_ohwi = kernel.permute(3, 0, 1, 2).contiguous()
         hip_fn = lambda: C.conv_fwd(x, w_ohwi, oh, ow, sh, sw, ph, pw)  # noqa: E731
-        if _pick(key, hip_fn, lambda: _ref_fwd(x, w_oihw, stride, pad)):
+        if _pick(key, hip_fn, lambda: _ref_fwd(x, w_oihw, stride, pad), y_bytes if stats_out is not None else 0):
             if stats_out is not None:  # + the following batch norm's partial channel sums
                 y, stats_out[0] = C.conv_fwd_stats(x, w_ohwi, oh, ow, sh, sw, ph, pw)
             else:
@@ -174,6 +182,8 @@ class _Conv(torch.autograd.Function):
         ctx.geo = (stride, pad)
         ctx.grad_out = grad_out
         ctx.box = box
+        ctx.bn_src = bn_src if (bn_src is not None and tuple(bn_src.shape) == tuple(x.shape)
+                                and bn_src.dtype == x.dtype) else None
         if box is not None:
             box.n += 1
         return y
@@ -209,15 +219,31 @@ class _Conv(torch.autograd.Function):
                     other = other.clone()
         if want_dx:
             kc = kernel.contiguous()
-            hip_fn = None
+            hip_fn = key = None
             if stride == (1, 1):
                 hip_fn = lambda r=None: C.conv_dgrad(dy, kc, x.shape[1], x.shape[2], pad[0], pad[1], r)  # noqa: E731
                 key = ("dgrad",) + shape_key
             elif stride == (2, 2) and (kh, kw) == (1, 1) and pad == (0, 0):
                 hip_fn = lambda r=None: C.conv_dgrad_s2(dy, kc, x.shape[1], x.shape[2], r)  # noqa: E731
                 key = ("dgrad_s2",) + shape_key
-            if hip_fn is not None and _pick(key, hip_fn, lambda: ref([True, False, False])()[0]):
-                dx = hip_fn(other)
+            # fused epilogues: a gradient sum saves an add pass (2 reads + 1 write of dx, one read back),
+            # the BN group reduction a read of dz, x, y and a write of dz
+            fuse_bn = other is not None and ctx.bn_src is not None and stride == (1, 1) and _FUSE_BN_BWD[0]
+            dx_bytes = x.numel() * x.element_size()
+            saved = (2 * dx_bytes if other is not None else 0) + (2 * dx_bytes if fuse_bn else 0)
+            key = (key + (other is not None, fuse_bn)) if hip_fn is not None else None
+            if hip_fn is not None and _pick(key, hip_fn, lambda: ref([True, False, False])()[0], saved):
+                src = ctx.bn_src
+                if fuse_bn:
+                    # full gradient of the BN -> Add -> ReLU group output x: mask it and reduce it for
+                    # the group's BN backward in the same epilogue (ops/batchnorm.py uses the part)
+                    src = src.contiguous()
+                    if src.data_ptr() % 16:
+                        src = src.clone()
+                    dx, part = C.conv_dgrad_bn(dy, kc, x.shape[1], x.shape[2], pad[0], pad[1], other, x, src)
+                    dx._tdl_bn_bwd_part = part
+                else:
+                    dx = hip_fn(other)
                 other = None
         if want_dw and x.shape[0] * dy.shape[1] * dy.shape[2] < (1 << 24):
             plan = _pick_wgrad(("wgrad",) + shape_key, C, x, dy, kh, kw, stride, pad,
@@ -243,7 +269,7 @@ class _Conv(torch.autograd.Function):
                 if gout is not None:
                     gout.add_(dw)
                     dw = None
-        return dx, dw, None, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None, None
 
 
 def _miopen_bwd(dy_nchw, x_nchw, w_oihw, stride, pad, mask):
@@ -253,16 +279,19 @@ def _miopen_bwd(dy_nchw, x_nchw, w_oihw, stride, pad, mask):
 
 
 def conv2d_nhwc(x, kernel_hwio, stride=(1, 1), pad=(0, 0), grad_out=None, w_ohwi=None, grad_box=None,
-                bn_stats=False):
+                bn_stats=False, bn_src=None):
     """y[N,OH,OW,K] = conv(x[N,H,W,C], kernel[KH,KW,C,K]) with symmetric zero padding ``pad = (ph, pw)``,
     bf16; the caller checked :func:`supported`.  ``grad_out``: f32 [KH,KW,C,K] tensor the weight
     gradient is added into (a trainer's gradient slab view; ``kernel_hwio`` then needs no autograd);
     ``w_ohwi``: the same kernel already in OHWI [K,KH,KW,C] layout (skips the per-call transpose);
     ``grad_box``: a :class:`GradBox` shared with the other consumer of ``x``; ``bn_stats``: the
     hand-written forward also writes the batch-norm partial channel sums of y, attached as
-    ``y._tdl_bn_part`` for the BN that consumes it (ops/batchnorm.py skips its statistics pass)."""
+    ``y._tdl_bn_part`` for the BN that consumes it (ops/batchnorm.py skips its statistics pass);
+    ``bn_src``: x is the output relu(bn(bn_src) + r) of a fused BN group; when this conv's input
+    gradient is the complete gradient of x (second GradBox participant), its epilogue also applies
+    the group's ReLU mask and reduces the group's BN backward sums."""
     holder = [None] if bn_stats else None
-    y = _Conv.apply(x, kernel_hwio, tuple(stride), tuple(pad), grad_out, w_ohwi, grad_box, holder)
+    y = _Conv.apply(x, kernel_hwio, tuple(stride), tuple(pad), grad_out, w_ohwi, grad_box, holder, bn_src)
     if holder is not None and holder[0] is not None:
         y._tdl_bn_part = holder[0]
     return y

@@ -123,3 +123,62 @@ def test_conv_epilogue_bn_statistics_match_bn_pass():
         scale = max(float(np.abs(b).max()), 1e-3)
         np.testing.assert_allclose(a, b, atol=2e-2 * scale, rtol=2e-2, err_msg=v.name)
     np.testing.assert_allclose(ha.history["loss"], hb.history["loss"], rtol=1e-2)
+
+
+def test_fused_bn_group_backward_in_conv_epilogue():
+    """The identity block's first conv computes the previous BN -> Add -> ReLU group's masked
+    gradient and BN reductions in its input-gradient epilogue; training matches the unfused path."""
+    from tensorflow_distributed_learning_amd.ops import batchnorm as B
+    from tensorflow_distributed_learning_amd.ops import conv as CV
+
+    L = tdl.keras.layers
+
+    def model():
+        tdl.keras.utils.set_random_seed(7)
+        inp = L.Input(shape=(8, 8, 64))
+        x = L.Conv2D(64, 3, padding="same")(inp)
+        x = L.BatchNormalization()(x)
+        x = L.Activation("relu")(x)
+        for _ in range(2):  # two identity blocks: the first's output feeds the second's conv + Add
+            y = L.Conv2D(64, 1)(x)
+            y = L.BatchNormalization()(y)
+            y = L.Activation("relu")(y)
+            y = L.Conv2D(64, 3, padding="same")(y)
+            y = L.BatchNormalization()(y)
+            x = L.Activation("relu")(L.Add()([x, y]))
+        x = L.GlobalAveragePooling2D()(x)
+        return tdl.keras.Model(inp, L.Dense(16)(x))
+
+    def run(fuse):
+        CV._FUSE_BN_BWD[0] = fuse
+        old = {k: os.environ.get(k) for k in ("TDL_GRAPH_STEP", "TDL_CONV")}
+        os.environ.update({"TDL_GRAPH_STEP": "0", "TDL_CONV": "hip"})
+        try:
+            tdl.keras.backend.clear_session()
+            tdl.keras.mixed_precision.set_global_policy("mixed_bfloat16")
+            g = torch.Generator().manual_seed(0)
+            ds = tdl.data.Dataset.from_tensor_slices((torch.rand(128, 8, 8, 64, generator=g),
+                                                      torch.randint(0, 16, (128,), generator=g))).batch(32).repeat()
+            with tdl.distribute.MirroredStrategy(devices=["/gpu:0"]).scope():
+                m = model()
+                m.compile(loss=tdl.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+                          optimizer=tdl.keras.optimizers.SGD(learning_rate=0.05, momentum=0.9))
+            n0 = B.FUSED_BWD[0]
+            h = m.fit(ds, epochs=1, steps_per_epoch=2, verbose=0)
+            return m, h, B.FUSED_BWD[0] - n0
+        finally:
+            CV._FUSE_BN_BWD[0] = True
+            tdl.keras.mixed_precision.set_global_policy("float32")
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+
+    mf, hf, nf = run(True)
+    mu, hu, nu = run(False)
+    assert nf == 2 and nu == 0  # one fused group per step (the first block's output), two steps
+    for v, a, b in zip(mf.weights, mf.get_weights(), mu.get_weights()):
+        scale = max(float(np.abs(b).max()), 1e-3)
+        np.testing.assert_allclose(a, b, atol=2e-2 * scale, rtol=2e-2, err_msg=v.name)
+    np.testing.assert_allclose(hf.history["loss"], hu.history["loss"], rtol=1e-2)
