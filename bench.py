@@ -35,9 +35,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 
-def _spe(K: int, cap: int = 200) -> int:
+def _spe(K: int, cap: int = 50) -> int:
     """Steps per execution: the largest divisor of K that is <= cap (one graph launch per
-    execution; the timed region replays K / spe graphs)."""
+    execution; the timed region replays K / spe graphs).  Measured at K=1000 on one MI355X
+    (profiles/mnist_bench_spe_sweep_r2.txt): 50 steps (200 kernel nodes) per graph run at 37.0
+    us/step, 100-1000 at 39.2-39.9 (larger graphs dispatch slower on the device)."""
     for d in range(min(K, cap), 0, -1):
         if K % d == 0:
             return d
