@@ -94,12 +94,12 @@ class MnistStep {
     a_.idx = idx_.data_ptr<int>() + off;
   }
 
-  // Individual stages (tests / profiling): 5 dP2 (+ dense weight grads if pending), 6 conv bwd,
+  // Individual stages (tests / profiling): 5 dense weight grads, 6 conv bwd,
   // 8 fwd conv (+dense1, +head), 9 finalize.
   void stage(int64_t k, bool apply_sgd) {
     hipStream_t s = cur_stream();
     switch (k) {
-      case 5: tdl::mnist_dense1_bwd(a_, !dense_pending_, s); break;
+      case 5: tdl::mnist_dense_wgrad(a_, s); break;
       case 6: tdl::mnist_conv_bwd(a_, s); break;
       case 8: tdl::mnist_fwd_conv(a_, s); break;
       case 9: tdl::mnist_finalize(a_, apply_sgd, dense_pending_, s); break;
@@ -113,7 +113,6 @@ class MnistStep {
     set_idx_offset(idx_off);
     hipStream_t s = cur_stream();
     tdl::mnist_fwd_conv(a_, s);
-    tdl::mnist_dense1_bwd(a_, false, s);
     tdl::mnist_conv_bwd(a_, s);
     dense_pending_ = true;
   }
@@ -124,7 +123,7 @@ class MnistStep {
     set_idx_offset(idx_off);
     hipStream_t s = cur_stream();
     tdl::mnist_fwd_conv(a_, s);
-    tdl::mnist_dense1_bwd(a_, true, s);
+    tdl::mnist_dense_wgrad(a_, s);
     dense_pending_ = false;
   }
   void backward_conv() { tdl::mnist_conv_bwd(a_, cur_stream()); }

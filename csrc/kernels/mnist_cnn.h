@@ -27,12 +27,12 @@ struct MnistArgs {
   uint8_t* A2;        // [b,1600]
   float* H;           // [b,128] relu(dense1)
   float* dH;          // [b,128] grad of dense1 out (ReLU-masked)
-  float* dP2;         // [b,1600] grad of the pooled conv2 output, ReLU-masked (k_dense1_bwd)
+  float* dP2;         // [b,1600] grad of the pooled conv2 output, ReLU-masked (k_fwd_conv)
   float* part2;       // [b][289][64] per-image partials of conv2 wgrad (row 288 = bias)
   float* part1;       // [2b][320] per-(image, pixel-half) partials of conv1 wgrad (+ bias)
   float* part3;       // [4][b][128] dense1 partials, one per conv2 channel quarter
   float* dL;          // [b][10] dlogits (already scaled by 1/(b*R))
-  unsigned* cnt;      // [b] per-image arrival counters of the 4 quarter workgroups (re-armed by K5)
+  unsigned* cnt;      // [b] per-image arrival (+ head-done) counters of k_fwd_conv (re-armed by KC)
   float* metrics;     // [0] loss sum, [1] correct, [2] count
   const float* lr;    // device scalar learning rate
   unsigned long long* stamps;  // optional [grid][8] phase timestamps (s_memrealtime), diagnostics
@@ -49,11 +49,12 @@ constexpr int kDense1Chunks = 4;  // dense1 partials: one per conv2 channel quar
 constexpr int kMnistPart1Cols = 320;
 __host__ __device__ inline int mnist_part1_rows(int b) { return 2 * b; }
 
-// dP2 (+ the dense weight gradients dW3/db3/dW4/db4 when with_dense)
-void mnist_dense1_bwd(const MnistArgs& a, bool with_dense, hipStream_t s);
+// the dense weight gradients dW3/db3/dW4/db4 (R > 1: ahead of the conv backward)
+void mnist_dense_wgrad(const MnistArgs& a, hipStream_t s);
 void mnist_conv_bwd(const MnistArgs& a, hipStream_t s);
 // conv1 + conv2 + dense1 partials per (image, quarter); with a.head the image's last quarter
-// workgroup also runs the loss head (dense1 sum + ReLU, dense2, softmax-xent, dlogits, metrics)
+// workgroup also runs the loss head (dense1 sum + ReLU, dense2, softmax-xent, dlogits, metrics),
+// and with a.head == 1 every workgroup then computes its quarter of dP2
 void mnist_fwd_conv(const MnistArgs& a, hipStream_t s);
 // partial-slab reductions (+ the dense weight gradients when with_dense) (+ SGD when apply_sgd)
 void mnist_finalize(const MnistArgs& a, bool apply_sgd, bool with_dense, hipStream_t s);

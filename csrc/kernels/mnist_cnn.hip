@@ -1,7 +1,7 @@
 // Fused MNIST-CNN training step for gfx950 (MI355X), f32 end to end.
 //
 // Replaces, for the reference model of tf_dist_example.py:40-52, the ~35 TF/cuDNN/Eigen kernels
-// of one replica step by four launches:
+// of one replica step by three launches (four at R > 1):
 //
 //   KA fwd_conv     : per (image, channel quarter), LDS-staged: gather(idx) + conv1 3x3 (1->32)
 //                     and conv2 3x3 (32->64) on v_mfma_f32_16x16x4_f32 with bias + ReLU + maxpool2
@@ -9,9 +9,11 @@
 //                     dense1 partial [1600/4 features] x W3 (W3 slice prefetched in registers);
 //                     the LAST of an image's 4 quarter workgroups (arrival counter) then runs the
 //                     head for that image: dense1 partial sum + bias + ReLU, dense2 + softmax-xent
-//                     + dlogits*(1/(b*R)) + loss/accuracy accumulators + dH (ReLU mask)
-//   K5 dense1_bwd   : dP2 = (dH W3^T) * relu-mask, one 16x16 MFMA tile per wave task (+ the
-//                     dense weight gradients dW3/db3/dW4/db4 when their bucket is all-reduced early)
+//                     + dlogits*(1/(b*R)) + loss/accuracy accumulators + dH (ReLU mask); every
+//                     quarter workgroup then waits for its image's dH and computes its 400
+//                     features of dP2 = (dH W3^T) * relu-mask from the W3 slice in its registers
+//   K5 dense1_bwd   : (R > 1 only) the dense weight gradients dW3/db3/dW4/db4, so their bucket's
+//                     all-reduce overlaps the conv backward
 //   KC conv_bwd     : per image (x4 parts), LDS-staged (dC2 expanded from dP2 + pool-2 argmax):
 //                     dW2 (+db2 as an extra "ones" row) and
 //                     dP1 = dC2 (*) W2^T on MFMA with pool1/ReLU backward AND conv1 wgrad in
@@ -98,6 +100,34 @@ __device__ __forceinline__ void wave_sum10(const float (&v)[10], int l, float (&
   }
 }
 
+// Sums over the 32 lanes of each half-wave of N <= 32 per-lane values (v[k], k >= N taken as 0):
+// a reduce-scatter butterfly (16 + 8 + 4 + 2 + 1 cross-lane moves); lane l returns the sum of
+// value (l & 31) over its half-wave.
+template <int N>
+__device__ __forceinline__ float reduce_scatter32(const float (&v)[N], int l) {
+  float s16[16];
+  const bool b16 = l & 16;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const float lo = k < N ? v[k] : 0.f, hi = k + 16 < N ? v[k + 16] : 0.f;
+    s16[k] = (b16 ? hi : lo) + __shfl_xor(b16 ? lo : hi, 16, 64);
+  }
+  float s8[8];
+  const bool b8 = l & 8;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s8[k] = (b8 ? s16[k + 8] : s16[k]) + __shfl_xor(b8 ? s16[k] : s16[k + 8], 8, 64);
+  float s4[4];
+  const bool b4 = l & 4;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) s4[k] = (b4 ? s8[k + 4] : s8[k]) + __shfl_xor(b4 ? s8[k] : s8[k + 4], 4, 64);
+  float s2[2];
+  const bool b2 = l & 2;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) s2[k] = (b2 ? s4[k + 2] : s4[k]) + __shfl_xor(b2 ? s4[k] : s4[k + 2], 2, 64);
+  const bool b1 = l & 1;
+  return (b1 ? s2[1] : s2[0]) + __shfl_xor(b1 ? s2[0] : s2[1], 1, 64);
+}
+
 __device__ __forceinline__ void head_row(const MnistArgs& a, int r, int l, int y, const HeadWeights& hw) {
   const float* wa = hw.wa;
   const float* wb = hw.wb;
@@ -153,8 +183,10 @@ __device__ __forceinline__ void head_row(const MnistArgs& a, int r, int l, int y
     d1 = fmaf(dl[c], wb[c], d1);
     mine = (l == c) ? dl[c] : mine;
   }
-  a.dH[r * 128 + l] = h0 > 0.f ? d0 : 0.f;
-  a.dH[r * 128 + l + 64] = h1 > 0.f ? d1 : 0.f;
+  // dH leaves with write-through (sc1) stores: the image's other quarter workgroups, on any XCD,
+  // read it for their dP2 slice once k_fwd_conv's head-done count says it is there
+  __hip_atomic_store(a.dH + r * 128 + l, h0 > 0.f ? d0 : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(a.dH + r * 128 + l + 64, h1 > 0.f ? d1 : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   a.H[r * 128 + l] = h0;
   a.H[r * 128 + l + 64] = h1;
   if (l < 10) a.dL[r * 10 + l] = mine;
@@ -305,54 +337,12 @@ __device__ __forceinline__ void dense_w_task(const MnistArgs& a, int T, int lane
   }
 }
 
-// K5: dP2 = (dH W3^T) * 1[P2 > 0] (M = b, N = 1600, K = 128), one 16x16 tile per wave task, the
-// pool-2 / ReLU mask in the epilogue (k_conv_bwd expands it to the conv2-output gradient); with
-// `with_dense` also the dense weight-gradient tasks (R > 1: that bucket's all-reduce then overlaps
-// the conv backward; at R = 1 k_finalize runs them).  Block 0 re-arms the forward's per-image
-// head counters for the next step.
-__global__ __launch_bounds__(256) void k_dense1_bwd(MnistArgs a, int with_dense) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int i = lane & 15, g = lane >> 4;
-  const int b = a.b;
-  const int MT = (b + 15) >> 4;
-  if (blockIdx.x == 0)
-    for (int r = threadIdx.x; r < b; r += 256) a.cnt[r] = 0u;
-  const int T = blockIdx.x * 4 + wave;
-  if (T >= MT * 100) {
-    if (with_dense && T - MT * 100 < kDenseTasks) dense_w_task(a, T - MT * 100, lane, false, 0.f);
-    return;
-  }
-  const int mt = T % MT, nt = T / MT;
-  const int row = mt * 16 + i;
-  const bool valid = row < b;
-  const float* ap = a.dH + (valid ? row : 0) * 128 + 4 * g;
-  const float* bp = a.W + a.ow3 + (size_t)(nt * 16 + i) * 128 + 4 * g;
-  f4 av[8], bv[8];
-#pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    av[s] = ld4(ap + s * 16);
-    bv[s] = ld4(bp + s * 16);
-  }
-  float p2v[4];  // the epilogue's ReLU-mask operands in the same round trip
-#pragma unroll
-  for (int r = 0; r < 4; ++r) p2v[r] = a.P2[(size_t)min(mt * 16 + 4 * g + r, b - 1) * 1600 + nt * 16 + i];
-  __builtin_amdgcn_sched_barrier(0);
-  const float vm = valid ? 1.f : 0.f;
-  f4 acc0 = zero4(), acc1 = zero4();
-#pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    const f4 x = av[s] * vm;
-    acc0 = mfma16x16x4(x.x, bv[s].x, acc0);
-    acc1 = mfma16x16x4(x.y, bv[s].y, acc1);
-    acc0 = mfma16x16x4(x.z, bv[s].z, acc0);
-    acc1 = mfma16x16x4(x.w, bv[s].w, acc1);
-  }
-  const f4 acc = acc0 + acc1;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int rr = mt * 16 + 4 * g + r;
-    if (rr < b) a.dP2[(size_t)rr * 1600 + nt * 16 + i] = p2v[r] > 0.f ? acc[r] : 0.f;
-  }
+// K5 (R > 1 only): the dense weight gradients dW3/db3/dW4/db4 of the step, one task per wave, so
+// that bucket's all-reduce overlaps the conv backward (at R = 1 k_finalize runs the same tasks
+// fused with SGD).  dP2 comes from k_fwd_conv.
+__global__ __launch_bounds__(256) void k_dense1_bwd(MnistArgs a) {
+  const int T = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (T < kDenseTasks) dense_w_task(a, T, threadIdx.x & 63, false, 0.f);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -393,6 +383,8 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
   const int i = lane & 15, g = lane >> 4;
   const int bi = blockIdx.x >> 2, p = blockIdx.x & 3;
   const int h = p & 1, half = p >> 1;
+  if (blockIdx.x == 0)  // re-arm k_fwd_conv's per-image head counters for the next step
+    for (int r = tid; r < a.b; r += 512) a.cnt[r] = 0u;
   stamp(a.stamps, 0);
   // ---- stage everything in LDS: every global load of the thread is issued first (one memory
   // round trip for the whole staging), then all LDS stores.  Out-of-range slots load a valid
@@ -629,7 +621,7 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   uint8_t* a1s = reinterpret_cast<uint8_t*>(p2s + 400);       // [169][32] pool-1 argmax
   uint8_t* a2s = a1s + 169 * 32;                               // [25][16] pool-2 argmax
   float* red = reinterpret_cast<float*>(a2s + 400);            // [16][128] dense1 row-group partials
-  int* s_last = reinterpret_cast<int*>(red + 16 * 128);        // head hand-off flag (one word)
+  int* s_last = reinterpret_cast<int*>(red + 16 * 128);        // head hand-off: [last?, base count]
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int i = lane & 15, g = lane >> 4;
   const int bi = blockIdx.x >> 2, cq = blockIdx.x & 3;
@@ -826,23 +818,71 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   // visibility, first table row): the storing wave drains its sc1 stores, a workgroup barrier,
   // ONE agent-scope add per workgroup on the image's counter; the workgroup whose add returns
   // 3 (mod 4) is last and reads the 4 partials with sc1 loads.  No workgroup ever waits for
-  // another (placement-independent).  k_dense1_bwd (the next launch of every training step)
+  // another (placement-independent).  k_conv_bwd (in every training step after this launch)
   // zeroes the counters, so a launch that did not add exactly 4 per image cannot shift the
   // election of later steps.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid == 0) *s_last = (__hip_atomic_fetch_add(a.cnt + bi, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 3u) == 3u;
+  if (tid == 0) {
+    const unsigned old = __hip_atomic_fetch_add(a.cnt + bi, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last[0] = (old & 3u) == 3u;
+    s_last[1] = (int)(old & ~3u);  // this launch's base count of the image (head done at base + 5)
+  }
   __syncthreads();
-  if (*s_last && wave == 0) {
-    if (a.head == 1) head_row(a, bi, lane, label, hw);
-    else head_eval(a, bi, lane, label, hw);
-    stamp(a.stamps, 7);
-    return;
+  const bool last = s_last[0] != 0;
+  if (last && wave == 0) {
+    if (a.head == 1) {
+      head_row(a, bi, lane, label, hw);
+      // head done: dH (sc1 stores) drained, then the image's count goes to base + 5
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_fetch_add(a.cnt + bi, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      head_eval(a, bi, lane, label, hw);
+    }
   }
   if (a.head != 1) return;  // evaluation: nothing is saved for a backward pass
   // saved activations leave LDS only now (off the head's critical path)
-  if (*s_last) store_saved_fwd(a, bi, cq, P1s, a1s, p2s, a2s, tid - 64, 448);
-  else store_saved_fwd(a, bi, cq, P1s, a1s, p2s, a2s, tid, 512);
+  if (!last) store_saved_fwd(a, bi, cq, P1s, a1s, p2s, a2s, tid, 512);
+  else if (wave != 0) store_saved_fwd(a, bi, cq, P1s, a1s, p2s, a2s, tid - 64, 448);
+  // ---- dP2 = (dH W3^T) * 1[P2 > 0] for this quarter's 400 features, from the W3 slice still in
+  // registers (no K5 launch, no second read of W3).  Every workgroup waits for its image's head:
+  // the head runs in the image's LAST-arriving workgroup, which is already resident, so the wait
+  // cannot depend on a workgroup that has not been dispatched.  Bounded: a head that never
+  // arrives poisons the loss metric instead of hanging the GPU.
+  if (!last && tid == 0) {
+    const unsigned want = (unsigned)s_last[1] + 5u;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    // polled with an atomic RMW: it executes past the XCD's L2, where a plain or sc1 load of the
+    // counter could keep hitting a line cached before the head's add (measured: ~3 us later)
+    while ((int)(__hip_atomic_fetch_add(a.cnt + bi, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000ull) {  // 20 ms at 100 MHz
+        atomicAdd(&a.metrics[0], __builtin_nanf(""));
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  f4 dh;
+  dh.x = __hip_atomic_load(a.dH + bi * 128 + n4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  dh.y = __hip_atomic_load(a.dH + bi * 128 + n4 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  dh.z = __hip_atomic_load(a.dH + bi * 128 + n4 + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  dh.w = __hip_atomic_load(a.dH + bi * 128 + n4 + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  float v[25];
+#pragma unroll
+  for (int j = 0; j < 25; ++j) {
+    const f4 p = w3v[j] * dh;
+    v[j] = (p.x + p.y) + (p.z + p.w);
+  }
+  // sum over the 32 lanes of the row group (column groups n4): reduce-scatter butterfly, lane
+  // (l & 31) ends with feature rg * 25 + (l & 31) (features 25..31 are zero padding)
+  const float d = reduce_scatter32<25>(v, lane);
+  const int j = lane & 31;
+  if (j < 25) {
+    const int kk = rg * 25 + j;
+    a.dP2[(size_t)bi * 1600 + (kk >> 4) * 64 + 16 * cq + (kk & 15)] = p2s[kk] > 0.f ? d : 0.f;
+  }
+  stamp(a.stamps, 7);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -953,9 +993,8 @@ __global__ __launch_bounds__(256) void k_sgd_momentum(float* __restrict__ w, con
 // --------------------------------------------------------------------------------------------
 // launchers
 // --------------------------------------------------------------------------------------------
-void mnist_dense1_bwd(const MnistArgs& a, bool with_dense, hipStream_t s) {
-  const int tasks = ((a.b + 15) / 16) * 100 + (with_dense ? kDenseTasks : 0);
-  hipLaunchKernelGGL(k_dense1_bwd, dim3((tasks + 3) / 4), dim3(256), 0, s, a, with_dense ? 1 : 0);
+void mnist_dense_wgrad(const MnistArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_dense1_bwd, dim3((kDenseTasks + 3) / 4), dim3(256), 0, s, a);
 }
 void mnist_conv_bwd(const MnistArgs& a, hipStream_t s) {
   static bool attr = false;

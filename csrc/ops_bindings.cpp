@@ -141,8 +141,9 @@ std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, c10::optional<a
   int given = 0;
   at::Tensor part;
   if (part_in.has_value() && part_in->defined()) {
-    // (dz, part) from conv_dgrad_bn: dy IS the group's masked gradient dz (returned as the residual's)
-    TORCH_CHECK(mode == 2, "batch_norm backward: precomputed partials are for the add+relu group");
+    // (dz, part) from conv_dgrad_bn: dy IS the group's masked gradient dz (for an add+relu group
+    // also returned as the residual's)
+    TORCH_CHECK(mode >= 1, "batch_norm backward: precomputed partials are for relu / add+relu groups");
     given = parts_rows(*part_in, C);
     part = *part_in;
   } else {

@@ -34,8 +34,6 @@ def main():
         st.forward_backward(0)
         st.finalize(True)
     for name, (k, waves, slots, grid) in KERNELS.items():
-        if grid is None:  # dense_bwd: 4 row tiles x 13 dP2 blocks + 25 dW3 blocks
-            grid = 4 * 13 + 25
         buf = torch.zeros(grid * 72, dtype=torch.int64, device=dev)
         st.forward_backward(0)
         st.finalize(True)
@@ -51,12 +49,6 @@ def main():
         starts = r[:, 0, 0]
         print(f"{name}: kernel span {span:.2f} us; workgroup start spread {(starts.max() - starts.min()) / 100:.2f} us"
               "  (median us since workgroup start, per wave)")
-        if name == "dense_bwd":
-            for lo, hi, lab in ((0, 52, "dP2"), (52, grid, "dW3")):
-                ph = [np.median((r[lo:hi, 0, k] - r[lo:hi, 0, 0]) / 100) for k in (3, 4, 5, 1, 2)]
-                print(f"  {lab:4s} blocks (median us): loads+H {ph[0]:.2f}  logits {ph[1]:.2f}  softmax {ph[2]:.2f}  "
-                      f"dH/head {ph[3]:.2f}  end {ph[4]:.2f}")
-            continue
         if name == "fwd_conv":
             # the loss head ran in the last quarter workgroup of each image: its phases
             # (0 hand-off won, 1 partials loaded, 2 logits/softmax, 3 end) follow the wave stamps

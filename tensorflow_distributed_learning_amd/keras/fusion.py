@@ -8,7 +8,9 @@ list; the plan rewrites, at execution time only (the layer graph, variables, che
   folded into the BN (only the moving mean sees it; its gradient is exactly zero in training mode),
   and the hand-written conv forward's epilogue computes the BN's batch statistics (per-tile
   channel sums of its bf16 output), so the BN skips its statistics pass over the tensor.
-* ``BatchNormalization -> ReLU``: one fused kernel pass (ops/batchnorm.py).
+* ``BatchNormalization -> ReLU``: one fused kernel pass (ops/batchnorm.py); when a Conv2D is the
+  only reader of the output, that conv's input-gradient epilogue applies the ReLU mask and reduces
+  the BN backward sums (the BN backward then skips its reduction pass over the tensor).
 * ``BatchNormalization -> Add(other) -> ReLU``: the ResNet block tail, one fused pass that also
   produces the residual's gradient.
 * ``ZeroPadding2D -> MaxPooling2D('valid')``: one pooling pass with implicit zero padding.
@@ -31,11 +33,14 @@ from . import layers as L
 
 
 class Group:
-    __slots__ = ("bn_node", "relu", "residual", "conv_layer", "out", "last")
+    __slots__ = ("bn_node", "relu", "residual", "conv_layer", "out", "last", "conv_reader")
 
-    def __init__(self, bn_node, relu, residual, conv_layer, out, last):
+    def __init__(self, bn_node, relu, residual, conv_layer, out, last, conv_reader=False):
         self.bn_node, self.relu, self.residual, self.conv_layer, self.out, self.last = (
             bn_node, relu, residual, conv_layer, out, last)
+        # BN -> ReLU whose output is read by exactly one Conv2D: that conv's input gradient is the
+        # group's whole output gradient, so its epilogue can run the group's backward reduction
+        self.conv_reader = conv_reader
 
 
 class Plan:
@@ -116,7 +121,9 @@ def plan(nodes: List[L.Node], outputs) -> Plan:
                 p.skip.add(id(c1))
         if last is not n:
             p.skip.add(id(n))
-        p.groups[id(last)] = Group(n, relu, residual, conv_layer, out, last)
+        reader = only_consumer(out) if relu and residual is None else None
+        conv_reader = reader is not None and isinstance(reader.layer, L.Conv2D) and reader.inputs is out
+        p.groups[id(last)] = Group(n, relu, residual, conv_layer, out, last, conv_reader)
     if os.environ.get("TDL_FUSE_GRAD_SUM", "1") == "1":
         _plan_grad_sums(p, nodes, consumers, outs)
     return p
@@ -178,7 +185,7 @@ def run_group(g: Group, vals, training, taps=None, boxes=None):
                          bn.beta.value if bn.beta is not None else None, bn.moving_mean.value,
                          bn.moving_variance.value, bn.momentum, bn.epsilon, relu=g.relu, residual=r, conv_bias=cb,
                          grad_out=bn._grad_targets(), part=getattr(x, "_tdl_bn_part", None))
-    if r is not None and g.relu and y.is_cuda:
+    if g.relu and (r is not None or g.conv_reader) and y.is_cuda:
         # a conv reading this group's output can fuse the group's backward reduction into its
         # input-gradient epilogue (ops/conv.py): it needs the BN input
         y._tdl_bn_src = x

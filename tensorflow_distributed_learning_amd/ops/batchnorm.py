@@ -59,7 +59,7 @@ class _BatchNormTrain(torch.autograd.Function):
         C = hip()
         xc, gamma, st, y, conv_bias = ctx.saved_tensors
         has_g, has_b, has_r, has_cb = ctx.flags
-        part = getattr(dy, "_tdl_bn_bwd_part", None) if ctx.mode == 2 else None
+        part = getattr(dy, "_tdl_bn_bwd_part", None) if ctx.mode >= 1 else None
         dy = _aligned(dy.to(xc.dtype))
         go = ctx.grad_out or (None, None)
         if part is not None and dy.dtype == xc.dtype and dy.is_contiguous() and dy.data_ptr() % 16 == 0:

@@ -228,14 +228,17 @@ class _Conv(torch.autograd.Function):
                 key = ("dgrad_s2",) + shape_key
             # fused epilogues: a gradient sum saves an add pass (2 reads + 1 write of dx, one read back),
             # the BN group reduction a read of dz, x, y and a write of dz
-            fuse_bn = other is not None and ctx.bn_src is not None and stride == (1, 1) and _FUSE_BN_BWD[0]
+            # the BN-group fusion needs the complete gradient of x: the second GradBox participant,
+            # or the only reader of x (no box)
+            fuse_bn = (ctx.bn_src is not None and (other is not None or ctx.box is None) and stride == (1, 1)
+                       and _FUSE_BN_BWD[0])
             dx_bytes = x.numel() * x.element_size()
             saved = (2 * dx_bytes if other is not None else 0) + (2 * dx_bytes if fuse_bn else 0)
             key = (key + (other is not None, fuse_bn)) if hip_fn is not None else None
             if hip_fn is not None and _pick(key, hip_fn, lambda: ref([True, False, False])()[0], saved):
                 src = ctx.bn_src
                 if fuse_bn:
-                    # full gradient of the BN -> Add -> ReLU group output x: mask it and reduce it for
+                    # full gradient of the BN (-> Add) -> ReLU group output x: mask it and reduce it for
                     # the group's BN backward in the same epilogue (ops/batchnorm.py uses the part)
                     src = src.contiguous()
                     if src.data_ptr() % 16:

@@ -127,7 +127,8 @@ def test_conv_epilogue_bn_statistics_match_bn_pass():
 
 def test_fused_bn_group_backward_in_conv_epilogue():
     """The identity block's first conv computes the previous BN -> Add -> ReLU group's masked
-    gradient and BN reductions in its input-gradient epilogue; training matches the unfused path."""
+    gradient and BN reductions in its input-gradient epilogue, and each block's 3x3 conv those of
+    the BN -> ReLU group it reads; training matches the unfused path."""
     from tensorflow_distributed_learning_amd.ops import batchnorm as B
     from tensorflow_distributed_learning_amd.ops import conv as CV
 
@@ -177,7 +178,8 @@ def test_fused_bn_group_backward_in_conv_epilogue():
 
     mf, hf, nf = run(True)
     mu, hu, nu = run(False)
-    assert nf == 2 and nu == 0  # one fused group per step (the first block's output), two steps
+    # per step: the first block's output group + the two blocks' inner BN -> ReLU groups; two steps
+    assert nf == 6 and nu == 0
     for v, a, b in zip(mf.weights, mf.get_weights(), mu.get_weights()):
         scale = max(float(np.abs(b).max()), 1e-3)
         np.testing.assert_allclose(a, b, atol=2e-2 * scale, rtol=2e-2, err_msg=v.name)
