@@ -70,6 +70,7 @@ class MnistStep {
     a_.dL = dL_.data_ptr<float>();
     a_.cnt = reinterpret_cast<unsigned*>(cnt_.data_ptr<int>());
     a_.head = 1;
+    a_.dp2_fwd = 0;
     a_.dP2 = dP2_.data_ptr<float>();
     a_.part2 = part2_.data_ptr<float>();
     a_.part1 = part1_.data_ptr<float>();
@@ -99,7 +100,7 @@ class MnistStep {
   void stage(int64_t k, bool apply_sgd) {
     hipStream_t s = cur_stream();
     switch (k) {
-      case 5: tdl::mnist_dense_wgrad(a_, s); break;
+      case 5: tdl::mnist_dense1_bwd(a_, false, s); break;
       case 6: tdl::mnist_conv_bwd(a_, s); break;
       case 8: tdl::mnist_fwd_conv(a_, s); break;
       case 9: tdl::mnist_finalize(a_, apply_sgd, dense_pending_, s); break;
@@ -113,9 +114,16 @@ class MnistStep {
     set_idx_offset(idx_off);
     hipStream_t s = cur_stream();
     tdl::mnist_fwd_conv(a_, s);
+    if (!a_.dp2_fwd) tdl::mnist_dense1_bwd(a_, false, s);
     tdl::mnist_conv_bwd(a_, s);
     dense_pending_ = true;
   }
+
+  // dP2 inside k_fwd_conv (its workgroups wait for their image's head) or in a K5 launch; the
+  // caller enables it only when the step's launches have the GPU to themselves and all 4b
+  // workgroups of k_fwd_conv fit on the device at once
+  void set_dp2_in_forward(bool on) { a_.dp2_fwd = on ? 1 : 0; }
+  bool dp2_in_forward() const { return a_.dp2_fwd != 0; }
 
   // the same step split at the point where the dense-layer gradients are final in G (after K5):
   // the engine all-reduces that bucket while backward_conv() runs
@@ -123,7 +131,7 @@ class MnistStep {
     set_idx_offset(idx_off);
     hipStream_t s = cur_stream();
     tdl::mnist_fwd_conv(a_, s);
-    tdl::mnist_dense_wgrad(a_, s);
+    tdl::mnist_dense1_bwd(a_, true, s);
     dense_pending_ = false;
   }
   void backward_conv() { tdl::mnist_conv_bwd(a_, cur_stream()); }
@@ -211,6 +219,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("forward_dense", &MnistStep::forward_dense)
       .def("backward_conv", &MnistStep::backward_conv)
       .def("finalize", &MnistStep::finalize)
+      .def("set_dp2_in_forward", &MnistStep::set_dp2_in_forward)
+      .def("dp2_in_forward", &MnistStep::dp2_in_forward)
       .def("buffers", &MnistStep::buffers)
       .def("set_stamps", &MnistStep::set_stamps);
   m.def("sgd", &sgd);

@@ -42,6 +42,9 @@ struct MnistArgs {
   float* logits;      // [b][10] logits output of head mode 2 (null: metrics only)
   int head;           // 1: training loss head (dH, dL, saved activations); 2: evaluation head
                       // (logits, loss / accuracy accumulators, nothing saved); 0: features only
+  int dp2_fwd;        // head == 1: dP2 computed at the end of k_fwd_conv (each quarter workgroup
+                      // waits for its image's head; only when the launch has the GPU to itself and
+                      // every workgroup fits at once), else by k_dense1_bwd
 };
 
 constexpr int kMnistPart2Rows = 289;
@@ -49,8 +52,9 @@ constexpr int kDense1Chunks = 4;  // dense1 partials: one per conv2 channel quar
 constexpr int kMnistPart1Cols = 320;
 __host__ __device__ inline int mnist_part1_rows(int b) { return 2 * b; }
 
-// the dense weight gradients dW3/db3/dW4/db4 (R > 1: ahead of the conv backward)
-void mnist_dense_wgrad(const MnistArgs& a, hipStream_t s);
+// K5: dP2 tiles (unless a.dp2_fwd) and, with `dense`, the dense weight gradients dW3/db3/dW4/db4
+// (R > 1: ahead of the conv backward, so their bucket's all-reduce overlaps it)
+void mnist_dense1_bwd(const MnistArgs& a, bool dense, hipStream_t s);
 void mnist_conv_bwd(const MnistArgs& a, hipStream_t s);
 // conv1 + conv2 + dense1 partials per (image, quarter); with a.head the image's last quarter
 // workgroup also runs the loss head (dense1 sum + ReLU, dense2, softmax-xent, dlogits, metrics),

@@ -1,7 +1,7 @@
 // Fused MNIST-CNN training step for gfx950 (MI355X), f32 end to end.
 //
 // Replaces, for the reference model of tf_dist_example.py:40-52, the ~35 TF/cuDNN/Eigen kernels
-// of one replica step by three launches (four at R > 1):
+// of one replica step by three launches (one replica alone on its GPU) or four:
 //
 //   KA fwd_conv     : per (image, channel quarter), LDS-staged: gather(idx) + conv1 3x3 (1->32)
 //                     and conv2 3x3 (32->64) on v_mfma_f32_16x16x4_f32 with bias + ReLU + maxpool2
@@ -9,10 +9,12 @@
 //                     dense1 partial [1600/4 features] x W3 (W3 slice prefetched in registers);
 //                     the LAST of an image's 4 quarter workgroups (arrival counter) then runs the
 //                     head for that image: dense1 partial sum + bias + ReLU, dense2 + softmax-xent
-//                     + dlogits*(1/(b*R)) + loss/accuracy accumulators + dH (ReLU mask); every
-//                     quarter workgroup then waits for its image's dH and computes its 400
+//                     + dlogits*(1/(b*R)) + loss/accuracy accumulators + dH (ReLU mask); with
+//                     dp2_fwd every quarter workgroup then waits for its image's dH and computes its 400
 //                     features of dP2 = (dH W3^T) * relu-mask from the W3 slice in its registers
-//   K5 dense1_bwd   : (R > 1 only) the dense weight gradients dW3/db3/dW4/db4, so their bucket's
+//   K5 dense1_bwd   : dP2 = (dH W3^T) * relu-mask when k_fwd_conv did not compute it (the
+//                     launch shares the GPU or its workgroups do not all fit at once), and at
+//                     R > 1 the dense weight gradients dW3/db3/dW4/db4, so their bucket's
 //                     all-reduce overlaps the conv backward
 //   KC conv_bwd     : per image (x4 parts), LDS-staged (dC2 expanded from dP2 + pool-2 argmax):
 //                     dW2 (+db2 as an extra "ones" row) and
@@ -337,12 +339,56 @@ __device__ __forceinline__ void dense_w_task(const MnistArgs& a, int T, int lane
   }
 }
 
-// K5 (R > 1 only): the dense weight gradients dW3/db3/dW4/db4 of the step, one task per wave, so
+// dP2 = (dH W3^T) * 1[P2 > 0] (M = b, N = 1600, K = 128): one 16x16 tile per wave task, the
+// pool-2 / ReLU mask in the epilogue (k_conv_bwd expands it to the conv2-output gradient)
+__device__ __forceinline__ void dp2_task(const MnistArgs& a, int T, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  const int b = a.b;
+  const int MT = (b + 15) >> 4;
+  const int mt = T % MT, nt = T / MT;
+  const int row = mt * 16 + i;
+  const bool valid = row < b;
+  const float* ap = a.dH + (valid ? row : 0) * 128 + 4 * g;
+  const float* bp = a.W + a.ow3 + (size_t)(nt * 16 + i) * 128 + 4 * g;
+  f4 av[8], bv[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    av[s] = ld4(ap + s * 16);
+    bv[s] = ld4(bp + s * 16);
+  }
+  float p2v[4];  // the epilogue's ReLU-mask operands in the same round trip
+#pragma unroll
+  for (int r = 0; r < 4; ++r) p2v[r] = a.P2[(size_t)min(mt * 16 + 4 * g + r, b - 1) * 1600 + nt * 16 + i];
+  __builtin_amdgcn_sched_barrier(0);
+  const float vm = valid ? 1.f : 0.f;
+  f4 acc0 = zero4(), acc1 = zero4();
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const f4 x = av[s] * vm;
+    acc0 = mfma16x16x4(x.x, bv[s].x, acc0);
+    acc1 = mfma16x16x4(x.y, bv[s].y, acc1);
+    acc0 = mfma16x16x4(x.z, bv[s].z, acc0);
+    acc1 = mfma16x16x4(x.w, bv[s].w, acc1);
+  }
+  const f4 acc = acc0 + acc1;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int rr = mt * 16 + 4 * g + r;
+    if (rr < b) a.dP2[(size_t)rr * 1600 + nt * 16 + i] = p2v[r] > 0.f ? acc[r] : 0.f;
+  }
+}
+
+// K5: tasks [0, ndp2) are dP2 tiles (when k_fwd_conv did not compute dP2), the next kDenseTasks
+// (R > 1: `dense`) the dense weight gradients dW3/db3/dW4/db4 of the step, one task per wave, so
 // that bucket's all-reduce overlaps the conv backward (at R = 1 k_finalize runs the same tasks
-// fused with SGD).  dP2 comes from k_fwd_conv.
-__global__ __launch_bounds__(256) void k_dense1_bwd(MnistArgs a) {
+// fused with SGD).
+__global__ __launch_bounds__(256) void k_dense1_bwd(MnistArgs a, int ndp2) {
   const int T = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (T < kDenseTasks) dense_w_task(a, T, threadIdx.x & 63, false, 0.f);
+  if (T < ndp2) {
+    dp2_task(a, T, threadIdx.x & 63);
+    return;
+  }
+  if (T - ndp2 < kDenseTasks) dense_w_task(a, T - ndp2, threadIdx.x & 63, false, 0.f);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -844,11 +890,13 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   // saved activations leave LDS only now (off the head's critical path)
   if (!last) store_saved_fwd(a, bi, cq, P1s, a1s, p2s, a2s, tid, 512);
   else if (wave != 0) store_saved_fwd(a, bi, cq, P1s, a1s, p2s, a2s, tid - 64, 448);
+  if (!a.dp2_fwd) return;  // dP2 by k_dense1_bwd
   // ---- dP2 = (dH W3^T) * 1[P2 > 0] for this quarter's 400 features, from the W3 slice still in
-  // registers (no K5 launch, no second read of W3).  Every workgroup waits for its image's head:
-  // the head runs in the image's LAST-arriving workgroup, which is already resident, so the wait
-  // cannot depend on a workgroup that has not been dispatched.  Bounded: a head that never
-  // arrives poisons the loss metric instead of hanging the GPU.
+  // registers (no K5 launch, no second read of W3).  Every workgroup waits for its image's head,
+  // which runs in the image's last-arriving workgroup: that one may not be dispatched yet when
+  // the others start waiting, so the host selects this mode only when the launch has the GPU to
+  // itself and all of its workgroups fit at once (FusedMnistTrainStep: one replica, 4b <= CUs).
+  // Bounded: a head that never arrives poisons the loss metric instead of hanging the GPU.
   if (!last && tid == 0) {
     const unsigned want = (unsigned)s_last[1] + 5u;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -993,8 +1041,10 @@ __global__ __launch_bounds__(256) void k_sgd_momentum(float* __restrict__ w, con
 // --------------------------------------------------------------------------------------------
 // launchers
 // --------------------------------------------------------------------------------------------
-void mnist_dense_wgrad(const MnistArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_dense1_bwd, dim3((kDenseTasks + 3) / 4), dim3(256), 0, s, a);
+void mnist_dense1_bwd(const MnistArgs& a, bool dense, hipStream_t s) {
+  const int ndp2 = a.dp2_fwd ? 0 : ((a.b + 15) / 16) * 100;
+  const int tasks = ndp2 + (dense ? kDenseTasks : 0);
+  if (tasks > 0) hipLaunchKernelGGL(k_dense1_bwd, dim3((tasks + 3) / 4), dim3(256), 0, s, a, ndp2);
 }
 void mnist_conv_bwd(const MnistArgs& a, hipStream_t s) {
   static bool attr = false;

@@ -5,12 +5,14 @@
 * :func:`reference_logits`  – plain-PyTorch functional forward (NHWC semantics); the fp32/fp64
   oracle for the fused HIP kernels.
 * :class:`FusedMnistTrainStep` – one replica's fused train step on the gfx950 kernels of
-  ``csrc/kernels/mnist_cnn.hip`` (4 launches: fwd + loss head, dP2, conv bwd, finalize = partial
-  reductions + dense weight gradients [+ SGD]).
+  ``csrc/kernels/mnist_cnn.hip`` (3 launches for one replica alone on its GPU: fwd + loss head +
+  dP2, conv bwd, finalize = partial reductions + dense weight gradients [+ SGD]; otherwise dP2 and,
+  at R > 1, the dense weight gradients in a K5 launch between fwd and conv bwd).
 """
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Optional, Sequence
 
 import torch
@@ -94,6 +96,21 @@ def build_mnist_cnn(keras_module=None):
     )
 
 
+def dp2_in_forward_ok(b: int, R: int, device: torch.device) -> bool:
+    """Whether k_fwd_conv may compute dP2 itself (one launch fewer per step).  Its quarter
+    workgroups then wait for their image's loss head, which runs in the image's last-arriving
+    workgroup; that is only safe when all 4b workgroups are resident together: one replica alone on
+    its GPU (no other process's kernels, no concurrent all-reduce) and 4b <= compute units.
+    ``TDL_MNIST_DP2_FWD=0/1`` overrides (1 still requires 4b <= CUs)."""
+    mode = os.environ.get("TDL_MNIST_DP2_FWD", "auto")
+    if mode == "0" or device.type != "cuda":
+        return False
+    fits = 4 * b <= torch.cuda.get_device_properties(device).multi_processor_count
+    if mode == "1":
+        return fits
+    return fits and R == 1 and os.environ.get("TDL_SHARE_GPU") != "1"
+
+
 class FusedMnistTrainStep:
     """One replica's MNIST train step on the hand-written gfx950 kernels.
 
@@ -122,6 +139,8 @@ class FusedMnistTrainStep:
         # G[dense_offset:] (dense kernels/biases) is final after forward_dense(); G[:dense_offset]
         # (conv kernels/biases) after backward_conv() + finalize()
         self.dense_offset = int(layout.offsets[4])
+        self.dp2_in_forward = dp2_in_forward_ok(self.b, self.R, W.device)
+        self._impl.set_dp2_in_forward(self.dp2_in_forward)
 
     def forward_backward(self, idx_offset: int) -> None:
         self._impl.forward_backward(int(idx_offset))

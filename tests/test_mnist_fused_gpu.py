@@ -38,6 +38,41 @@ def test_fused_grads_match_reference(cuda, b, R):
     step.forward_backward(off)
     step.finalize(False)
     torch.cuda.synchronize()
+    _check_step(step, X, Y, params, layout, G, idx, off, b, R)
+
+
+@pytest.mark.parametrize("mode", ["0", "1"])
+@pytest.mark.parametrize("split", [False, True])
+def test_fused_dp2_modes(cuda, monkeypatch, mode, split):
+    """dP2 in the forward kernel (workgroups wait for their image's head) or in the K5 launch, on
+    the single-launch-sequence path and on the R > 1 split (forward_dense / backward_conv)."""
+    monkeypatch.setenv("TDL_MNIST_DP2_FWD", mode)
+    b, R = 64, 2
+    X, Y, params, layout, W, G, idx, lr, step = _setup(cuda, b, R)
+    assert step.dp2_in_forward == (mode == "1")
+    off = 2 * b
+    if split:
+        step.forward_dense(off)
+        step.backward_conv()
+    else:
+        step.forward_backward(off)
+    step.finalize(False)
+    torch.cuda.synchronize()
+    _check_step(step, X, Y, params, layout, G, idx, off, b, R)
+
+
+def test_dp2_mode_selection(cuda, monkeypatch):
+    monkeypatch.delenv("TDL_MNIST_DP2_FWD", raising=False)
+    monkeypatch.delenv("TDL_SHARE_GPU", raising=False)
+    cus = torch.cuda.get_device_properties(cuda).multi_processor_count
+    assert M.dp2_in_forward_ok(cus // 4, 1, cuda)
+    assert not M.dp2_in_forward_ok(cus // 4 + 1, 1, cuda)  # not every workgroup resident at once
+    assert not M.dp2_in_forward_ok(16, 2, cuda)  # replicas: concurrent all-reduce kernels
+    monkeypatch.setenv("TDL_SHARE_GPU", "1")
+    assert not M.dp2_in_forward_ok(16, 1, cuda)
+
+
+def _check_step(step, X, Y, params, layout, G, idx, off, b, R):
     ids = idx[off:off + b].long()
     x, y = X[ids], Y[ids]
     grads, logits, ce = _ref_grads(params, x, y, R)
