@@ -7,10 +7,13 @@ SparseCategoricalAccuracy) on a GPU replica is compiled into:
 * the model's flat parameter/gradient slabs (the same storage its MirroredVariables view);
 * a device-resident dataset (data/device.py) with per-step index vectors;
 * :class:`~..models.mnist_cnn.FusedMnistTrainStep` (hand-written gfx950 kernels);
-* the cross-replica gradient all-reduce on RCCL (``world > 1``) followed by the SGD kernel;
-* ONE hipGraph per execution of ``steps_per_execution`` steps, replayed with a new index vector;
-  with R > 1 the RCCL all-reduce is captured inside it as two buckets on a side stream, the dense
-  bucket overlapping the conv backward kernel (``_train_step``).
+* the cross-replica gradient all-reduce (``world > 1``): on one node the xGMI all-reduce kernel
+  with the SGD update fused into it, one 900 KB message per step; RCCL otherwise, followed by the
+  SGD kernel;
+* ONE hipGraph per execution of ``steps_per_execution`` steps, replayed with a new index vector,
+  the all-reduce captured inside it on the step's stream (serial; the side-stream overlap of a
+  dense bucket with the conv backward is opt-in, TDL_OVERLAP_ALLREDUCE=1, and measured slower:
+  profiles/mnist_side_stream_ab_r2.txt).
 
 Host work per execution: one H2D copy of K*B int32 indices and one graph launch.  Metrics (loss
 sum, correct count, sample count) are accumulated by the loss kernel on the device and reduced
@@ -92,6 +95,12 @@ def eligible(model, dataset=None) -> Optional[str]:
     return None
 
 
+def overlap_enabled() -> bool:
+    """TDL_OVERLAP_ALLREDUCE=1: R > 1 steps all-reduce the dense bucket on a side stream while the
+    conv backward runs (a forked execution graph); default serial."""
+    return os.environ.get("TDL_OVERLAP_ALLREDUCE", "0") == "1"
+
+
 class FusedMnistTrainer:
     kind = "fused"
 
@@ -120,7 +129,13 @@ class FusedMnistTrainer:
         # fails on some rank; then each step's graph is followed by an eager all-reduce + update.
         self._capture_comm = None
         self._comm_stream = None
-        self.overlap = os.environ.get("TDL_OVERLAP_ALLREDUCE", "1") == "1"
+        # R > 1: the dense bucket's all-reduce on a side stream overlapping the conv backward is
+        # opt-in; serial is the default: on one MI355X (2 replica processes sharing it) the forked
+        # execution graph ran 350 us/step against 68.6 serial (profiles/mnist_side_stream_ab_r2.txt)
+        self.overlap = overlap_enabled()
+        # off by default: measured 52.2 vs 36.2 us/step at K=1000 (profiles/mnist_side_stream_ab_r2.txt);
+        # the fork/join of a parallel hipGraph branch costs more than the ~4.5 us it hides
+        self.side_sgd = os.environ.get("TDL_MNIST_SIDE_SGD", "0") == "1"
         # index-upload slots (one captured graph each): the host may run this many executions ahead
         # of the GPU, which absorbs host hiccups such as an epoch's shuffle (~ms) without starving it
         self._nslots = max(2, int(os.environ.get("TDL_INDEX_SLOTS", "4")))
@@ -175,22 +190,31 @@ class FusedMnistTrainer:
         return st
 
     def _apply(self, st, global_b: int):
-        """finalize + (all-reduce) + optimizer for one step."""
+        """finalize + (all-reduce) + optimizer for one step.  R > 1 with plain SGD: one all-reduce
+        of the whole 900 KB slab with the SGD update fused into it (xGMI kernel), when the
+        communicator has one."""
         opt = self.optimizer
         plain = opt.momentum == 0
         if self.R == 1 and plain:
             st.finalize(True)
             return
         st.finalize(False)
+        if self.R > 1 and plain and self.comm.all_reduce_sgd(self.G, self.W, opt.lr_dev):
+            return
         self._reduce_and_update()
 
     def _train_step(self, st, off: int, global_b: int):
-        """One whole step on the current stream.  With R > 1 the gradient all-reduce runs as two
+        """One whole step on the current stream.  R > 1 default (serial): forward + backward,
+        finalize, then ONE all-reduce of the 900 KB gradient slab with the SGD update fused into it
+        (_apply).  With TDL_OVERLAP_ALLREDUCE=1 the gradient all-reduce instead runs as two
         buckets: the dense-layer bucket (G[dense_offset:], 91% of the bytes) is final after
         forward_dense() and reduces on a side stream while the conv backward runs; the conv bucket
         follows finalize().  With the xGMI one-shot communicator each bucket's all-reduce also
         applies plain SGD to its own parameter range (W[dense_offset:] is not read again in the
         step), so no separate optimizer kernel runs; otherwise the optimizer waits for both."""
+        if self.R == 1 and self.side_sgd and self.optimizer.momentum == 0:
+            st.train_step_sgd(off)  # dense wgrad + SGD on a side stream, concurrent with conv bwd
+            return
         if self.R == 1 or not self.overlap:
             st.forward_backward(off)
             self._apply(st, global_b)

@@ -99,16 +99,18 @@ def build_mnist_cnn(keras_module=None):
 def dp2_in_forward_ok(b: int, R: int, device: torch.device) -> bool:
     """Whether k_fwd_conv may compute dP2 itself (one launch fewer per step).  Its quarter
     workgroups then wait for their image's loss head, which runs in the image's last-arriving
-    workgroup; that is only safe when all 4b workgroups are resident together: one replica alone on
-    its GPU (no other process's kernels, no concurrent all-reduce) and 4b <= compute units.
-    ``TDL_MNIST_DP2_FWD=0/1`` overrides (1 still requires 4b <= CUs)."""
+    workgroup; that is only safe when all 4b workgroups are resident together: 4b <= compute units
+    and no other process's kernels on the GPU (not TDL_SHARE_GPU).  Within a replica nothing runs
+    alongside k_fwd_conv: every all-reduce of step k (also the side-stream one of the overlap
+    option) completes before step k+1's forward.  ``TDL_MNIST_DP2_FWD=0/1`` overrides (1 still
+    requires 4b <= CUs)."""
     mode = os.environ.get("TDL_MNIST_DP2_FWD", "auto")
     if mode == "0" or device.type != "cuda":
         return False
     fits = 4 * b <= torch.cuda.get_device_properties(device).multi_processor_count
     if mode == "1":
         return fits
-    return fits and R == 1 and os.environ.get("TDL_SHARE_GPU") != "1"
+    return fits and os.environ.get("TDL_SHARE_GPU") != "1"
 
 
 class FusedMnistTrainStep:
@@ -144,6 +146,11 @@ class FusedMnistTrainStep:
 
     def forward_backward(self, idx_offset: int) -> None:
         self._impl.forward_backward(int(idx_offset))
+
+    def train_step_sgd(self, idx_offset: int) -> None:
+        """One replica, plain SGD: the whole step (forward, backward, SGD); the dense weight
+        gradients and their update run on a side stream while the conv backward runs."""
+        self._impl.train_step_sgd(int(idx_offset))
 
     def forward_eval(self, idx_offset: int, logits: Optional[torch.Tensor] = None) -> None:
         """Forward only (evaluate / predict): loss, correct and sample counts of the b rows at
