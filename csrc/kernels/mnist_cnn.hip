@@ -131,7 +131,8 @@ __device__ __forceinline__ float reduce_scatter32(const float (&v)[N], int l) {
   return (b1 ? s2[1] : s2[0]) + __shfl_xor(b1 ? s2[0] : s2[1], 1, 64);
 }
 
-__device__ __forceinline__ void head_row(const MnistArgs& a, int r, int l, int y, const HeadWeights& hw) {
+__device__ __forceinline__ void head_row(const MnistArgs& a, int r, int l, int y, const HeadWeights& hw, float* sdh,
+                                         uint32_t tag) {
   const float* wa = hw.wa;
   const float* wb = hw.wb;
   head_stamp(a.stamps, 0);
@@ -186,10 +187,21 @@ __device__ __forceinline__ void head_row(const MnistArgs& a, int r, int l, int y
     d1 = fmaf(dl[c], wb[c], d1);
     mine = (l == c) ? dl[c] : mine;
   }
-  // dH leaves with write-through (sc1) stores: the image's other quarter workgroups, on any XCD,
-  // read it for their dP2 slice once k_fwd_conv's head-done count says it is there
-  __hip_atomic_store(a.dH + r * 128 + l, h0 > 0.f ? d0 : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(a.dH + r * 128 + l + 64, h1 > 0.f ? d1 : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const float dh0 = h0 > 0.f ? d0 : 0.f, dh1 = h1 > 0.f ? d1 : 0.f;
+  if (a.dp2_fwd) {
+    // (value, step tag) in ONE 8-B write-through (sc1) store per feature: the image's other quarter
+    // workgroups, on any XCD, poll these words themselves (data and flag in one granule: no
+    // counter round trip, no second load); this workgroup's own waves read them from LDS
+    __hip_atomic_store(a.dHt + r * 128 + l, (unsigned long long)__float_as_uint(dh0) | ((unsigned long long)tag << 32),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.dHt + r * 128 + l + 64,
+                       (unsigned long long)__float_as_uint(dh1) | ((unsigned long long)tag << 32), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    sdh[l] = dh0;
+    sdh[l + 64] = dh1;
+  }
+  a.dH[r * 128 + l] = dh0;  // plain: read by later launches (dense weight gradients, K5 dP2)
+  a.dH[r * 128 + l + 64] = dh1;
   a.H[r * 128 + l] = h0;
   a.H[r * 128 + l + 64] = h1;
   if (l < 10) a.dL[r * 10 + l] = mine;
@@ -432,8 +444,10 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
   const int i = lane & 15, g = lane >> 4;
   const int bi = blockIdx.x >> 2, p = blockIdx.x & 3;
   const int h = p & 1, half = p >> 1;
-  if (blockIdx.x == 0)  // re-arm k_fwd_conv's per-image head counters for the next step
+  if (blockIdx.x == 0) {  // re-arm k_fwd_conv's per-image head counters, next step's dP2 tag
     for (int r = tid; r < a.b; r += 512) a.cnt[r] = 0u;
+    if (tid == 0) a.ep[0] += 1u;
+  }
   stamp(a.stamps, 0);
   // ---- stage everything in LDS: every global load of the thread is issued first (one memory
   // round trip for the whole staging), then all LDS stores.  Out-of-range slots load a valid
@@ -866,8 +880,8 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   // ---- hand-off to the image's last quarter workgroup (MI355X_MICROARCH.md, inter-workgroup
   // visibility, first table row): the storing wave drains its sc1 stores, a workgroup barrier,
   // ONE agent-scope add per workgroup on the image's counter; the workgroup whose add returns
-  // 3 (mod 4) is last and reads the 4 partials with sc1 loads.  No workgroup ever waits for
-  // another (placement-independent).  k_conv_bwd (in every training step after this launch)
+  // 3 (mod 4) is last and reads the 4 partials with sc1 loads.  The election itself never waits
+  // (placement-independent).  k_conv_bwd (in every training step after this launch)
   // zeroes the counters, so a launch that did not add exactly 4 per image cannot shift the
   // election of later steps.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -875,19 +889,15 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   if (tid == 0) {
     const unsigned old = __hip_atomic_fetch_add(a.cnt + bi, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last[0] = (old & 3u) == 3u;
-    s_last[1] = (int)(old & ~3u);  // this launch's base count of the image (head done at base + 5)
   }
   __syncthreads();
   const bool last = s_last[0] != 0;
+  // dP2 hand-off tag of this step (KC advanced the epoch after the previous training forward)
+  const uint32_t tag = a.ep[0] + 1u;
+  float* sdh = red;  // [128] dH of this image (the dense1 row-group scratch is free now)
   if (last && wave == 0) {
-    if (a.head == 1) {
-      head_row(a, bi, lane, label, hw);
-      // head done: dH (sc1 stores) drained, then the image's count goes to base + 5
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) __hip_atomic_fetch_add(a.cnt + bi, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      head_eval(a, bi, lane, label, hw);
-    }
+    if (a.head == 1) head_row(a, bi, lane, label, hw, sdh, tag);
+    else head_eval(a, bi, lane, label, hw);
   }
   if (a.head != 1) return;  // evaluation: nothing is saved for a backward pass
   // saved activations leave LDS only now (off the head's critical path)
@@ -898,27 +908,37 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   // registers (no K5 launch, no second read of W3).  Every workgroup waits for its image's head,
   // which runs in the image's last-arriving workgroup: that one may not be dispatched yet when
   // the others start waiting, so the host selects this mode only when the launch has the GPU to
-  // itself and all of its workgroups fit at once (FusedMnistTrainStep: one replica, 4b <= CUs).
-  // Bounded: a head that never arrives poisons the loss metric instead of hanging the GPU.
-  if (!last && tid == 0) {
-    const unsigned want = (unsigned)s_last[1] + 5u;
+  // itself and all of its workgroups fit at once (FusedMnistTrainStep: 4b <= CUs, GPU not shared).
+  // Wave 0 of a waiting workgroup polls the image's 128 tagged dH words (lane i: features 4i..4i+3,
+  // 8-B sc1 loads, the same granules the head stored) until every tag is this step's, then hands
+  // the values to its workgroup through LDS.  Bounded: a head that never arrives poisons the loss
+  // metric instead of hanging the GPU.
+  if (!last && wave == 0) {
+    const unsigned long long* p = a.dHt + (size_t)bi * 128 + 4 * (lane & 31);
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    // polled with an atomic RMW: it executes past the XCD's L2, where a plain or sc1 load of the
-    // counter could keep hitting a line cached before the head's add (measured: ~3 us later)
-    while ((int)(__hip_atomic_fetch_add(a.cnt + bi, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
+    bool ok = lane >= 32;
+    f4 v = zero4();
+    for (;;) {
+      if (!ok) {
+        unsigned long long w[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w[k] = __hip_atomic_load(p + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = (uint32_t)(w[0] >> 32) == tag && (uint32_t)(w[1] >> 32) == tag && (uint32_t)(w[2] >> 32) == tag &&
+             (uint32_t)(w[3] >> 32) == tag;
+        v = f4{__uint_as_float((uint32_t)w[0]), __uint_as_float((uint32_t)w[1]), __uint_as_float((uint32_t)w[2]),
+               __uint_as_float((uint32_t)w[3])};
+      }
+      if (__all(ok)) break;
       __builtin_amdgcn_s_sleep(1);
       if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000ull) {  // 20 ms at 100 MHz
-        atomicAdd(&a.metrics[0], __builtin_nanf(""));
+        if (lane == 0) atomicAdd(&a.metrics[0], __builtin_nanf(""));
         break;
       }
     }
+    if (lane < 32) st4(sdh + 4 * lane, v);
   }
   __syncthreads();
-  f4 dh;
-  dh.x = __hip_atomic_load(a.dH + bi * 128 + n4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  dh.y = __hip_atomic_load(a.dH + bi * 128 + n4 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  dh.z = __hip_atomic_load(a.dH + bi * 128 + n4 + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  dh.w = __hip_atomic_load(a.dH + bi * 128 + n4 + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const f4 dh = ld4(sdh + n4);
   float v[25];
 #pragma unroll
   for (int j = 0; j < 25; ++j) {
