@@ -51,6 +51,7 @@ class MnistStep {
     cnt_ = at::zeros({b}, f.dtype(at::kInt));
     dHt_ = at::zeros({b * 128}, f.dtype(at::kLong));  // tag 0 never matches (tags start at 1)
     ep_ = at::zeros({1}, f.dtype(at::kInt));
+    part3t_ = at::zeros({(int64_t)tdl::kDense1Chunks * b * 128}, f.dtype(at::kLong));
     dP2_ = at::empty({b * 1600}, f);
     part2_ = at::zeros({b * tdl::kMnistPart2Rows * 64}, f);
     part1_ = at::zeros({(int64_t)tdl::mnist_part1_rows((int)b) * tdl::kMnistPart1Cols}, f);
@@ -73,6 +74,7 @@ class MnistStep {
     a_.cnt = reinterpret_cast<unsigned*>(cnt_.data_ptr<int>());
     a_.dHt = reinterpret_cast<unsigned long long*>(dHt_.data_ptr<int64_t>());
     a_.ep = reinterpret_cast<unsigned*>(ep_.data_ptr<int>());
+    a_.part3t = reinterpret_cast<unsigned long long*>(part3t_.data_ptr<int64_t>());
     a_.head = 1;
     a_.dp2_fwd = 0;
     a_.dP2 = dP2_.data_ptr<float>();
@@ -213,7 +215,7 @@ class MnistStep {
 
  private:
   at::Tensor X_, Y_, idx_, W_, G_, lr_, metrics_;
-  at::Tensor P1_, A1_, P2_, A2_, H_, dH_, dP2_, part2_, part1_, part3_, dL_, cnt_, dHt_, ep_;
+  at::Tensor P1_, A1_, P2_, A2_, H_, dH_, dP2_, part2_, part1_, part3_, dL_, cnt_, dHt_, ep_, part3t_;
   int dense_mode_ = 0;  // see tdl::mnist_finalize
   hipStream_t side_ = nullptr;
   hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;

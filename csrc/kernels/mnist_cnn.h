@@ -34,7 +34,9 @@ struct MnistArgs {
   float* dL;          // [b][10] dlogits (already scaled by 1/(b*R))
   unsigned* cnt;      // [b] per-image arrival counters of k_fwd_conv (re-armed by KC)
   unsigned long long* dHt;  // [b][128] dP2 hand-off: dH bits | tag << 32 (8-B write-through stores)
-  unsigned* ep;       // step epoch: k_fwd_conv tags dHt with *ep + 1, KC advances it
+  unsigned* ep;       // step epoch: k_fwd_conv tags dHt / part3t with *ep + 1, KC advances it
+  unsigned long long* part3t;  // [4][b][128] dense1 partials as (value | tag << 32) words: the
+                               // hand-off to the image's head in quarter workgroup 3 (dp2_fwd)
   float* metrics;     // [0] loss sum, [1] correct, [2] count
   const float* lr;    // device scalar learning rate
   unsigned long long* stamps;  // optional [grid][8] phase timestamps (s_memrealtime), diagnostics

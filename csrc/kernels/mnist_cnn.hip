@@ -131,17 +131,49 @@ __device__ __forceinline__ float reduce_scatter32(const float (&v)[N], int l) {
   return (b1 ? s2[1] : s2[0]) + __shfl_xor(b1 ? s2[0] : s2[1], 1, 64);
 }
 
+constexpr int kHeadQuarter = 3;  // dp2_fwd: the quarter workgroup that runs its image's head
+
+// sown != null (dp2_fwd): the partials of the other three quarters arrive as tagged words in
+// part3t, polled here until every tag is this step's; the head quarter's own partial is in LDS
 __device__ __forceinline__ void head_row(const MnistArgs& a, int r, int l, int y, const HeadWeights& hw, float* sdh,
-                                         uint32_t tag) {
+                                         uint32_t tag, const float* sown) {
   const float* wa = hw.wa;
   const float* wb = hw.wb;
   head_stamp(a.stamps, 0);
   float hp0[kDense1Chunks], hp1[kDense1Chunks];
+  if (sown != nullptr) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    bool ok = false;
+    for (;;) {
+      if (!ok) {
+        ok = true;
 #pragma unroll
-  for (int c = 0; c < kDense1Chunks; ++c) {
-    hp0[c] = __hip_atomic_load(a.part3 + ((size_t)c * a.b + r) * 128 + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    hp1[c] = __hip_atomic_load(a.part3 + ((size_t)c * a.b + r) * 128 + l + 64, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+        for (int c = 0; c < kDense1Chunks; ++c) {
+          if (c == kHeadQuarter) continue;
+          const unsigned long long* p = a.part3t + ((size_t)c * a.b + r) * 128 + l;
+          const unsigned long long w0 = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const unsigned long long w1 = __hip_atomic_load(p + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = ok && (uint32_t)(w0 >> 32) == tag && (uint32_t)(w1 >> 32) == tag;
+          hp0[c] = __uint_as_float((uint32_t)w0);
+          hp1[c] = __uint_as_float((uint32_t)w1);
+        }
+      }
+      if (__all(ok)) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000ull) {  // 20 ms at 100 MHz
+        if (l == 0) atomicAdd(&a.metrics[0], __builtin_nanf(""));
+        break;
+      }
+    }
+    hp0[kHeadQuarter] = sown[l];
+    hp1[kHeadQuarter] = sown[l + 64];
+  } else {
+#pragma unroll
+    for (int c = 0; c < kDense1Chunks; ++c) {
+      hp0[c] = __hip_atomic_load(a.part3 + ((size_t)c * a.b + r) * 128 + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      hp1[c] = __hip_atomic_load(a.part3 + ((size_t)c * a.b + r) * 128 + l + 64, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   float h0 = hw.b3a, h1 = hw.b3b;
 #pragma unroll
@@ -647,7 +679,7 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
 //   with the 205 KB W3 slice loaded into registers at kernel start (its latency hides behind the
 //   convolutions); the head sums the 4 quarter partials + bias + ReLU.
 // --------------------------------------------------------------------------------------------
-constexpr int kLdsFwd = 784 + 320 + 169 * kP1Stride + 72 * 16 * 4 + 400 + 169 * 32 / 4 + 400 / 4 + 16 * 128 + 4;
+constexpr int kLdsFwd = 784 + 320 + 169 * kP1Stride + 72 * 16 * 4 + 400 + 169 * 32 / 4 + 400 / 4 + 16 * 128 + 4 + 128;
 
 // Saved-for-backward activations of one (image, quarter) workgroup, written from LDS AFTER the
 // head hand-off (no global store sits in the conv phases, where it would queue behind the W3
@@ -861,12 +893,32 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
     st4(red + rg * 128 + n4, hs);
   }
   __syncthreads();
+  // dp2_fwd (training): every workgroup resident at once, so the head runs in a fixed quarter
+  // workgroup that polls the other quarters' tagged partials; otherwise the last to arrive runs it
+  const bool tagged = a.head == 1 && a.dp2_fwd;
+  const uint32_t tag = a.ep[0] + 1u;  // this step's hand-off tag (KC advanced the epoch)
+  float* sown = red + 16 * 128 + 4;   // [128] the head quarter's own partial
   if (tid < 32) {
     f4 hsum = zero4();
 #pragma unroll
     for (int k = 0; k < 16; ++k) hsum += ld4(red + k * 128 + 4 * tid);
-    // 16-B sc1 store: the image's head may run on another XCD (hand-off below)
-    st4_sc1(buf_rsrc(a.part3 + ((size_t)cq * a.b + bi) * 128, 512), tid * 16, hsum);
+    if (!tagged) {
+      // 16-B sc1 store: the image's head may run on another XCD (hand-off below)
+      st4_sc1(buf_rsrc(a.part3 + ((size_t)cq * a.b + bi) * 128, 512), tid * 16, hsum);
+    } else if (cq == kHeadQuarter) {
+      st4(sown + 4 * tid, hsum);
+    } else {
+      // (value, tag) words, 8-B write-through stores, polled by the head quarter
+      unsigned long long* p = a.part3t + ((size_t)cq * a.b + bi) * 128 + 4 * tid;
+      const unsigned long long tg = (unsigned long long)tag << 32;
+      __hip_atomic_store(p, (unsigned long long)__float_as_uint(hsum.x) | tg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p + 1, (unsigned long long)__float_as_uint(hsum.y) | tg, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p + 2, (unsigned long long)__float_as_uint(hsum.z) | tg, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p + 3, (unsigned long long)__float_as_uint(hsum.w) | tg, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   stamp(a.stamps, 6);
   if (a.head == 0) {
@@ -884,19 +936,19 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   // (placement-independent).  k_conv_bwd (in every training step after this launch)
   // zeroes the counters, so a launch that did not add exactly 4 per image cannot shift the
   // election of later steps.
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    const unsigned old = __hip_atomic_fetch_add(a.cnt + bi, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last[0] = (old & 3u) == 3u;
+  if (!tagged) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned old = __hip_atomic_fetch_add(a.cnt + bi, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last[0] = (old & 3u) == 3u;
+    }
   }
-  __syncthreads();
-  const bool last = s_last[0] != 0;
-  // dP2 hand-off tag of this step (KC advanced the epoch after the previous training forward)
-  const uint32_t tag = a.ep[0] + 1u;
+  __syncthreads();  // (tagged: the head quarter's own partial in LDS)
+  const bool last = tagged ? cq == kHeadQuarter : s_last[0] != 0;
   float* sdh = red;  // [128] dH of this image (the dense1 row-group scratch is free now)
   if (last && wave == 0) {
-    if (a.head == 1) head_row(a, bi, lane, label, hw, sdh, tag);
+    if (a.head == 1) head_row(a, bi, lane, label, hw, sdh, tag, tagged ? sown : nullptr);
     else head_eval(a, bi, lane, label, hw);
   }
   if (a.head != 1) return;  // evaluation: nothing is saved for a backward pass
