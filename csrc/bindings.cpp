@@ -125,39 +125,6 @@ class MnistStep {
     dense_mode_ = 0;
   }
 
-  // one replica, plain SGD: the whole step.  The dense weight gradients + their SGD (K5) run on a
-  // side stream concurrently with the conv backward (neither reads what the other writes; inside a
-  // captured hipGraph they are parallel branches), finalize then reduces the conv partial slabs
-  // and applies SGD to the conv weights only
-  void train_step_sgd(int64_t idx_off) {
-    set_idx_offset(idx_off);
-    hipStream_t s = cur_stream();
-    if (side_ == nullptr) {
-      TORCH_CHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking) == hipSuccess, "side stream");
-      TORCH_CHECK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming) == hipSuccess, "event");
-      TORCH_CHECK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming) == hipSuccess, "event");
-    }
-    tdl::mnist_fwd_conv(a_, s);
-    if (!a_.dp2_fwd) tdl::mnist_dense1_bwd(a_, true, false, false, s);  // dP2 reads W3 before its SGD
-    TORCH_CHECK(hipEventRecord(ev_fork_, s) == hipSuccess, "event record");
-    TORCH_CHECK(hipStreamWaitEvent(side_, ev_fork_, 0) == hipSuccess, "stream wait");
-    tdl::mnist_dense1_bwd(a_, false, true, true, side_);
-    TORCH_CHECK(hipEventRecord(ev_join_, side_) == hipSuccess, "event record");
-    tdl::mnist_conv_bwd(a_, s);
-    TORCH_CHECK(hipStreamWaitEvent(s, ev_join_, 0) == hipSuccess, "stream wait");
-    tdl::mnist_finalize(a_, true, 2, s);
-    dense_mode_ = 2;
-  }
-
-  ~MnistStep() {
-    if (side_ != nullptr) {
-      (void)hipStreamSynchronize(side_);
-      (void)hipEventDestroy(ev_fork_);
-      (void)hipEventDestroy(ev_join_);
-      (void)hipStreamDestroy(side_);
-    }
-  }
-
   // dP2 inside k_fwd_conv (its workgroups wait for their image's head) or in a K5 launch; the
   // caller enables it only when the step's launches have the GPU to themselves and all 4b
   // workgroups of k_fwd_conv fit on the device at once
@@ -217,8 +184,6 @@ class MnistStep {
   at::Tensor X_, Y_, idx_, W_, G_, lr_, metrics_;
   at::Tensor P1_, A1_, P2_, A2_, H_, dH_, dP2_, part2_, part1_, part3_, dL_, cnt_, dHt_, ep_, part3t_;
   int dense_mode_ = 0;  // see tdl::mnist_finalize
-  hipStream_t side_ = nullptr;
-  hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
   at::Tensor stamps_;
   tdl::MnistArgs a_;
 };
@@ -255,7 +220,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_metrics", &MnistStep::set_metrics)
       .def("stage", &MnistStep::stage, pybind11::arg("k"), pybind11::arg("apply_sgd") = false)
       .def("forward_backward", &MnistStep::forward_backward)
-      .def("train_step_sgd", &MnistStep::train_step_sgd)
       .def("forward_features", &MnistStep::forward_features)
       .def("forward_eval", &MnistStep::forward_eval, pybind11::arg("idx_off"), pybind11::arg("logits") = pybind11::none())
       .def("forward_dense", &MnistStep::forward_dense)

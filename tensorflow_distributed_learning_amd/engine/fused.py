@@ -133,9 +133,6 @@ class FusedMnistTrainer:
         # opt-in; serial is the default: on one MI355X (2 replica processes sharing it) the forked
         # execution graph ran 350 us/step against 68.6 serial (profiles/mnist_side_stream_ab_r2.txt)
         self.overlap = overlap_enabled()
-        # off by default: measured 52.2 vs 36.2 us/step at K=1000 (profiles/mnist_side_stream_ab_r2.txt);
-        # the fork/join of a parallel hipGraph branch costs more than the ~4.5 us it hides
-        self.side_sgd = os.environ.get("TDL_MNIST_SIDE_SGD", "0") == "1"
         # index-upload slots (one captured graph each): the host may run this many executions ahead
         # of the GPU, which absorbs host hiccups such as an epoch's shuffle (~ms) without starving it
         self._nslots = max(2, int(os.environ.get("TDL_INDEX_SLOTS", "4")))
@@ -212,9 +209,6 @@ class FusedMnistTrainer:
         follows finalize().  With the xGMI one-shot communicator each bucket's all-reduce also
         applies plain SGD to its own parameter range (W[dense_offset:] is not read again in the
         step), so no separate optimizer kernel runs; otherwise the optimizer waits for both."""
-        if self.R == 1 and self.side_sgd and self.optimizer.momentum == 0:
-            st.train_step_sgd(off)  # dense wgrad + SGD on a side stream, concurrent with conv bwd
-            return
         if self.R == 1 or not self.overlap:
             st.forward_backward(off)
             self._apply(st, global_b)

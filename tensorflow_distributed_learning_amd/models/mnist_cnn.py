@@ -147,11 +147,6 @@ class FusedMnistTrainStep:
     def forward_backward(self, idx_offset: int) -> None:
         self._impl.forward_backward(int(idx_offset))
 
-    def train_step_sgd(self, idx_offset: int) -> None:
-        """One replica, plain SGD: the whole step (forward, backward, SGD); the dense weight
-        gradients and their update run on a side stream while the conv backward runs."""
-        self._impl.train_step_sgd(int(idx_offset))
-
     def forward_eval(self, idx_offset: int, logits: Optional[torch.Tensor] = None) -> None:
         """Forward only (evaluate / predict): loss, correct and sample counts of the b rows at
         ``idx_offset`` accumulate into ``metrics``; ``logits`` [>= b*10] receives their logits."""

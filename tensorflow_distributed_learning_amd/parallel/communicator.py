@@ -160,7 +160,11 @@ class TorchCommunicator(Communicator):
     def prepare_all_reduce(self, *numels):
         if self.xgmi is not None:
             if self.xgmi.prepare(*numels):
-                self.algorithm = "xgmi-oneshot+" + ("rccl" if self.backend == "nccl" else self.backend)
+                from .xgmi import choose_algo
+
+                two = any(choose_algo(int(n), self.world_size) == 1 for n in numels if 0 < int(n) <= self.xgmi.limit)
+                self.algorithm = ("xgmi-twoshot+" if two else "xgmi-oneshot+") + \
+                    ("rccl" if self.backend == "nccl" else self.backend)
             else:
                 self.xgmi = None
 

@@ -207,7 +207,12 @@ def maybe_spawn_local_replicas(n: int, spawn: Optional[bool] = None) -> Optional
     def _join():
         code = g.wait()
         if code != 0:
+            # a failed replica fails the job: this process exits non-zero as well (the replicas'
+            # own output, e.g. a GPU fault report, went to the shared stderr)
             sys.stderr.write(f"[tdl] a spawned replica exited with code {code}\n")
+            sys.stderr.flush()
+            sys.stdout.flush()
+            os._exit(code if 0 < code < 256 else 1)
 
     atexit.register(_join)
     return {"rank": 0, "world_size": n, "local_rank": 0, "local_world_size": n}

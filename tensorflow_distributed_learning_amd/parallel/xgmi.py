@@ -148,7 +148,9 @@ class XgmiAllReduce:
             graph.replay()
             torch.cuda.synchronize(dev)
             ok &= bool(torch.equal(y, want))
-        w = torch.randn(n, generator=g).to(dev)
+        # the same parameters on every rank, as in training: the two-shot SGD epilogue updates each
+        # shard on its owner and the other ranks copy the owner's result
+        w = torch.randn(n, generator=torch.Generator(device="cpu").manual_seed(4321)).to(dev)
         w_ref = w - 0.5 * want
         lr = torch.tensor([0.5], device=dev)
         ch.all_reduce_sgd(x, w, lr, 1.0)

@@ -38,6 +38,17 @@ def test_bench_two_replicas_self_launched_shared_gpu():
     assert d["config"]["replicas_identical"] is True
 
 
+def test_bench_three_replicas_two_shot_shared_gpu():
+    """R >= 3: the 900 KB slab takes the two-shot xGMI all-reduce (reduce-scatter + all-gather, SGD
+    applied by each shard's owner); its start-up self-test must pass (it used to compare every
+    rank's result with its own random parameters, which the owner-applied update cannot match)."""
+    d = _bench(["--gpus", "3", "--steps", "20", "--warmup", "5"], TDL_SHARE_GPU="1")
+    assert d["n_gpus"] == 3 and d["config"]["global_batch"] == 192
+    assert d["config"]["allreduce"] == "xgmi-twoshot+gloo", d["config"]
+    assert d["config"]["allreduce_in_graph"] is True
+    assert d["config"]["replicas_identical"] is True
+
+
 def test_bench_two_replicas_under_torchrun_shared_gpu():
     """The driver's launch form: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N."""
     import socket

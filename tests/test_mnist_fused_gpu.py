@@ -89,41 +89,6 @@ def _check_step(step, X, Y, params, layout, G, idx, off, b, R):
     assert m[2].item() == b
 
 
-@pytest.mark.parametrize("graph", [False, True])
-def test_train_step_sgd_side_stream(cuda, graph):
-    """The one-replica whole step (dense wgrad + SGD on a side stream, concurrent with the conv
-    backward) updates W exactly like forward_backward + finalize(apply_sgd)."""
-    b = 64
-    X, Y, params, layout, W, G, idx, lr, step = _setup(cuda, b, 1)
-    W0 = W.clone()
-    for k in range(3):
-        step.forward_backward((k % 3) * b)
-        step.finalize(True)
-    torch.cuda.synchronize()
-    W_ref, G_ref, m_ref = W.clone(), G.clone(), step.metrics.clone()
-    W.copy_(W0)
-    step.metrics.zero_()
-    if graph:
-        g = torch.cuda.CUDAGraph()
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.graph(g, stream=s):
-            for k in range(3):
-                step.train_step_sgd((k % 3) * b)
-        torch.cuda.synchronize()
-        W.copy_(W0)
-        step.metrics.zero_()
-        g.replay()
-    else:
-        for k in range(3):
-            step.train_step_sgd((k % 3) * b)
-    torch.cuda.synchronize()
-    assert torch.equal(W, W_ref)
-    assert torch.equal(G[: layout.offsets[4]], G_ref[: layout.offsets[4]])  # conv grads land in G
-    assert torch.equal(step.metrics[1:3], m_ref[1:3])  # loss sums use float atomics (any order)
-    assert torch.allclose(step.metrics[0], m_ref[0], rtol=1e-5)
-
-
 def test_fused_sgd_update(cuda):
     b = 64
     X, Y, params, layout, W, G, idx, lr, step = _setup(cuda, b, 1)
