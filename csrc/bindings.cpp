@@ -106,10 +106,10 @@ class MnistStep {
   void stage(int64_t k, bool apply_sgd) {
     hipStream_t s = cur_stream();
     switch (k) {
-      case 5: tdl::mnist_dense1_bwd(a_, !a_.dp2_fwd, false, false, s); break;
+      case 5: tdl::mnist_dense1_bwd(a_, !a_.dp2_fwd, false, s); break;
       case 6: tdl::mnist_conv_bwd(a_, s); break;
       case 8: tdl::mnist_fwd_conv(a_, s); break;
-      case 9: tdl::mnist_finalize(a_, apply_sgd, dense_mode_, s); break;
+      case 9: tdl::mnist_finalize(a_, apply_sgd, dense_pending_, s); break;
       default: TORCH_CHECK(false, "unknown stage");
     }
   }
@@ -120,9 +120,9 @@ class MnistStep {
     set_idx_offset(idx_off);
     hipStream_t s = cur_stream();
     tdl::mnist_fwd_conv(a_, s);
-    if (!a_.dp2_fwd) tdl::mnist_dense1_bwd(a_, true, false, false, s);
+    if (!a_.dp2_fwd) tdl::mnist_dense1_bwd(a_, true, false, s);
     tdl::mnist_conv_bwd(a_, s);
-    dense_mode_ = 0;
+    dense_pending_ = true;
   }
 
   // dP2 inside k_fwd_conv (its workgroups wait for their image's head) or in a K5 launch; the
@@ -137,12 +137,12 @@ class MnistStep {
     set_idx_offset(idx_off);
     hipStream_t s = cur_stream();
     tdl::mnist_fwd_conv(a_, s);
-    tdl::mnist_dense1_bwd(a_, !a_.dp2_fwd, true, false, s);
-    dense_mode_ = 1;
+    tdl::mnist_dense1_bwd(a_, !a_.dp2_fwd, true, s);
+    dense_pending_ = false;
   }
   void backward_conv() { tdl::mnist_conv_bwd(a_, cur_stream()); }
 
-  void finalize(bool apply_sgd) { tdl::mnist_finalize(a_, apply_sgd, dense_mode_, cur_stream()); }
+  void finalize(bool apply_sgd) { tdl::mnist_finalize(a_, apply_sgd, dense_pending_, cur_stream()); }
 
   // forward-only evaluation / inference of the b rows at idx_off: loss, correct count and sample
   // count accumulate into the metrics tensor; logits ([>= b*10] f32, optional) receive the logits
@@ -183,7 +183,7 @@ class MnistStep {
  private:
   at::Tensor X_, Y_, idx_, W_, G_, lr_, metrics_;
   at::Tensor P1_, A1_, P2_, A2_, H_, dH_, dP2_, part2_, part1_, part3_, dL_, cnt_, dHt_, ep_, part3t_;
-  int dense_mode_ = 0;  // see tdl::mnist_finalize
+  bool dense_pending_ = true;  // finalize computes the dense weight gradients (forward_backward)
   at::Tensor stamps_;
   tdl::MnistArgs a_;
 };

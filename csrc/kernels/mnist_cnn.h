@@ -56,19 +56,16 @@ constexpr int kDense1Chunks = 4;  // dense1 partials: one per conv2 channel quar
 constexpr int kMnistPart1Cols = 320;
 __host__ __device__ inline int mnist_part1_rows(int b) { return 2 * b; }
 
-// K5: with `dp2` the dP2 tiles, with `dense` the dense weight gradients dW3/db3/dW4/db4 (R > 1:
-// ahead of the conv backward, so their bucket's all-reduce overlaps it), with `sgd` fused with plain
-// SGD of those weights (one replica: on a side stream, concurrent with the conv backward)
-void mnist_dense1_bwd(const MnistArgs& a, bool dp2, bool dense, bool sgd, hipStream_t s);
+// K5: with `dp2` the dP2 tiles, with `dense` the dense weight gradients dW3/db3/dW4/db4 (R > 1 with
+// the overlapped all-reduce: ahead of the conv backward, so their bucket's all-reduce overlaps it)
+void mnist_dense1_bwd(const MnistArgs& a, bool dp2, bool dense, hipStream_t s);
 void mnist_conv_bwd(const MnistArgs& a, hipStream_t s);
 // conv1 + conv2 + dense1 partials per (image, quarter); with a.head the image's last quarter
 // workgroup also runs the loss head (dense1 sum + ReLU, dense2, softmax-xent, dlogits, metrics),
 // and with a.head == 1 every workgroup then computes its quarter of dP2
 void mnist_fwd_conv(const MnistArgs& a, hipStream_t s);
-// partial-slab reductions (+ SGD when apply_sgd); dense_mode 0: also the dense weight gradients
-// (+ their SGD), 1: dense gradients already in G (their SGD sweep when apply_sgd), 2: dense
-// gradients and their SGD done by K5
-void mnist_finalize(const MnistArgs& a, bool apply_sgd, int dense_mode, hipStream_t s);
+// partial-slab reductions (+ the dense weight gradients when with_dense) (+ SGD when apply_sgd)
+void mnist_finalize(const MnistArgs& a, bool apply_sgd, bool with_dense, hipStream_t s);
 
 // Plain SGD over a flat slab: w -= lr * g  (lr read from device memory).
 void sgd_apply(float* w, const float* g, const float* lr, int64_t n, hipStream_t s);

@@ -427,15 +427,13 @@ __device__ __forceinline__ void dp2_task(const MnistArgs& a, int T, int lane) {
 // (R > 1: `dense`) the dense weight gradients dW3/db3/dW4/db4 of the step, one task per wave, so
 // that bucket's all-reduce overlaps the conv backward (at R = 1 k_finalize runs the same tasks
 // fused with SGD).
-// With `sgd` the dense tasks also apply plain SGD to their outputs (one replica: this launch then
-// runs on a side stream concurrently with k_conv_bwd, which reads none of W3 / b3 / W4 / b4).
-__global__ __launch_bounds__(256) void k_dense1_bwd(MnistArgs a, int ndp2, int sgd) {
+__global__ __launch_bounds__(256) void k_dense1_bwd(MnistArgs a, int ndp2) {
   const int T = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (T < ndp2) {
     dp2_task(a, T, threadIdx.x & 63);
     return;
   }
-  if (T - ndp2 < kDenseTasks) dense_w_task(a, T - ndp2, threadIdx.x & 63, sgd != 0, sgd ? *a.lr : 0.f);
+  if (T - ndp2 < kDenseTasks) dense_w_task(a, T - ndp2, threadIdx.x & 63, false, 0.f);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -1116,10 +1114,10 @@ __global__ __launch_bounds__(256) void k_sgd_momentum(float* __restrict__ w, con
 // --------------------------------------------------------------------------------------------
 // launchers
 // --------------------------------------------------------------------------------------------
-void mnist_dense1_bwd(const MnistArgs& a, bool dp2, bool dense, bool sgd, hipStream_t s) {
+void mnist_dense1_bwd(const MnistArgs& a, bool dp2, bool dense, hipStream_t s) {
   const int ndp2 = dp2 ? ((a.b + 15) / 16) * 100 : 0;
   const int tasks = ndp2 + (dense ? kDenseTasks : 0);
-  if (tasks > 0) hipLaunchKernelGGL(k_dense1_bwd, dim3((tasks + 3) / 4), dim3(256), 0, s, a, ndp2, sgd ? 1 : 0);
+  if (tasks > 0) hipLaunchKernelGGL(k_dense1_bwd, dim3((tasks + 3) / 4), dim3(256), 0, s, a, ndp2);
 }
 void mnist_conv_bwd(const MnistArgs& a, hipStream_t s) {
   static bool attr = false;
@@ -1137,9 +1135,9 @@ void mnist_fwd_conv(const MnistArgs& a, hipStream_t s) {
   }
   hipLaunchKernelGGL(k_fwd_conv, dim3(a.b * 4), dim3(512), kLdsFwd * sizeof(float), s, a);
 }
-void mnist_finalize(const MnistArgs& a, bool apply_sgd, int dense_mode, hipStream_t s) {
-  const int ndb = dense_mode == 0 ? (kDenseTasks + 3) / 4 : 0;
-  const int nbs = (apply_sgd && dense_mode == 1) ? (a.nslab - a.ow3 + 255) / 256 : 0;
+void mnist_finalize(const MnistArgs& a, bool apply_sgd, bool with_dense, hipStream_t s) {
+  const int ndb = with_dense ? (kDenseTasks + 3) / 4 : 0;
+  const int nbs = (apply_sgd && !with_dense) ? (a.nslab - a.ow3 + 255) / 256 : 0;
   const int nb2 = (kMnistPart2Rows * 64 * 4 + 255) / 256;
   const int nb1 = (kMnistPart1Cols * 16 + 255) / 256;
   hipLaunchKernelGGL(k_finalize, dim3(ndb + nbs + nb2 + nb1), dim3(256), 0, s, a, apply_sgd ? 1 : 0, ndb, nbs, nb2,
