@@ -48,3 +48,65 @@ def test_communication_options_plumbing():
     tr = m._get_trainer()
     # the plan is always computed and reported; a CPU replica keeps f32 on the wire
     assert tr.plan.world == 1 and tr.plan.wire_dtype == "float32" and MNIST <= tr.plan.grad_numel < MNIST + 256
+
+
+class _FakeRccl:
+    """A world-2 'rccl' communicator that records the bucket all-reduces (identity sums)."""
+    name = "rccl"
+    algorithm = "rccl"
+    world_size = 2
+    rank = 0
+    capturable = False
+
+    def __init__(self):
+        self.calls = 0
+
+    def all_reduce_async(self, t, op="sum"):
+        self.calls += 1
+
+        class _Work:
+            def wait(self):
+                return None
+
+        return _Work()
+
+    def all_reduce(self, t, op="sum"):
+        return t
+
+    def check_health(self):
+        pass
+
+
+def test_bucket_hooks_follow_rebuilt_leaves():
+    """evaluate()/predict() rebuild the trainer's autograd leaves (GenericTrainer._make_leaves);
+    the per-bucket all-reduce hooks must move to the new leaves, or the next eager step would
+    launch no bucket all-reduce and fail with 'hooks did not fire' (advisor finding, round 1)."""
+    import torch
+
+    import tensorflow_distributed_learning_amd as tdl
+
+    tdl.keras.backend.clear_session()
+    tdl.keras.utils.set_random_seed(0)
+    strategy = tdl.distribute.OneDeviceStrategy("/cpu:0")
+    with strategy.scope():
+        inp = tdl.keras.layers.Input(shape=(6,))
+        h = tdl.keras.layers.Dense(8, activation="relu")(inp)
+        out = tdl.keras.layers.Dense(4)(h)
+        m = tdl.keras.Model(inp, out)
+        m.compile(loss=tdl.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+                  optimizer=tdl.keras.optimizers.SGD(0.1), bucket_bytes=64)
+    tr = m._get_trainer()
+    assert tr.kind == "generic"
+    fake = _FakeRccl()
+    tr.comm = fake
+    tr._buckets = tr._make_buckets()
+    assert tr._buckets is not None and len(tr._bucket_ranges) >= 2
+    x, y = torch.randn(16, 6), torch.randint(0, 4, (16,))
+    tr.train_step((x, y), 16)
+    first = fake.calls
+    assert first == len(tr._bucket_ranges)
+    old = list(tr._leaves)
+    tr._make_leaves()  # what evaluate() / predict() do
+    assert all(a is not b for a, b in zip(old, tr._leaves))
+    tr.train_step((x, y), 16)  # raised 'gradient bucket hooks did not fire' before the fix
+    assert fake.calls == 2 * first
