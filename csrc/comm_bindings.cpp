@@ -4,6 +4,9 @@
 #include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 
+#include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -13,6 +16,25 @@ namespace {
 
 void hip_ok(hipError_t e, const char* what) {
   TORCH_CHECK(e == hipSuccess, "xgmi: ", what, " failed: ", hipGetErrorString(e));
+}
+
+// ONE error word per device, shared by every channel (and by kernels that run an exchange in
+// their own workgroups): after the first timed-out wait every xGMI exchange on the device returns
+// at entry, so a dead peer costs one timeout instead of one per launch.  Never freed (process
+// lifetime; graphs may still reference it).
+uint32_t* device_error_word(int device) {
+  static std::mutex mu;
+  static std::map<int, uint32_t*> words;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = words.find(device);
+  if (it != words.end()) return it->second;
+  c10::hip::HIPGuard guard((c10::DeviceIndex)device);
+  uint32_t* p = nullptr;
+  hip_ok(hipMalloc(&p, sizeof(uint32_t)), "hipMalloc(error)");
+  hip_ok(hipMemset(p, 0, sizeof(uint32_t)), "hipMemset(error)");
+  hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  words[device] = p;
+  return p;
 }
 
 class XgmiChannel {
@@ -39,11 +61,10 @@ class XgmiChannel {
       hip_ok(hipMalloc(&sig_, sig_bytes), "hipMalloc(signals)");
     }
     hip_ok(hipMalloc(&epoch_, (size_t)blocks_ * sizeof(uint32_t)), "hipMalloc(epochs)");
-    hip_ok(hipMalloc(&err_, sizeof(uint32_t)), "hipMalloc(error)");
+    err_ = device_error_word(device_);
     hip_ok(hipMemset(buf_, 0, (size_t)(4 * cap_) * sizeof(float)), "hipMemset");
     hip_ok(hipMemset(sig_, 0, sig_bytes), "hipMemset");
     hip_ok(hipMemset(epoch_, 0, (size_t)blocks_ * sizeof(uint32_t)), "hipMemset");
-    hip_ok(hipMemset(err_, 0, sizeof(uint32_t)), "hipMemset");
     hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
     for (int r = 0; r < tdl::kXgmiMaxRanks; ++r) {
       peers_.buf[r] = nullptr;
@@ -60,7 +81,6 @@ class XgmiChannel {
     (void)hipFree(buf_);
     (void)hipFree(sig_);
     (void)hipFree(epoch_);
-    (void)hipFree(err_);
   }
 
   int64_t cap() const { return cap_; }

@@ -27,48 +27,14 @@
 // call e (and with it every read of the half) has completed.  Calls on a channel must therefore be
 // stream-ordered on each rank and issued in the same order on every rank (as for any collective).
 // The per-workgroup epoch counters live on the device, so the kernel replays inside hipGraphs.
-#include "kernels/common.h"
-#include "kernels/xgmi.h"
+#include "kernels/xgmi_device.h"
 
 namespace tdl {
 namespace {
 
-__device__ __forceinline__ bool reached(uint32_t v, uint32_t e) { return (int32_t)(v - e) >= 0; }
-
-// All stores of this workgroup done -> system-scope release -> epoch e into word [blk][rank] of
-// every peer's signal array `round` -> wait for every peer's word [blk][q] in our own array ->
-// system-scope acquire.  Returns with the whole workgroup past a barrier: true when every peer
-// arrived, false when a bounded wait timed out (error word set; the caller then writes nothing,
-// so a dead or lagging peer can never leave a half-reduced gradient or weight behind).
 template <int R>
-__device__ __forceinline__ bool xgmi_exchange(const XgmiArgs& a, int round, int blk, uint32_t e) {
-  const int tid = threadIdx.x;
-  int timed_out = 0;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid < kWave) {
-    // release: writes the XCD's L2 back so the peers' remote reads see this workgroup's stores
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const size_t word = ((size_t)round * a.sig_blocks + blk) * kXgmiMaxRanks;
-    if (tid < R && tid != a.rank)
-      __hip_atomic_store(a.p.sig[tid] + word + a.rank, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (tid < R && tid != a.rank) {  // one lane per peer; bounded wait
-      const uint32_t* f = a.p.sig[a.rank] + word + tid;
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while (!reached(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM), e)) {
-        __builtin_amdgcn_s_sleep(1);
-        if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout) {
-          __hip_atomic_fetch_or(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          timed_out = 1;
-          break;
-        }
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  return __syncthreads_or(timed_out) == 0;
+__device__ __forceinline__ bool exchange(const XgmiArgs& a, int round, int blk, uint32_t e) {
+  return xgmi_exchange<R>(a.p, a.rank, a.sig_blocks, a.timeout, a.err, round, blk, e);
 }
 
 // rank-order sum of element i (float4) over the R input halves
@@ -117,6 +83,10 @@ __global__ __launch_bounds__(256) void k_xgmi_oneshot(XgmiArgs a) {
   const int64_t i = (int64_t)blk * kXgmiBlockElems + tid * 4;
   const bool full = i + 3 < a.n;
   float* out = MODE == 0 ? a.dst : a.w;
+  if (xgmi_failed(a.err)) {  // a peer already failed to arrive: do not wait again
+    if (tid == 0) a.epoch[blk] = e;
+    return;
+  }
 
   // 1. publish
   float* mine = a.p.buf[a.rank] + half;
@@ -126,7 +96,7 @@ __global__ __launch_bounds__(256) void k_xgmi_oneshot(XgmiArgs a) {
     for (int64_t j = i; j < a.n && j < i + 4; ++j) mine[j] = a.src[j];
   }
   // 2-3. signal the peers, wait for them
-  if (!xgmi_exchange<R>(a, 0, blk, e)) {
+  if (!exchange<R>(a, 0, blk, e)) {
     if (tid == 0) a.epoch[blk] = e;
     return;
   }
@@ -149,6 +119,10 @@ __global__ __launch_bounds__(256) void k_xgmi_twoshot(XgmiArgs a) {
   const int64_t within = (int64_t)c * kXgmiBlockElems + tid * 4;
   float* out = MODE == 0 ? a.dst : a.w;
   float* mine = a.p.buf[a.rank];
+  if (xgmi_failed(a.err)) {
+    if (tid == 0) a.epoch[c] = e;
+    return;
+  }
 
   // 1. publish chunk c of every shard (reads all of src before any write of out: in place is safe)
 #pragma unroll
@@ -160,7 +134,7 @@ __global__ __launch_bounds__(256) void k_xgmi_twoshot(XgmiArgs a) {
       for (int64_t j = i; j < a.n && j < i + 4; ++j) mine[half + j] = a.src[j];
     }
   }
-  if (!xgmi_exchange<R>(a, 0, c, e)) {
+  if (!exchange<R>(a, 0, c, e)) {
     if (tid == 0) a.epoch[c] = e;
     return;
   }
@@ -177,7 +151,7 @@ __global__ __launch_bounds__(256) void k_xgmi_twoshot(XgmiArgs a) {
       for (int64_t j = i; j < a.n && j < i + 4; ++j) mine[res + j] = finish1<MODE>(a, j, sum_ranks1<R>(a, half + j));
     }
   }
-  if (!xgmi_exchange<R>(a, 1, c, e)) {
+  if (!exchange<R>(a, 1, c, e)) {
     if (tid == 0) a.epoch[c] = e;
     return;
   }

@@ -101,6 +101,17 @@ def overlap_enabled() -> bool:
     return os.environ.get("TDL_OVERLAP_ALLREDUCE", "0") == "1"
 
 
+
+def _source_key(x, y):
+    """Identity of a host data source: the tensors themselves (strong references, so a freed
+    tensor's id can never be reused for a different dataset) plus their in-place version counters."""
+    return (x, y, x._version, None if y is None else y._version)
+
+
+def _same_source(a, b) -> bool:
+    return a is not None and b is not None and a[0] is b[0] and a[1] is b[1] and a[2:] == b[2:]
+
+
 class FusedMnistTrainer:
     kind = "fused"
 
@@ -164,8 +175,8 @@ class FusedMnistTrainer:
             return None
         if lp.batch_size % self.R:
             raise ValueError(f"global batch {lp.batch_size} is not divisible by {self.R} replicas")
-        key = (id(x), id(y))
-        if key != self._data_key:
+        key = _source_key(x, y)
+        if not _same_source(self._data_key, key):
             self.X = x.reshape(len(x), 28, 28, 1).to(self.device, torch.float32).contiguous()
             self.Y = y.to(self.device, torch.int32).contiguous()
             self._data_key = key
@@ -469,9 +480,9 @@ class FusedMnistTrainer:
             return None
         if labels and (not isinstance(y, torch.Tensor) or y.dim() != 1):
             return None
-        key = (id(x), id(y) if labels else None)
+        key = _source_key(x, y if labels else None)
         cached = getattr(self, "_eval_cache", None)
-        if cached is None or cached[0] != key:
+        if cached is None or not _same_source(cached[0], key):
             X = x.reshape(len(x), 28, 28, 1).to(self.device, torch.float32).contiguous()
             Y = (y.to(self.device, torch.int32) if labels else torch.zeros(len(x), dtype=torch.int32, device=self.device)).contiguous()
             self._eval_cache = cached = (key, X, Y, {})

@@ -263,15 +263,15 @@ class _Conv(torch.autograd.Function):
             gx, gw, _ = ref([need_dx, need_dw, False])()
             if need_dx:
                 dx = gx.permute(0, 2, 3, 1)
-        if other is not None:  # library input gradient: one add
-            dx = dx + other.view_as(dx)
-        if first:  # park this contribution for the other consumer's backward
-            box.g, dx = dx, None
-            if need_dw:
+            if need_dw:  # library weight gradient: into the slab view, or returned
                 dw = gw.permute(2, 3, 1, 0)
                 if gout is not None:
                     gout.add_(dw)
                     dw = None
+        if other is not None:  # library input gradient: one add
+            dx = dx + other.view_as(dx)
+        if first:  # park this contribution for the other consumer's backward
+            box.g, dx = dx, None
         return dx, dw, None, None, None, None, None, None, None
 
 

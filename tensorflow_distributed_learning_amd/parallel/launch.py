@@ -26,8 +26,9 @@ import signal
 import socket
 import subprocess
 import sys
-import warnings
+import threading
 import time
+import warnings
 from typing import Dict, List, Optional
 
 
@@ -51,14 +52,36 @@ def free_ports(n: int, host: str = "127.0.0.1") -> List[int]:
     return ports
 
 
+def _die_with_parent():
+    """preexec hook of every replica process: the kernel sends it SIGKILL when the process that
+    started it dies (Linux PR_SET_PDEATHSIG), so replicas never outlive a crashed launcher or a
+    crashed replica 0 and spin in a collective until their own timeouts."""
+    try:
+        import ctypes
+
+        libc = ctypes.CDLL("libc.so.6", use_errno=True)
+        libc.prctl(1, int(signal.SIGKILL), 0, 0, 0)  # PR_SET_PDEATHSIG
+    except Exception:
+        pass
+
+
 class _Group:
     def __init__(self):
         self.procs: List[subprocess.Popen] = []
 
     def start(self, cmd: List[str], env: Dict[str, str]):
-        p = subprocess.Popen(cmd, env=env, start_new_session=True)
+        p = subprocess.Popen(cmd, env=env, start_new_session=True,
+                             preexec_fn=_die_with_parent if sys.platform.startswith("linux") else None)
         self.procs.append(p)
         return p
+
+    def first_failure(self) -> Optional[int]:
+        """Exit code of the first child that failed, else None."""
+        for p in self.procs:
+            c = p.poll()
+            if c not in (None, 0):
+                return c
+        return None
 
     def terminate(self, sig=signal.SIGTERM):
         for p in self.procs:
@@ -203,6 +226,7 @@ def maybe_spawn_local_replicas(n: int, spawn: Optional[bool] = None) -> Optional
     os.environ.update(RANK="0", WORLD_SIZE=str(n), LOCAL_RANK="0", LOCAL_WORLD_SIZE=str(n),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TDL_LAUNCHED="1")
     _SPAWNED = g
+    _supervise(g)
 
     def _join():
         code = g.wait()
@@ -216,6 +240,33 @@ def maybe_spawn_local_replicas(n: int, spawn: Optional[bool] = None) -> Optional
 
     atexit.register(_join)
     return {"rank": 0, "world_size": n, "local_rank": 0, "local_world_size": n}
+
+
+def _supervise(g: "_Group", poll: float = 0.2) -> threading.Thread:
+    """Replica 0 supervises the replicas it spawned: the moment one of them fails, the others are
+    terminated and this process exits with the failing code (it may be blocked inside a collective
+    with the dead replica, so this cannot wait for the main thread)."""
+
+    def run():
+        while True:
+            code = g.first_failure()
+            if code is not None:
+                sys.stderr.write(f"[tdl] a spawned replica exited with code {code}; ending the job\n")
+                sys.stderr.flush()
+                g.terminate()
+                deadline = time.time() + 5
+                while time.time() < deadline and any(p.poll() is None for p in g.procs):
+                    time.sleep(0.05)
+                g.terminate(signal.SIGKILL)
+                sys.stdout.flush()
+                os._exit(code if 0 < code < 256 else 1)
+            if all(p.poll() == 0 for p in g.procs):
+                return
+            time.sleep(poll)
+
+    t = threading.Thread(target=run, name="tdl-replica-supervisor", daemon=True)
+    t.start()
+    return t
 
 
 def main(argv=None) -> int:

@@ -292,6 +292,9 @@ class Strategy:
         if wd is not None:
             wd.stop()
             self.extended.watchdog = None
+            lv = getattr(wd, "liveness", None)
+            if lv is not None:
+                lv.shutdown()
         try:
             self.extended.communicator.shutdown()
         except Exception:
@@ -385,15 +388,7 @@ class MirroredStrategy(Strategy):
             from .launch import maybe_spawn_local_replicas
 
             launched = maybe_spawn_local_replicas(len(devs), spawn=spawn)
-            if launched is None:
-                import warnings
-
-                warnings.warn(
-                    f"MirroredStrategy: {len(devs)} devices requested but replica processes cannot be spawned "
-                    "from this entry point (interactive / `python -c` / `-m` / pytest, or TDL_AUTO_SPAWN=0); "
-                    f"running ONE replica on {devs[0]}. Start the script with "
-                    "`python -m tensorflow_distributed_learning_amd.launch --nproc-per-node N` for N replicas.",
-                    RuntimeWarning, stacklevel=2)
+            if launched is None:  # (maybe_spawn_local_replicas warned and said why)
                 devs = devs[:1]
         if launched is None:
             dev = _shared_gpu(devs[0])
@@ -404,7 +399,7 @@ class MirroredStrategy(Strategy):
             if devices is not None:
                 if lr >= len(devs):
                     raise ValueError(f"local rank {lr} has no device in {devices}")
-                dev = _shared_gpu(devs[lr])
+                dev = _shared_gpu(_task_device(devs[lr], lr))
             else:
                 dev = _replica_device(lr)
             if dev.type == "cuda":
@@ -414,6 +409,9 @@ class MirroredStrategy(Strategy):
             ext = StrategyExtended(self, dev, launched["rank"], launched["world_size"], lr, comm, opts)
         super().__init__(ext)
         if ext.world_size > 1:
+            from ..cluster.liveness import start_for_process_group
+
+            ext.watchdog = start_for_process_group(ext.rank, ext.world_size)
             ext.communicator.barrier()
 
 
@@ -458,6 +456,7 @@ class MultiWorkerMirroredStrategy(Strategy):
         cfg = resolver.config if isinstance(resolver, TFConfigClusterResolver) else parse_tf_config()
         launched = _launched()
         rendezvous = None
+        watchdog = None
         if cfg is not None and cfg.task is not None and not cfg.is_training_task:
             raise ClusterConfigError(
                 f"this process is the '{cfg.task.type}' task; MultiWorkerMirroredStrategy trains only on "
@@ -468,6 +467,10 @@ class MultiWorkerMirroredStrategy(Strategy):
             rank, world, lr, dev = local
             comm = _select_communicator(opts.implementation, dev, rank, world,
                                         timeout=opts.timeout_seconds or 1800.0) if world > 1 else LocalCommunicator(dev)
+            if world > 1:
+                from ..cluster.liveness import start_for_process_group
+
+                watchdog = start_for_process_group(rank, world)
         else:
             from ..cluster.rendezvous import Rendezvous
 
@@ -487,6 +490,7 @@ class MultiWorkerMirroredStrategy(Strategy):
             comm = _select_communicator(opts.implementation, dev, rank, world, store=rendezvous.store,
                                         host_hint=host_hint, timeout=opts.timeout_seconds or 1800.0)
         ext = StrategyExtended(self, dev, rank, world, lr, comm, opts, tf_config=cfg, rendezvous=rendezvous)
+        ext.watchdog = watchdog
         super().__init__(ext, cluster_resolver=resolver)
         if rendezvous is not None and world > 1 and os.environ.get("TDL_WATCHDOG", "1") == "1":
             from ..utils.fault import PeerWatchdog
@@ -533,6 +537,17 @@ def _shared_gpu(dev: torch.device) -> torch.device:
         if n > 0:
             return torch.device("cuda", (dev.index or 0) % n)
     return dev
+
+
+def _task_device(dev: torch.device, local_rank: int) -> torch.device:
+    """An explicit ``devices=`` entry of a task started by ``launch --local-workers``: the task's
+    devices are numbered from its first GPU (TDL_DEVICE_INDEX = first GPU + local rank), as if the
+    task ran alone on its own host."""
+    pinned = os.environ.get("TDL_DEVICE_INDEX")
+    if dev.type != "cuda" or not pinned:
+        return dev
+    first = int(pinned) - local_rank
+    return torch.device("cuda", first + (dev.index or 0))
 
 
 def _replica_device(local_rank: int) -> torch.device:

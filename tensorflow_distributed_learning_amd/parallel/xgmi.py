@@ -53,7 +53,10 @@ class XgmiAllReduce:
         self.rank, self.world, self.device, self.group = rank, world, torch.device(device), group
         # device of the small control collectives (the process group's own: cpu for gloo)
         self.ctrl = torch.device(ctrl_device) if ctrl_device is not None else self.device
-        self.timeout = float(os.environ.get("TDL_XGMI_TIMEOUT", "600"))
+        # bounded in-kernel waits: a peer that does not arrive within this many seconds sets the
+        # device's error word; every later exchange then returns at entry and the host raises at the
+        # next health check (log read / execution boundary)
+        self.timeout = float(os.environ.get("TDL_XGMI_TIMEOUT", "60"))
         self.limit = max_bytes() // 4
         self._chans: Dict[int, object] = {}
         self._selftest_chans = []
@@ -196,10 +199,11 @@ class XgmiAllReduce:
 
     def check(self) -> None:
         """Raise if any kernel of this rank timed out waiting for a peer (host sync)."""
-        for n, ch in self._chans.items():
+        for n, ch in self._chans.items():  # (one error word per device, shared by every channel)
             if ch.error():
                 raise RuntimeError(f"xgmi all-reduce: a peer did not arrive within {self.timeout:.0f} s "
                                    f"(channel of {n} elements); the job's ranks are out of step or one died")
+            break
 
     def close(self) -> None:
         self._chans.clear()

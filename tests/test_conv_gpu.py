@@ -213,3 +213,42 @@ def test_conv_fwd_bn_stats_epilogue(shape):
     torch.testing.assert_close(mm1, mm0, atol=1e-5, rtol=1e-4)
     torch.testing.assert_close(mv1, mv0, atol=1e-5, rtol=1e-4)
     torch.testing.assert_close(yb.float(), ya.float(), atol=2e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("with_box", [False, True])
+def test_conv2d_library_wgrad_reaches_slab(monkeypatch, with_box):
+    """When the autotuner picks MIOpen for a weight gradient (forced here through its decision
+    cache) the gradient still lands in the slab view ``grad_out``, with and without a GradBox
+    shared by two consumers of x (advisor finding, round 2)."""
+    monkeypatch.setenv("TDL_CONV", "auto")
+    from tensorflow_distributed_learning_amd.ops import conv as CV
+
+    shape = (4, 12, 12, 64, 64, 3, 3, 1, 1)
+    x, k = _mk(shape, "cuda:0")
+    k2 = (k.float() * 0.5).bfloat16()
+    key = (tuple(x.shape), tuple(k.shape), (1, 1), (1, 1))
+    saved = dict(CV._choice)
+    try:
+        CV._choice[("wgrad",) + key] = None  # MIOpen
+        gout = torch.zeros(k.shape, device="cuda:0")
+        gout2 = torch.zeros(k.shape, device="cuda:0")
+        xg = x.clone().requires_grad_(True)
+        box = CV.GradBox() if with_box else None
+        y = CV.conv2d_nhwc(xg, k, (1, 1), (1, 1), grad_out=gout, grad_box=box)
+        dy = torch.randn(y.shape, device="cuda:0").bfloat16()
+        if with_box:
+            y2 = CV.conv2d_nhwc(xg, k2, (1, 1), (1, 1), grad_out=gout2, grad_box=box)
+            dy2 = torch.randn(y2.shape, device="cuda:0").bfloat16()
+            torch.autograd.backward([y, y2], [dy, dy2])
+        else:
+            y.backward(dy)
+        dx_ref, dw_ref = _ref_grads(x, k, 1, 1, dy)
+        torch.testing.assert_close(gout, dw_ref, atol=0.5, rtol=3e-2)
+        if with_box:
+            dx2_ref, dw2_ref = _ref_grads(x, k2, 1, 1, dy2)
+            torch.testing.assert_close(gout2, dw2_ref, atol=0.5, rtol=3e-2)
+            dx_ref = dx_ref + dx2_ref
+        torch.testing.assert_close(xg.grad.float(), dx_ref, atol=8e-2, rtol=3e-2)
+    finally:
+        CV._choice.clear()
+        CV._choice.update(saved)
