@@ -10,6 +10,7 @@
 
 #include "kernels/mnist_cnn.h"
 #include "kernels/ops.h"
+#include "xgmi_channel.h"
 
 namespace {
 
@@ -54,7 +55,8 @@ class MnistStep {
     part3t_ = at::zeros({(int64_t)tdl::kDense1Chunks * b * 128}, f.dtype(at::kLong));
     dP2_ = at::empty({b * 1600}, f);
     part2_ = at::zeros({b * tdl::kMnistPart2Rows * 64}, f);
-    part1_ = at::zeros({(int64_t)tdl::mnist_part1_rows((int)b) * tdl::kMnistPart1Cols}, f);
+    part1_ = at::zeros({(int64_t)tdl::mnist_part1_rows((int)b, true) * tdl::kMnistPart1Cols}, f);
+    err_ = at::zeros({1}, f.dtype(at::kInt));
     part3_ = at::zeros({(int64_t)tdl::kDense1Chunks * b * 128}, f);
     a_ = tdl::MnistArgs{};
     a_.X = X_.data_ptr<float>();
@@ -77,6 +79,9 @@ class MnistStep {
     a_.part3t = reinterpret_cast<unsigned long long*>(part3t_.data_ptr<int64_t>());
     a_.head = 1;
     a_.dp2_fwd = 0;
+    a_.fused_bwd = 0;
+    a_.err = reinterpret_cast<unsigned*>(err_.data_ptr<int>());
+    a_.xchg = 0;
     a_.dP2 = dP2_.data_ptr<float>();
     a_.part2 = part2_.data_ptr<float>();
     a_.part1 = part1_.data_ptr<float>();
@@ -108,8 +113,11 @@ class MnistStep {
     switch (k) {
       case 5: tdl::mnist_dense1_bwd(a_, !a_.dp2_fwd, false, s); break;
       case 6: tdl::mnist_conv_bwd(a_, s); break;
-      case 8: tdl::mnist_fwd_conv(a_, s); break;
-      case 9: tdl::mnist_finalize(a_, apply_sgd, dense_pending_, s); break;
+      case 8:
+        a_.fused_bwd = (fused_bwd_ && a_.dp2_fwd) ? 1 : 0;
+        tdl::mnist_fwd_conv(a_, s);
+        break;
+      case 9: finalize(apply_sgd, false); break;
       default: TORCH_CHECK(false, "unknown stage");
     }
   }
@@ -119,9 +127,15 @@ class MnistStep {
   void forward_backward(int64_t idx_off) {
     set_idx_offset(idx_off);
     hipStream_t s = cur_stream();
-    tdl::mnist_fwd_conv(a_, s);
-    if (!a_.dp2_fwd) tdl::mnist_dense1_bwd(a_, true, false, s);
-    tdl::mnist_conv_bwd(a_, s);
+    if (fused_bwd_ && a_.dp2_fwd) {  // ONE launch: forward, loss head, dP2 and the conv backward
+      a_.fused_bwd = 1;
+      tdl::mnist_fwd_conv(a_, s);
+    } else {
+      a_.fused_bwd = 0;
+      tdl::mnist_fwd_conv(a_, s);
+      if (!a_.dp2_fwd) tdl::mnist_dense1_bwd(a_, true, false, s);
+      tdl::mnist_conv_bwd(a_, s);
+    }
     dense_pending_ = true;
   }
 
@@ -130,19 +144,55 @@ class MnistStep {
   // workgroups of k_fwd_conv fit on the device at once
   void set_dp2_in_forward(bool on) { a_.dp2_fwd = on ? 1 : 0; }
   bool dp2_in_forward() const { return a_.dp2_fwd != 0; }
+  // with dP2 in the forward kernel, also run the conv backward there (forward_backward only)
+  void set_fused_bwd(bool on) { fused_bwd_ = on; }
+  bool fused_bwd() const { return fused_bwd_ && a_.dp2_fwd; }
+
+  // error word of the in-kernel hand-offs (bit 1: a wait timed out; host sync); reset=true clears it
+  int64_t error(bool reset) {
+    int64_t v = err_.item<int>();
+    if (reset) err_.zero_();
+    return v;
+  }
 
   // the same step split at the point where the dense-layer gradients are final in G (after K5):
   // the engine all-reduces that bucket while backward_conv() runs
   void forward_dense(int64_t idx_off) {
     set_idx_offset(idx_off);
     hipStream_t s = cur_stream();
+    a_.fused_bwd = 0;
     tdl::mnist_fwd_conv(a_, s);
     tdl::mnist_dense1_bwd(a_, !a_.dp2_fwd, true, s);
     dense_pending_ = false;
   }
   void backward_conv() { tdl::mnist_conv_bwd(a_, cur_stream()); }
 
-  void finalize(bool apply_sgd) { tdl::mnist_finalize(a_, apply_sgd, dense_pending_, cur_stream()); }
+  // partial reductions + dense weight gradients (+ SGD).  After a fused forward_backward the
+  // fused finalize runs; with `exchange` (fused, apply_sgd, a channel set) it also all-reduces the
+  // gradient across the replicas over xGMI before the update (one launch, see k_finalize_x)
+  void finalize(bool apply_sgd, bool exchange) {
+    if (a_.fused_bwd) {
+      TORCH_CHECK(!exchange || (apply_sgd && xchg_ready_), "finalize: the exchange needs apply_sgd and set_exchange()");
+      tdl::MnistArgs f = a_;
+      f.xchg = exchange ? 1 : 0;
+      tdl::mnist_finalize_x(f, apply_sgd, cur_stream());
+      return;
+    }
+    TORCH_CHECK(!exchange, "finalize: the exchange needs the fused backward (forward_backward with fused_bwd)");
+    tdl::mnist_finalize(a_, apply_sgd, dense_pending_, cur_stream());
+  }
+
+  // the xGMI channel finalize(exchange=true) all-reduces through: exchange slots at slab offsets
+  // (capacity >= slab), one signal / epoch slot per finalize workgroup
+  void set_exchange(const tdl_host::XgmiChannel& ch) {
+    TORCH_CHECK(ch.device() == W_.get_device(), "set_exchange: channel on another device");
+    TORCH_CHECK(ch.cap() >= W_.numel(), "set_exchange: channel smaller than the slab");
+    TORCH_CHECK(ch.sig_blocks() >= tdl::kFxBlocks, "set_exchange: channel needs >= ", tdl::kFxBlocks, " signal slots");
+    TORCH_CHECK(a_.ow4 == a_.ob3 + 128 && a_.ob4 == a_.ow4 + 1280, "set_exchange: dense bias/kernel ranges not contiguous");
+    ch.fill_args(a_.xa);
+    xchg_ready_ = true;
+  }
+  bool has_exchange() const { return xchg_ready_; }
 
   // forward-only evaluation / inference of the b rows at idx_off: loss, correct count and sample
   // count accumulate into the metrics tensor; logits ([>= b*10] f32, optional) receive the logits
@@ -150,6 +200,7 @@ class MnistStep {
     set_idx_offset(idx_off);
     tdl::MnistArgs f = a_;
     f.head = 2;
+    f.fused_bwd = 0;
     f.logits = nullptr;
     if (logits.has_value()) {
       check_cuda_f32(*logits, "logits");
@@ -164,6 +215,7 @@ class MnistStep {
     set_idx_offset(idx_off);
     tdl::MnistArgs f = a_;
     f.head = 0;
+    f.fused_bwd = 0;
     tdl::mnist_fwd_conv(f, cur_stream());
   }
 
@@ -182,7 +234,9 @@ class MnistStep {
 
  private:
   at::Tensor X_, Y_, idx_, W_, G_, lr_, metrics_;
-  at::Tensor P1_, A1_, P2_, A2_, H_, dH_, dP2_, part2_, part1_, part3_, dL_, cnt_, dHt_, ep_, part3t_;
+  at::Tensor P1_, A1_, P2_, A2_, H_, dH_, dP2_, part2_, part1_, part3_, dL_, cnt_, dHt_, ep_, part3t_, err_;
+  bool fused_bwd_ = false;
+  bool xchg_ready_ = false;
   bool dense_pending_ = true;  // finalize computes the dense weight gradients (forward_backward)
   at::Tensor stamps_;
   tdl::MnistArgs a_;
@@ -224,9 +278,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("forward_eval", &MnistStep::forward_eval, pybind11::arg("idx_off"), pybind11::arg("logits") = pybind11::none())
       .def("forward_dense", &MnistStep::forward_dense)
       .def("backward_conv", &MnistStep::backward_conv)
-      .def("finalize", &MnistStep::finalize)
+      .def("finalize", &MnistStep::finalize, pybind11::arg("apply_sgd"), pybind11::arg("exchange") = false)
+      .def("set_exchange", &MnistStep::set_exchange)
+      .def("has_exchange", &MnistStep::has_exchange)
       .def("set_dp2_in_forward", &MnistStep::set_dp2_in_forward)
       .def("dp2_in_forward", &MnistStep::dp2_in_forward)
+      .def("set_fused_bwd", &MnistStep::set_fused_bwd)
+      .def("fused_bwd", &MnistStep::fused_bwd)
+      .def("error", &MnistStep::error, pybind11::arg("reset") = false)
       .def("buffers", &MnistStep::buffers)
       .def("set_stamps", &MnistStep::set_stamps);
   m.def("sgd", &sgd);

@@ -38,6 +38,12 @@ __device__ __forceinline__ void st4_sc1(__amdgpu_buffer_rsrc_t r, int byte_off, 
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), r, byte_off, 0, 16);
 }
 
+// Workgroup barrier for LDS data only: waits for this wave's LDS operations, not for its global
+// loads still in flight (__syncthreads() also drains vmcnt, i.e. waits for every outstanding
+// global load of the wave -- e.g. operand prefetches meant to overlap the next phase).  The
+// memory clobber keeps the compiler from moving LDS accesses across it.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // Sum across the four 16-lane groups of a wave (lanes l, l^16, l^32, l^48).
 __device__ __forceinline__ float sum_lane_groups(float v) {
   v += __shfl_xor(v, 16, 64);

@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "kernels/xgmi.h"
+
 namespace tdl {
 
 struct MnistArgs {
@@ -29,7 +31,7 @@ struct MnistArgs {
   float* dH;          // [b,128] grad of dense1 out (ReLU-masked)
   float* dP2;         // [b,1600] grad of the pooled conv2 output, ReLU-masked (k_fwd_conv)
   float* part2;       // [b][289][64] per-image partials of conv2 wgrad (row 288 = bias)
-  float* part1;       // [2b][320] per-(image, pixel-half) partials of conv1 wgrad (+ bias)
+  float* part1;       // [2b or 4b][320] partials of conv1 wgrad (+ bias), see mnist_part1_rows
   float* part3;       // [4][b][128] dense1 partials, one per conv2 channel quarter
   float* dL;          // [b][10] dlogits (already scaled by 1/(b*R))
   unsigned* cnt;      // [b] per-image arrival counters of k_fwd_conv (re-armed by KC)
@@ -49,12 +51,30 @@ struct MnistArgs {
   int dp2_fwd;        // head == 1: dP2 computed at the end of k_fwd_conv (each quarter workgroup
                       // waits for its image's head; only when the launch has the GPU to itself and
                       // every workgroup fits at once), else by k_dense1_bwd
+  int fused_bwd;      // dp2_fwd only: the conv backward runs at the end of k_fwd_conv, per (image,
+                      // quarter) workgroup from what it already holds in LDS: conv2 wgrad of its 16
+                      // output channels, the conv2 dgrad partial over them + pool1/ReLU backward +
+                      // conv1 wgrad (part1 rows = image quarters); no k_conv_bwd launch
+  unsigned* err;      // bit 1: an in-kernel hand-off (dense1 partials / dH) timed out; that image's
+                      // gradient contribution was zeroed (MnistStep.error() raises on the host)
+  // fused_bwd finalize with the cross-replica all-reduce built in (xchg): every finalize workgroup
+  // publishes the gradient range it just reduced into its slot of a dedicated xGMI channel (slab
+  // offsets), exchanges with the same workgroup of every peer, sums the R contributions in rank
+  // order and applies SGD to that range -- no separate all-reduce or optimizer launch
+  XgmiArgs xa;
+  int xchg;
 };
+
+// finalize workgroups of the fused_bwd step (k_finalize_x): 101 dense (dW3 rows 16m..16m+15 = 2048
+// slab floats each; the last: db3 + dW4 + db4), 289 conv2 rows (64 floats), 20 conv1 groups (16)
+constexpr int kFxDense = 101, kFxConv1 = 20;
+constexpr int kFxBlocks = kFxDense + 289 + kFxConv1;
 
 constexpr int kMnistPart2Rows = 289;
 constexpr int kDense1Chunks = 4;  // dense1 partials: one per conv2 channel quarter (k_fwd_conv)
 constexpr int kMnistPart1Cols = 320;
-__host__ __device__ inline int mnist_part1_rows(int b) { return 2 * b; }
+// conv1 wgrad partial rows: (image, pixel half) of k_conv_bwd, or (image, quarter) of fused_bwd
+__host__ __device__ inline int mnist_part1_rows(int b, bool fused_bwd = false) { return fused_bwd ? 4 * b : 2 * b; }
 
 // K5: with `dp2` the dP2 tiles, with `dense` the dense weight gradients dW3/db3/dW4/db4 (R > 1 with
 // the overlapped all-reduce: ahead of the conv backward, so their bucket's all-reduce overlaps it)
@@ -66,6 +86,9 @@ void mnist_conv_bwd(const MnistArgs& a, hipStream_t s);
 void mnist_fwd_conv(const MnistArgs& a, hipStream_t s);
 // partial-slab reductions (+ the dense weight gradients when with_dense) (+ SGD when apply_sgd)
 void mnist_finalize(const MnistArgs& a, bool apply_sgd, bool with_dense, hipStream_t s);
+// fused_bwd finalize: partial-slab reductions + dense weight gradients into G; with apply_sgd the
+// SGD update, and with a.xchg (apply_sgd only) the cross-replica sum first (xGMI exchange)
+void mnist_finalize_x(const MnistArgs& a, bool apply_sgd, hipStream_t s);
 
 // Plain SGD over a flat slab: w -= lr * g  (lr read from device memory).
 void sgd_apply(float* w, const float* g, const float* lr, int64_t n, hipStream_t s);

@@ -31,6 +31,7 @@
 
 #include "common.h"
 #include "mnist_cnn.h"
+#include "xgmi_device.h"
 
 namespace tdl {
 
@@ -131,16 +132,22 @@ __device__ __forceinline__ float reduce_scatter32(const float (&v)[N], int l) {
   return (b1 ? s2[1] : s2[0]) + __shfl_xor(b1 ? s2[0] : s2[1], 1, 64);
 }
 
-constexpr int kHeadQuarter = 3;  // dp2_fwd: the quarter workgroup that runs its image's head
+constexpr int kHeadQuarter = 3;  // dp2_fwd: the quarter workgroup whose head writes metrics / H / dH / dL
 
-// sown != null (dp2_fwd): the partials of the other three quarters arrive as tagged words in
-// part3t, polled here until every tag is this step's; the head quarter's own partial is in LDS
+// sown != null (dp2_fwd): EVERY quarter workgroup cq of the image runs this head redundantly (one
+// all-to-all exchange of the dense1 partials instead of a partials -> head -> dH round trip): the
+// other three quarters' partials arrive as tagged words in part3t, polled here until every tag
+// is this step's; its own partial is in LDS.  The sums run in quarter order in every workgroup, so
+// all four compute bit-identical dH; only the `primary` one accumulates the metrics and stores
+// H / dH / dL for the dense weight gradients.
 __device__ __forceinline__ void head_row(const MnistArgs& a, int r, int l, int y, const HeadWeights& hw, float* sdh,
-                                         uint32_t tag, const float* sown) {
+                                         uint32_t tag, const float* sown, int cq = kHeadQuarter,
+                                         bool primary = true) {
   const float* wa = hw.wa;
   const float* wb = hw.wb;
   head_stamp(a.stamps, 0);
   float hp0[kDense1Chunks], hp1[kDense1Chunks];
+  bool timed_out = false;
   if (sown != nullptr) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     bool ok = false;
@@ -149,7 +156,7 @@ __device__ __forceinline__ void head_row(const MnistArgs& a, int r, int l, int y
         ok = true;
 #pragma unroll
         for (int c = 0; c < kDense1Chunks; ++c) {
-          if (c == kHeadQuarter) continue;
+          if (c == cq) continue;
           const unsigned long long* p = a.part3t + ((size_t)c * a.b + r) * 128 + l;
           const unsigned long long w0 = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           const unsigned long long w1 = __hip_atomic_load(p + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -161,12 +168,22 @@ __device__ __forceinline__ void head_row(const MnistArgs& a, int r, int l, int y
       if (__all(ok)) break;
       __builtin_amdgcn_s_sleep(1);
       if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000ull) {  // 20 ms at 100 MHz
-        if (l == 0) atomicAdd(&a.metrics[0], __builtin_nanf(""));
+        // a quarter's partial never arrived: poison the loss metric, flag the error word, and
+        // give this image NO gradient (dH = dL = 0 below) instead of one from stale partials
+        if (l == 0) {
+          atomicAdd(&a.metrics[0], __builtin_nanf(""));
+          if (a.err != nullptr) __hip_atomic_fetch_or(a.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        timed_out = true;
         break;
       }
     }
-    hp0[kHeadQuarter] = sown[l];
-    hp1[kHeadQuarter] = sown[l + 64];
+    const float o0 = sown[l], o1 = sown[l + 64];
+#pragma unroll
+    for (int c = 0; c < kDense1Chunks; ++c) {  // (static register indices)
+      hp0[c] = c == cq ? o0 : hp0[c];
+      hp1[c] = c == cq ? o1 : hp1[c];
+    }
   } else {
 #pragma unroll
     for (int c = 0; c < kDense1Chunks; ++c) {
@@ -219,19 +236,14 @@ __device__ __forceinline__ void head_row(const MnistArgs& a, int r, int l, int y
     d1 = fmaf(dl[c], wb[c], d1);
     mine = (l == c) ? dl[c] : mine;
   }
-  const float dh0 = h0 > 0.f ? d0 : 0.f, dh1 = h1 > 0.f ? d1 : 0.f;
-  if (a.dp2_fwd) {
-    // (value, step tag) in ONE 8-B write-through (sc1) store per feature: the image's other quarter
-    // workgroups, on any XCD, poll these words themselves (data and flag in one granule: no
-    // counter round trip, no second load); this workgroup's own waves read them from LDS
-    __hip_atomic_store(a.dHt + r * 128 + l, (unsigned long long)__float_as_uint(dh0) | ((unsigned long long)tag << 32),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(a.dHt + r * 128 + l + 64,
-                       (unsigned long long)__float_as_uint(dh1) | ((unsigned long long)tag << 32), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+  const float dh0 = (h0 > 0.f && !timed_out) ? d0 : 0.f, dh1 = (h1 > 0.f && !timed_out) ? d1 : 0.f;
+  if (timed_out) mine = 0.f;
+  if (a.dp2_fwd) {  // this workgroup's waves read dH from LDS for their dP2
     sdh[l] = dh0;
     sdh[l + 64] = dh1;
   }
+  head_stamp(a.stamps, 3);
+  if (!primary) return;
   a.dH[r * 128 + l] = dh0;  // plain: read by later launches (dense weight gradients, K5 dP2)
   a.dH[r * 128 + l + 64] = dh1;
   a.H[r * 128 + l] = h0;
@@ -242,7 +254,6 @@ __device__ __forceinline__ void head_row(const MnistArgs& a, int r, int l, int y
     atomicAdd(&a.metrics[1], am == y ? 1.f : 0.f);
     atomicAdd(&a.metrics[2], 1.f);
   }
-  head_stamp(a.stamps, 3);
 }
 
 // Evaluation / inference head of ONE batch row (head mode 2): logits (optionally stored), loss and
@@ -327,7 +338,8 @@ __device__ __forceinline__ f4 gemm_tn_rows(int b, int g, FA fa, FB fb) {
 // SGD of its outputs: nothing else in the launch reads W3 / W4 then).
 constexpr int kDenseTasks = kD1TasksW3 + 9;
 
-__device__ __forceinline__ void dense_w_task(const MnistArgs& a, int T, int lane, bool sgd, float lr) {
+__device__ __forceinline__ void dense_w_task(const MnistArgs& a, int T, int lane, bool sgd, float lr,
+                                             float* xdst = nullptr) {
   const int i = lane & 15, g = lane >> 4;
   const int b = a.b;
   if (T < kD1TasksW3) {
@@ -343,6 +355,7 @@ __device__ __forceinline__ void dense_w_task(const MnistArgs& a, int T, int lane
       for (int r = 0; r < 4; ++r) {
         const int e = a.ow3 + (mt * 16 + 4 * g + r) * 128 + n;
         a.G[e] = acc[r];
+        if (xdst != nullptr) xdst[e] = acc[r];
         if (sgd) a.W[e] = wold[r] - lr * acc[r];
       }
     } else {  // db3: A = e_0 (row 0 of the tile = column sums of dH)
@@ -351,6 +364,7 @@ __device__ __forceinline__ void dense_w_task(const MnistArgs& a, int T, int lane
           b, g, [&](int) { return i == 0 ? 1.f : 0.f; }, [&](int r) { return a.dH[r * 128 + n]; });
       if (g == 0) {
         a.G[a.ob3 + n] = acc[0];
+        if (xdst != nullptr) xdst[a.ob3 + n] = acc[0];
         if (sgd) a.W[a.ob3 + n] = wold - lr * acc[0];
       }
     }
@@ -374,10 +388,12 @@ __device__ __forceinline__ void dense_w_task(const MnistArgs& a, int T, int lane
         for (int r = 0; r < 4; ++r) {
           const int e = a.ow4 + (T3 * 16 + 4 * g + r) * 10 + i;
           a.G[e] = acc[r];
+          if (xdst != nullptr) xdst[e] = acc[r];
           if (sgd) a.W[e] = wold[r] - lr * acc[r];
         }
       } else if (g == 0) {
         a.G[a.ob4 + i] = acc[0];
+        if (xdst != nullptr) xdst[a.ob4 + i] = acc[0];
         if (sgd) a.W[a.ob4 + i] = wold[0] - lr * acc[0];
       }
     }
@@ -678,6 +694,230 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
 //   convolutions); the head sums the 4 quarter partials + bias + ReLU.
 // --------------------------------------------------------------------------------------------
 constexpr int kLdsFwd = 784 + 320 + 169 * kP1Stride + 72 * 16 * 4 + 400 + 169 * 32 / 4 + 400 / 4 + 16 * 128 + 4 + 128;
+// fused_bwd: this quarter's conv2-output gradient dC2 [15][15 cells][16 channels + 4 pad] with a
+// zero border of 2 (the dgrad reads cells (ih - kh + 2, iw - kw + 2) without bounds checks).
+// Cell stride 20 floats: 16 consecutive cells of a dgrad A read (ds_read_b128) land on 16
+// distinct 4-bank groups; the 4 consecutive cells of a wgrad B read (ds_read_b32) on 4 x 16 banks.
+constexpr int kDcF = 15, kDcFStride = 20;
+constexpr int kLdsFwdFused = kLdsFwd + kDcF * kDcF * kDcFStride;
+// conv2 wgrad row tiles (first, count) per wave of the fused backward: waves w and w + 4 share a
+// SIMD; with tap skipping the dgrad MFMAs per SIMD are 192 / 168 / 144 / 144, so SIMDs 0..3 take
+// 4 / 4 / 5 / 6 of the 19 tiles (292 / 268 / 269 / 294 MFMAs per SIMD)
+__constant__ int kFusedWgradTiles[8][2] = {{0, 2}, {2, 2}, {4, 3}, {7, 3}, {10, 2}, {12, 2}, {14, 2}, {16, 3}};
+
+// phase stamp k < 4 of the fused backward, per wave, after the head stamps:
+// buf[grid*72 + (workgroup*8 + wave)*4 + k] (the buffer then holds grid * 104 words)
+__device__ __forceinline__ void bwd_stamp(unsigned long long* buf, int k) {
+  if (buf != nullptr && (threadIdx.x & 63) == 0)
+    buf[(size_t)gridDim.x * 72 + (blockIdx.x * 8 + (threadIdx.x >> 6)) * 4 + k] = __builtin_amdgcn_s_memrealtime();
+}
+
+// N consecutive conv2 wgrad row tiles t0 .. t0+N-1 (tile 18 = the bias row: A = unit vector) of
+// the fused backward, advanced together over the 25 k-steps; stores part2 rows of image bi.
+template <int N>
+__device__ __forceinline__ void fused_wgrad_tiles(const MnistArgs& a, int bi, int cq, int t0, const float* P1s,
+                                                  const float* dCs) {
+  const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  const float* pa0[N];
+  bool bias[N];
+#pragma unroll
+  for (int u = 0; u < N; ++u) {
+    const int mt = t0 + u;
+    bias[u] = mt == 18;
+    const int k = mt * 16 + i;
+    const int tap = bias[u] ? 0 : k >> 5, ci = k & 31;
+    const int kh = tap / 3, kw = tap - kh * 3;
+    pa0[u] = P1s + (kh * 13 + kw + g) * kP1Stride + ci;
+  }
+  // positions p = 10q + r + g; for r = 8 lanes g >= 2 wrap to the next row: +3 P1 cells, +5 dC cells
+  const int wrapA = g >= 2 ? 3 * kP1Stride : 0, wrapB = g >= 2 ? 5 * kDcFStride : 0;
+  const float* pb0 = dCs + (2 * kDcF + 2 + g) * kDcFStride + i;
+  const float unit_a = (i == 0) ? 1.f : 0.f;
+  f4 acc[N];
+#pragma unroll
+  for (int u = 0; u < N; ++u) acc[u] = zero4();
+  // software pipeline over blocks of kS k-steps: the operands of block n + 1 are read while the
+  // MFMAs of block n issue (sched barriers keep the compiler from sinking the reads back to their
+  // first use, which exposed the LDS latency before every MFMA); <= 12 reads in flight
+  constexpr int kS = 3, kBlocks = (25 + kS - 1) / kS;
+  float bv[2][kS], av[2][kS][N];
+  auto load = [&](int buf, int blk) {
+#pragma unroll
+    for (int j = 0; j < kS; ++j) {
+      const int st = blk * kS + j;
+      if (st >= 25) break;
+      const int q = (4 * st) / 10, r = (4 * st) % 10;
+      const bool strad = r == 8;
+      bv[buf][j] = pb0[(q * kDcF + r) * kDcFStride + (strad ? wrapB : 0)];
+#pragma unroll
+      for (int u = 0; u < N; ++u) av[buf][j][u] = pa0[u][(q * 13 + r) * kP1Stride + (strad ? wrapA : 0)];
+    }
+  };
+  load(0, 0);
+#pragma unroll
+  for (int blk = 0; blk < kBlocks; ++blk) {
+    if (blk + 1 < kBlocks) load((blk + 1) & 1, blk + 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < kS; ++j) {
+      if (blk * kS + j >= 25) break;
+#pragma unroll
+      for (int u = 0; u < N; ++u) acc[u] = mfma16x16x4(bias[u] ? unit_a : av[blk & 1][j][u], bv[blk & 1][j], acc[u]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int u = 0; u < N; ++u) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = (t0 + u) * 16 + 4 * g + r;
+      if (row < kMnistPart2Rows) a.part2[((size_t)bi * kMnistPart2Rows + row) * 64 + 16 * cq + i] = acc[u][r];
+    }
+  }
+}
+
+// ---- fused conv backward of one (image bi, channel quarter cq) workgroup, after its dP2 ----
+// dp2s: [25 windows][16] this quarter's masked dP2 (LDS), a2s its pool-2 argmax bytes, P1s/a1s/xs
+// the image's pooled conv1 output / pool-1 argmax / input (LDS), dCs the dC2 grid scratch, red
+// >= 8*10*16 floats of scratch, bwd this wave's dgrad operands W2[tap][ci][16cq + 4g + j]
+// (registers, loaded by the caller ahead of time).  Writes part2 columns 16cq.. of image bi and
+// part1 row 4bi + cq.
+__device__ __forceinline__ void fused_conv_bwd(const MnistArgs& a, int bi, int cq, const float* dp2s,
+                                               const uint8_t* a2s, const float* P1s, const uint8_t* a1s,
+                                               const float* xs, float* dCs, float* red, const f4 (&bwd)[9]) {
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int i = lane & 15, g = lane >> 4;
+  // dC2 grid: cell (y + 2, x + 2), channel c gets dP2 of window (y/2, x/2) where the pool-2 argmax
+  // is (y & 1) * 2 + (x & 1); zero elsewhere (border, row / column 10 of the 11 x 11 conv output)
+  for (int e4 = tid; e4 < kDcF * kDcF * (kDcFStride / 4); e4 += 512) {
+    const int cell = e4 / (kDcFStride / 4), c4 = e4 - cell * (kDcFStride / 4);
+    const int y = cell / kDcF - 2, x = cell - (cell / kDcF) * kDcF - 2;
+    f4 v = zero4();
+    if (c4 < 4 && y >= 0 && y < 10 && x >= 0 && x < 10) {
+      const int wo = (y >> 1) * 5 + (x >> 1);
+      const unsigned s = (unsigned)((y & 1) * 2 + (x & 1));
+      const f4 d = ld4(dp2s + wo * 16 + c4 * 4);
+      const unsigned q = *reinterpret_cast<const unsigned*>(a2s + wo * 16 + c4 * 4);
+      v = f4{(q & 0xffu) == s ? d.x : 0.f, ((q >> 8) & 0xffu) == s ? d.y : 0.f, ((q >> 16) & 0xffu) == s ? d.z : 0.f,
+             (q >> 24) == s ? d.w : 0.f};
+    }
+    st4(dCs + e4 * 4, v);
+  }
+  lds_barrier();
+  bwd_stamp(a.stamps, 0);
+
+  // ---- conv2 wgrad: dW2[k = tap*32 + ci][16cq + co] over the 100 used positions (row tile 18 =
+  // the bias row).  k-step s covers positions 4s + g of the 10 x 10 grid (see k_conv_bwd).  All of
+  // a wave's row tiles advance together: one dC2 (B) read per k-step serves N MFMAs on N
+  // independent accumulators ----
+  {
+    const int t0 = kFusedWgradTiles[wave][0], ntiles = kFusedWgradTiles[wave][1];
+    if (ntiles == 2) fused_wgrad_tiles<2>(a, bi, cq, t0, P1s, dCs);
+    else fused_wgrad_tiles<3>(a, bi, cq, t0, P1s, dCs);
+  }
+  bwd_stamp(a.stamps, 1);
+
+  // ---- conv2 dgrad over this quarter's 16 output channels (a partial sum of dP1; everything after
+  // it -- ReLU mask, pool-1 routing, conv1 wgrad -- is linear in dP1, so the four quarters'
+  // conv1 weight gradients simply add up in the finalize reduction).  Waves 4nt .. 4nt+3 own input
+  // channels ci = 16nt + i and pixel tiles w, w + 4, w + 8 (16 pixels each), advanced together ----
+  float dw[10];
+#pragma unroll
+  for (int j = 0; j < 10; ++j) dw[j] = 0.f;
+  {
+    const int nt = wave >> 2, wt = wave & 3;
+    const int ci = 16 * nt + i;
+    constexpr int kT = 3;
+    f4 acc[kT][2];
+    int ih[kT], iw[kT], khlo[kT], khhi[kT];
+#pragma unroll
+    for (int u = 0; u < kT; ++u) {
+      const int t = wt + 4 * u;  // t = 11 (wave 3's third) is empty: khlo > khhi, no MFMA, no store
+      const int Pc = min(t * 16 + i, 168);
+      ih[u] = Pc / 13;
+      iw[u] = Pc - ih[u] * 13;
+      const int ih_lo = min(t * 16, 168) / 13, ih_hi = min(t * 16 + 15, 168) / 13;
+      khlo[u] = t < 11 ? max(0, ih_lo - 9) : 3;  // kernel rows with 0 <= ih - kh <= 9 somewhere in the tile
+      khhi[u] = min(2, ih_hi);
+      acc[u][0] = zero4();
+      acc[u][1] = zero4();
+    }
+    // epilogue operands (ReLU mask source P1, pool-1 argmax) read ahead of the MFMAs
+    float p1v[kT][4];
+    unsigned q1v[kT][4];
+#pragma unroll
+    for (int u = 0; u < kT; ++u)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int Pr = min((wt + 4 * u) * 16 + 4 * g + r, 168);
+        p1v[u][r] = P1s[Pr * kP1Stride + ci];
+        q1v[u][r] = a1s[Pr * 32 + ci];
+      }
+    // taps software-pipelined: the dC2 reads of tap k + 1 are in flight while tap k's MFMAs issue
+    f4 av[2][kT];
+    auto load = [&](int buf, int tap) {
+      const int kh = tap / 3, kw = tap - kh * 3;
+#pragma unroll
+      for (int u = 0; u < kT; ++u)
+        av[buf][u] = ld4(dCs + ((ih[u] - kh + 2) * kDcF + (iw[u] - kw + 2)) * kDcFStride + 4 * g);
+    };
+    load(0, 0);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      if (tap + 1 < 9) load((tap + 1) & 1, tap + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      const int kh = tap / 3;
+      const f4 bv = bwd[tap];
+#pragma unroll
+      for (int u = 0; u < kT; ++u) {
+        if (kh < khlo[u] || kh > khhi[u]) continue;  // wave-uniform
+        const f4 x = av[tap & 1][u];
+        acc[u][0] = mfma16x16x4(x.x, bv.x, acc[u][0]);
+        acc[u][1] = mfma16x16x4(x.y, bv.y, acc[u][1]);
+        acc[u][0] = mfma16x16x4(x.z, bv.z, acc[u][0]);
+        acc[u][1] = mfma16x16x4(x.w, bv.w, acc[u][1]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int u = 0; u < kT; ++u) {
+      const int t = wt + 4 * u;
+      if (t >= 11) continue;
+      const f4 ac = acc[u][0] + acc[u][1];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int Pr = t * 16 + 4 * g + r;
+        if (Pr < 169) {
+          const float v = p1v[u][r] > 0.f ? ac[r] : 0.f;
+          const unsigned q1 = q1v[u][r];
+          const int ph = Pr / 13, pw = Pr - ph * 13;
+          const float* img = xs + (2 * ph + (q1 >> 1)) * 28 + 2 * pw + (q1 & 1);
+#pragma unroll
+          for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) dw[kh * 3 + kw] = fmaf(img[kh * 28 + kw], v, dw[kh * 3 + kw]);
+          dw[9] += v;
+        }
+      }
+    }
+  }
+  bwd_stamp(a.stamps, 2);
+#pragma unroll
+  for (int j = 0; j < 10; ++j) dw[j] = sum_lane_groups(dw[j]);
+  if (g == 0) {
+#pragma unroll
+    for (int j = 0; j < 10; ++j) red[(wave * 10 + j) * 16 + i] = dw[j];
+  }
+  lds_barrier();
+  bwd_stamp(a.stamps, 3);
+  if (tid < kMnistPart1Cols) {
+    const int j = tid >> 5, c = tid & 31, nt = c >> 4, ii = c & 15;
+    float sum = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) sum += red[((4 * nt + w) * 10 + j) * 16 + ii];
+    a.part1[((size_t)bi * 4 + cq) * kMnistPart1Cols + tid] = sum;
+  }
+}
 
 // Saved-for-backward activations of one (image, quarter) workgroup, written from LDS AFTER the
 // head hand-off (no global store sits in the conv phases, where it would queue behind the W3
@@ -686,7 +926,9 @@ constexpr int kLdsFwd = 784 + 320 + 169 * kP1Stride + 72 * 16 * 4 + 400 + 169 * 
 __device__ __forceinline__ void store_saved_fwd(const MnistArgs& a, int bi, int cq, const float* P1s,
                                                 const uint8_t* a1s, const float* p2s, const uint8_t* a2s,
                                                 int t, int nt) {
-  for (int e = t; e < 2 * 338 + 200; e += nt) {
+  // fused_bwd: the conv backward runs in this workgroup from LDS; only P2 (dense1 weight gradient)
+  // leaves the kernel
+  for (int e = (a.fused_bwd ? 676 : 0) + t; e < (a.fused_bwd ? 776 : 2 * 338 + 200); e += nt) {
     if (e < 338) {
       const int e4 = cq * 338 + e, pos = e4 >> 3, c4 = (e4 & 7) * 4;
       st4(a.P1 + (size_t)bi * 5408 + e4 * 4, ld4(P1s + pos * kP1Stride + c4));
@@ -835,7 +1077,7 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
     }
   }
   stamp(a.stamps, 3);
-  __syncthreads();
+  lds_barrier();  // P1 / A1 in LDS; the W3 prefetch loads stay in flight
   stamp(a.stamps, 4);
   // ---- conv2 on MFMA: wave w < 7 takes row tile w (windows 4w .. 4w+3); the last 9 W3 loads
   // ride along, one per tap ----
@@ -890,12 +1132,12 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
     for (int j = 0; j < 25; ++j) hs += p2s[rg * 25 + j] * w3v[j];
     st4(red + rg * 128 + n4, hs);
   }
-  __syncthreads();
-  // dp2_fwd (training): every workgroup resident at once, so the head runs in a fixed quarter
-  // workgroup that polls the other quarters' tagged partials; otherwise the last to arrive runs it
+  lds_barrier();
+  // dp2_fwd (training): every workgroup resident at once, so every quarter workgroup runs the head
+  // itself from the other quarters' tagged partials; otherwise the last to arrive runs it
   const bool tagged = a.head == 1 && a.dp2_fwd;
-  const uint32_t tag = a.ep[0] + 1u;  // this step's hand-off tag (KC advanced the epoch)
-  float* sown = red + 16 * 128 + 4;   // [128] the head quarter's own partial
+  const uint32_t tag = a.ep[0] + 1u;  // this step's hand-off tag (advanced by KC / KF)
+  float* sown = red + 16 * 128 + 4;   // [128] this quarter's own partial
   if (tid < 32) {
     f4 hsum = zero4();
 #pragma unroll
@@ -903,10 +1145,9 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
     if (!tagged) {
       // 16-B sc1 store: the image's head may run on another XCD (hand-off below)
       st4_sc1(buf_rsrc(a.part3 + ((size_t)cq * a.b + bi) * 128, 512), tid * 16, hsum);
-    } else if (cq == kHeadQuarter) {
-      st4(sown + 4 * tid, hsum);
     } else {
-      // (value, tag) words, 8-B write-through stores, polled by the head quarter
+      st4(sown + 4 * tid, hsum);
+      // (value, tag) words, 8-B write-through stores, polled by the other three quarters
       unsigned long long* p = a.part3t + ((size_t)cq * a.b + bi) * 128 + 4 * tid;
       const unsigned long long tg = (unsigned long long)tag << 32;
       __hip_atomic_store(p, (unsigned long long)__float_as_uint(hsum.x) | tg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -942,11 +1183,11 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
       s_last[0] = (old & 3u) == 3u;
     }
   }
-  __syncthreads();  // (tagged: the head quarter's own partial in LDS)
-  const bool last = tagged ? cq == kHeadQuarter : s_last[0] != 0;
+  lds_barrier();  // (tagged: this quarter's own partial in LDS)
+  const bool last = tagged || s_last[0] != 0;  // (tagged: every quarter runs the head)
   float* sdh = red;  // [128] dH of this image (the dense1 row-group scratch is free now)
   if (last && wave == 0) {
-    if (a.head == 1) head_row(a, bi, lane, label, hw, sdh, tag, tagged ? sown : nullptr);
+    if (a.head == 1) head_row(a, bi, lane, label, hw, sdh, tag, tagged ? sown : nullptr, cq, !tagged || cq == kHeadQuarter);
     else head_eval(a, bi, lane, label, hw);
   }
   if (a.head != 1) return;  // evaluation: nothing is saved for a backward pass
@@ -955,39 +1196,17 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   else if (wave != 0) store_saved_fwd(a, bi, cq, P1s, a1s, p2s, a2s, tid - 64, 448);
   if (!a.dp2_fwd) return;  // dP2 by k_dense1_bwd
   // ---- dP2 = (dH W3^T) * 1[P2 > 0] for this quarter's 400 features, from the W3 slice still in
-  // registers (no K5 launch, no second read of W3).  Every workgroup waits for its image's head,
-  // which runs in the image's last-arriving workgroup: that one may not be dispatched yet when
-  // the others start waiting, so the host selects this mode only when the launch has the GPU to
-  // itself and all of its workgroups fit at once (FusedMnistTrainStep: 4b <= CUs, GPU not shared).
-  // Wave 0 of a waiting workgroup polls the image's 128 tagged dH words (lane i: features 4i..4i+3,
-  // 8-B sc1 loads, the same granules the head stored) until every tag is this step's, then hands
-  // the values to its workgroup through LDS.  Bounded: a head that never arrives poisons the loss
-  // metric instead of hanging the GPU.
-  if (!last && wave == 0) {
-    const unsigned long long* p = a.dHt + (size_t)bi * 128 + 4 * (lane & 31);
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    bool ok = lane >= 32;
-    f4 v = zero4();
-    for (;;) {
-      if (!ok) {
-        unsigned long long w[4];
+  // registers (no K5 launch, no second read of W3), dH from this workgroup's own head (LDS) ----
+  lds_barrier();
+  // fused_bwd: this wave's conv2 dgrad operands W2[tap][16nt + i][16cq + 4g .. +3] (L2), issued
+  // after the head hand-off (whose polls they would queue behind) and consumed after dP2, the dC2
+  // grid and the wgrad
+  f4 bwd[9];
+  if (a.fused_bwd) {
+    const int nt = wave >> 2;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) w[k] = __hip_atomic_load(p + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = (uint32_t)(w[0] >> 32) == tag && (uint32_t)(w[1] >> 32) == tag && (uint32_t)(w[2] >> 32) == tag &&
-             (uint32_t)(w[3] >> 32) == tag;
-        v = f4{__uint_as_float((uint32_t)w[0]), __uint_as_float((uint32_t)w[1]), __uint_as_float((uint32_t)w[2]),
-               __uint_as_float((uint32_t)w[3])};
-      }
-      if (__all(ok)) break;
-      __builtin_amdgcn_s_sleep(1);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000ull) {  // 20 ms at 100 MHz
-        if (lane == 0) atomicAdd(&a.metrics[0], __builtin_nanf(""));
-        break;
-      }
-    }
-    if (lane < 32) st4(sdh + 4 * lane, v);
+    for (int tap = 0; tap < 9; ++tap) bwd[tap] = ld4(a.W + a.ow2 + (size_t)(tap * 32 + 16 * nt + i) * 64 + 16 * cq + 4 * g);
   }
-  __syncthreads();
   const f4 dh = ld4(sdh + n4);
   float v[25];
 #pragma unroll
@@ -999,6 +1218,16 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   // (l & 31) ends with feature rg * 25 + (l & 31) (features 25..31 are zero padding)
   const float d = reduce_scatter32<25>(v, lane);
   const int j = lane & 31;
+  if (a.fused_bwd) {
+    // masked dP2 of this quarter stays in LDS (over P2, which this lane alone reads here)
+    if (j < 25) {
+      const int kk = rg * 25 + j;
+      p2s[kk] = p2s[kk] > 0.f ? d : 0.f;
+    }
+    lds_barrier();  // (the dgrad operand loads stay in flight)
+    fused_conv_bwd(a, bi, cq, p2s, a2s, P1s, a1s, xs, red + 16 * 128 + 4 + 128, red, bwd);
+    return;
+  }
   if (j < 25) {
     const int kk = rg * 25 + j;
     a.dP2[(size_t)bi * 1600 + (kk >> 4) * 64 + 16 * cq + (kk & 15)] = p2s[kk] > 0.f ? d : 0.f;
@@ -1053,7 +1282,7 @@ __global__ __launch_bounds__(256) void k_finalize(MnistArgs a, int apply_sgd, in
   }
   const int t = (blk - nbs - nb2) * 256 + threadIdx.x;
   const int o = t >> 4, sub = t & 15;  // o in [0, 320)
-  const int rows = mnist_part1_rows(a.b);
+  const int rows = mnist_part1_rows(a.b, a.fused_bwd != 0);
   float s = 0.f;
   const int oc = min(o, kMnistPart1Cols - 1);
   const int e = oc < 288 ? a.ow1 + oc : a.ob1 + (oc - 288);
@@ -1070,6 +1299,133 @@ __global__ __launch_bounds__(256) void k_finalize(MnistArgs a, int apply_sgd, in
   if (sub == 0 && o < kMnistPart1Cols) {
     a.G[e] = s;
     if (apply_sgd) a.W[e] = wold - lr * s;
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// KF-X: finalize of the fused_bwd step, one workgroup per contiguous slab range (kFxBlocks):
+//   [0, 100)    dW3 rows 16m .. 16m+15 (2048 floats): 8 dense tasks, 2 per wave
+//   100         db3 + dW4 + db4 (1418 floats, contiguous): 17 dense tasks
+//   [101, 390)  conv2 kernel row k (64 floats; row 288 = bias): 4 threads per output
+//   [390, 410)  conv1 kernel / bias outputs 16q .. 16q+15: 16 threads per output
+// Each writes its gradient range into G.  R = 1 with SGD: W -= lr * G of the range.  R > 1 with
+// the exchange (a.xchg): the range is also published into this workgroup's slot of the channel's
+// exchange buffer (at its slab offsets), then the xGMI exchange with workgroup j of every peer
+// (epoch / parity protocol of csrc/kernels/xgmi.hip, bounded waits), then W -= lr * (sum of the R
+// contributions in rank order): bit-identical on every replica, and the all-reduce of one range
+// overlaps the reductions of the others inside ONE launch.
+// --------------------------------------------------------------------------------------------
+__device__ __forceinline__ void fx_range(const MnistArgs& a, int j, int& lo, int& cnt) {
+  if (j < 100) {
+    lo = a.ow3 + j * 2048;
+    cnt = 2048;
+  } else if (j == 100) {
+    lo = a.ob3;  // ob3, ow4, ob4 are contiguous (checked on the host)
+    cnt = 128 + 1280 + 10;
+  } else if (j < kFxDense + 288) {
+    lo = a.ow2 + (j - kFxDense) * 64;
+    cnt = 64;
+  } else if (j == kFxDense + 288) {
+    lo = a.ob2;
+    cnt = 64;
+  } else {
+    const int q = j - kFxDense - 289;
+    lo = q < 18 ? a.ow1 + q * 16 : a.ob1 + (q - 18) * 16;
+    cnt = 16;
+  }
+}
+
+template <int R>
+__global__ __launch_bounds__(256) void k_finalize_x(MnistArgs a, int apply_sgd) {
+  const int j = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const float lr = *a.lr;
+  const bool xchg = R > 1 && a.xchg && apply_sgd;
+  if (j == 0 && tid == 0) a.ep[0] += 1u;  // the next step's hand-off tag (no k_conv_bwd launch)
+  uint32_t e = 0;
+  float* xdst = nullptr;
+  int64_t half = 0;
+  if (xchg) {
+    if (xgmi_failed(a.xa.err)) return;  // a peer already failed: no exchange, no update
+    e = __builtin_amdgcn_readfirstlane(a.xa.epoch[j]) + 1u;
+    half = (int64_t)(e & 1u) * 2 * a.xa.cap;
+    xdst = a.xa.p.buf[a.xa.rank] + half;
+  }
+  const bool sgd_local = R == 1 && apply_sgd;  // single replica: SGD fused into the reduction
+  // ---- this workgroup's gradient range ----
+  if (j < 100) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) dense_w_task(a, j * 8 + 2 * wave + k, lane, sgd_local, lr, xdst);
+  } else if (j == 100) {
+    for (int T = kD1TasksW3 - 8 + wave; T < kDenseTasks; T += 4) dense_w_task(a, T, lane, sgd_local, lr, xdst);
+  } else if (j < kFxDense + 289) {
+    const int row = j - kFxDense, c = tid >> 2, sub = tid & 3;
+    const int n = kMnistPart2Rows * 64, oc = row * 64 + c;
+    const int e2 = row < 288 ? a.ow2 + oc : a.ob2 + c;
+    const float wold = sgd_local ? a.W[e2] : 0.f;
+    float sum = 0.f;
+    for (int base = 0; base < a.b; base += 64) {
+      float v[16];
+#pragma unroll
+      for (int jj = 0; jj < 16; ++jj) v[jj] = a.part2[(size_t)min(base + sub + 4 * jj, a.b - 1) * n + oc];
+#pragma unroll
+      for (int jj = 0; jj < 16; ++jj) sum += (base + sub + 4 * jj < a.b) ? v[jj] : 0.f;
+    }
+    sum += __shfl_xor(sum, 1, 64);
+    sum += __shfl_xor(sum, 2, 64);
+    if (sub == 0) {
+      a.G[e2] = sum;
+      if (xdst != nullptr) xdst[e2] = sum;
+      if (sgd_local) a.W[e2] = wold - lr * sum;
+    }
+  } else {
+    const int q = j - kFxDense - 289, o = q * 16 + (tid >> 4), sub = tid & 15;
+    const int rows = mnist_part1_rows(a.b, true);
+    const int e1 = o < 288 ? a.ow1 + o : a.ob1 + (o - 288);
+    const float wold = sgd_local ? a.W[e1] : 0.f;
+    float sum = 0.f;
+    for (int base = 0; base < rows; base += 128) {
+      float v[8];
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) v[jj] = a.part1[(size_t)min(base + sub + 16 * jj, rows - 1) * kMnistPart1Cols + o];
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) sum += (base + sub + 16 * jj < rows) ? v[jj] : 0.f;
+    }
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1) sum += __shfl_xor(sum, m, 64);
+    if (sub == 0) {
+      a.G[e1] = sum;
+      if (xdst != nullptr) xdst[e1] = sum;
+      if (sgd_local) a.W[e1] = wold - lr * sum;
+    }
+  }
+  if constexpr (R > 1) {
+    if (!xchg) return;
+    // ---- exchange with workgroup j of every peer, rank-order sum, SGD of the range ----
+    if (!xgmi_exchange<R>(a.xa.p, a.xa.rank, a.xa.sig_blocks, a.xa.timeout, a.xa.err, 0, j, e)) {
+      if (tid == 0) a.xa.epoch[j] = e;
+      return;
+    }
+    int lo, cnt;
+    fx_range(a, j, lo, cnt);
+    const int n4 = cnt >> 2;  // (every range starts 16-B aligned: slab offsets are multiples of 4)
+    for (int t = tid; t < n4; t += 256) {
+      const int64_t off = lo + 4 * t;
+      f4 v[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[r] = ld4(a.xa.p.buf[r] + half + off);
+      f4 acc = v[0];
+#pragma unroll
+      for (int r = 1; r < R; ++r) acc += v[r];
+      st4(a.W + off, ld4(a.W + off) - lr * acc);
+    }
+    for (int t = 4 * n4 + tid; t < cnt; t += 256) {
+      const int64_t off = lo + t;
+      float acc = a.xa.p.buf[0][half + off];
+#pragma unroll
+      for (int r = 1; r < R; ++r) acc += a.xa.p.buf[r][half + off];
+      a.W[off] -= lr * acc;
+    }
+    if (tid == 0) a.xa.epoch[j] = e;
   }
 }
 
@@ -1133,7 +1489,8 @@ void mnist_fwd_conv(const MnistArgs& a, hipStream_t s) {
     (void)hipFuncSetAttribute((const void*)k_fwd_conv, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL(k_fwd_conv, dim3(a.b * 4), dim3(512), kLdsFwd * sizeof(float), s, a);
+  const bool fused = a.head == 1 && a.dp2_fwd && a.fused_bwd;
+  hipLaunchKernelGGL(k_fwd_conv, dim3(a.b * 4), dim3(512), (fused ? kLdsFwdFused : kLdsFwd) * sizeof(float), s, a);
 }
 void mnist_finalize(const MnistArgs& a, bool apply_sgd, bool with_dense, hipStream_t s) {
   const int ndb = with_dense ? (kDenseTasks + 3) / 4 : 0;
@@ -1142,6 +1499,20 @@ void mnist_finalize(const MnistArgs& a, bool apply_sgd, bool with_dense, hipStre
   const int nb1 = (kMnistPart1Cols * 16 + 255) / 256;
   hipLaunchKernelGGL(k_finalize, dim3(ndb + nbs + nb2 + nb1), dim3(256), 0, s, a, apply_sgd ? 1 : 0, ndb, nbs, nb2,
                      nb1);
+}
+void mnist_finalize_x(const MnistArgs& a, bool apply_sgd, hipStream_t s) {
+  const int R = (a.xchg && apply_sgd) ? a.xa.world : 1;
+  const int sgd = apply_sgd ? 1 : 0;
+  switch (R) {  // the rank count is a template parameter (straight-line rank-order sums)
+    case 2: hipLaunchKernelGGL(k_finalize_x<2>, dim3(kFxBlocks), dim3(256), 0, s, a, sgd); break;
+    case 3: hipLaunchKernelGGL(k_finalize_x<3>, dim3(kFxBlocks), dim3(256), 0, s, a, sgd); break;
+    case 4: hipLaunchKernelGGL(k_finalize_x<4>, dim3(kFxBlocks), dim3(256), 0, s, a, sgd); break;
+    case 5: hipLaunchKernelGGL(k_finalize_x<5>, dim3(kFxBlocks), dim3(256), 0, s, a, sgd); break;
+    case 6: hipLaunchKernelGGL(k_finalize_x<6>, dim3(kFxBlocks), dim3(256), 0, s, a, sgd); break;
+    case 7: hipLaunchKernelGGL(k_finalize_x<7>, dim3(kFxBlocks), dim3(256), 0, s, a, sgd); break;
+    case 8: hipLaunchKernelGGL(k_finalize_x<8>, dim3(kFxBlocks), dim3(256), 0, s, a, sgd); break;
+    default: hipLaunchKernelGGL(k_finalize_x<1>, dim3(kFxBlocks), dim3(256), 0, s, a, sgd); break;
+  }
 }
 void sgd_apply(float* w, const float* g, const float* lr, int64_t n, hipStream_t s) {
   const int64_t nt = (n + 3) / 4;

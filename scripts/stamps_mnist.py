@@ -33,8 +33,12 @@ def main():
     for _ in range(20):
         st.forward_backward(0)
         st.finalize(True)
+    fused = bool(st.fused_bwd)
+    print(f"fused_bwd={fused}")
     for name, (k, waves, slots, grid) in KERNELS.items():
-        buf = torch.zeros(grid * 72, dtype=torch.int64, device=dev)
+        if fused and name == "conv_bwd":
+            continue
+        buf = torch.zeros(grid * 104, dtype=torch.int64, device=dev)
         st.forward_backward(0)
         st.finalize(True)
         st._impl.set_stamps(buf)
@@ -42,7 +46,7 @@ def main():
         st._impl.set_stamps(None)
         torch.cuda.synchronize()
         r = buf[:grid * 64].view(grid, 8, 8).cpu().numpy().astype(np.int64)
-        hs = buf[grid * 64:].view(grid, 8).cpu().numpy().astype(np.int64)
+        hs = buf[grid * 64:grid * 72].view(grid, 8).cpu().numpy().astype(np.int64)
         t0 = r[:, :waves, 0].min(axis=1, keepdims=True)
         rel = (r - t0[:, :, None]) * 10 / 1000.0  # us since the workgroup's first wave started
         span = (r[:, :waves][r[:, :waves] > 0].max() - r[:, :waves, 0].min()) * 10 / 1000.0
@@ -60,6 +64,13 @@ def main():
                   f"{np.median(p6):.2f}/{p6.max():.2f}; head won {np.median(h[:, 0]):.2f}/{h[:, 0].max():.2f}; "
                   f"partials loaded {np.median(h[:, 1]):.2f}/{h[:, 1].max():.2f}; softmax {np.median(h[:, 2]):.2f}/"
                   f"{h[:, 2].max():.2f}; dH published {np.median(h[:, 3]):.2f}/{h[:, 3].max():.2f}")
+        if name == "fwd_conv" and fused:
+            bs = buf[grid * 72:].view(grid, 8, 4).cpu().numpy().astype(np.int64)
+            t0w = r[:, :waves, 0].min(axis=1)
+            relb = (bs - t0w[:, None, None]) * 10 / 1000.0
+            for k2, label in enumerate(["bwd dC2 ready", "bwd wgrad done", "bwd dgrad done", "bwd reduced"]):
+                vals = [np.median(relb[:, w, k2]) for w in range(waves)]
+                print(f"  {label:14s}" + " ".join(f"{v:6.2f}" for v in vals))
         print("  slot/wave " + " ".join(f"{w:>6d}" for w in range(waves)))
         for s, label in sorted(slots.items(), key=lambda kv: np.median(rel[:, 0, kv[0]])):
             vals = [np.median(rel[:, w, s]) if (r[:, w, s] > 0).all() else float("nan") for w in range(waves)]

@@ -140,6 +140,7 @@ class FusedMnistTrainer:
         # fails on some rank; then each step's graph is followed by an eager all-reduce + update.
         self._capture_comm = None
         self._comm_stream = None
+        self.allreduce_mode = "local" if self.R == 1 else None
         # R > 1: the dense bucket's all-reduce on a side stream overlapping the conv backward is
         # opt-in; serial is the default: on one MI355X (2 replica processes sharing it) the forked
         # execution graph ran 350 us/step against 68.6 serial (profiles/mnist_side_stream_ab_r2.txt)
@@ -206,6 +207,10 @@ class FusedMnistTrainer:
         if self.R == 1 and plain:
             st.finalize(True)
             return
+        if self.R > 1 and plain and st.has_exchange:
+            # fused backward: the finalize launch itself all-reduces over xGMI and applies SGD
+            st.finalize(True, exchange=True)
+            return
         st.finalize(False)
         if self.R > 1 and plain and self.comm.all_reduce_sgd(self.G, self.W, opt.lr_dev):
             return
@@ -252,13 +257,24 @@ class FusedMnistTrainer:
         else:
             self._update()
 
-    def _prepare_comm(self, d0: int):
+    def _prepare_comm(self, st):
         """Collective set-up of the communicator's all-reduce channels for this step's buckets
-        (must precede any graph capture; every rank reaches it at the same point)."""
-        if self.R > 1 and not getattr(self, "_comm_prepared", False):
-            n = self.W.numel()
+        (must precede any graph capture; every rank reaches it at the same point).  With the fused
+        backward and plain SGD the finalize kernel all-reduces through a dedicated xGMI channel
+        (one exchange slot per finalize workgroup)."""
+        if self.R == 1:
+            return
+        if not getattr(self, "_comm_prepared", False):
+            n, d0 = self.W.numel(), st.dense_offset
             self.comm.prepare_all_reduce(n - d0, d0, n)
+            self._xchg = None
+            if st.fused_bwd and self.optimizer.momentum == 0 and os.environ.get("TDL_MNIST_FINALIZE_XCHG", "1") == "1":
+                self._xchg = self.comm.exchange_channel(n, M.FINALIZE_BLOCKS)
+            self.allreduce_mode = ("xgmi-in-finalize" if self._xchg is not None else
+                                   getattr(self.comm, "algorithm", self.comm.name))
             self._comm_prepared = True
+        if self._xchg is not None and st.fused_bwd and not st.has_exchange:
+            st.set_exchange(self._xchg)
 
     def _update(self, lo: int = 0, hi: Optional[int] = None):
         from .. import ops
@@ -300,7 +316,7 @@ class FusedMnistTrainer:
         self._ragged_ev = torch.cuda.Event()
         self._ragged_ev.record(torch.cuda.current_stream(self.device))
         st = self._step(b, idx_buf, global_b)
-        self._prepare_comm(st.dense_offset)
+        self._prepare_comm(st)
         self._train_step(st, 0, global_b)
         self.optimizer.iterations += 1
 
@@ -312,7 +328,7 @@ class FusedMnistTrainer:
             return g
         idx_buf = torch.zeros(K * b, dtype=torch.int32, device=self.device)
         st = self._step(b, idx_buf)
-        self._prepare_comm(st.dense_offset)
+        self._prepare_comm(st)
         graph = None
         if self.capture:
             s = torch.cuda.Stream(self.device)
@@ -590,6 +606,8 @@ class FusedMnistTrainer:
             m.reset_state()
 
     def logs(self) -> Dict[str, float]:
+        for st in list(self._steps.values()):
+            st.check()
         t = self.metrics_dev.clone()
         if self.R > 1:
             self.comm.check_health()

@@ -383,6 +383,12 @@ class Model(Layer):
         if self._initial_epoch_override is not None:
             initial_epoch = max(initial_epoch, self._initial_epoch_override)
         want_batch = cb_list.wants_batch_logs or (verbose == 1 and sys.stdout.isatty())
+        # replica-consistency checks (one 2-word collective each, parallel/consistency.py): every
+        # TDL_CHECK_REPLICAS_EVERY epochs (default 1) and every TDL_CHECK_REPLICAS_EXECUTIONS
+        # executions (default 100), plus once at the end of fit; 0 disables either
+        check_epochs = int(os.environ.get("TDL_CHECK_REPLICAS_EVERY", "1") or 0)
+        check_exec = int(os.environ.get("TDL_CHECK_REPLICAS_EXECUTIONS", "100") or 0)
+        self._executions = getattr(self, "_executions", 0)
         K = max(1, self._steps_per_execution)
         persistent = steps_per_epoch is not None  # Q5: one iterator across epochs
         handler.new_iterator()
@@ -399,8 +405,11 @@ class Model(Layer):
                 n = K if steps is None else min(K, steps - done)
                 if want_batch:
                     cb_list.on_train_batch_begin(done)
-                got = _run_guarded(trainer, handler, n, strategy)
+                got = _run_guarded(trainer, handler, n, strategy, self)
                 done += got
+                self._executions += 1
+                if check_exec > 0 and self._executions % check_exec == 0:
+                    self._check_replicas(trainer)
                 if want_batch and got:
                     cb_list.on_train_batch_end(done - 1, _LazyLogs(trainer))
                 if got < n:
@@ -419,8 +428,7 @@ class Model(Layer):
                 logs.update({f"val_{k}": v for k, v in val.items()})
                 trainer = self._get_trainer()
             cb_list.on_epoch_end(epoch, logs)
-            every = int(os.environ.get("TDL_CHECK_REPLICAS_EVERY", "0") or 0)
-            if every > 0 and (epoch + 1) % every == 0:
+            if check_epochs > 0 and (epoch + 1) % check_epochs == 0:
                 self._check_replicas(trainer)
             if exhausted:
                 if self._is_chief():
@@ -780,7 +788,7 @@ def clone_model(model):
     return model_from_config(model.get_config_full())
 
 
-def _run_guarded(trainer, handler, n, strategy):
+def _run_guarded(trainer, handler, n, strategy, model=None):
     """One execution of ``n`` steps with failure detection (utils/fault.py): a collective that
     fails because a peer died is re-raised as PeerLostError with the watchdog's diagnosis, and the
     fault-injection hook runs at the execution boundary."""
@@ -802,4 +810,6 @@ def _run_guarded(trainer, handler, n, strategy):
         raise
     fault.check()
     fault.maybe_inject(strategy.extended.rank, int(trainer.optimizer.iterations))
+    if model is not None:
+        fault.maybe_corrupt(strategy.extended.rank, int(trainer.optimizer.iterations), getattr(model, "_W", None))
     return got

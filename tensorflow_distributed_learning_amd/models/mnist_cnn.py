@@ -5,9 +5,9 @@
 * :func:`reference_logits`  – plain-PyTorch functional forward (NHWC semantics); the fp32/fp64
   oracle for the fused HIP kernels.
 * :class:`FusedMnistTrainStep` – one replica's fused train step on the gfx950 kernels of
-  ``csrc/kernels/mnist_cnn.hip`` (3 launches for one replica alone on its GPU: fwd + loss head +
-  dP2, conv bwd, finalize = partial reductions + dense weight gradients [+ SGD]; otherwise dP2 and,
-  at R > 1, the dense weight gradients in a K5 launch between fwd and conv bwd).
+  ``csrc/kernels/mnist_cnn.hip`` (2 launches for one replica alone on its GPU: fwd + loss head +
+  dP2 + conv bwd, then finalize = partial reductions + dense weight gradients [+ SGD]; on a shared
+  GPU a separate conv-bwd launch and a K5 launch for dP2 / the dense weight gradients).
 """
 from __future__ import annotations
 
@@ -31,6 +31,7 @@ MNIST_CNN_VARIABLES = [
     ("dense_1/bias:0", (10,)),
 ]
 MNIST_NUM_PARAMS = 225_034
+FINALIZE_BLOCKS = 410  # workgroups of the fused finalize (kFxBlocks): one exchange slot each
 
 
 def mnist_layout() -> SlabLayout:
@@ -143,9 +144,21 @@ class FusedMnistTrainStep:
         self.dense_offset = int(layout.offsets[4])
         self.dp2_in_forward = dp2_in_forward_ok(self.b, self.R, W.device)
         self._impl.set_dp2_in_forward(self.dp2_in_forward)
+        # with dP2 in the forward kernel the conv backward runs there too (one launch for forward
+        # + loss + backward; TDL_MNIST_FUSED_BWD=0 keeps the separate k_conv_bwd launch)
+        self._impl.set_fused_bwd(os.environ.get("TDL_MNIST_FUSED_BWD", "1") == "1")
+        self.fused_bwd = bool(self._impl.fused_bwd())
 
     def forward_backward(self, idx_offset: int) -> None:
         self._impl.forward_backward(int(idx_offset))
+
+    def check(self) -> None:
+        """Raise if an in-kernel hand-off of this step timed out (host sync).  Such a step gave
+        the affected images no gradient and poisoned the loss metric; it indicates that the
+        launch did not have the GPU to itself (see :func:`dp2_in_forward_ok`)."""
+        if self._impl.error(False):
+            raise RuntimeError("fused MNIST step: an in-kernel hand-off timed out (the GPU is shared or not every "
+                               "workgroup was resident); set TDL_MNIST_DP2_FWD=0 or TDL_SHARE_GPU=1")
 
     def forward_eval(self, idx_offset: int, logits: Optional[torch.Tensor] = None) -> None:
         """Forward only (evaluate / predict): loss, correct and sample counts of the b rows at
@@ -160,8 +173,20 @@ class FusedMnistTrainStep:
         """Conv backward into per-image partial slabs (reduced into G by finalize)."""
         self._impl.backward_conv()
 
-    def finalize(self, apply_sgd: bool) -> None:
-        self._impl.finalize(bool(apply_sgd))
+    def finalize(self, apply_sgd: bool, exchange: bool = False) -> None:
+        """Partial-slab reductions + dense weight gradients into G (+ SGD).  ``exchange`` (fused
+        backward + :meth:`set_exchange`): the same launch all-reduces the gradient across the
+        replicas over xGMI before the SGD update (each finalize workgroup exchanges its own range)."""
+        self._impl.finalize(bool(apply_sgd), bool(exchange))
+
+    def set_exchange(self, channel) -> None:
+        """Use this xGMI channel (``_C.XgmiChannel`` with capacity >= the slab and
+        >= ``FINALIZE_BLOCKS`` signal slots, connected to every replica) for ``finalize(exchange=True)``."""
+        self._impl.set_exchange(channel)
+
+    @property
+    def has_exchange(self) -> bool:
+        return bool(self._impl.has_exchange())
 
     def stage(self, k: int, apply_sgd: bool = False) -> None:
         self._impl.stage(int(k), bool(apply_sgd))

@@ -69,6 +69,11 @@ class Communicator:
         (returns False otherwise; the caller then all-reduces and applies SGD itself)."""
         return False
 
+    def exchange_channel(self, numel: int, min_blocks: int):
+        """Collective: a device exchange channel for kernels that all-reduce inside their own
+        workgroups (xGMI); None when the communicator has none."""
+        return None
+
     def shutdown(self) -> None:
         pass
 
@@ -170,6 +175,13 @@ class TorchCommunicator(Communicator):
 
     def all_reduce_sgd(self, g, w, lr):
         return self.xgmi is not None and self.xgmi.all_reduce_sgd(g, w, lr)
+
+    def exchange_channel(self, numel: int, min_blocks: int):
+        """Collective: a dedicated xGMI channel for a kernel with a built-in exchange (None when
+        this communicator has no xGMI path)."""
+        if self.xgmi is None:
+            return None
+        return self.xgmi.dedicated(numel, min_blocks)
 
     def check_health(self):
         if self.xgmi is not None:

@@ -60,13 +60,15 @@ class XgmiAllReduce:
         self.limit = max_bytes() // 4
         self._chans: Dict[int, object] = {}
         self._selftest_chans = []
+        self._dedicated = []
         self.ok: Optional[bool] = None  # None = not yet tested
         self.reason = ""
 
     # ------------------------------------------------------------------ set-up (collective)
-    def _make(self, numel: int, timeout: Optional[float] = None):
+    def _make(self, numel: int, timeout: Optional[float] = None, min_blocks: int = 0):
         ch = self.C.XgmiChannel(self.rank, self.world, numel, self.device.index or 0,
-                                self.timeout if timeout is None else timeout, choose_algo(numel, self.world))
+                                self.timeout if timeout is None else timeout, choose_algo(numel, self.world),
+                                int(min_blocks))
         mine = (bytes(ch.handle(False)), bytes(ch.handle(True)))
         allh = [None] * self.world
         dist.all_gather_object(allh, mine, group=self.group)
@@ -163,6 +165,16 @@ class XgmiAllReduce:
         self._selftest_chans.append(ch)  # kept alive (see close); not reused for traffic
         return bool(ok)
 
+    def dedicated(self, numel: int, min_blocks: int):
+        """Collective: a channel of its own (not shared with ``all_reduce``) for a kernel that runs
+        the exchange protocol in its own workgroups (``min_blocks`` signal slots); None if xGMI is
+        disabled on this job."""
+        if not self._ensure_tested():
+            return None
+        ch = self._make(int(numel), min_blocks=int(min_blocks))
+        self._dedicated.append(ch)
+        return ch
+
     # ------------------------------------------------------------------ collectives
     def _channel(self, n: int):
         ch = self._chans.get(n)
@@ -208,6 +220,7 @@ class XgmiAllReduce:
     def close(self) -> None:
         self._chans.clear()
         self._selftest_chans.clear()
+        self._dedicated.clear()
 
 
 def single_node(group=None) -> bool:

@@ -15,6 +15,8 @@ stalls the job.  Here a job fails fast and says why:
   of RCCL/gloo stay as the last line of defence.)
 * **Injection.**  ``TDL_FAULT_KILL_AT_STEP="rank:step"`` makes that rank die abruptly
   (``os._exit``) once its optimizer has taken ``step`` steps — the fault the tests inject.
+  ``TDL_FAULT_CORRUPT_AT_STEP="rank:step"`` silently perturbs that rank's parameters instead
+  (caught by the periodic replica-consistency check of ``fit``).
 
 The job is not elastic: recovery is a restart that resumes from the chief's checkpoint
 (``keras.callbacks.BackupAndRestore``), as with TF.
@@ -52,6 +54,30 @@ def maybe_inject(rank: int, step: int) -> None:
         sys.stderr.write(f"[tdl] fault injection: rank {rank} exits at step {step}\n")
         sys.stderr.flush()
         os._exit(EXIT_INJECTED)
+
+
+_CORRUPTED = set()
+
+
+def maybe_corrupt(rank: int, step: int, slab) -> bool:
+    """Fault injection hook: ``TDL_FAULT_CORRUPT_AT_STEP="rank:step"`` silently perturbs that
+    rank's parameter slab once, at the first execution boundary at or after ``step`` (a broken
+    fabric hand-off that no collective reports).  The periodic replica-consistency check of
+    ``fit`` must catch it (parallel/consistency.py)."""
+    spec = os.environ.get("TDL_FAULT_CORRUPT_AT_STEP")
+    if not spec or slab is None:
+        return False
+    r, s = (int(v) for v in spec.split(":"))
+    if r != rank or step < s or (r, s) in _CORRUPTED:
+        return False
+    _CORRUPTED.add((r, s))
+    import torch
+
+    with torch.no_grad():
+        slab.view(-1)[: min(64, slab.numel())] += 0.5
+    sys.stderr.write(f"[tdl] fault injection: rank {rank} parameters perturbed at step {step}\n")
+    sys.stderr.flush()
+    return True
 
 
 def check() -> None:

@@ -41,15 +41,18 @@ def test_fused_grads_match_reference(cuda, b, R):
     _check_step(step, X, Y, params, layout, G, idx, off, b, R)
 
 
-@pytest.mark.parametrize("mode", ["0", "1"])
+@pytest.mark.parametrize("mode,fused", [("0", "1"), ("1", "0"), ("1", "1")])
 @pytest.mark.parametrize("split", [False, True])
-def test_fused_dp2_modes(cuda, monkeypatch, mode, split):
-    """dP2 in the forward kernel (workgroups wait for their image's head) or in the K5 launch, on
-    the single-launch-sequence path and on the R > 1 split (forward_dense / backward_conv)."""
+def test_fused_dp2_modes(cuda, monkeypatch, mode, fused, split):
+    """dP2 in the forward kernel (workgroups wait for their image's head) or in the K5 launch, with
+    the conv backward in the forward kernel too (fused_bwd) or in its own launch, on the
+    single-launch-sequence path and on the R > 1 split (forward_dense / backward_conv)."""
     monkeypatch.setenv("TDL_MNIST_DP2_FWD", mode)
+    monkeypatch.setenv("TDL_MNIST_FUSED_BWD", fused)
     b, R = 64, 2
     X, Y, params, layout, W, G, idx, lr, step = _setup(cuda, b, R)
     assert step.dp2_in_forward == (mode == "1")
+    assert step.fused_bwd == (mode == "1" and fused == "1")
     off = 2 * b
     if split:
         step.forward_dense(off)
@@ -59,6 +62,26 @@ def test_fused_dp2_modes(cuda, monkeypatch, mode, split):
     step.finalize(False)
     torch.cuda.synchronize()
     _check_step(step, X, Y, params, layout, G, idx, off, b, R)
+    step.check()  # no in-kernel hand-off timed out
+
+
+def test_fused_bwd_steps_match_unfused(cuda, monkeypatch):
+    """Several consecutive fused steps (hand-off tags advanced by finalize, not by k_conv_bwd)
+    track the unfused launch sequence to f32 rounding."""
+    b = 64
+    outs = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("TDL_MNIST_FUSED_BWD", fused)
+        X, Y, params, layout, W, G, idx, lr, step = _setup(cuda, b, 1)
+        assert step.fused_bwd == (fused == "1")
+        for k in range(3):
+            step.forward_backward(k * b)
+            step.finalize(True)
+        torch.cuda.synchronize()
+        step.check()
+        outs.append((W.clone(), step.metrics.clone()))
+    torch.testing.assert_close(outs[1][0], outs[0][0], atol=1e-6, rtol=1e-5)
+    torch.testing.assert_close(outs[1][1][:3], outs[0][1][:3], atol=1e-3, rtol=1e-5)
 
 
 def test_dp2_mode_selection(cuda, monkeypatch):

@@ -210,3 +210,52 @@ def test_corrupted_replica_detected_and_repaired(tmp_path):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     for s in _results(tmp_path, 2):
         assert s["warned"] and s["identical_after"] and s["raised"], s
+
+
+CORRUPT = """
+import json, os, sys, numpy as np, torch
+import tensorflow_distributed_learning_amd as tdl
+from tensorflow_distributed_learning_amd.models.mnist_cnn import build_mnist_cnn
+from tensorflow_distributed_learning_amd.data.tfds import synthetic_mnist
+from tensorflow_distributed_learning_amd.parallel.consistency import ReplicaDivergenceError
+out = sys.argv[1]
+strategy = tdl.distribute.MultiWorkerMirroredStrategy(communication="RING")
+rank = strategy.extended.rank
+x, y = synthetic_mnist(1024, 3)
+ds = tdl.data.Dataset.from_tensor_slices((x.reshape(-1, 28, 28, 1), y))
+ds = ds.map(lambda i, l: (i.to(torch.float32) / 255, l)).batch(64).repeat()
+with strategy.scope():
+    m = build_mnist_cnn()
+    m.compile(loss=tdl.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+              optimizer=tdl.keras.optimizers.SGD(0.05))
+res = {"rank": rank}
+try:
+    m.fit(ds, epochs=2, steps_per_epoch=6, verbose=0)
+    res["status"] = "ok"
+except ReplicaDivergenceError as e:
+    res["status"] = "raised"
+    res["error"] = str(e)
+w = np.concatenate([v.ravel() for v in m.get_weights()])
+res["w"] = [float(w[0]), float(np.abs(w).sum())]
+json.dump(res, open(os.path.join(out, f"out{rank}.json"), "w"))
+"""
+
+
+@pytest.mark.parametrize("mode", ["repair", "raise"])
+def test_periodic_replica_check_catches_silent_corruption(tmp_path, mode):
+    """Rank 1's parameters are silently perturbed after step 2 (TDL_FAULT_CORRUPT_AT_STEP): the
+    per-execution consistency check (TDL_CHECK_REPLICAS_EXECUTIONS) repairs them from rank 0 mid-fit,
+    or raises on every rank under TDL_REPLICA_MISMATCH=raise."""
+    env = {"TDL_FAULT_CORRUPT_AT_STEP": "1:2", "TDL_CHECK_REPLICAS_EXECUTIONS": "1", "TDL_REPLICA_MISMATCH": mode,
+           "TDL_CHECK_REPLICAS": "0", "TDL_CHECK_REPLICAS_EVERY": "0"}
+    r = _launch(tmp_path, CORRUPT, ["--local-workers", "2"], env=env)
+    a, b = _results(tmp_path, 2)
+    assert "perturbed" in r.stderr, r.stderr[-2000:]
+    if mode == "repair":
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+        assert a["status"] == b["status"] == "ok"
+        assert a["w"] == b["w"], (a, b)  # repaired: identical again at the end, with no end-of-fit check
+        assert "replica divergence detected" in r.stderr
+    else:
+        assert a["status"] == b["status"] == "raised", (a, b)
+        assert "replica divergence" in a["error"]
