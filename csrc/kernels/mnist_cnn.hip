@@ -779,12 +779,10 @@ __device__ __forceinline__ void fused_wgrad_tiles(const MnistArgs& a, int bi, in
 // ---- fused conv backward of one (image bi, channel quarter cq) workgroup, after its dP2 ----
 // dp2s: [25 windows][16] this quarter's masked dP2 (LDS), a2s its pool-2 argmax bytes, P1s/a1s/xs
 // the image's pooled conv1 output / pool-1 argmax / input (LDS), dCs the dC2 grid scratch, red
-// >= 8*10*16 floats of scratch, bwd this wave's dgrad operands W2[tap][ci][16cq + 4g + j]
-// (registers, loaded by the caller ahead of time).  Writes part2 columns 16cq.. of image bi and
-// part1 row 4bi + cq.
+// >= 8*10*16 floats of scratch.  Writes part2 columns 16cq.. of image bi and part1 row 4bi + cq.
 __device__ __forceinline__ void fused_conv_bwd(const MnistArgs& a, int bi, int cq, const float* dp2s,
                                                const uint8_t* a2s, const float* P1s, const uint8_t* a1s,
-                                               const float* xs, float* dCs, float* red, const f4 (&bwd)[9]) {
+                                               const float* xs, float* dCs, float* red) {
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int i = lane & 15, g = lane >> 4;
   // dC2 grid: cell (y + 2, x + 2), channel c gets dP2 of window (y/2, x/2) where the pool-2 argmax
@@ -805,6 +803,14 @@ __device__ __forceinline__ void fused_conv_bwd(const MnistArgs& a, int bi, int c
   }
   lds_barrier();
   bwd_stamp(a.stamps, 0);
+  // this wave's conv2 dgrad operands W2[tap][16nt + i][16cq + 4g .. +3] (L2): issued now, consumed
+  // after the wgrad (issued any earlier, the compiler's vmcnt bookkeeping stalled dP2 on them)
+  f4 bwd[9];
+  {
+    const int nt = wave >> 2;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) bwd[tap] = ld4(a.W + a.ow2 + (size_t)(tap * 32 + 16 * nt + i) * 64 + 16 * cq + 4 * g);
+  }
 
   // ---- conv2 wgrad: dW2[k = tap*32 + ci][16cq + co] over the 100 used positions (row tile 18 =
   // the bias row).  k-step s covers positions 4s + g of the 10 x 10 grid (see k_conv_bwd).  All of
@@ -1198,15 +1204,6 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   // ---- dP2 = (dH W3^T) * 1[P2 > 0] for this quarter's 400 features, from the W3 slice still in
   // registers (no K5 launch, no second read of W3), dH from this workgroup's own head (LDS) ----
   lds_barrier();
-  // fused_bwd: this wave's conv2 dgrad operands W2[tap][16nt + i][16cq + 4g .. +3] (L2), issued
-  // after the head hand-off (whose polls they would queue behind) and consumed after dP2, the dC2
-  // grid and the wgrad
-  f4 bwd[9];
-  if (a.fused_bwd) {
-    const int nt = wave >> 2;
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) bwd[tap] = ld4(a.W + a.ow2 + (size_t)(tap * 32 + 16 * nt + i) * 64 + 16 * cq + 4 * g);
-  }
   const f4 dh = ld4(sdh + n4);
   float v[25];
 #pragma unroll
@@ -1224,8 +1221,8 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
       const int kk = rg * 25 + j;
       p2s[kk] = p2s[kk] > 0.f ? d : 0.f;
     }
-    lds_barrier();  // (the dgrad operand loads stay in flight)
-    fused_conv_bwd(a, bi, cq, p2s, a2s, P1s, a1s, xs, red + 16 * 128 + 4 + 128, red, bwd);
+    lds_barrier();
+    fused_conv_bwd(a, bi, cq, p2s, a2s, P1s, a1s, xs, red + 16 * 128 + 4 + 128, red);
     return;
   }
   if (j < 25) {
@@ -1304,10 +1301,11 @@ __global__ __launch_bounds__(256) void k_finalize(MnistArgs a, int apply_sgd, in
 
 // --------------------------------------------------------------------------------------------
 // KF-X: finalize of the fused_bwd step, one workgroup per contiguous slab range (kFxBlocks):
-//   [0, 100)    dW3 rows 16m .. 16m+15 (2048 floats): 8 dense tasks, 2 per wave
+// (512 threads = 8 waves each)
+//   [0, 100)    dW3 rows 16m .. 16m+15 (2048 floats): 8 dense tasks, one per wave
 //   100         db3 + dW4 + db4 (1418 floats, contiguous): 17 dense tasks
-//   [101, 390)  conv2 kernel row k (64 floats; row 288 = bias): 4 threads per output
-//   [390, 410)  conv1 kernel / bias outputs 16q .. 16q+15: 16 threads per output
+//   [101, 390)  conv2 kernel row k (64 floats; row 288 = bias): 8 threads per output
+//   [390, 410)  conv1 kernel / bias outputs 16q .. 16q+15: 32 threads per output
 // Each writes its gradient range into G.  R = 1 with SGD: W -= lr * G of the range.  R > 1 with
 // the exchange (a.xchg): the range is also published into this workgroup's slot of the channel's
 // exchange buffer (at its slab offsets), then the xGMI exchange with workgroup j of every peer
@@ -1336,7 +1334,7 @@ __device__ __forceinline__ void fx_range(const MnistArgs& a, int j, int& lo, int
 }
 
 template <int R>
-__global__ __launch_bounds__(256) void k_finalize_x(MnistArgs a, int apply_sgd) {
+__global__ __launch_bounds__(512) void k_finalize_x(MnistArgs a, int apply_sgd) {
   const int j = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const float lr = *a.lr;
   const bool xchg = R > 1 && a.xchg && apply_sgd;
@@ -1353,45 +1351,45 @@ __global__ __launch_bounds__(256) void k_finalize_x(MnistArgs a, int apply_sgd) 
   const bool sgd_local = R == 1 && apply_sgd;  // single replica: SGD fused into the reduction
   // ---- this workgroup's gradient range ----
   if (j < 100) {
-#pragma unroll
-    for (int k = 0; k < 2; ++k) dense_w_task(a, j * 8 + 2 * wave + k, lane, sgd_local, lr, xdst);
+    dense_w_task(a, j * 8 + wave, lane, sgd_local, lr, xdst);
   } else if (j == 100) {
-    for (int T = kD1TasksW3 - 8 + wave; T < kDenseTasks; T += 4) dense_w_task(a, T, lane, sgd_local, lr, xdst);
+    for (int T = kD1TasksW3 - 8 + wave; T < kDenseTasks; T += 8) dense_w_task(a, T, lane, sgd_local, lr, xdst);
   } else if (j < kFxDense + 289) {
-    const int row = j - kFxDense, c = tid >> 2, sub = tid & 3;
+    const int row = j - kFxDense, c = tid >> 3, sub = tid & 7;
     const int n = kMnistPart2Rows * 64, oc = row * 64 + c;
     const int e2 = row < 288 ? a.ow2 + oc : a.ob2 + c;
     const float wold = sgd_local ? a.W[e2] : 0.f;
     float sum = 0.f;
-    for (int base = 0; base < a.b; base += 64) {
-      float v[16];
+    for (int base = 0; base < a.b; base += 64) {  // 8 images per thread in flight
+      float v[8];
 #pragma unroll
-      for (int jj = 0; jj < 16; ++jj) v[jj] = a.part2[(size_t)min(base + sub + 4 * jj, a.b - 1) * n + oc];
+      for (int jj = 0; jj < 8; ++jj) v[jj] = a.part2[(size_t)min(base + sub + 8 * jj, a.b - 1) * n + oc];
 #pragma unroll
-      for (int jj = 0; jj < 16; ++jj) sum += (base + sub + 4 * jj < a.b) ? v[jj] : 0.f;
+      for (int jj = 0; jj < 8; ++jj) sum += (base + sub + 8 * jj < a.b) ? v[jj] : 0.f;
     }
     sum += __shfl_xor(sum, 1, 64);
     sum += __shfl_xor(sum, 2, 64);
+    sum += __shfl_xor(sum, 4, 64);
     if (sub == 0) {
       a.G[e2] = sum;
       if (xdst != nullptr) xdst[e2] = sum;
       if (sgd_local) a.W[e2] = wold - lr * sum;
     }
   } else {
-    const int q = j - kFxDense - 289, o = q * 16 + (tid >> 4), sub = tid & 15;
+    const int q = j - kFxDense - 289, o = q * 16 + (tid >> 5), sub = tid & 31;
     const int rows = mnist_part1_rows(a.b, true);
     const int e1 = o < 288 ? a.ow1 + o : a.ob1 + (o - 288);
     const float wold = sgd_local ? a.W[e1] : 0.f;
     float sum = 0.f;
-    for (int base = 0; base < rows; base += 128) {
+    for (int base = 0; base < rows; base += 256) {
       float v[8];
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) v[jj] = a.part1[(size_t)min(base + sub + 16 * jj, rows - 1) * kMnistPart1Cols + o];
+      for (int jj = 0; jj < 8; ++jj) v[jj] = a.part1[(size_t)min(base + sub + 32 * jj, rows - 1) * kMnistPart1Cols + o];
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) sum += (base + sub + 16 * jj < rows) ? v[jj] : 0.f;
+      for (int jj = 0; jj < 8; ++jj) sum += (base + sub + 32 * jj < rows) ? v[jj] : 0.f;
     }
 #pragma unroll
-    for (int m = 1; m < 16; m <<= 1) sum += __shfl_xor(sum, m, 64);
+    for (int m = 1; m < 32; m <<= 1) sum += __shfl_xor(sum, m, 64);
     if (sub == 0) {
       a.G[e1] = sum;
       if (xdst != nullptr) xdst[e1] = sum;
@@ -1408,7 +1406,7 @@ __global__ __launch_bounds__(256) void k_finalize_x(MnistArgs a, int apply_sgd) 
     int lo, cnt;
     fx_range(a, j, lo, cnt);
     const int n4 = cnt >> 2;  // (every range starts 16-B aligned: slab offsets are multiples of 4)
-    for (int t = tid; t < n4; t += 256) {
+    for (int t = tid; t < n4; t += 512) {
       const int64_t off = lo + 4 * t;
       f4 v[R];
 #pragma unroll
@@ -1418,7 +1416,7 @@ __global__ __launch_bounds__(256) void k_finalize_x(MnistArgs a, int apply_sgd) 
       for (int r = 1; r < R; ++r) acc += v[r];
       st4(a.W + off, ld4(a.W + off) - lr * acc);
     }
-    for (int t = 4 * n4 + tid; t < cnt; t += 256) {
+    for (int t = 4 * n4 + tid; t < cnt; t += 512) {
       const int64_t off = lo + t;
       float acc = a.xa.p.buf[0][half + off];
 #pragma unroll
@@ -1504,14 +1502,14 @@ void mnist_finalize_x(const MnistArgs& a, bool apply_sgd, hipStream_t s) {
   const int R = (a.xchg && apply_sgd) ? a.xa.world : 1;
   const int sgd = apply_sgd ? 1 : 0;
   switch (R) {  // the rank count is a template parameter (straight-line rank-order sums)
-    case 2: hipLaunchKernelGGL(k_finalize_x<2>, dim3(kFxBlocks), dim3(256), 0, s, a, sgd); break;
-    case 3: hipLaunchKernelGGL(k_finalize_x<3>, dim3(kFxBlocks), dim3(256), 0, s, a, sgd); break;
-    case 4: hipLaunchKernelGGL(k_finalize_x<4>, dim3(kFxBlocks), dim3(256), 0, s, a, sgd); break;
-    case 5: hipLaunchKernelGGL(k_finalize_x<5>, dim3(kFxBlocks), dim3(256), 0, s, a, sgd); break;
-    case 6: hipLaunchKernelGGL(k_finalize_x<6>, dim3(kFxBlocks), dim3(256), 0, s, a, sgd); break;
-    case 7: hipLaunchKernelGGL(k_finalize_x<7>, dim3(kFxBlocks), dim3(256), 0, s, a, sgd); break;
-    case 8: hipLaunchKernelGGL(k_finalize_x<8>, dim3(kFxBlocks), dim3(256), 0, s, a, sgd); break;
-    default: hipLaunchKernelGGL(k_finalize_x<1>, dim3(kFxBlocks), dim3(256), 0, s, a, sgd); break;
+    case 2: hipLaunchKernelGGL(k_finalize_x<2>, dim3(kFxBlocks), dim3(512), 0, s, a, sgd); break;
+    case 3: hipLaunchKernelGGL(k_finalize_x<3>, dim3(kFxBlocks), dim3(512), 0, s, a, sgd); break;
+    case 4: hipLaunchKernelGGL(k_finalize_x<4>, dim3(kFxBlocks), dim3(512), 0, s, a, sgd); break;
+    case 5: hipLaunchKernelGGL(k_finalize_x<5>, dim3(kFxBlocks), dim3(512), 0, s, a, sgd); break;
+    case 6: hipLaunchKernelGGL(k_finalize_x<6>, dim3(kFxBlocks), dim3(512), 0, s, a, sgd); break;
+    case 7: hipLaunchKernelGGL(k_finalize_x<7>, dim3(kFxBlocks), dim3(512), 0, s, a, sgd); break;
+    case 8: hipLaunchKernelGGL(k_finalize_x<8>, dim3(kFxBlocks), dim3(512), 0, s, a, sgd); break;
+    default: hipLaunchKernelGGL(k_finalize_x<1>, dim3(kFxBlocks), dim3(512), 0, s, a, sgd); break;
   }
 }
 void sgd_apply(float* w, const float* g, const float* lr, int64_t n, hipStream_t s) {

@@ -22,10 +22,13 @@ def short(name: str) -> str:
 
 def category(name: str) -> str:
     n = name.lower()
+    # the framework's own kernels first: their names contain "conv" / "gemm" as well
+    if "tdl::" in n:
+        if "conv" in n or "gemm" in n:
+            return "tdl conv/gemm (hand-written)"
+        return "tdl HIP kernels (bn/pool/other)"
     if "igemm" in n or "conv" in n or "gemm" in n or "cijk" in n:
         return "conv/gemm (library)"
-    if "tdl::" in n:
-        return "tdl HIP kernels"
     if "subtensor" in n or "fillbuffer" in n or "copybuffer" in n:
         return "MIOpen/runtime fill+cast"
     if "at::native" in n:

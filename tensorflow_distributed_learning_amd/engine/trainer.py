@@ -230,15 +230,28 @@ class GenericTrainer:
         self.plan = bucketing.plan(self.G.numel(), self.comm.world_size, lw, self._wire, per_pack,
                                    algorithm=getattr(self.comm, "algorithm", self.comm.name))
         self._wire_full = None
-        if self.comm.world_size == 1 or self.comm.name != "rccl":
+        if self.comm.world_size == 1 or self.device.type != "cuda":
             return None
         if explicit == 0:
             self.plan.n_buckets, self.plan.bucket_bytes = 1, self.plan.wire_bytes
             return None
+        xg = getattr(self.comm, "xgmi", None)
+        if self.comm.name != "rccl":
+            # no RCCL (replicas sharing one GPU: gloo control plane): the xGMI kernel is the
+            # device data plane, f32 on the wire, buckets within its message limit
+            if xg is None:
+                return None
+            self._wire, wb = "float32", 4
+            self.plan.wire_dtype, self.plan.wire_bytes = "float32", self.G.numel() * 4
+            self.plan.bucket_bytes = min(self.plan.bucket_bytes, xg.limit * 4)
+            self.plan.algorithm = getattr(self.comm, "algorithm", "xgmi")
         layout = self.model._layout
         ranges = layout.buckets(self.plan.bucket_bytes, elem_bytes=wb)
         self.plan.n_buckets = len(ranges)
-        if len(ranges) <= 1:
+        if len(ranges) <= 1 and self.comm.name == "rccl":
+            return None
+        # collective (every rank computes the same ranges): RCCL, or an xGMI channel per size
+        if not self.comm.device_bucket_capable([e - s for s, e in ranges]):
             return None
         var_bucket = {}
         for bi, (s, e) in enumerate(ranges):

@@ -74,6 +74,11 @@ class Communicator:
         workgroups (xGMI); None when the communicator has none."""
         return None
 
+    def device_bucket_capable(self, numels) -> bool:
+        """Collective: whether bucketed all-reduces of these sizes can run asynchronously on the
+        device and inside a captured hipGraph (RCCL, or the xGMI kernel)."""
+        return False
+
     def shutdown(self) -> None:
         pass
 
@@ -201,11 +206,30 @@ class TorchCommunicator(Communicator):
         return t
 
     def all_reduce_async(self, t, op="sum"):
+        if self.xgmi is not None and op in ("sum", "mean") and self.xgmi.applicable(t) and \
+                self.xgmi.has_channel(t.numel()):
+            # xGMI kernel on a side stream (forked from the current one, joined by wait()): the
+            # bucket's exchange overlaps the rest of the backward and records into a hipGraph
+            return _SideStreamWork(self, t, op)
         if op == "mean" and not self._avg_native:
             work = dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True)
             return _ScaleOnWait(work, t, 1.0 / self.world_size)
         rop = dist.ReduceOp.AVG if op == "mean" else _TORCH_OPS[op]
         return dist.all_reduce(t, op=rop, async_op=True)
+
+    def device_bucket_capable(self, numels) -> bool:
+        """Whether bucketed all-reduces of these sizes can be issued asynchronously from backward
+        hooks and recorded into a whole-step hipGraph: RCCL, or the xGMI kernel for every size
+        (channels prepared collectively here; the only device data plane of replicas sharing a GPU)."""
+        if self.backend == "nccl":
+            return True
+        if self.xgmi is None:
+            return False
+        numels = [int(n) for n in numels]
+        if any(n > self.xgmi.limit for n in numels):
+            return False
+        self.prepare_all_reduce(*numels)
+        return self.xgmi is not None and all(self.xgmi.has_channel(n) for n in numels)
 
     def broadcast(self, t, src=0):
         dist.broadcast(t, src=src)
@@ -241,14 +265,22 @@ class TorchCommunicator(Communicator):
         dev = self.device
         flag = torch.ones(1, device=dev)
         t = torch.full((64,), float(self.rank + 1), device=dev)
+        u = torch.full((4096,), float(self.rank + 1), device=dev)
         dist.all_reduce(t)  # warm the communicator outside capture
+        self.all_reduce_async(u).wait()
         g = None
         try:
             s = torch.cuda.Stream(dev)
             s.wait_stream(torch.cuda.current_stream(dev))
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=s):
+                # the two patterns the engines record: a synchronous all-reduce, and an async one
+                # launched mid-computation (as from a backward hook) and waited for later
                 dist.all_reduce(t)
+                u.mul_(1.0)
+                work = self.all_reduce_async(u)
+                t.add_(0.0)
+                work.wait()
             torch.cuda.synchronize(dev)
         except Exception:  # capture unsupported by this RCCL/torch build
             g = None
@@ -257,10 +289,11 @@ class TorchCommunicator(Communicator):
         ok = bool(flag.item() > 0.5)
         if ok:
             t.fill_(float(self.rank + 1))
+            u.fill_(float(self.rank + 1))
             g.replay()
             torch.cuda.synchronize(dev)
             want = float(self.world_size * (self.world_size + 1) // 2)
-            flag.fill_(1.0 if bool(torch.all(t == want)) else 0.0)
+            flag.fill_(1.0 if bool(torch.all(t == want)) and bool(torch.all(u == want)) else 0.0)
             dist.all_reduce(flag, op=dist.ReduceOp.MIN)
             ok = bool(flag.item() > 0.5)
         self._capture_ok = ok
@@ -280,6 +313,27 @@ class TorchCommunicator(Communicator):
             except Exception:
                 pass
             self._owns_group = False
+
+
+class _SideStreamWork:
+    """An all-reduce issued on the communicator's side stream (forked from the caller's current
+    stream); ``wait()`` joins it back into the stream current at wait time."""
+
+    def __init__(self, comm, t, op):
+        dev = t.device
+        if getattr(comm, "_side", None) is None:
+            comm._side = torch.cuda.Stream(dev)
+        side = comm._side
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            comm.xgmi.all_reduce(t, op)
+        self._side, self._dev = side, dev
+
+    def wait(self):
+        torch.cuda.current_stream(self._dev).wait_stream(self._side)
+
+    def is_completed(self):
+        return self._side.query()
 
 
 class _ScaleOnWait:

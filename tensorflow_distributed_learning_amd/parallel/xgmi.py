@@ -185,6 +185,9 @@ class XgmiAllReduce:
         self._chans[n] = self._make(n)
         return self._chans[n]
 
+    def has_channel(self, n: int) -> bool:
+        return bool(self.ok) and int(n) in self._chans
+
     def applicable(self, t: torch.Tensor) -> bool:
         return (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.data_ptr() % 16 == 0 and
                 0 < t.numel() <= self.limit)
