@@ -267,7 +267,9 @@ class TorchCommunicator(Communicator):
         t = torch.full((64,), float(self.rank + 1), device=dev)
         u = torch.full((4096,), float(self.rank + 1), device=dev)
         dist.all_reduce(t)  # warm the communicator outside capture
-        self.all_reduce_async(u).wait()
+        torch.cuda.synchronize(dev)
+        # (no eager async warm-up: with torch's cached collective events, an eager async work the
+        # PG watchdog still tracks can see its event re-recorded inside the capture below)
         g = None
         try:
             s = torch.cuda.Stream(dev)

@@ -76,7 +76,10 @@ def test_captured_overlapped_allreduce_matches_eager(tmp_path):
     script = tmp_path / "job.py"
     script.write_text(textwrap.dedent(BODY))
     res = tmp_path / "res.json"
-    env = dict(os.environ, PYTHONPATH=ROOT, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    # (the overlap option splits the step into forward_dense / backward_conv launches; the compared
+    # eager and serial paths must use the same unfused kernels to be bit-comparable)
+    env = dict(os.environ, PYTHONPATH=ROOT, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+               TDL_MNIST_FUSED_BWD="0")
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "TF_CONFIG", "TDL_CAPTURE_ALLREDUCE"):
         env.pop(k, None)
     r = subprocess.run([sys.executable, str(script), str(res)], env=env, capture_output=True, text=True,
