@@ -637,8 +637,13 @@ class FusedMnistTrainer:
         if getattr(self.comm, "xgmi", None) is not None:
             self.comm.xgmi = None
             self.comm.algorithm = "rccl" if self.comm.name == "rccl" else self.comm.name
+            self.comm._capture_ok = None  # re-probe: without xGMI a gloo group cannot be captured
         self._graphs = {}
+        self._steps = {}
         self._capture_comm = None
+        self._comm_prepared = False
+        self._xchg = None
+        self.allreduce_mode = getattr(self.comm, "algorithm", self.comm.name)
 
 
 class _IndexProducer:

@@ -230,7 +230,7 @@ class GenericTrainer:
         self.plan = bucketing.plan(self.G.numel(), self.comm.world_size, lw, self._wire, per_pack,
                                    algorithm=getattr(self.comm, "algorithm", self.comm.name))
         self._wire_full = None
-        if self.comm.world_size == 1 or self.device.type != "cuda":
+        if self.comm.world_size == 1:
             return None
         if explicit == 0:
             self.plan.n_buckets, self.plan.bucket_bytes = 1, self.plan.wire_bytes
@@ -251,7 +251,8 @@ class GenericTrainer:
         if len(ranges) <= 1 and self.comm.name == "rccl":
             return None
         # collective (every rank computes the same ranges): RCCL, or an xGMI channel per size
-        if not self.comm.device_bucket_capable([e - s for s, e in ranges]):
+        capable = getattr(self.comm, "device_bucket_capable", None)
+        if capable is not None and not capable([e - s for s, e in ranges]):
             return None
         var_bucket = {}
         for bi, (s, e) in enumerate(ranges):

@@ -6,8 +6,8 @@ Model of one MI355X node (MI355X_MICROARCH.md): every GPU has 7 point-to-point x
 153.6 GB/s per direction each, to the 7 other GPUs (a full mesh; no switch).  A ring all-reduce
 moves ``2 (R-1)/R x bytes`` through every GPU; RCCL runs one ring channel per direct link, so at
 R GPUs ``min(R-1, 7)`` links carry it in parallel and one ring alone would be bound by ONE link.
-Each collective call also pays a fixed latency (launch + the ring's 2(R-1) dependent hops, taken
-here as 25 us on one node, measured order of magnitude for RCCL on MI300-class xGMI).
+Each collective call also pays a fixed latency (launch + the ring's 2(R-1) dependent hops; a
+modelled 25 us for RCCL, the measured 4.7 us for the xGMI one-shot kernel).
 
     t(bucket) = L + 2 (R-1)/R * bucket_bytes / (eff * 153.6 GB/s * min(R-1, 7))
 
@@ -23,10 +23,16 @@ from __future__ import annotations
 from dataclasses import asdict, dataclass
 from typing import Optional
 
-XGMI_LINK_GBPS = 153.6       # per direction, per link
+XGMI_LINK_GBPS = 153.6       # per direction, per link (MI355X_MICROARCH.md)
 XGMI_LINKS = 7               # point-to-point links per GPU (8-GPU full mesh)
-RCCL_CALL_LATENCY_US = 25.0  # per collective call on one node (order of magnitude)
-LINK_EFFICIENCY = 0.6        # achieved fraction of the link rate for ring traffic
+# Per-call fixed costs.  MEASURED on one MI355X (profiles/comm_fixed_costs_r3.jsonl,
+# scripts/bench_comm_fixed.py): the xGMI one-shot kernel between 2 replica processes sharing the GPU
+# costs 4.7 us at 64 KiB (flags, fences, launch; no fabric hop).  RCCL's per-call latency is NOT
+# measurable on a one-GPU box (a world-1 RCCL all-reduce launches nothing: 0.07 us) and stays the
+# modelled 25 us for 2(R-1) dependent ring hops on one node.  The link term is modelled too.
+XGMI_CALL_US = 4.7           # measured (see above)
+RCCL_CALL_LATENCY_US = 25.0  # modelled
+LINK_EFFICIENCY = 0.6        # modelled achieved fraction of the link rate
 MIN_BUCKET_BYTES = 4 << 20
 MIN_BUCKETS = 4
 
@@ -51,6 +57,13 @@ class BucketPlan:
         d = asdict(self)
         d["per_bucket_us"] = round(self.per_bucket_us, 1)
         d["total_us"] = round(self.total_us, 1)
+        xg = self.algorithm.startswith("xgmi")
+        d["cost_model"] = {
+            "per_bucket_us": "modelled",
+            "call_latency_us": XGMI_CALL_US if xg else RCCL_CALL_LATENCY_US,
+            "call_latency_source": "measured (profiles/comm_fixed_costs_r3.jsonl)" if xg else "modelled",
+            "fabric": f"modelled: {XGMI_LINK_GBPS} GB/s per xGMI link x efficiency {LINK_EFFICIENCY}",
+        }
         return d
 
 
@@ -61,6 +74,14 @@ def ring_allreduce_us(nbytes: int, world: int, links: Optional[int] = None) -> f
     links = links if links is not None else min(world - 1, XGMI_LINKS)
     bw = LINK_EFFICIENCY * XGMI_LINK_GBPS * 1e9 * links
     return RCCL_CALL_LATENCY_US + 2.0 * (world - 1) / world * nbytes / bw * 1e6
+
+
+def xgmi_oneshot_us(nbytes: int, world: int) -> float:
+    """Time of one xGMI one-shot all-reduce: the measured fixed cost + every rank pulling the
+    ``nbytes`` of each peer over its own direct link, all links in parallel (modelled)."""
+    if world <= 1:
+        return 0.0
+    return XGMI_CALL_US + nbytes / (LINK_EFFICIENCY * XGMI_LINK_GBPS * 1e9) * 1e6
 
 
 def plan(grad_numel: int, world: int, local_world: Optional[int] = None, wire_dtype: str = "float32",
@@ -80,6 +101,6 @@ def plan(grad_numel: int, world: int, local_world: Optional[int] = None, wire_dt
     bucket = max(1, min(bucket, wire_bytes))
     n = max(1, -(-wire_bytes // bucket))
     links = min(max(local_world - 1, 1), XGMI_LINKS)
-    per = ring_allreduce_us(bucket, world, links)
+    per = xgmi_oneshot_us(bucket, world) if algorithm.startswith("xgmi") else ring_allreduce_us(bucket, world, links)
     return BucketPlan(algorithm, world, local_world, grad_numel, wire_dtype, wire_bytes, n, bucket, links, per,
                       per * n if world > 1 else 0.0)

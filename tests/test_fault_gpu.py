@@ -150,6 +150,7 @@ def test_corrupted_replica_is_caught(tmp_path, mode):
                                              TDL_REPLICA_MISMATCH=mode, TDL_CHECK_REPLICAS="0",
                                              TDL_CHECK_REPLICAS_EVERY="0"))
     assert "perturbed" in r.stderr, r.stderr[-3000:]
+    assert all((tmp_path / f"r{i}.json").exists() for i in range(2)), r.stderr[-4000:]
     a, b = (json.load(open(tmp_path / f"r{i}.json")) for i in range(2))
     assert a["engine"] == "fused"
     if mode == "repair":
