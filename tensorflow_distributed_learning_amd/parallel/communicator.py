@@ -77,7 +77,7 @@ class Communicator:
     def device_bucket_capable(self, numels) -> bool:
         """Collective: whether bucketed all-reduces of these sizes can run asynchronously on the
         device and inside a captured hipGraph (RCCL, or the xGMI kernel)."""
-        return False
+        return self.name == "rccl"
 
     def shutdown(self) -> None:
         pass
