@@ -167,7 +167,9 @@ def main():
             "config": {"model": "tf_dist_example.py MNIST CNN (Conv32-Pool-Conv64-Pool-Dense128-Dense10, 225,034 params)",
                        "global_batch": B, "seq_len": None, "image_shape": [28, 28, 1],
                        "parallelism": f"dp{R}", "engine": trainer.kind, "communicator": comm.name,
-                       "allreduce": getattr(comm, "algorithm", comm.name),
+                       "allreduce": getattr(trainer, "allreduce_mode", None) or getattr(comm, "algorithm", comm.name),
+                       "kernels_per_step": 2 if getattr(trainer, "_steps", None) and all(
+                           getattr(st, "fused_bwd", False) for st in trainer._steps.values()) else None,
                        "steps_per_execution": spe, "graph_captured": bool(trainer.capture),
                        "input_prefetch_executions": 1,
                        "allreduce_in_graph": bool(trainer.capture_comm and R > 1),

@@ -2,10 +2,10 @@
 
 Tensor bundle (``<prefix>.index`` + ``<prefix>.data-00000-of-00001``):
   * ``.data`` – raw little-endian tensor bytes, 64-byte aligned, in variable order;
-  * ``.index`` – JSON ``{"format": "tdl-bundle-v1", "tensors": {name: {dtype, shape, offset,
-    nbytes, crc32c}}}``.  (TF's own index is a LevelDB table of protobufs; the directory layout,
-    file names and TF variable names/layouts – HWIO conv kernels, [in,out] dense kernels – are kept
-    so the files line up with what a TF user expects; the index encoding is documented JSON.)
+  * ``.index`` – TensorFlow's own format: a LevelDB-format table of ``BundleHeaderProto`` /
+    ``BundleEntryProto`` records (ckpt/tensor_bundle.py), with TF variable names and layouts (HWIO
+    conv kernels, [in,out] dense kernels).  ``TDL_CKPT_INDEX=json`` writes the round-1/2 JSON index
+    ``{"format": "tdl-bundle-v1", ...}`` instead; both are read.
 
 Model directory (``model.save(path)``)::
 
@@ -29,6 +29,7 @@ import numpy as np
 import torch
 
 from ..utils.events import crc32c
+from . import tensor_bundle as TB
 
 FORMAT = "tdl-bundle-v1"
 _DT = {torch.float32: "float32", torch.float64: "float64", torch.float16: "float16", torch.bfloat16: "bfloat16",
@@ -56,16 +57,27 @@ def write_bundle(prefix: str, tensors: Dict[str, torch.Tensor]) -> None:
                                       "nbytes": len(raw), "crc32c": crc32c(raw)}
             off += len(raw)
     os.replace(tmp_data, prefix + ".data-00000-of-00001")
-    with open(prefix + ".index.tmp", "w") as f:
-        json.dump(index, f)
+    if os.environ.get("TDL_CKPT_INDEX", "tf") == "json":
+        with open(prefix + ".index.tmp", "w") as f:
+            json.dump(index, f)
+    else:
+        TB.write_index(prefix + ".index.tmp", index["tensors"])
     os.replace(prefix + ".index.tmp", prefix + ".index")
 
 
-def read_bundle(prefix: str, verify: bool = True) -> Dict[str, torch.Tensor]:
-    with open(prefix + ".index") as f:
+def _read_index(prefix: str) -> dict:
+    path = prefix + ".index"
+    if TB.is_table(path):
+        return {"format": "tf-tensor-bundle", "tensors": TB.read_index(path)}
+    with open(path) as f:
         index = json.load(f)
     if index.get("format") != FORMAT:
-        raise ValueError(f"{prefix}.index is not a {FORMAT} index")
+        raise ValueError(f"{path} is neither a TF tensor-bundle index nor a {FORMAT} index")
+    return index
+
+
+def read_bundle(prefix: str, verify: bool = True) -> Dict[str, torch.Tensor]:
+    index = _read_index(prefix)
     out = {}
     with open(prefix + ".data-00000-of-00001", "rb") as f:
         data = f.read()
@@ -83,9 +95,7 @@ def read_bundle(prefix: str, verify: bool = True) -> Dict[str, torch.Tensor]:
 
 
 def list_variables(prefix: str):
-    with open(prefix + ".index") as f:
-        index = json.load(f)
-    return [(n, tuple(e["shape"])) for n, e in index["tensors"].items()]
+    return [(n, tuple(e["shape"])) for n, e in _read_index(prefix)["tensors"].items()]
 
 
 # ------------------------------------------------------------------------------------------------

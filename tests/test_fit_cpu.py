@@ -120,8 +120,10 @@ def test_save_load_model_and_weights(tmp_path):
     m.save(p)
     assert set(os.listdir(p)) >= {"saved_model.json", "variables", "assets"}
     assert sorted(os.listdir(os.path.join(p, "variables"))) == ["variables.data-00000-of-00001", "variables.index"]
-    idx = json.load(open(os.path.join(p, "variables", "variables.index")))
-    assert "conv2d/kernel:0" in idx["tensors"] and idx["tensors"]["conv2d/kernel:0"]["shape"] == [3, 3, 1, 32]
+    from tensorflow_distributed_learning_amd.ckpt import checkpoint as ck
+
+    idx = dict(ck.list_variables(os.path.join(p, "variables", "variables")))  # TF tensor-bundle index
+    assert idx["conv2d/kernel:0"] == (3, 3, 1, 32)
     m2 = keras.models.load_model(p)
     x = torch.rand(4, 28, 28, 1)
     assert torch.allclose(m(x), m2(x), atol=1e-6)

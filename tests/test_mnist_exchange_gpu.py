@@ -145,3 +145,23 @@ def test_finalize_exchange_multi_process(tmp_path, R):
     for rc, out in outs:
         assert rc == 0, out[-3000:]
         assert "exchange ok" in out
+
+
+def test_bench_two_replicas_exchange_in_finalize(tmp_path):
+    """bench.py at N=2 end to end on the R > 1 production path: the fused forward/backward kernel
+    and the finalize whose workgroups all-reduce over xGMI, captured in the execution graphs.  On
+    the shared GPU this needs both replicas' kernels resident beside each other, so the per-replica
+    batch is 16 (64 fused workgroups each); on one GPU per replica b = 64 is the default."""
+    env = dict(os.environ, PYTHONPATH=ROOT, TDL_SHARE_GPU="1", TDL_MNIST_DP2_FWD="1", TDL_XGMI_TIMEOUT="30")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "TF_CONFIG", "TDL_LAUNCHED", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--per-replica-batch", "16", "--steps", "40",
+                        "--warmup", "8"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    import json as _json
+
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    d = _json.loads(line)
+    cfg = d["config"]
+    assert d["n_gpus"] == 2 and cfg["allreduce"] == "xgmi-in-finalize", cfg
+    assert cfg["kernels_per_step"] == 2 and cfg["allreduce_in_graph"] and cfg["replicas_identical"], cfg
