@@ -44,11 +44,40 @@ __device__ __forceinline__ void st4_sc1(__amdgpu_buffer_rsrc_t r, int byte_off, 
 // memory clobber keeps the compiler from moving LDS accesses across it.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// Sum across the four 16-lane groups of a wave (lanes l, l^16, l^32, l^48).
+// ---- cross-lane exchanges on the VALU (gfx950 v_permlane{16,32}_swap, DPP) instead of
+// ds_bpermute (__shfl_xor), which goes through the LDS pipe with its latency ----
+// Reduce-scatter step across the 16-lane row pairs (lane l <-> l ^ 16): a lane in an even row
+// returns lo(l) + lo(l ^ 16), a lane in an odd row hi(l) + hi(l ^ 16).  v_permlane16_swap swaps the
+// odd rows of its first operand with the even rows of its second, which leaves exactly those two
+// addends in the two results.
+__device__ __forceinline__ float rs_swap16(float lo, float hi) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(lo), __float_as_uint(hi), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// the same across the wave halves (lane l <-> l ^ 32)
+__device__ __forceinline__ float rs_swap32(float lo, float hi) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(lo), __float_as_uint(hi), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// DPP partner values within a 16-lane row: xor 8 (row_ror:8), the 8-lane half mirror (l <-> 7 - l:
+// pairs each lane of a 4-lane half with one of the other half, as xor 4 does), xor 2 / xor 1 (quad_perm)
+__device__ __forceinline__ float dpp_xor8(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x128, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float dpp_mirror8(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x141, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float dpp_xor2(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x4E, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float dpp_xor1(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false));
+}
+
+// Sum across the four 16-lane groups of a wave (lanes l, l^16, l^32, l^48), in every lane.
 __device__ __forceinline__ float sum_lane_groups(float v) {
-  v += __shfl_xor(v, 16, 64);
-  v += __shfl_xor(v, 32, 64);
-  return v;
+  v = rs_swap16(v, v);
+  return rs_swap32(v, v);
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -71,30 +71,23 @@ __device__ __forceinline__ void head_stamp(unsigned long long* buf, int k) {
 // (lane halves keep 5 / 3 / 2 / 1 of the classes: 13 cross-lane moves instead of 10 x 6) whose
 // class sums end in lane groups, then broadcast by v_readlane.
 __device__ __forceinline__ void wave_sum10(const float (&v)[10], int l, float (&out)[10]) {
-  const bool b32 = l & 32, b16 = l & 16, b8 = l & 8, b4 = l & 4;
-  float u[5];
+  const bool b8 = l & 8, b4 = l & 4;
+  float u[5];  // lanes 0..31 keep v[0..4], lanes 32..63 v[5..9] (v_permlane32_swap)
 #pragma unroll
-  for (int j = 0; j < 5; ++j) {
-    const float send = b32 ? v[j] : v[j + 5];
-    u[j] = (b32 ? v[j + 5] : v[j]) + __shfl_xor(send, 32, 64);
-  }
-  float w[3];  // b16 = 0 keeps u[0..2], b16 = 1 keeps u[3..4] (+0)
+  for (int j = 0; j < 5; ++j) u[j] = rs_swap32(v[j], v[j + 5]);
+  float w[3];  // even 16-lane rows keep u[0..2], odd rows u[3..4] (+0) (v_permlane16_swap)
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const float hi = j + 3 < 5 ? u[j + 3] : 0.f;
-    const float send = b16 ? u[j] : hi;
-    w[j] = (b16 ? hi : u[j]) + __shfl_xor(send, 16, 64);
-  }
-  float x[2];  // b8 = 0 keeps w[0..1], b8 = 1 keeps w[2] (+0)
+  for (int j = 0; j < 3; ++j) w[j] = rs_swap16(u[j], j + 3 < 5 ? u[j + 3] : 0.f);
+  float x[2];  // b8 = 0 keeps w[0..1], b8 = 1 keeps w[2] (+0) (DPP row_ror:8)
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const float hi = j + 2 < 3 ? w[j + 2] : 0.f;
-    const float send = b8 ? w[j] : hi;
-    x[j] = (b8 ? hi : w[j]) + __shfl_xor(send, 8, 64);
+    x[j] = (b8 ? hi : w[j]) + dpp_xor8(b8 ? w[j] : hi);
   }
-  float y = (b4 ? x[1] : x[0]) + __shfl_xor(b4 ? x[0] : x[1], 4, 64);
-  y += __shfl_xor(y, 2, 64);
-  y += __shfl_xor(y, 1, 64);
+  // b4 = 0 keeps x[0], b4 = 1 x[1]; the partner is the 8-lane mirror (it has the other b4)
+  float y = (b4 ? x[1] : x[0]) + dpp_mirror8(b4 ? x[0] : x[1]);
+  y += dpp_xor2(y);
+  y += dpp_xor1(y);
   // class c sits in lane 32*hi + 16*b + 8*c8 + 4*d: c = 5*hi + (b ? 3 : 0) + (2*c8 + d)
 #pragma unroll
   for (int c = 0; c < 10; ++c) {
@@ -107,29 +100,28 @@ __device__ __forceinline__ void wave_sum10(const float (&v)[10], int l, float (&
 // Sums over the 32 lanes of each half-wave of N <= 32 per-lane values (v[k], k >= N taken as 0):
 // a reduce-scatter butterfly (16 + 8 + 4 + 2 + 1 cross-lane moves); lane l returns the sum of
 // value (l & 31) over its half-wave.
+// (every step on the VALU: v_permlane16_swap for the 16-lane rows, DPP within a row; the 8-lane
+// mirror stands in for xor 4 -- which half a lane keeps is set by its own lane bits, so the lane
+// that ends with value k is the same as with a plain xor butterfly)
 template <int N>
 __device__ __forceinline__ float reduce_scatter32(const float (&v)[N], int l) {
   float s16[16];
-  const bool b16 = l & 16;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const float lo = k < N ? v[k] : 0.f, hi = k + 16 < N ? v[k + 16] : 0.f;
-    s16[k] = (b16 ? hi : lo) + __shfl_xor(b16 ? lo : hi, 16, 64);
-  }
+  for (int k = 0; k < 16; ++k) s16[k] = rs_swap16(k < N ? v[k] : 0.f, k + 16 < N ? v[k + 16] : 0.f);
   float s8[8];
   const bool b8 = l & 8;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) s8[k] = (b8 ? s16[k + 8] : s16[k]) + __shfl_xor(b8 ? s16[k] : s16[k + 8], 8, 64);
+  for (int k = 0; k < 8; ++k) s8[k] = (b8 ? s16[k + 8] : s16[k]) + dpp_xor8(b8 ? s16[k] : s16[k + 8]);
   float s4[4];
   const bool b4 = l & 4;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) s4[k] = (b4 ? s8[k + 4] : s8[k]) + __shfl_xor(b4 ? s8[k] : s8[k + 4], 4, 64);
+  for (int k = 0; k < 4; ++k) s4[k] = (b4 ? s8[k + 4] : s8[k]) + dpp_mirror8(b4 ? s8[k] : s8[k + 4]);
   float s2[2];
   const bool b2 = l & 2;
 #pragma unroll
-  for (int k = 0; k < 2; ++k) s2[k] = (b2 ? s4[k + 2] : s4[k]) + __shfl_xor(b2 ? s4[k] : s4[k + 2], 2, 64);
+  for (int k = 0; k < 2; ++k) s2[k] = (b2 ? s4[k + 2] : s4[k]) + dpp_xor2(b2 ? s4[k] : s4[k + 2]);
   const bool b1 = l & 1;
-  return (b1 ? s2[1] : s2[0]) + __shfl_xor(b1 ? s2[0] : s2[1], 1, 64);
+  return (b1 ? s2[1] : s2[0]) + dpp_xor1(b1 ? s2[0] : s2[1]);
 }
 
 constexpr int kHeadQuarter = 3;  // dp2_fwd: the quarter workgroup whose head writes metrics / H / dH / dL
@@ -1367,9 +1359,9 @@ __global__ __launch_bounds__(512) void k_finalize_x(MnistArgs a, int apply_sgd) 
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) sum += (base + sub + 8 * jj < a.b) ? v[jj] : 0.f;
     }
-    sum += __shfl_xor(sum, 1, 64);
-    sum += __shfl_xor(sum, 2, 64);
-    sum += __shfl_xor(sum, 4, 64);
+    sum += dpp_xor1(sum);  // (8-lane all-reduce on the VALU)
+    sum += dpp_xor2(sum);
+    sum += dpp_mirror8(sum);
     if (sub == 0) {
       a.G[e2] = sum;
       if (xdst != nullptr) xdst[e2] = sum;
@@ -1389,7 +1381,11 @@ __global__ __launch_bounds__(512) void k_finalize_x(MnistArgs a, int apply_sgd) 
       for (int jj = 0; jj < 8; ++jj) sum += (base + sub + 32 * jj < rows) ? v[jj] : 0.f;
     }
 #pragma unroll
-    for (int m = 1; m < 32; m <<= 1) sum += __shfl_xor(sum, m, 64);
+    sum += dpp_xor1(sum);  // (32-lane all-reduce on the VALU)
+    sum += dpp_xor2(sum);
+    sum += dpp_mirror8(sum);
+    sum += dpp_xor8(sum);
+    sum = rs_swap16(sum, sum);
     if (sub == 0) {
       a.G[e1] = sum;
       if (xdst != nullptr) xdst[e1] = sum;
