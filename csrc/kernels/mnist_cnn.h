@@ -67,7 +67,7 @@ struct MnistArgs {
 
 // finalize workgroups of the fused_bwd step (k_finalize_x): 101 dense (dW3 rows 16m..16m+15 = 2048
 // slab floats each; the last: db3 + dW4 + db4), 289 conv2 rows (64 floats), 20 conv1 groups (16)
-constexpr int kFxDense = 101, kFxConv1 = 20;
+constexpr int kFxDense = 103, kFxConv1 = 20;  // dW3 rows x100, db3, dW4, db4 | conv2 rows | conv1
 constexpr int kFxBlocks = kFxDense + 289 + kFxConv1;
 
 constexpr int kMnistPart2Rows = 289;

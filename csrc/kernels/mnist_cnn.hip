@@ -1295,9 +1295,10 @@ __global__ __launch_bounds__(256) void k_finalize(MnistArgs a, int apply_sgd, in
 // KF-X: finalize of the fused_bwd step, one workgroup per contiguous slab range (kFxBlocks):
 // (512 threads = 8 waves each)
 //   [0, 100)    dW3 rows 16m .. 16m+15 (2048 floats): 8 dense tasks, one per wave
-//   100         db3 + dW4 + db4 (1418 floats, contiguous): 17 dense tasks
-//   [101, 390)  conv2 kernel row k (64 floats; row 288 = bias): 8 threads per output
-//   [390, 410)  conv1 kernel / bias outputs 16q .. 16q+15: 32 threads per output
+//   100 / 101   db3 (128 floats) / dW4 (1280 floats): 8 dense tasks each, one per wave
+//   102         db4 (10 floats): 1 dense task
+//   [103, 392)  conv2 kernel row k (64 floats; row 288 = bias): 8 threads per output
+//   [392, 412)  conv1 kernel / bias outputs 16q .. 16q+15: 4 rows x 16 columns per wave load
 // Each writes its gradient range into G.  R = 1 with SGD: W -= lr * G of the range.  R > 1 with
 // the exchange (a.xchg): the range is also published into this workgroup's slot of the channel's
 // exchange buffer (at its slab offsets), then the xGMI exchange with workgroup j of every peer
@@ -1310,8 +1311,14 @@ __device__ __forceinline__ void fx_range(const MnistArgs& a, int j, int& lo, int
     lo = a.ow3 + j * 2048;
     cnt = 2048;
   } else if (j == 100) {
-    lo = a.ob3;  // ob3, ow4, ob4 are contiguous (checked on the host)
-    cnt = 128 + 1280 + 10;
+    lo = a.ob3;
+    cnt = 128;
+  } else if (j == 101) {
+    lo = a.ow4;
+    cnt = 1280;
+  } else if (j == 102) {
+    lo = a.ob4;
+    cnt = 10;
   } else if (j < kFxDense + 288) {
     lo = a.ow2 + (j - kFxDense) * 64;
     cnt = 64;
@@ -1326,7 +1333,20 @@ __device__ __forceinline__ void fx_range(const MnistArgs& a, int j, int& lo, int
 }
 
 template <int R>
+__device__ __forceinline__ void finalize_x_body(const MnistArgs& a, int apply_sgd);
+
+// phase stamps of KF-X (diagnostics), after the fused kernel's grid*104 words: per wave, start and end
+template <int R>
 __global__ __launch_bounds__(512) void k_finalize_x(MnistArgs a, int apply_sgd) {
+  unsigned long long* sb = a.stamps == nullptr ? nullptr
+      : a.stamps + (size_t)a.b * 4 * 104 + ((size_t)blockIdx.x * 8 + (threadIdx.x >> 6)) * 2;
+  if (sb != nullptr && (threadIdx.x & 63) == 0) sb[0] = __builtin_amdgcn_s_memrealtime();
+  finalize_x_body<R>(a, apply_sgd);
+  if (sb != nullptr && (threadIdx.x & 63) == 0) sb[1] = __builtin_amdgcn_s_memrealtime();
+}
+
+template <int R>
+__device__ __forceinline__ void finalize_x_body(const MnistArgs& a, int apply_sgd) {
   const int j = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const float lr = *a.lr;
   const bool xchg = R > 1 && a.xchg && apply_sgd;
@@ -1344,8 +1364,10 @@ __global__ __launch_bounds__(512) void k_finalize_x(MnistArgs a, int apply_sgd) 
   // ---- this workgroup's gradient range ----
   if (j < 100) {
     dense_w_task(a, j * 8 + wave, lane, sgd_local, lr, xdst);
-  } else if (j == 100) {
-    for (int T = kD1TasksW3 - 8 + wave; T < kDenseTasks; T += 8) dense_w_task(a, T, lane, sgd_local, lr, xdst);
+  } else if (j < kFxDense) {
+    // db3 (tasks kD1TasksW3 - 8 ..), dW4 (kD1TasksW3 ..), db4 (kD1TasksW3 + 8): <= one task per wave
+    const int T = j == 100 ? kD1TasksW3 - 8 + wave : (j == 101 ? kD1TasksW3 + wave : kD1TasksW3 + 8);
+    if (j < 102 || wave == 0) dense_w_task(a, T, lane, sgd_local, lr, xdst);
   } else if (j < kFxDense + 289) {
     const int row = j - kFxDense, c = tid >> 3, sub = tid & 7;
     const int n = kMnistPart2Rows * 64, oc = row * 64 + c;
@@ -1368,28 +1390,32 @@ __global__ __launch_bounds__(512) void k_finalize_x(MnistArgs a, int apply_sgd) 
       if (sgd_local) a.W[e2] = wold - lr * sum;
     }
   } else {
-    const int q = j - kFxDense - 289, o = q * 16 + (tid >> 5), sub = tid & 31;
+    // conv1 columns 16q .. 16q+15 over the part1 rows: lane (c = lane & 15, rg = lane >> 4) of wave
+    // w reads rows 32 jj + 4 w + rg, so every wave load is 4 rows x one 64-B column segment; then a
+    // lane-group sum and the 8 waves' sums in LDS (fixed order)
+    __shared__ float fx_red[8][16];
+    const int q = j - kFxDense - 289, c = lane & 15, rg = lane >> 4, o = q * 16 + c;
     const int rows = mnist_part1_rows(a.b, true);
     const int e1 = o < 288 ? a.ow1 + o : a.ob1 + (o - 288);
-    const float wold = sgd_local ? a.W[e1] : 0.f;
+    const float wold = sgd_local && wave == 0 ? a.W[e1] : 0.f;
     float sum = 0.f;
-    for (int base = 0; base < rows; base += 256) {
+    for (int base = 4 * wave + rg; base < rows; base += 256) {
       float v[8];
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) v[jj] = a.part1[(size_t)min(base + sub + 32 * jj, rows - 1) * kMnistPart1Cols + o];
+      for (int jj = 0; jj < 8; ++jj) v[jj] = a.part1[(size_t)min(base + 32 * jj, rows - 1) * kMnistPart1Cols + o];
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) sum += (base + sub + 32 * jj < rows) ? v[jj] : 0.f;
+      for (int jj = 0; jj < 8; ++jj) sum += (base + 32 * jj < rows) ? v[jj] : 0.f;
     }
+    sum = sum_lane_groups(sum);
+    if (rg == 0) fx_red[wave][c] = sum;
+    __syncthreads();
+    if (wave == 0 && rg == 0) {
+      float s = 0.f;
 #pragma unroll
-    sum += dpp_xor1(sum);  // (32-lane all-reduce on the VALU)
-    sum += dpp_xor2(sum);
-    sum += dpp_mirror8(sum);
-    sum += dpp_xor8(sum);
-    sum = rs_swap16(sum, sum);
-    if (sub == 0) {
-      a.G[e1] = sum;
-      if (xdst != nullptr) xdst[e1] = sum;
-      if (sgd_local) a.W[e1] = wold - lr * sum;
+      for (int w = 0; w < 8; ++w) s += fx_red[w][c];
+      a.G[e1] = s;
+      if (xdst != nullptr) xdst[e1] = s;
+      if (sgd_local) a.W[e1] = wold - lr * s;
     }
   }
   if constexpr (R > 1) {
