@@ -54,7 +54,7 @@ class MnistStep {
     ep_ = at::zeros({1}, f.dtype(at::kInt));
     part3t_ = at::zeros({(int64_t)tdl::kDense1Chunks * b * 128}, f.dtype(at::kLong));
     dP2_ = at::empty({b * 1600}, f);
-    part2_ = at::zeros({b * tdl::kMnistPart2Rows * 64}, f);
+    part2_ = at::zeros({b * std::max(tdl::kMnistPart2Rows * 64, tdl::kP2QuadFloats)}, f);
     part1_ = at::zeros({(int64_t)tdl::mnist_part1_rows((int)b, true) * tdl::kMnistPart1Cols}, f);
     err_ = at::zeros({1}, f.dtype(at::kInt));
     part3_ = at::zeros({(int64_t)tdl::kDense1Chunks * b * 128}, f);

@@ -30,7 +30,8 @@ struct MnistArgs {
   float* H;           // [b,128] relu(dense1)
   float* dH;          // [b,128] grad of dense1 out (ReLU-masked)
   float* dP2;         // [b,1600] grad of the pooled conv2 output, ReLU-masked (k_fwd_conv)
-  float* part2;       // [b][289][64] per-image partials of conv2 wgrad (row 288 = bias)
+  float* part2;       // [b][289][64] per-image partials of conv2 wgrad (row 288 = bias); fused_bwd:
+                      // [b][kP2Quads][64][4] (see kP2Quads)
   float* part1;       // [2b or 4b][320] partials of conv1 wgrad (+ bias), see mnist_part1_rows
   float* part3;       // [4][b][128] dense1 partials, one per conv2 channel quarter
   float* dL;          // [b][10] dlogits (already scaled by 1/(b*R))
@@ -65,12 +66,17 @@ struct MnistArgs {
   int xchg;
 };
 
-// finalize workgroups of the fused_bwd step (k_finalize_x): 101 dense (dW3 rows 16m..16m+15 = 2048
-// slab floats each; the last: db3 + dW4 + db4), 289 conv2 rows (64 floats), 20 conv1 groups (16)
-constexpr int kFxDense = 103, kFxConv1 = 20;  // dW3 rows x100, db3, dW4, db4 | conv2 rows | conv1
-constexpr int kFxBlocks = kFxDense + 289 + kFxConv1;
-
 constexpr int kMnistPart2Rows = 289;
+// fused_bwd layout of part2: [b][73 row quads][64 columns][4 rows] (quad 72 = the bias row + 3 zero
+// rows): each lane of the wgrad tiles owns 4 consecutive rows of one column, stored as ONE 16-B
+// write-through store
+constexpr int kP2Quads = 73, kP2QuadFloats = kP2Quads * 256;
+
+// finalize workgroups of the fused_bwd step (k_finalize_x): 103 dense (dW3 rows 16m..16m+15 = 2048
+// slab floats each x 100, db3, dW4, db4), 146 conv2 (row quad, 32-column half) pieces (4 x 32
+// floats; the last quad: the bias row), 20 conv1 groups (16)
+constexpr int kFxDense = 103, kFxConv2 = 2 * kP2Quads, kFxConv1 = 20;
+constexpr int kFxBlocks = kFxDense + kFxConv2 + kFxConv1;
 constexpr int kDense1Chunks = 4;  // dense1 partials: one per conv2 channel quarter (k_fwd_conv)
 constexpr int kMnistPart1Cols = 320;
 // conv1 wgrad partial rows: (image, pixel half) of k_conv_bwd, or (image, quarter) of fused_bwd

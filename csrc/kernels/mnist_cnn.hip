@@ -758,13 +758,14 @@ __device__ __forceinline__ void fused_wgrad_tiles(const MnistArgs& a, int bi, in
     }
     __builtin_amdgcn_sched_barrier(0);
   }
+  // lane (i, g) holds rows 4g .. 4g+3 of column 16cq + i: one 16-B write-through (sc1) store into
+  // the row-quad layout, so the launch leaves no dirty L2 lines of its 18.7 KB per workgroup for the
+  // kernel-end write-back (MI355X_MICROARCH.md: boundary + dirty bytes / 6 TB/s; publish-large)
+  const auto rs = buf_rsrc(a.part2 + (size_t)bi * kP2QuadFloats, kP2QuadFloats * 4);
 #pragma unroll
   for (int u = 0; u < N; ++u) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = (t0 + u) * 16 + 4 * g + r;
-      if (row < kMnistPart2Rows) a.part2[((size_t)bi * kMnistPart2Rows + row) * 64 + 16 * cq + i] = acc[u][r];
-    }
+    const int qd = (t0 + u) * 4 + g;
+    if (qd < kP2Quads) st4_sc1(rs, ((qd * 64 + 16 * cq + i) * 4) * 4, acc[u]);
   }
 }
 
@@ -1297,8 +1298,8 @@ __global__ __launch_bounds__(256) void k_finalize(MnistArgs a, int apply_sgd, in
 //   [0, 100)    dW3 rows 16m .. 16m+15 (2048 floats): 8 dense tasks, one per wave
 //   100 / 101   db3 (128 floats) / dW4 (1280 floats): 8 dense tasks each, one per wave
 //   102         db4 (10 floats): 1 dense task
-//   [103, 392)  conv2 kernel row k (64 floats; row 288 = bias): 8 threads per output
-//   [392, 412)  conv1 kernel / bias outputs 16q .. 16q+15: 4 rows x 16 columns per wave load
+//   [103, 249)  conv2 (kernel row quad, 32-column half) pieces (the last quad: the bias row)
+//   [249, 269)  conv1 kernel / bias outputs 16q .. 16q+15: 4 rows x 16 columns per wave load
 // Each writes its gradient range into G.  R = 1 with SGD: W -= lr * G of the range.  R > 1 with
 // the exchange (a.xchg): the range is also published into this workgroup's slot of the channel's
 // exchange buffer (at its slab offsets), then the xGMI exchange with workgroup j of every peer
@@ -1306,7 +1307,10 @@ __global__ __launch_bounds__(256) void k_finalize(MnistArgs a, int apply_sgd, in
 // contributions in rank order): bit-identical on every replica, and the all-reduce of one range
 // overlaps the reductions of the others inside ONE launch.
 // --------------------------------------------------------------------------------------------
-__device__ __forceinline__ void fx_range(const MnistArgs& a, int j, int& lo, int& cnt) {
+// slab range of finalize workgroup j: nseg segments of cnt floats, stride floats apart
+__device__ __forceinline__ void fx_range(const MnistArgs& a, int j, int& lo, int& cnt, int& nseg, int& stride) {
+  nseg = 1;
+  stride = 0;
   if (j < 100) {
     lo = a.ow3 + j * 2048;
     cnt = 2048;
@@ -1319,14 +1323,19 @@ __device__ __forceinline__ void fx_range(const MnistArgs& a, int j, int& lo, int
   } else if (j == 102) {
     lo = a.ob4;
     cnt = 10;
-  } else if (j < kFxDense + 288) {
-    lo = a.ow2 + (j - kFxDense) * 64;
-    cnt = 64;
-  } else if (j == kFxDense + 288) {
-    lo = a.ob2;
-    cnt = 64;
+  } else if (j < kFxDense + kFxConv2) {
+    const int qd = (j - kFxDense) >> 1, h = (j - kFxDense) & 1;
+    if (qd == kP2Quads - 1) {
+      lo = a.ob2 + 32 * h;
+      cnt = 32;
+    } else {
+      lo = a.ow2 + qd * 256 + 32 * h;  // rows 4qd .. 4qd+3, columns 32h .. 32h+31
+      cnt = 32;
+      nseg = 4;
+      stride = 64;
+    }
   } else {
-    const int q = j - kFxDense - 289;
+    const int q = j - kFxDense - kFxConv2;
     lo = q < 18 ? a.ow1 + q * 16 : a.ob1 + (q - 18) * 16;
     cnt = 16;
   }
@@ -1368,33 +1377,48 @@ __device__ __forceinline__ void finalize_x_body(const MnistArgs& a, int apply_sg
     // db3 (tasks kD1TasksW3 - 8 ..), dW4 (kD1TasksW3 ..), db4 (kD1TasksW3 + 8): <= one task per wave
     const int T = j == 100 ? kD1TasksW3 - 8 + wave : (j == 101 ? kD1TasksW3 + wave : kD1TasksW3 + 8);
     if (j < 102 || wave == 0) dense_w_task(a, T, lane, sgd_local, lr, xdst);
-  } else if (j < kFxDense + 289) {
-    const int row = j - kFxDense, c = tid >> 3, sub = tid & 7;
-    const int n = kMnistPart2Rows * 64, oc = row * 64 + c;
-    const int e2 = row < 288 ? a.ow2 + oc : a.ob2 + c;
-    const float wold = sgd_local ? a.W[e2] : 0.f;
-    float sum = 0.f;
-    for (int base = 0; base < a.b; base += 64) {  // 8 images per thread in flight
-      float v[8];
+  } else if (j < kFxDense + kFxConv2) {
+    // conv2 row quad qd (kernel rows 4qd .. 4qd+3; the last quad: the bias row), columns 32h ..
+    // 32h+31: thread (column c = tid & 31, image group grp = tid >> 5) sums the quad's 4 rows (one
+    // 16-B load) over images grp, grp + 16, .. (a wave load: 2 x 512 contiguous bytes); then the
+    // two groups of a wave via permlane32 and the 8 waves in LDS (fixed order)
+    __shared__ f4 fx_red2[8][32];
+    const int qd = (j - kFxDense) >> 1, h = (j - kFxDense) & 1, c = tid & 31, grp = tid >> 5;
+    const bool biasq = qd == kP2Quads - 1;
+    f4 sum = zero4();
+    for (int base = 0; base < a.b; base += 64) {  // 4 images per thread in flight
+      f4 v[4];
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) v[jj] = a.part2[(size_t)min(base + sub + 8 * jj, a.b - 1) * n + oc];
+      for (int jj = 0; jj < 4; ++jj)
+        v[jj] = ld4(a.part2 + (size_t)min(base + grp + 16 * jj, a.b - 1) * kP2QuadFloats + (qd * 64 + 32 * h + c) * 4);
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) sum += (base + sub + 8 * jj < a.b) ? v[jj] : 0.f;
+      for (int jj = 0; jj < 4; ++jj)
+        if (base + grp + 16 * jj < a.b) sum += v[jj];
     }
-    sum += dpp_xor1(sum);  // (8-lane all-reduce on the VALU)
-    sum += dpp_xor2(sum);
-    sum += dpp_mirror8(sum);
-    if (sub == 0) {
-      a.G[e2] = sum;
-      if (xdst != nullptr) xdst[e2] = sum;
-      if (sgd_local) a.W[e2] = wold - lr * sum;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sum[r] = rs_swap32(sum[r], sum[r]);
+    if (lane < 32) fx_red2[wave][c] = sum;
+    __syncthreads();
+    if (tid < 128) {
+      const int cc = tid >> 2, r = tid & 3;
+      if (!biasq || r == 0) {
+        const int col = 32 * h + cc;
+        const int e2 = biasq ? a.ob2 + col : a.ow2 + (4 * qd + r) * 64 + col;
+        const float wold = sgd_local ? a.W[e2] : 0.f;
+        float s2 = 0.f;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) s2 += fx_red2[w][cc][r];
+        a.G[e2] = s2;
+        if (xdst != nullptr) xdst[e2] = s2;
+        if (sgd_local) a.W[e2] = wold - lr * s2;
+      }
     }
   } else {
     // conv1 columns 16q .. 16q+15 over the part1 rows: lane (c = lane & 15, rg = lane >> 4) of wave
     // w reads rows 32 jj + 4 w + rg, so every wave load is 4 rows x one 64-B column segment; then a
     // lane-group sum and the 8 waves' sums in LDS (fixed order)
     __shared__ float fx_red[8][16];
-    const int q = j - kFxDense - 289, c = lane & 15, rg = lane >> 4, o = q * 16 + c;
+    const int q = j - kFxDense - kFxConv2, c = lane & 15, rg = lane >> 4, o = q * 16 + c;
     const int rows = mnist_part1_rows(a.b, true);
     const int e1 = o < 288 ? a.ow1 + o : a.ob1 + (o - 288);
     const float wold = sgd_local && wave == 0 ? a.W[e1] : 0.f;
@@ -1425,11 +1449,11 @@ __device__ __forceinline__ void finalize_x_body(const MnistArgs& a, int apply_sg
       if (tid == 0) a.xa.epoch[j] = e;
       return;
     }
-    int lo, cnt;
-    fx_range(a, j, lo, cnt);
-    const int n4 = cnt >> 2;  // (every range starts 16-B aligned: slab offsets are multiples of 4)
-    for (int t = tid; t < n4; t += 512) {
-      const int64_t off = lo + 4 * t;
+    int lo, cnt, nseg, stride;
+    fx_range(a, j, lo, cnt, nseg, stride);
+    const int n4 = cnt >> 2;  // (every segment starts 16-B aligned: slab offsets are multiples of 4)
+    for (int t = tid; t < n4 * nseg; t += 512) {
+      const int64_t off = lo + (int64_t)(t / n4) * stride + 4 * (t % n4);
       f4 v[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) v[r] = ld4(a.xa.p.buf[r] + half + off);

@@ -10,8 +10,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from tensorflow_distributed_learning_amd.models import mnist_cnn as M  # noqa: E402
 
 
-CATS = {"dW3 rows (0-99)": (0, 100), "db3/dW4/db4 (100-102)": (100, 103), "conv2 rows (103-391)": (103, 392),
-        "conv1 (392-411)": (392, 412)}
+CATS = {"dW3 rows (0-99)": (0, 100), "db3/dW4/db4 (100-102)": (100, 103), "conv2 pieces (103-248)": (103, 249),
+        "conv1 (249-268)": (249, 269)}
 
 
 def main():
