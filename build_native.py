@@ -84,12 +84,15 @@ def build_hip_ext(nproc, verbose=False):
     os.makedirs(odir, exist_ok=True)
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     common = ["-O3", "-std=c++17", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", f"-I{CSRC}", f"-I{ROCM}/include"]
+    # diagnostics builds (A/B variants of a kernel): extra device-compile flags, e.g. "-DTDL_W3_SCHED"
+    # (touch the source or --clean when switching: objects are rebuilt by modification time only)
+    extra = os.environ.get("TDL_EXTRA_HIPFLAGS", "").split()
     jobs, objs = [], []
     for src in sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))):
         obj = os.path.join(odir, os.path.basename(src) + ".o")
         objs.append(obj)
         if _stale(src, obj, hdr):
-            jobs.append(([hipcc, "-c", "-x", "hip", f"--offload-arch={ARCH}", "-fno-gpu-rdc", *common, src, "-o", obj], obj))
+            jobs.append(([hipcc, "-c", "-x", "hip", f"--offload-arch={ARCH}", "-fno-gpu-rdc", *common, *extra, src, "-o", obj], obj))
     host_defs = ["-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DTORCH_API_INCLUDE_EXTENSION_H", "-DTORCH_EXTENSION_NAME=_C"]
     for src in [os.path.join(CSRC, n) for n in ("bindings.cpp", "ops_bindings.cpp", "comm_bindings.cpp")]:
         obj = os.path.join(odir, os.path.basename(src) + ".o")

@@ -1023,11 +1023,13 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
       tap_off[s3] = (k / 3) * 28 + (k % 3);
     }
     // row tiles mt0 and mt0 + 8 per iteration, both channel tiles each: 4 independent MFMA
-    // chains sharing 6 LDS loads (the two channel tiles read the same image values)
-#pragma unroll
-    for (int it = 0; it < 3; ++it) {
+    // chains sharing 6 LDS loads (the two channel tiles read the same image values).  The operand
+    // reads of iteration it + 1 are issued right behind iteration it's MFMAs, so their LDS latency
+    // hides behind the MFMA drain and the epilogue; the conv1 biases live in registers.
+    const float bias[2] = {w1s[288 + i], w1s[288 + 16 + i]};
+    float xa[2][2][3];
+    auto load_x = [&](int buf, int it) {
       const int mt0 = wave + 16 * it;
-      float xa[2][3];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int mt = min(mt0 + 8 * u, 42);
@@ -1036,8 +1038,13 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
         const int y = 2 * (wc / 13) + (q >> 1), x = 2 * (wc % 13) + (q & 1);
         const float* xb = xs + y * 28 + x;
 #pragma unroll
-        for (int s3 = 0; s3 < 3; ++s3) xa[u][s3] = xb[tap_off[s3]];
+        for (int s3 = 0; s3 < 3; ++s3) xa[buf][u][s3] = xb[tap_off[s3]];
       }
+    };
+    load_x(0, 0);
+#pragma unroll
+    for (int it = 0; it < 3; ++it) {
+      const int mt0 = wave + 16 * it;
       f4 acc[2][2];
 #pragma unroll
       for (int u = 0; u < 2; ++u)
@@ -1048,9 +1055,11 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
 #pragma unroll
         for (int u = 0; u < 2; ++u)
 #pragma unroll
-          for (int nt = 0; nt < 2; ++nt) acc[u][nt] = mfma16x16x4(xa[u][s3], bw[nt][s3], acc[u][nt]);
+          for (int nt = 0; nt < 2; ++nt) acc[u][nt] = mfma16x16x4(xa[it & 1][u][s3], bw[nt][s3], acc[u][nt]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (it < 2) load_x((it + 1) & 1, it + 1);
+      __builtin_amdgcn_sched_barrier(0);
       if (it < 2) {
-        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int j = 6 + 5 * it; j < 11 + 5 * it; ++j) ldw3(j);
         __builtin_amdgcn_sched_barrier(0);
@@ -1068,7 +1077,7 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
           if (ac.z > m) { m = ac.z; am = 2; }
           if (ac.w > m) { m = ac.w; am = 3; }
           const int co = nt * 16 + i;
-          const float v = fmaxf(m + w1s[288 + co], 0.f);
+          const float v = fmaxf(m + bias[nt], 0.f);
           P1s[wo * kP1Stride + co] = v;
           a1s[wo * 32 + co] = (uint8_t)am;
         }
