@@ -270,11 +270,67 @@ class FusedMnistTrainer:
             self._xchg = None
             if st.fused_bwd and self.optimizer.momentum == 0 and os.environ.get("TDL_MNIST_FINALIZE_XCHG", "1") == "1":
                 self._xchg = self.comm.exchange_channel(n, M.FINALIZE_BLOCKS)
+                if self._xchg is not None and not self._selftest_exchange(st.b):
+                    self._xchg = None
             self.allreduce_mode = ("xgmi-in-finalize" if self._xchg is not None else
                                    getattr(self.comm, "algorithm", self.comm.name))
             self._comm_prepared = True
         if self._xchg is not None and st.fused_bwd and not st.has_exchange:
             st.set_exchange(self._xchg)
+
+    def _selftest_exchange(self, b: int) -> bool:
+        """Collective start-up check of the exchange-in-finalize path on this job's devices: one
+        real step (replica-specific samples) through a scratch step object with the exchange, whose
+        updated weights must equal W0 - lr * (sum of the replicas' local gradients) taken through
+        the communicator's own (self-tested) all-reduce, and be bit-identical on every replica.
+        Parameters, gradients and metrics are restored afterwards.  Any failure on any rank: every
+        rank keeps the serial all-reduce (TDL_XCHG_SELFTEST=0 skips the check)."""
+        if os.environ.get("TDL_XCHG_SELFTEST", "1") != "1":
+            return True
+        import warnings
+
+        from ..parallel import consistency
+
+        dev = self.device
+        n = len(self.X)
+        idx = ((torch.arange(b, dtype=torch.int64) * 7919 + self.rank * 104729) % n).to(torch.int32).to(dev)
+        saved = (self.W.clone(), self.G.clone())
+        ok, why = True, ""
+        try:
+            tst = M.FusedMnistTrainStep(self.X, self.Y, idx, self.W, self.G, self.layout, b, self.R,
+                                        self.optimizer.lr_dev, torch.zeros(4, dtype=torch.float32, device=dev),
+                                        global_batch=b * self.R)
+            if tst.fused_bwd:
+                tst.set_exchange(self._xchg)
+                torch.cuda.synchronize(dev)
+                tst.forward_backward(0)
+                tst.finalize(True, exchange=True)
+                torch.cuda.synchronize(dev)
+                tst.check()
+                if self._xchg.error():
+                    raise RuntimeError("exchange timed out")
+                w_x, g_local = self.W.clone(), self.G.clone()
+                self.comm.all_reduce(g_local, "sum")
+                lr = float(self.optimizer.lr_dev.item())
+                w_ref = saved[0] - lr * g_local
+                if os.environ.get("TDL_FAULT_XCHG_SELFTEST") == str(self.rank):  # fault injection (tests)
+                    w_ref = w_ref + 1.0
+                if not torch.allclose(w_x, w_ref, rtol=1e-5, atol=1e-7):
+                    ok, why = False, f"max |W - W_ref| = {float((w_x - w_ref).abs().max()):.3g}"
+                if not consistency.replicas_identical(self.comm, w_x):
+                    ok, why = False, "replicas differ"
+            del tst
+        except Exception as e:  # noqa: BLE001 - any failure means the serial path
+            ok, why = False, f"{type(e).__name__}: {e}"
+        self.W.copy_(saved[0])
+        self.G.copy_(saved[1])
+        f = torch.tensor([1.0 if ok else 0.0], device=dev if self.comm.name == "rccl" else "cpu")
+        self.comm.all_reduce(f, "min")
+        agreed = bool(f.item() > 0.5)
+        if not agreed and self.rank == 0:
+            warnings.warn(f"exchange-in-finalize self-test failed ({why or 'on another rank'}); "
+                          "using the serial gradient all-reduce")
+        return agreed
 
     def _update(self, lo: int = 0, hi: Optional[int] = None):
         from .. import ops

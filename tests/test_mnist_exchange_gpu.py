@@ -147,6 +147,30 @@ def test_finalize_exchange_multi_process(tmp_path, R):
         assert "exchange ok" in out
 
 
+def _bench2(extra_env):
+    env = dict(os.environ, PYTHONPATH=ROOT, TDL_SHARE_GPU="1", TDL_MNIST_DP2_FWD="1", TDL_XGMI_TIMEOUT="30",
+               **extra_env)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "TF_CONFIG", "TDL_LAUNCHED", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--per-replica-batch", "16", "--steps", "40",
+                        "--warmup", "8"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    import json as _json
+
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    return _json.loads(line), r.stderr
+
+
+def test_bench_exchange_selftest_failure_falls_back(tmp_path):
+    """A start-up self-test failure of the exchange-in-finalize path on ONE rank (injected:
+    TDL_FAULT_XCHG_SELFTEST=1 makes rank 1 see a wrong result) moves EVERY rank to the serial
+    all-reduce, and the run still ends with bit-identical replicas."""
+    d, err = _bench2({"TDL_FAULT_XCHG_SELFTEST": "1"})
+    cfg = d["config"]
+    assert cfg["allreduce"] != "xgmi-in-finalize" and cfg["replicas_identical"], cfg
+    assert "self-test failed" in err, err[-3000:]
+
+
 def test_bench_two_replicas_exchange_in_finalize(tmp_path):
     """bench.py at N=2 end to end on the R > 1 production path: the fused forward/backward kernel
     and the finalize whose workgroups all-reduce over xGMI, captured in the execution graphs.  On
