@@ -82,6 +82,7 @@ class MnistStep {
     a_.fused_bwd = 0;
     a_.err = reinterpret_cast<unsigned*>(err_.data_ptr<int>());
     a_.xchg = 0;
+    a_.xtwo = 0;
     a_.dP2 = dP2_.data_ptr<float>();
     a_.part2 = part2_.data_ptr<float>();
     a_.part1 = part1_.data_ptr<float>();
@@ -193,6 +194,10 @@ class MnistStep {
     xchg_ready_ = true;
   }
   bool has_exchange() const { return xchg_ready_; }
+  // 0: one-shot exchange in finalize (every rank sums every range); 1: two-shot (reduce-scatter of
+  // 1/R of every range + copy of the owners' updated weights: 2 (R-1)/R of the slab over the fabric)
+  void set_exchange_algo(int algo) { a_.xtwo = algo != 0; }
+  int exchange_algo() const { return a_.xtwo; }
 
   // forward-only evaluation / inference of the b rows at idx_off: loss, correct count and sample
   // count accumulate into the metrics tensor; logits ([>= b*10] f32, optional) receive the logits
@@ -281,6 +286,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("finalize", &MnistStep::finalize, pybind11::arg("apply_sgd"), pybind11::arg("exchange") = false)
       .def("set_exchange", &MnistStep::set_exchange)
       .def("has_exchange", &MnistStep::has_exchange)
+      .def("set_exchange_algo", &MnistStep::set_exchange_algo)
+      .def("exchange_algo", &MnistStep::exchange_algo)
       .def("set_dp2_in_forward", &MnistStep::set_dp2_in_forward)
       .def("dp2_in_forward", &MnistStep::dp2_in_forward)
       .def("set_fused_bwd", &MnistStep::set_fused_bwd)

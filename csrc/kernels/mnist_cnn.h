@@ -64,6 +64,8 @@ struct MnistArgs {
   // order and applies SGD to that range -- no separate all-reduce or optimizer launch
   XgmiArgs xa;
   int xchg;
+  int xtwo;  // exchange algorithm: 0 one-shot (every rank sums every range), 1 two-shot (each rank
+             // sums and updates 1/R of every range, the others copy its updated weights)
 };
 
 constexpr int kMnistPart2Rows = 289;

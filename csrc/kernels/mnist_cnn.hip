@@ -1461,16 +1461,48 @@ __device__ __forceinline__ void finalize_x_body(const MnistArgs& a, int apply_sg
     int lo, cnt, nseg, stride;
     fx_range(a, j, lo, cnt, nseg, stride);
     const int n4 = cnt >> 2;  // (every segment starts 16-B aligned: slab offsets are multiples of 4)
-    for (int t = tid; t < n4 * nseg; t += 512) {
-      const int64_t off = lo + (int64_t)(t / n4) * stride + 4 * (t % n4);
-      f4 v[R];
+    const int tot = n4 * nseg;
+    auto off_of = [&](int t) { return (int64_t)lo + (int64_t)(t / n4) * stride + 4 * (t % n4); };
+    if (a.xtwo) {
+      // two-shot: f4 t of the range belongs to rank (t R) / tot.  Reduce-scatter: the owner sums its
+      // share in rank order and stages the updated weights in its result region; after the second
+      // round every rank copies each share from its owner (bit-identical by construction, and W is
+      // written only after both rounds: a timeout leaves it untouched).  2 (R-1)/R of the range
+      // crosses the fabric per rank instead of (R-1) x the range.
+      const int64_t res = half + a.xa.cap;
+      float* mine = a.xa.p.buf[a.xa.rank];
+      for (int t = tid; t < tot; t += 512) {
+        if ((t * R) / tot != a.xa.rank) continue;
+        const int64_t off = off_of(t);
+        f4 v[R];
 #pragma unroll
-      for (int r = 0; r < R; ++r) v[r] = ld4(a.xa.p.buf[r] + half + off);
-      f4 acc = v[0];
+        for (int r = 0; r < R; ++r) v[r] = ld4(a.xa.p.buf[r] + half + off);
+        f4 acc = v[0];
 #pragma unroll
-      for (int r = 1; r < R; ++r) acc += v[r];
-      st4(a.W + off, ld4(a.W + off) - lr * acc);
+        for (int r = 1; r < R; ++r) acc += v[r];
+        st4(mine + res + off, ld4(a.W + off) - lr * acc);
+      }
+      if (!xgmi_exchange<R>(a.xa.p, a.xa.rank, a.xa.sig_blocks, a.xa.timeout, a.xa.err, 1, j, e)) {
+        if (tid == 0) a.xa.epoch[j] = e;
+        return;
+      }
+      for (int t = tid; t < tot; t += 512) {
+        const int64_t off = off_of(t);
+        st4(a.W + off, ld4(a.xa.p.buf[(t * R) / tot] + res + off));
+      }
+    } else {
+      for (int t = tid; t < tot; t += 512) {
+        const int64_t off = off_of(t);
+        f4 v[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[r] = ld4(a.xa.p.buf[r] + half + off);
+        f4 acc = v[0];
+#pragma unroll
+        for (int r = 1; r < R; ++r) acc += v[r];
+        st4(a.W + off, ld4(a.W + off) - lr * acc);
+      }
     }
+    // scalar tail of a range (db4: 10 floats), summed by every rank itself in rank order
     for (int t = 4 * n4 + tid; t < cnt; t += 512) {
       const int64_t off = lo + t;
       float acc = a.xa.p.buf[0][half + off];

@@ -268,15 +268,17 @@ class FusedMnistTrainer:
             n, d0 = self.W.numel(), st.dense_offset
             self.comm.prepare_all_reduce(n - d0, d0, n)
             self._xchg = None
+            # one-shot moves (R-1) slabs per rank over the fabric, two-shot 2 (R-1)/R in two rounds
+            self._xchg_twoshot = self.R >= int(os.environ.get("TDL_FX_TWOSHOT_MIN_R", "3"))
             if st.fused_bwd and self.optimizer.momentum == 0 and os.environ.get("TDL_MNIST_FINALIZE_XCHG", "1") == "1":
                 self._xchg = self.comm.exchange_channel(n, M.FINALIZE_BLOCKS)
                 if self._xchg is not None and not self._selftest_exchange(st.b):
                     self._xchg = None
-            self.allreduce_mode = ("xgmi-in-finalize" if self._xchg is not None else
-                                   getattr(self.comm, "algorithm", self.comm.name))
+            self.allreduce_mode = (("xgmi-in-finalize-twoshot" if self._xchg_twoshot else "xgmi-in-finalize")
+                                   if self._xchg is not None else getattr(self.comm, "algorithm", self.comm.name))
             self._comm_prepared = True
         if self._xchg is not None and st.fused_bwd and not st.has_exchange:
-            st.set_exchange(self._xchg)
+            st.set_exchange(self._xchg, twoshot=self._xchg_twoshot)
 
     def _selftest_exchange(self, b: int) -> bool:
         """Collective start-up check of the exchange-in-finalize path on this job's devices: one
@@ -301,7 +303,7 @@ class FusedMnistTrainer:
                                         self.optimizer.lr_dev, torch.zeros(4, dtype=torch.float32, device=dev),
                                         global_batch=b * self.R)
             if tst.fused_bwd:
-                tst.set_exchange(self._xchg)
+                tst.set_exchange(self._xchg, twoshot=self._xchg_twoshot)
                 torch.cuda.synchronize(dev)
                 tst.forward_backward(0)
                 tst.finalize(True, exchange=True)

@@ -179,10 +179,17 @@ class FusedMnistTrainStep:
         replicas over xGMI before the SGD update (each finalize workgroup exchanges its own range)."""
         self._impl.finalize(bool(apply_sgd), bool(exchange))
 
-    def set_exchange(self, channel) -> None:
+    def set_exchange(self, channel, twoshot: bool = False) -> None:
         """Use this xGMI channel (``_C.XgmiChannel`` with capacity >= the slab and
-        >= ``FINALIZE_BLOCKS`` signal slots, connected to every replica) for ``finalize(exchange=True)``."""
+        >= ``FINALIZE_BLOCKS`` signal slots, connected to every replica) for ``finalize(exchange=True)``;
+        ``twoshot``: reduce-scatter + all-gather of the updated weights instead of every rank
+        summing every range (2 (R-1)/R instead of (R-1) slabs over the fabric per rank)."""
         self._impl.set_exchange(channel)
+        self._impl.set_exchange_algo(1 if twoshot else 0)
+
+    @property
+    def exchange_twoshot(self) -> bool:
+        return bool(self._impl.exchange_algo())
 
     @property
     def has_exchange(self) -> bool:

@@ -165,6 +165,8 @@ class TorchCommunicator(Communicator):
             return False
         ctrl = self.device if self.backend == "nccl" else torch.device("cpu")
         self.xgmi = xgmi.XgmiAllReduce(self.rank, self.world_size, self.device, ctrl_device=ctrl)
+        # over gloo the kernel is the only device data plane: messages above its limit go in chunks
+        self.xgmi.chunked = self.backend != "nccl"
         return True
 
     def prepare_all_reduce(self, *numels):
@@ -192,9 +194,17 @@ class TorchCommunicator(Communicator):
         if self.xgmi is not None:
             self.xgmi.check()
 
+    def _no_host_collective_in_capture(self, t):
+        # a gloo collective stages through the host (a device sync), which would invalidate a
+        # graph capture for the whole process; fail before issuing anything, so that the capture
+        # ends cleanly and the caller can fall back to eager steps
+        if self.backend != "nccl" and t.is_cuda and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError(f"{self.backend} all-reduce of {t.numel()} elements cannot be recorded in a hipGraph")
+
     def all_reduce(self, t, op="sum"):
         if self.xgmi is not None and self.xgmi.all_reduce(t, op):
             return t
+        self._no_host_collective_in_capture(t)
         if op == "mean":
             if self._avg_native:
                 dist.all_reduce(t, op=dist.ReduceOp.AVG)
@@ -211,6 +221,7 @@ class TorchCommunicator(Communicator):
             # xGMI kernel on a side stream (forked from the current one, joined by wait()): the
             # bucket's exchange overlaps the rest of the backward and records into a hipGraph
             return _SideStreamWork(self, t, op)
+        self._no_host_collective_in_capture(t)
         if op == "mean" and not self._avg_native:
             work = dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True)
             return _ScaleOnWait(work, t, 1.0 / self.world_size)
@@ -226,7 +237,7 @@ class TorchCommunicator(Communicator):
         if self.xgmi is None:
             return False
         numels = [int(n) for n in numels]
-        if any(n > self.xgmi.limit for n in numels):
+        if any(n > self.xgmi.limit for n in numels) and not self.xgmi.chunked:
             return False
         self.prepare_all_reduce(*numels)
         return self.xgmi is not None and all(self.xgmi.has_channel(n) for n in numels)

@@ -63,6 +63,15 @@ class XgmiAllReduce:
         self._dedicated = []
         self.ok: Optional[bool] = None  # None = not yet tested
         self.reason = ""
+        # messages above the channel limit in limit-sized chunks (one launch each) -- only where the
+        # kernel is the job's sole device data plane (gloo control plane: replicas sharing a GPU);
+        # with RCCL beside it, large messages belong to RCCL's bandwidth-optimal rings
+        self.chunked = False
+        # chunked mode: elements per launch.  Replicas sharing one GPU spin in their exchange
+        # workgroups until the peer's workgroup of the same index arrives, so every replica's launch
+        # (beside the backward kernels still running) must fit on the GPU at once: 256 workgroups
+        # per launch, not the 1024 of a full 4 MiB channel
+        self.chunk = min(self.limit, int(os.environ.get("TDL_XGMI_CHUNK_ELEMS", str(256 * BLOCK))))
 
     # ------------------------------------------------------------------ set-up (collective)
     def _make(self, numel: int, timeout: Optional[float] = None, min_blocks: int = 0):
@@ -86,14 +95,22 @@ class XgmiAllReduce:
         dist.all_reduce(f, op=dist.ReduceOp.MIN, group=self.group)
         return bool(f.item() > 0.5)
 
+    def _chunks(self, n: int):
+        """[(offset, size)] of a message of n elements: one piece, or (chunked) ``chunk``-sized
+        pieces (offsets multiples of the chunk: 16-B aligned) and the remainder."""
+        n = int(n)
+        if not self.chunked:
+            return [(0, n)]
+        return [(o, min(self.chunk, n - o)) for o in range(0, n, self.chunk)]
+
     def prepare(self, *numels: int) -> bool:
         """Create (collectively) the channels for these message sizes; False if disabled."""
         if not self._ensure_tested():
             return False
         for n in numels:
-            n = int(n)
-            if 0 < n <= self.limit and n not in self._chans:
-                self._chans[n] = self._make(n)
+            for _, c in self._chunks(int(n)):
+                if 0 < c <= self.limit and c not in self._chans:
+                    self._chans[c] = self._make(c)
         return True
 
     def _ensure_tested(self) -> bool:
@@ -186,30 +203,46 @@ class XgmiAllReduce:
         return self._chans[n]
 
     def has_channel(self, n: int) -> bool:
-        return bool(self.ok) and int(n) in self._chans
+        return bool(self.ok) and int(n) > 0 and all(c in self._chans for _, c in self._chunks(int(n)))
 
     def applicable(self, t: torch.Tensor) -> bool:
         return (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.data_ptr() % 16 == 0 and
-                0 < t.numel() <= self.limit)
+                0 < t.numel() and (t.numel() <= self.limit or self.chunked))
+
+    def _pieces(self, n: int):
+        """[(offset, size, channel)] for a message of n elements, or None (some channel missing)."""
+        out = []
+        for o, c in self._chunks(n):
+            ch = self._channel(c)
+            if ch is None:
+                return None
+            out.append((o, c, ch))
+        return out
 
     def all_reduce(self, t: torch.Tensor, op: str) -> bool:
         """In-place sum/mean of ``t`` on the current stream; False = not handled (use RCCL)."""
         if op not in ("sum", "mean") or not self.applicable(t) or not self._ensure_tested():
             return False
-        ch = self._channel(t.numel())
-        if ch is None:
+        pieces = self._pieces(t.numel())
+        if pieces is None:
             return False
-        ch.all_reduce(t, t, 1.0 / self.world if op == "mean" else 1.0)
+        flat = t.view(-1)
+        scale = 1.0 / self.world if op == "mean" else 1.0
+        for o, c, ch in pieces:
+            x = flat[o:o + c]
+            ch.all_reduce(x, x, scale)
         return True
 
     def all_reduce_sgd(self, g: torch.Tensor, w: torch.Tensor, lr: torch.Tensor) -> bool:
-        """``w -= lr * sum_over_ranks(g)`` in one kernel; False = not handled."""
-        if not (self.applicable(g) and self.applicable(w)) or not self._ensure_tested():
+        """``w -= lr * sum_over_ranks(g)`` (one kernel per piece); False = not handled."""
+        if not (self.applicable(g) and self.applicable(w)) or g.numel() != w.numel() or not self._ensure_tested():
             return False
-        ch = self._channel(g.numel())
-        if ch is None:
+        pieces = self._pieces(g.numel())
+        if pieces is None:
             return False
-        ch.all_reduce_sgd(g, w, lr, 1.0)
+        gf, wf = g.view(-1), w.view(-1)
+        for o, c, ch in pieces:
+            ch.all_reduce_sgd(gf[o:o + c], wf[o:o + c], lr, 1.0)
         return True
 
     def check(self) -> None:

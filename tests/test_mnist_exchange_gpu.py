@@ -22,7 +22,7 @@ import os, sys, torch, torch.distributed as dist
 sys.path.insert(0, sys.argv[2])
 from tensorflow_distributed_learning_amd import ops
 from tensorflow_distributed_learning_amd.models import mnist_cnn as M
-rank, R = int(sys.argv[1]), int(sys.argv[4])
+rank, R, two = int(sys.argv[1]), int(sys.argv[4]), sys.argv[5] == "1"
 dist.init_process_group("gloo", rank=rank, world_size=R, init_method="tcp://127.0.0.1:" + sys.argv[3])
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
@@ -43,8 +43,8 @@ ch = C.XgmiChannel(rank, R, W.numel(), 0, 20.0, 0, M.FINALIZE_BLOCKS)
 hs = [None] * R
 dist.all_gather_object(hs, (bytes(ch.handle(False)), bytes(ch.handle(True))))
 ch.open([h[0] for h in hs], [h[1] for h in hs])
-st.set_exchange(ch)
-assert st.has_exchange
+st.set_exchange(ch, twoshot=two)
+assert st.has_exchange and st.exchange_twoshot == two
 
 
 def step(k, graph=None):
@@ -117,8 +117,9 @@ print("exchange ok", rank, flush=True)
 """
 
 
+@pytest.mark.parametrize("two", [False, True], ids=["oneshot", "twoshot"])
 @pytest.mark.parametrize("R", [2])
-def test_finalize_exchange_multi_process(tmp_path, R):
+def test_finalize_exchange_multi_process(tmp_path, R, two):
     """(R = 2 only: the exchange needs workgroup j of every replica resident at some point, and a
     one-GPU box holds 768 of the finalize's 512-thread workgroups: 2 x 410 leave the second replica
     at least a prefix of its grid, 3 x 410 can starve the third.  With one GPU per replica all
@@ -132,7 +133,8 @@ def test_finalize_exchange_multi_process(tmp_path, R):
     env = dict(os.environ, TDL_MNIST_DP2_FWD="1", TDL_MNIST_FUSED_BWD="1")
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "TF_CONFIG", "TDL_SHARE_GPU"):
         env.pop(k, None)
-    procs = [subprocess.Popen([sys.executable, str(f), str(r), ROOT, port, str(R)], env=env, stdout=subprocess.PIPE,
+    procs = [subprocess.Popen([sys.executable, str(f), str(r), ROOT, port, str(R), "1" if two else "0"], env=env,
+                              stdout=subprocess.PIPE,
                               stderr=subprocess.STDOUT, text=True) for r in range(R)]
     outs = []
     for p in procs:
@@ -167,7 +169,7 @@ def test_bench_exchange_selftest_failure_falls_back(tmp_path):
     all-reduce, and the run still ends with bit-identical replicas."""
     d, err = _bench2({"TDL_FAULT_XCHG_SELFTEST": "1"})
     cfg = d["config"]
-    assert cfg["allreduce"] != "xgmi-in-finalize" and cfg["replicas_identical"], cfg
+    assert not cfg["allreduce"].startswith("xgmi-in-finalize") and cfg["replicas_identical"], cfg
     assert "self-test failed" in err, err[-3000:]
 
 
@@ -189,3 +191,11 @@ def test_bench_two_replicas_exchange_in_finalize(tmp_path):
     cfg = d["config"]
     assert d["n_gpus"] == 2 and cfg["allreduce"] == "xgmi-in-finalize", cfg
     assert cfg["kernels_per_step"] == 2 and cfg["allreduce_in_graph"] and cfg["replicas_identical"], cfg
+
+
+def test_bench_two_replicas_exchange_in_finalize_twoshot(tmp_path):
+    """The same with the two-shot exchange (the default from R = 3; forced at R = 2 here): every
+    rank reduces and updates half of each finalize range and copies the other half."""
+    d, _ = _bench2({"TDL_FX_TWOSHOT_MIN_R": "2"})
+    cfg = d["config"]
+    assert cfg["allreduce"] == "xgmi-in-finalize-twoshot" and cfg["replicas_identical"], cfg
