@@ -16,6 +16,7 @@ built); CPU tensors use PyTorch ops with the same semantics.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -37,6 +38,19 @@ def _aligned(t: torch.Tensor) -> torch.Tensor:
     return t if t.data_ptr() % 16 == 0 else t.clone()
 
 
+_DEBUG_SEEN = set()
+
+
+def _debug(*key):
+    """TDL_BN_DEBUG=1: name each (direction, shape, mode, fused) combination once on stderr (which
+    BN layers still take a separate statistics / gradient-sum pass)."""
+    if os.environ.get("TDL_BN_DEBUG") == "1" and key not in _DEBUG_SEEN:
+        import sys
+
+        _DEBUG_SEEN.add(key)
+        print(f"[tdl bn] {key}", file=sys.stderr, flush=True)
+
+
 class _BatchNormTrain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, residual, conv_bias, moving_mean, moving_var, momentum, eps, relu, grad_out,
@@ -47,6 +61,7 @@ class _BatchNormTrain(torch.autograd.Function):
         y, st = C.bn_forward_train(xc, gamma, beta, moving_mean, moving_var, float(momentum), float(eps), bool(relu),
                                    rc, conv_bias.detach() if conv_bias is not None else None, part)
         ctx.mode = 2 if residual is not None else (1 if relu else 0)
+        _debug("fwd", tuple(x.shape), ctx.mode, "stats-fused" if part is not None else "stats-pass")
         ctx.flags = (gamma is not None, beta is not None, residual is not None, conv_bias is not None)
         ctx.res_dtype = residual.dtype if residual is not None else None
         ctx.grad_out = grad_out
@@ -62,7 +77,9 @@ class _BatchNormTrain(torch.autograd.Function):
         part = getattr(dy, "_tdl_bn_bwd_part", None) if ctx.mode >= 1 else None
         dy = _aligned(dy.to(xc.dtype))
         go = ctx.grad_out or (None, None)
-        if part is not None and dy.dtype == xc.dtype and dy.is_contiguous() and dy.data_ptr() % 16 == 0:
+        fused = part is not None and dy.dtype == xc.dtype and dy.is_contiguous() and dy.data_ptr() % 16 == 0
+        _debug("bwd", tuple(xc.shape), ctx.mode, "sums-fused" if fused else "sums-pass")
+        if fused:
             # dy is already this group's masked dz, reduced by the consuming conv's dgrad epilogue
             FUSED_BWD[0] += 1
             out = C.bn_backward(dy, xc, None, gamma if has_g else None, st, ctx.mode, go[0], go[1], part)
