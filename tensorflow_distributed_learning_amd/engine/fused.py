@@ -378,19 +378,14 @@ class FusedMnistTrainer:
         self._train_step(st, 0, global_b)
         self.optimizer.iterations += 1
 
-    def _graph_for(self, K: int, b: int, slot: int = 0, start: int = 0):
+    def _graph_for(self, K: int, b: int, slot: int = 0):
         """Graph of one K-step execution reading its sample ids from its own index buffer; the
-        slots rotate so the host uploads execution i+1's indices while execution i runs.
-        ``start`` > 0: the graph of steps start .. K-1 only (same index buffer and step object),
-        replayed after ``start`` eagerly launched lead steps (see run_train)."""
-        g = self._graphs.get((K, b, slot, start))
+        slots rotate so the host uploads execution i+1's indices while execution i runs."""
+        g = self._graphs.get((K, b, slot))
         if g is not None:
             return g
-        if start:
-            _, idx_buf, st = self._graph_for(K, b, slot)
-        else:
-            idx_buf = torch.zeros(K * b, dtype=torch.int32, device=self.device)
-            st = self._step(b, idx_buf)
+        idx_buf = torch.zeros(K * b, dtype=torch.int32, device=self.device)
+        st = self._step(b, idx_buf)
         self._prepare_comm(st)
         graph = None
         if self.capture:
@@ -403,7 +398,7 @@ class FusedMnistTrainer:
                 # whole execution (K steps incl. all-reduce + optimizer) in one graph
                 graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(graph, stream=s):
-                    for k in range(start, K):
+                    for k in range(K):
                         self._train_step(st, k * b, b * self.R)
             else:
                 # one graph per step holding the fused fwd/bwd/finalize; the RCCL all-reduce and
@@ -422,16 +417,8 @@ class FusedMnistTrainer:
             for k, v in saved[2].items():
                 self.optimizer.slots()[k].copy_(v)
         g = (graph, idx_buf, st)
-        self._graphs[(K, b, slot, start)] = g
+        self._graphs[(K, b, slot)] = g
         return g
-
-    def _lead_steps(self, K: int) -> int:
-        """Steps of an execution that starts on an idle GPU to launch eagerly in front of its graph
-        (a direct launch reaches an idle GPU in a few us, a graph replay in ~10-16 us; the lead
-        steps keep the GPU busy while the graph of the remaining steps is launched).
-        TDL_EAGER_LEAD_STEPS (default 0: off)."""
-        lead = int(os.environ.get("TDL_EAGER_LEAD_STEPS", "0"))
-        return lead if 0 < lead < K and self.capture and self.capture_comm else 0
 
     def warm_graphs(self, steps: int, b: Optional[int] = None):
         """Capture every graph ``run_train(steps)`` will replay, ahead of a timed region."""
@@ -445,9 +432,6 @@ class FusedMnistTrainer:
         for K in sizes:
             for slot in range(self._nslots):
                 self._graph_for(K, b, slot)
-                lead = self._lead_steps(K)
-                if lead:
-                    self._graph_for(K, b, slot, lead)
         # pinned staging buffers of every slot at full size now: a pinned (hipHostMalloc)
         # allocation inside the launch loop waited ~30 ms for the device
         if sizes:
@@ -493,7 +477,7 @@ class FusedMnistTrainer:
         tc = time.perf_counter()
         self._upload(idx, idx_buf, slot)
         self._last_take = (tb - ta, tc - tb, time.perf_counter() - tc)
-        return (handler, K, idx.size // handler.b, graph, st, slot)
+        return (handler, K, idx.size // handler.b, graph, st)
 
     def prefetch(self, handler: "DeviceHandler", K: int) -> bool:
         """Input prefetch of depth one execution (tf.data ``prefetch`` semantics): take and upload
@@ -516,7 +500,6 @@ class FusedMnistTrainer:
         if not hasattr(self, "_stage"):
             self._stage, self._stage_ev, self._slot = [None] * self._nslots, [None] * self._nslots, 0
         timing = self._host_times is not None
-        first = True  # the first execution of this call starts on an idle GPU
         while done < steps:
             K = min(self.K, steps - done)
             t0 = time.perf_counter() if timing else 0.0
@@ -536,15 +519,8 @@ class FusedMnistTrainer:
                 done += 1
                 continue
             opt._sync_lr()
-            _, _, Kr, graph, st, slot = r
-            lead = self._lead_steps(K) if first and Kr == K and graph is not None and not isinstance(graph, list) else 0
-            first = False
-            if lead:
-                # eager lead steps on the idle GPU, then the graph of the remaining steps
-                for k in range(lead):
-                    self._train_step(st, k * b, b * self.R)
-                self._graph_for(K, b, slot, lead)[0].replay()
-            elif Kr < K:
+            _, _, Kr, graph, st = r
+            if Kr < K:
                 # the full batches in front of an epoch's partial batch: same slot buffers and
                 # step object, launched eagerly (no per-step host sync, no new graph size)
                 for k in range(Kr):

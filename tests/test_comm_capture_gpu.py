@@ -49,7 +49,7 @@ def run(capture, overlap, momentum):
     tr.warm_graphs(12)
     n = tr.run_train(h, 12)
     torch.cuda.synchronize()
-    graph = tr._graphs[(4, 64, 0, 0)][0]
+    graph = tr._graphs[(4, 64, 0)][0]
     kind = "list" if isinstance(graph, list) else ("whole" if graph is not None else "none")
     return tr.W.detach().cpu().clone(), n, kind, bool(tr.capture_comm)
 
