@@ -19,6 +19,7 @@
 // remap below hands each XCD a contiguous run of logical tiles (the column tiles of a row block
 // are adjacent), and the row block's activations are read into one L2 instead of eight.
 #include "kernels/conv.h"
+#include "kernels/common.h"
 
 namespace tdl {
 namespace {
@@ -112,27 +113,35 @@ __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
   const int ntn = a.K / BN;
   const int tn = wg % ntn, tm = wg / ntn;
 
+  // Operands are read with raw buffer loads: byte voffset per thread (fixed for the whole k loop),
+  // wave-uniform soffset per k-tile, and the buffer's range check supplies the zeros of padding
+  // taps (voffset 0x80000000 is past any tensor this kernel takes: conv_bf16_supported keeps both
+  // under 2 GiB).  The image resource starts `bias` elements before x, so that every in-image
+  // offset (kh, kw >= 0 added to a row's top-left tap, which may lie in the padding) is >= 0.
   // per-thread A rows: chunk j = tid + 256 i -> row j >> 3, 16-B column j & 7
   const int col8 = (tid & 7) * 8;
-  long long a_base[A_LD];
-  int a_ih[A_LD], a_iw[A_LD];
+  const long long bias = ((long long)a.PT * a.W + a.PL) * a.C;
+  const auto x_rsrc = buf_rsrc(a.x - bias, (unsigned)(((long long)a.N * a.H * a.W * a.C + bias) * 2));
+  const auto w_rsrc = buf_rsrc(a.w, (unsigned)((long long)a.KH * a.KW * a.C * a.K * 2));
+  int a_vo[A_LD];
+  uint32_t a_tap[A_LD];  // bit (kh * KW + kw): that tap of this row lies inside the image
 #pragma unroll
   for (int i = 0; i < A_LD; ++i) {
     const int m = tm * BM + (tid >> 3) + RP * i;
+    a_tap[i] = 0u;
+    a_vo[i] = 0;
     if (m < a.M) {
       const int ow = m % a.OW, t = m / a.OW, oh = t % a.OH, n = t / a.OH;
-      a_ih[i] = oh * a.SH - a.PT;
-      a_iw[i] = ow * a.SW - a.PL;
-      a_base[i] = (((long long)n * a.H + a_ih[i]) * a.W + a_iw[i]) * a.C + col8;
-    } else {
-      a_ih[i] = -(1 << 28);
-      a_iw[i] = 0;
-      a_base[i] = 0;
+      const int ih = oh * a.SH - a.PT, iw = ow * a.SW - a.PL;
+      a_vo[i] = (int)(((((long long)n * a.H + ih) * a.W + iw) * a.C + col8 + bias) * 2);
+      for (int kh = 0; kh < a.KH; ++kh)
+        for (int kw = 0; kw < a.KW; ++kw)
+          if ((unsigned)(ih + kh) < (unsigned)a.H && (unsigned)(iw + kw) < (unsigned)a.W) a_tap[i] |= 1u << (kh * a.KW + kw);
     }
   }
-  long long b_base[B_LD];
+  int b_vo[B_LD];
 #pragma unroll
-  for (int i = 0; i < B_LD; ++i) b_base[i] = (long long)(tn * BN + (tid >> 3) + RP * i) * a.w_col + col8;
+  for (int i = 0; i < B_LD; ++i) b_vo[i] = (int)(((long long)(tn * BN + (tid >> 3) + RP * i) * a.w_col + col8) * 2);
 
   // register staging sets: DEPTH 2 keeps two tiles of global loads in flight (tile t+2 is issued
   // while tile t computes and tile t+1's registers are written to LDS), DEPTH 1 one tile
@@ -151,19 +160,18 @@ __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
         ++n_kh;
       }
     }
-    const long long aoff = ((long long)kh * a.W + kw) * a.C + c0;
+    const int tap = kh * a.KW + kw;
+    const int soff_a = (int)((((long long)kh * a.W + kw) * a.C + c0) * 2);
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
-      const int ih = a_ih[i] + kh, iw = a_iw[i] + kw;
-      if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
-        pa[i] = *reinterpret_cast<const u32x4*>(a.x + a_base[i] + aoff);
-      else
-        pa[i] = u32x4{0u, 0u, 0u, 0u};
+      const int vo = ((a_tap[i] >> tap) & 1u) ? a_vo[i] : (int)0x80000000;
+      pa[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(x_rsrc, vo, soff_a, 0));
     }
     const int wkh = a.flip ? a.KH - 1 - kh : kh, wkw = a.flip ? a.KW - 1 - kw : kw;
-    const long long boff = wkh * a.w_kh + wkw * a.w_kw + c0;
+    const int soff_b = (int)((wkh * a.w_kh + wkw * a.w_kw + c0) * 2);
 #pragma unroll
-    for (int i = 0; i < B_LD; ++i) pb[i] = *reinterpret_cast<const u32x4*>(a.w + b_base[i] + boff);
+    for (int i = 0; i < B_LD; ++i)
+      pb[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(w_rsrc, b_vo[i], soff_b, 0));
   };
   const int scol = ((tid & 7) ^ swz(tid >> 3)) * 8;  // swizzled LDS column of this thread's chunk (RP % 16 == 0)
   auto sstore = [&](int buf, const u32x4* pa, const u32x4* pb) {
@@ -395,8 +403,16 @@ void conv_force_tile(int tile) { g_forced_tile = tile; }
 void conv_force_depth(int depth) { g_depth = depth == 1 ? 1 : 2; }
 
 bool conv_bf16_supported(const ConvGeom& g) {
-  return g.C % 64 == 0 && g.K % 64 == 0 && g.N > 0 && g.OH > 0 && g.OW > 0 &&
-         (long long)g.N * g.OH * g.OW < (1ll << 31) && (long long)g.N * g.H * g.W * g.C < (1ll << 40);
+  // byte offsets of every operand and output within 2 GiB (32-bit buffer offsets), <= 32 taps
+  // (the per-row tap-validity bitmask of the operand loader), padding < the filter size (the
+  // image resource's base offset is non-negative in both directions)
+  const long long two_gib_elems = 1ll << 30;
+  return g.C % 64 == 0 && g.K % 64 == 0 && g.N > 0 && g.OH > 0 && g.OW > 0 && g.KH * g.KW <= 32 &&
+         g.PT >= 0 && g.PL >= 0 && g.PT < g.KH && g.PL < g.KW &&
+         (long long)g.N * g.H * g.W * g.C + ((long long)g.PT * g.W + g.PL) * g.C < two_gib_elems &&
+         (long long)g.N * g.OH * g.OW * g.K + ((long long)(g.KH - 1 - g.PT) * g.OW + (g.KW - 1 - g.PL)) * g.K <
+             two_gib_elems &&
+         (long long)g.KH * g.KW * g.C * g.K < two_gib_elems;
 }
 
 int conv_fwd_row_tile(const ConvGeom& g) {
