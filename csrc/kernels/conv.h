@@ -36,16 +36,23 @@ int conv_fwd_row_tile(const ConvGeom& g);
 // whose output is this conv's input bn_y and whose BN input is bn_x: dx := (dgrad + residual) *
 // [bn_y > 0] (the group's dz) and bn_part[ceil(M / conv_dgrad_row_tile)][2][C] := per-tile channel
 // sums of dz and dz * bn_x (bn_backward(part=...) then skips its reduction pass)
+// bn_part2 (with bn_x2, shaped like dx; needs bn_part): the group's residual is the output of a plain
+// BN (projection shortcut) with input bn_x2 and no other reader: bn_part2 := per-tile sums of dz and
+// dz * bn_x2, that BN's backward reduction
 void conv_dgrad_bf16(const void* dy, const void* w_hwio, void* dx, const ConvGeom& g, hipStream_t s,
                      const void* residual = nullptr, const void* bn_y = nullptr, const void* bn_x = nullptr,
-                     float* bn_part = nullptr);
+                     float* bn_part = nullptr, const void* bn_x2 = nullptr, float* bn_part2 = nullptr);
 int conv_dgrad_row_tile(const ConvGeom& g);
 
 // Input gradient of a 1x1, stride-2, unpadded convolution (the strided shortcut / first 1x1 of a
 // ResNet-50 stage): dx[n][2i][2j] = dy[n][i][j] . w^T, the other three pixels of every 2x2 block are
-// zero (written by the same kernel's epilogue; H <= 2*OH, W <= 2*OW).
+// zero (written by the same kernel's epilogue; H <= 2*OH, W <= 2*OW).  residual / bn_*: as for
+// conv_dgrad_bf16, over all four pixels of each 2x2 block (the part rows are the row tiles of the
+// N*OH*OW dy pixels, conv_dgrad_s2_row_tile)
 void conv_dgrad_s2_1x1_bf16(const void* dy, const void* w_hwio, void* dx, const ConvGeom& g, hipStream_t s,
-                            const void* residual = nullptr);
+                            const void* residual = nullptr, const void* bn_y = nullptr, const void* bn_x = nullptr,
+                            float* bn_part = nullptr, const void* bn_x2 = nullptr, float* bn_part2 = nullptr);
+int conv_dgrad_s2_row_tile(const ConvGeom& g);
 
 // Weight gradient, split-K over output pixels with a deterministic partial-slab reduction.
 struct WgradPlan {

@@ -58,7 +58,34 @@ struct Igemm {
   const uint16_t* bn_y;  // the conv's input (the group output), for the ReLU mask
   const uint16_t* bn_x;  // the group's BN input
   float* bn_part;
+  // optional, with bn_part: the group's residual is the output of a plain BN (a projection
+  // shortcut's) whose only reader is the group's Add, so that BN's output gradient is dz as well:
+  // bn_part2 [row tiles][2][K] gets the per-tile channel sums of dz and dz * bn_x2 (its input)
+  const uint16_t* bn_x2;
+  float* bn_part2;
 };
+
+// per-channel sums of 8 packed bf16 values v: s += v, q += v * w (w also 8 packed bf16)
+__device__ __forceinline__ void accum_bf16x8(u32x4 v, u32x4 w, float* s, float* q) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float lo = __uint_as_float(v[j] << 16), hi = __uint_as_float(v[j] & 0xffff0000u);
+    const float wl = __uint_as_float(w[j] << 16), wh = __uint_as_float(w[j] & 0xffff0000u);
+    s[2 * j] += lo;
+    q[2 * j] = fmaf(lo, wl, q[2 * j]);
+    s[2 * j + 1] += hi;
+    q[2 * j + 1] = fmaf(hi, wh, q[2 * j + 1]);
+  }
+}
+
+// q += v * w for 8 packed bf16 values
+__device__ __forceinline__ void dot_bf16x8(u32x4 v, u32x4 w, float* q) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    q[2 * j] = fmaf(__uint_as_float(v[j] << 16), __uint_as_float(w[j] << 16), q[2 * j]);
+    q[2 * j + 1] = fmaf(__uint_as_float(v[j] & 0xffff0000u), __uint_as_float(w[j] & 0xffff0000u), q[2 * j + 1]);
+  }
+}
 
 // v * [y > 0] for 8 packed bf16 (y > 0: sign clear and not +0)
 __device__ __forceinline__ u32x4 relu_mask_bf16x8(u32x4 v, u32x4 y) {
@@ -93,7 +120,10 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return (uint16_t)(u >> 16);
 }
 
-template <int BM, int BN, int DEPTH>
+// EK selects the epilogue a variant carries (registers: the VGPR peak of the heaviest epilogue sets the
+// occupancy of the whole kernel, so the plain variant must not pay for the fused ones): 0 plain
+// (+ residual, + BN statistics), 1 fused BN-group backward, 2 stride-2 scatter (+ residual, + BN group)
+template <int BM, int BN, int DEPTH, int EK>
 __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
   constexpr int NT = BM * 2;         // threads: (BM / 64) x 2 waves, each 64 x BN/2
   constexpr int RP = NT / 8;         // tile rows per staging pass (8 x 16-B chunks per 128-B row)
@@ -249,8 +279,8 @@ __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
   static_assert(BM * SEG % NT == 0, "epilogue segments must divide evenly");
   // residual (gradient sum): all of this thread's loads issued here, before the LDS round trip, so
   // their latency overlaps it instead of serialising the store loop
-  u32x4 rv[EPI];
-  if (a.res && !a.scatter) {
+  u32x4 rv[EK == 2 ? 1 : EPI];
+  if (EK != 2 && a.res) {
 #pragma unroll
     for (int e = 0; e < EPI; ++e) {
       const int s = tid + e * NT, row = s / SEG, seg = s % SEG, m = tm * BM + row;
@@ -270,23 +300,29 @@ __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
           make_uint2(lo, hi);
     }
   // BN-backward fusion operands (the accumulators are dead now: registers to spare)
-  u32x4 ry[EPI], rx[EPI];
-  if (a.bn_part && !a.scatter) {
+  constexpr int BNE = EK == 1 ? EPI : 1;
+  u32x4 ry[BNE], rx[BNE], rx2[BNE];
+  if constexpr (EK == 1) {
 #pragma unroll
     for (int e = 0; e < EPI; ++e) {
       const int s = tid + e * NT, row = s / SEG, seg = s % SEG, m = tm * BM + row;
       const long long o = (long long)m * a.K + tn * BN + seg * 8;
-      ry[e] = m < a.M ? *reinterpret_cast<const u32x4*>(a.bn_y + o) : u32x4{0u, 0u, 0u, 0u};
-      rx[e] = m < a.M ? *reinterpret_cast<const u32x4*>(a.bn_x + o) : u32x4{0u, 0u, 0u, 0u};
+      const bool in = m < a.M;
+      ry[e] = in ? *reinterpret_cast<const u32x4*>(a.bn_y + o) : u32x4{0u, 0u, 0u, 0u};
+      rx[e] = in ? *reinterpret_cast<const u32x4*>(a.bn_x + o) : u32x4{0u, 0u, 0u, 0u};
+      rx2[e] = (in && a.bn_x2) ? *reinterpret_cast<const u32x4*>(a.bn_x2 + o) : u32x4{0u, 0u, 0u, 0u};
     }
   }
   __syncthreads();
-  if (!a.scatter) {
-    static_assert(NT % SEG == 0, "a thread keeps one 8-channel segment across its rows");
-    float* sums = a.stats ? a.stats : a.bn_part;  // per-tile channel sums: (y, y^2) or (dz, dz * xb)
-    float cs[8], cq[8];
+  static_assert(NT % SEG == 0, "a thread keeps one 8-channel segment across its rows");
+  // per-tile channel sums: (y, y^2) of the forward output, or (dz, dz * xb) [and dz * xb2] of a fused
+  // BN group backward
+  float* sums = a.stats ? a.stats : (EK != 0 ? a.bn_part : nullptr);
+  float* sums2 = (EK != 0 && a.bn_part) ? a.bn_part2 : nullptr;
+  float cs[8], cq[8], cq2[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) cs[j] = cq[j] = 0.f;
+  for (int j = 0; j < 8; ++j) cs[j] = cq[j] = cq2[j] = 0.f;
+  if constexpr (EK != 2) {
 #pragma unroll
     for (int e = 0; e < EPI; ++e) {
       const int s = tid + e * NT, row = s / SEG, seg = s % SEG;
@@ -295,43 +331,11 @@ __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
         const long long o = (long long)m * a.K + tn * BN + seg * 8;
         u32x4 v = *reinterpret_cast<const u32x4*>(lds + row * OUT_LD + seg * 8);
         if (a.res) v = add_bf16x8(v, rv[e]);
-        if (a.bn_part) v = relu_mask_bf16x8(v, ry[e]);
+        if constexpr (EK == 1) v = relu_mask_bf16x8(v, ry[e]);
         *reinterpret_cast<u32x4*>(a.y + o) = v;
-        if (sums) {
-          const u32x4 w = a.bn_part ? rx[e] : v;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float lo = __uint_as_float(v[j] << 16), hi = __uint_as_float(v[j] & 0xffff0000u);
-            const float wl = __uint_as_float(w[j] << 16), wh = __uint_as_float(w[j] & 0xffff0000u);
-            cs[2 * j] += lo;
-            cq[2 * j] = fmaf(lo, wl, cq[2 * j]);
-            cs[2 * j + 1] += hi;
-            cq[2 * j + 1] = fmaf(hi, wh, cq[2 * j + 1]);
-          }
-        }
-      }
-    }
-    if (sums) {
-      // fixed-order reduction over the NT / SEG threads of each segment, through the (now free) LDS
-      constexpr int TPS = NT / SEG;  // threads per segment
-      static_assert(2 * TPS * BN * 4 <= 2 * (BM + BN) * LDS_ROW * 2, "stats scratch must fit the operand LDS");
-      __syncthreads();  // every thread has read its tile rows
-      float* red = reinterpret_cast<float*>(lds);
-      const int seg = tid % SEG, grp = tid / SEG;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        red[grp * BN + seg * 8 + j] = cs[j];
-        red[TPS * BN + grp * BN + seg * 8 + j] = cq[j];
-      }
-      __syncthreads();
-      for (int c = tid; c < BN; c += NT) {
-        float S = 0.f, Q = 0.f;
-        for (int g2 = 0; g2 < TPS; ++g2) {
-          S += red[g2 * BN + c];
-          Q += red[TPS * BN + g2 * BN + c];
-        }
-        sums[((long long)tm * 2) * a.K + tn * BN + c] = S;
-        sums[((long long)tm * 2 + 1) * a.K + tn * BN + c] = Q;
+        if (sums) accum_bf16x8(v, EK == 1 ? rx[e] : v, cs, cq);
+        if constexpr (EK == 1)
+          if (sums2) dot_bf16x8(v, rx2[e], cq2);
       }
     }
   } else {
@@ -342,33 +346,66 @@ __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
       const int ow = m % a.OW, t = m / a.OW, oh = t % a.OH, n = t / a.OH;
       const int h = 2 * oh, w = 2 * ow;
       const long long off = (((long long)n * a.XH + h) * a.XW + w) * a.K + tn * BN + seg * 8;
-      uint16_t* o = a.y + off;
       const long long rs = (long long)a.XW * a.K;
-      u32x4 v = *reinterpret_cast<const u32x4*>(lds + row * OUT_LD + seg * 8);
-      if (a.res) {
-        // the other gradient contribution: added at the computed pixel, copied to the three others
-        // (the four loads issued together)
-        const uint16_t* rp = a.res + off;
-        const bool w1 = w + 1 < a.XW, h1 = h + 1 < a.XH;
-        const u32x4 z{0u, 0u, 0u, 0u};
-        const u32x4 r00 = *reinterpret_cast<const u32x4*>(rp);
-        const u32x4 r01 = w1 ? *reinterpret_cast<const u32x4*>(rp + a.K) : z;
-        const u32x4 r10 = h1 ? *reinterpret_cast<const u32x4*>(rp + rs) : z;
-        const u32x4 r11 = (w1 && h1) ? *reinterpret_cast<const u32x4*>(rp + rs + a.K) : z;
-        *reinterpret_cast<u32x4*>(o) = add_bf16x8(v, r00);
-        if (w1) *reinterpret_cast<u32x4*>(o + a.K) = r01;
-        if (h1) {
-          *reinterpret_cast<u32x4*>(o + rs) = r10;
-          if (w1) *reinterpret_cast<u32x4*>(o + rs + a.K) = r11;
-        }
-        continue;
-      }
+      const bool w1 = w + 1 < a.XW, h1 = h + 1 < a.XH;
+      // the 2x2 block of dx pixels this output row owns: (2oh, 2ow) gets the computed gradient, the
+      // other three only the other contribution (or zeros)
+      const bool ok[4] = {true, w1, h1, w1 && h1};
+      const long long po[4] = {off, off + a.K, off + rs, off + rs + a.K};
       const u32x4 z{0u, 0u, 0u, 0u};
-      *reinterpret_cast<u32x4*>(o) = v;
-      if (w + 1 < a.XW) *reinterpret_cast<u32x4*>(o + a.K) = z;
-      if (h + 1 < a.XH) {
-        *reinterpret_cast<u32x4*>(o + rs) = z;
-        if (w + 1 < a.XW) *reinterpret_cast<u32x4*>(o + rs + a.K) = z;
+      u32x4 p[4];
+      // every load of the block issued before any math
+#pragma unroll
+      for (int q = 0; q < 4; ++q) p[q] = (a.res && ok[q]) ? *reinterpret_cast<const u32x4*>(a.res + po[q]) : z;
+      u32x4 by[4], bx[4], bx2[4];
+      if (a.bn_part) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          by[q] = ok[q] ? *reinterpret_cast<const u32x4*>(a.bn_y + po[q]) : z;
+          bx[q] = ok[q] ? *reinterpret_cast<const u32x4*>(a.bn_x + po[q]) : z;
+          bx2[q] = (ok[q] && a.bn_x2) ? *reinterpret_cast<const u32x4*>(a.bn_x2 + po[q]) : z;
+        }
+      }
+      const u32x4 v = *reinterpret_cast<const u32x4*>(lds + row * OUT_LD + seg * 8);
+      p[0] = a.res ? add_bf16x8(v, p[0]) : v;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (!ok[q]) continue;
+        if (a.bn_part) {
+          p[q] = relu_mask_bf16x8(p[q], by[q]);
+          accum_bf16x8(p[q], bx[q], cs, cq);
+          if (sums2) dot_bf16x8(p[q], bx2[q], cq2);
+        }
+        *reinterpret_cast<u32x4*>(a.y + po[q]) = p[q];
+      }
+    }
+  }
+  if (sums) {
+    // fixed-order reduction over the NT / SEG threads of each segment, through the (now free) LDS
+    constexpr int TPS = NT / SEG;  // threads per segment
+    static_assert(3 * TPS * BN * 4 <= 2 * (BM + BN) * LDS_ROW * 2, "stats scratch must fit the operand LDS");
+    __syncthreads();  // every thread has read its tile rows
+    float* red = reinterpret_cast<float*>(lds);
+    const int seg = tid % SEG, grp = tid / SEG;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[grp * BN + seg * 8 + j] = cs[j];
+      red[TPS * BN + grp * BN + seg * 8 + j] = cq[j];
+      if (sums2) red[2 * TPS * BN + grp * BN + seg * 8 + j] = cq2[j];
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += NT) {
+      float S = 0.f, Q = 0.f, Q2 = 0.f;
+      for (int g2 = 0; g2 < TPS; ++g2) {
+        S += red[g2 * BN + c];
+        Q += red[TPS * BN + g2 * BN + c];
+        if (sums2) Q2 += red[2 * TPS * BN + g2 * BN + c];
+      }
+      sums[((long long)tm * 2) * a.K + tn * BN + c] = S;
+      sums[((long long)tm * 2 + 1) * a.K + tn * BN + c] = Q;
+      if (sums2) {
+        sums2[((long long)tm * 2) * a.K + tn * BN + c] = S;
+        sums2[((long long)tm * 2 + 1) * a.K + tn * BN + c] = Q2;
       }
     }
   }
@@ -376,13 +413,23 @@ __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
 
 int g_depth = 2;  // register prefetch depth (tiles in flight); conv_force_depth for A/B sweeps
 
+template <int BM, int BN, int DEPTH>
+void launch_epi(const Igemm& a, hipStream_t s) {
+  const dim3 grid((a.M + BM - 1) / BM * (a.K / BN)), block(BM * 2);
+  if (a.scatter)
+    hipLaunchKernelGGL((k_conv_igemm<BM, BN, DEPTH, 2>), grid, block, 0, s, a);
+  else if (a.bn_part)
+    hipLaunchKernelGGL((k_conv_igemm<BM, BN, DEPTH, 1>), grid, block, 0, s, a);
+  else
+    hipLaunchKernelGGL((k_conv_igemm<BM, BN, DEPTH, 0>), grid, block, 0, s, a);
+}
+
 template <int BM, int BN>
 void launch_tile(const Igemm& a, hipStream_t s) {
-  const int mt = (a.M + BM - 1) / BM;
   if (g_depth == 1)
-    hipLaunchKernelGGL((k_conv_igemm<BM, BN, 1>), dim3(mt * (a.K / BN)), dim3(BM * 2), 0, s, a);
+    launch_epi<BM, BN, 1>(a, s);
   else
-    hipLaunchKernelGGL((k_conv_igemm<BM, BN, 2>), dim3(mt * (a.K / BN)), dim3(BM * 2), 0, s, a);
+    launch_epi<BM, BN, 2>(a, s);
 }
 
 int g_forced_tile = 0;  // 0: heuristic below; 1: 128 x 64, 2: 128 x 128, 3: 256 x 128 (tile sweeps)
@@ -422,6 +469,8 @@ int conv_fwd_row_tile(const ConvGeom& g) {
 
 int conv_dgrad_row_tile(const ConvGeom& g) { return (g_forced_tile == 3 && g.C % 128 == 0) ? 256 : 128; }
 
+int conv_dgrad_s2_row_tile(const ConvGeom& g) { return (g_forced_tile == 3 && g.C % 128 == 0) ? 256 : 128; }
+
 void conv_fwd_bf16(const void* x, const void* w_ohwi, void* y, const ConvGeom& g, hipStream_t s, float* stats) {
   Igemm a{static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w_ohwi), static_cast<uint16_t*>(y),
           g.N, g.H, g.W, g.C, g.OH, g.OW, g.K, g.KH, g.KW, g.SH, g.SW, g.PT, g.PL, 0,
@@ -431,24 +480,28 @@ void conv_fwd_bf16(const void* x, const void* w_ohwi, void* y, const ConvGeom& g
 }
 
 void conv_dgrad_bf16(const void* dy, const void* w_hwio, void* dx, const ConvGeom& g, hipStream_t s,
-                     const void* residual, const void* bn_y, const void* bn_x, float* bn_part) {
+                     const void* residual, const void* bn_y, const void* bn_x, float* bn_part, const void* bn_x2,
+                     float* bn_part2) {
   // image = dy [N][OH][OW][K] (reduction channels K), output = dx [N][H][W][C] (columns C), stride 1,
   // mirrored taps with padding KH-1-PT / KW-1-PL
   Igemm a{static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w_hwio), static_cast<uint16_t*>(dx),
           g.N, g.OH, g.OW, g.K, g.H, g.W, g.C, g.KH, g.KW, 1, 1, g.KH - 1 - g.PT, g.KW - 1 - g.PL, 1,
           (long long)g.K, (long long)g.KW * g.C * g.K, (long long)g.C * g.K, g.N * g.H * g.W, 0, 0, 0,
           static_cast<const uint16_t*>(residual), nullptr, static_cast<const uint16_t*>(bn_y),
-          static_cast<const uint16_t*>(bn_x), bn_part};
+          static_cast<const uint16_t*>(bn_x), bn_part, static_cast<const uint16_t*>(bn_x2), bn_part2};
   launch(a, s);
 }
 
 void conv_dgrad_s2_1x1_bf16(const void* dy, const void* w_hwio, void* dx, const ConvGeom& g, hipStream_t s,
-                            const void* residual) {
+                            const void* residual, const void* bn_y, const void* bn_x, float* bn_part,
+                            const void* bn_x2, float* bn_part2) {
   // a 1x1 stride-1 "convolution" of dy [N][OH][OW][K] with the HWIO rows [C][K] (columns C, reduction K),
   // scattered to the even pixels of dx [N][H][W][C]
   Igemm a{static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w_hwio), static_cast<uint16_t*>(dx),
           g.N, g.OH, g.OW, g.K, g.OH, g.OW, g.C, 1, 1, 1, 1, 0, 0, 0,
-          (long long)g.K, 0, 0, g.N * g.OH * g.OW, 2, g.H, g.W, static_cast<const uint16_t*>(residual)};
+          (long long)g.K, 0, 0, g.N * g.OH * g.OW, 2, g.H, g.W, static_cast<const uint16_t*>(residual), nullptr,
+          static_cast<const uint16_t*>(bn_y), static_cast<const uint16_t*>(bn_x), bn_part,
+          static_cast<const uint16_t*>(bn_x2), bn_part2};
   launch(a, s);
 }
 

@@ -1,5 +1,8 @@
 // Bindings of the generic HIP ops (csrc/kernels/ops.hip).
 #include <torch/extension.h>
+
+#include <cstdlib>
+#include <limits>
 #include <c10/hip/HIPStream.h>
 
 #include "kernels/bn.h"
@@ -7,9 +10,23 @@
 #include "kernels/gemm.h"
 #include "kernels/ops.h"
 #include "kernels/pool.h"
+#include "kernels/stem.h"
 
 namespace {
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+// TDL_DEBUG_POISON=1: outputs and partial-sum buffers of the conv kernels start as NaN instead of
+// uninitialised (a row or pixel a kernel fails to write then shows up in the results)
+int poison() {  // 1: partial-sum buffers, 2: and the gradient outputs
+  static const int on = [] {
+    const char* e = std::getenv("TDL_DEBUG_POISON");
+    return e != nullptr ? std::atoi(e) : 0;
+  }();
+  return on;
+}
+at::Tensor fresh(at::IntArrayRef shape, const at::TensorOptions& o, int level = 1) {
+  return poison() >= level ? at::full(shape, std::numeric_limits<float>::quiet_NaN(), o) : at::empty(shape, o);
+}
 
 at::Tensor gather_rows(at::Tensor src, at::Tensor idx, double scale) {
   TORCH_CHECK(src.is_cuda() && idx.is_cuda(), "gather_rows: GPU tensors expected");
@@ -142,8 +159,8 @@ std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, c10::optional<a
   at::Tensor part;
   if (part_in.has_value() && part_in->defined()) {
     // (dz, part) from conv_dgrad_bn: dy IS the group's masked gradient dz (for an add+relu group
-    // also returned as the residual's)
-    TORCH_CHECK(mode >= 1, "batch_norm backward: precomputed partials are for relu / add+relu groups");
+    // also returned as the residual's); mode 0: a plain BN whose output gradient is such a group's
+    // dz (part2 of conv_dgrad_bn: sums of dz and dz * x)
     given = parts_rows(*part_in, C);
     part = *part_in;
   } else {
@@ -235,7 +252,7 @@ std::vector<at::Tensor> conv_fwd_stats(at::Tensor x, at::Tensor w_ohwi, int64_t 
   auto y = at::empty({x.size(0), oh, ow, w_ohwi.size(0)}, x.options());
   const int64_t M = (int64_t)g.N * g.OH * g.OW, bm = tdl::conv_fwd_row_tile(g);
   const int64_t P = (M + bm - 1) / bm;
-  auto part = at::empty({P + (P + 63) / 64, 2, (int64_t)g.K}, x.options().dtype(at::kFloat));
+  auto part = fresh({P + (P + 63) / 64, 2, (int64_t)g.K}, x.options().dtype(at::kFloat));
   tdl::conv_fwd_bf16(x.data_ptr(), w_ohwi.data_ptr(), y.data_ptr(), g, cur_stream(), part.data_ptr<float>());
   return {y, part};
 }
@@ -253,47 +270,72 @@ const void* opt_residual(const c10::optional<at::Tensor>& r, const at::Tensor& l
 
 std::vector<at::Tensor> conv_dgrad_impl(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w, int64_t pt,
                                         int64_t pl, c10::optional<at::Tensor> residual,
-                                        c10::optional<at::Tensor> bn_y, c10::optional<at::Tensor> bn_x);
+                                        c10::optional<at::Tensor> bn_y, c10::optional<at::Tensor> bn_x,
+                                        c10::optional<at::Tensor> bn_x2);
+
+// BN-group fusion operands of an input gradient (see conv.h): (bn_y, bn_x[, bn_x2]) tensors shaped
+// like dx, and the part buffers [P + ceil(P/64)][2][C] for P row tiles
+struct DgradBn {
+  const void *by = nullptr, *bx = nullptr, *bx2 = nullptr;
+  at::Tensor part, part2;
+  DgradBn(const c10::optional<at::Tensor>& bn_y, const c10::optional<at::Tensor>& bn_x,
+          const c10::optional<at::Tensor>& bn_x2, const at::Tensor& dy, int64_t h, int64_t w, int64_t c,
+          int64_t P) {
+    by = opt_residual(bn_y, dy, dy.size(0), h, w, c);
+    bx = opt_residual(bn_x, dy, dy.size(0), h, w, c);
+    bx2 = opt_residual(bn_x2, dy, dy.size(0), h, w, c);
+    TORCH_CHECK((by == nullptr) == (bx == nullptr), "conv_dgrad: bn_y and bn_x go together");
+    TORCH_CHECK(bx2 == nullptr || by != nullptr, "conv_dgrad: bn_x2 needs bn_y / bn_x");
+    auto f = dy.options().dtype(at::kFloat);
+    if (by) part = fresh({P + (P + 63) / 64, 2, c}, f);
+    if (bx2) part2 = fresh({P + (P + 63) / 64, 2, c}, f);
+  }
+  float* p() { return by ? part.data_ptr<float>() : nullptr; }
+  float* p2() { return bx2 ? part2.data_ptr<float>() : nullptr; }
+  std::vector<at::Tensor> out(const at::Tensor& dx) {
+    if (bx2) return {dx, part, part2};
+    if (by) return {dx, part};
+    return {dx};
+  }
+};
 
 at::Tensor conv_dgrad(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w, int64_t pt, int64_t pl,
                       c10::optional<at::Tensor> residual) {
-  return conv_dgrad_impl(dy, w_hwio, h, w, pt, pl, residual, c10::nullopt, c10::nullopt)[0];
+  return conv_dgrad_impl(dy, w_hwio, h, w, pt, pl, residual, c10::nullopt, c10::nullopt, c10::nullopt)[0];
 }
 
 // input gradient with the fused backward of the BN -> Add -> ReLU group that produced the conv's
-// input bn_y from bn_x: returns (dz, part[P + ceil(P/64)][2][C])
+// input bn_y from bn_x: returns (dz, part[P + ceil(P/64)][2][C][, part2]); bn_x2: the input of the
+// plain BN whose output is the group's residual (part2: its backward sums)
 std::vector<at::Tensor> conv_dgrad_bn(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w, int64_t pt, int64_t pl,
-                                      c10::optional<at::Tensor> residual, at::Tensor bn_y, at::Tensor bn_x) {
-  return conv_dgrad_impl(dy, w_hwio, h, w, pt, pl, residual, bn_y, bn_x);
+                                      c10::optional<at::Tensor> residual, at::Tensor bn_y, at::Tensor bn_x,
+                                      c10::optional<at::Tensor> bn_x2) {
+  return conv_dgrad_impl(dy, w_hwio, h, w, pt, pl, residual, bn_y, bn_x, bn_x2);
 }
 
 std::vector<at::Tensor> conv_dgrad_impl(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w, int64_t pt,
                                         int64_t pl, c10::optional<at::Tensor> residual,
-                                        c10::optional<at::Tensor> bn_y, c10::optional<at::Tensor> bn_x) {
+                                        c10::optional<at::Tensor> bn_y, c10::optional<at::Tensor> bn_x,
+                                        c10::optional<at::Tensor> bn_x2) {
   conv_check(dy, "dy");
   conv_check(w_hwio, "w");
   TORCH_CHECK(w_hwio.dim() == 4 && w_hwio.size(3) == dy.size(3), "conv_dgrad: weights must be HWIO [KH,KW,C,K]");
   tdl::ConvGeom g{(int)dy.size(0), (int)h, (int)w, (int)w_hwio.size(2), (int)dy.size(1), (int)dy.size(2),
                   (int)dy.size(3), (int)w_hwio.size(0), (int)w_hwio.size(1), 1, 1, (int)pt, (int)pl};
   TORCH_CHECK(tdl::conv_bf16_supported(g), "conv_dgrad: unsupported geometry (C and K must be multiples of 64)");
-  auto dx = at::empty({dy.size(0), h, w, w_hwio.size(2)}, dy.options());
-  const void* by = opt_residual(bn_y, dy, dy.size(0), h, w, w_hwio.size(2));
-  const void* bx = opt_residual(bn_x, dy, dy.size(0), h, w, w_hwio.size(2));
-  TORCH_CHECK((by == nullptr) == (bx == nullptr), "conv_dgrad: bn_y and bn_x go together");
-  at::Tensor part;
-  if (by) {
-    const int64_t M = (int64_t)g.N * g.H * g.W, bm = tdl::conv_dgrad_row_tile(g);
-    const int64_t P = (M + bm - 1) / bm;
-    part = at::empty({P + (P + 63) / 64, 2, (int64_t)g.C}, dy.options().dtype(at::kFloat));
-  }
+  auto dx = fresh({dy.size(0), h, w, w_hwio.size(2)}, dy.options(), 2);
+  const int64_t M = (int64_t)g.N * g.H * g.W, bm = tdl::conv_dgrad_row_tile(g);
+  DgradBn bn(bn_y, bn_x, bn_x2, dy, h, w, w_hwio.size(2), (M + bm - 1) / bm);
   tdl::conv_dgrad_bf16(dy.data_ptr(), w_hwio.data_ptr(), dx.data_ptr(), g, cur_stream(),
-                       opt_residual(residual, dy, dy.size(0), h, w, w_hwio.size(2)), by, bx,
-                       by ? part.data_ptr<float>() : nullptr);
-  if (by) return {dx, part};
-  return {dx};
+                       opt_residual(residual, dy, dy.size(0), h, w, w_hwio.size(2)), bn.by, bn.bx, bn.p(), bn.bx2,
+                       bn.p2());
+  return bn.out(dx);
 }
-// input gradient of a 1x1 stride-2 unpadded conv: dx[N,H,W,C] from dy[N,OH,OW,K] and w_hwio[1,1,C,K]
-at::Tensor conv_dgrad_s2(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w, c10::optional<at::Tensor> residual) {
+// input gradient of a 1x1 stride-2 unpadded conv: dx[N,H,W,C] from dy[N,OH,OW,K] and w_hwio[1,1,C,K];
+// with bn_y / bn_x[ / bn_x2] the fused BN-group backward as in conv_dgrad_bn: (dz, part[, part2])
+std::vector<at::Tensor> conv_dgrad_s2_impl(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w,
+                                           c10::optional<at::Tensor> residual, c10::optional<at::Tensor> bn_y,
+                                           c10::optional<at::Tensor> bn_x, c10::optional<at::Tensor> bn_x2) {
   conv_check(dy, "dy");
   conv_check(w_hwio, "w");
   TORCH_CHECK(w_hwio.dim() == 4 && w_hwio.size(0) == 1 && w_hwio.size(1) == 1 && w_hwio.size(3) == dy.size(3),
@@ -303,10 +345,23 @@ at::Tensor conv_dgrad_s2(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w,
   tdl::ConvGeom g{(int)dy.size(0), (int)h, (int)w, (int)w_hwio.size(2), (int)dy.size(1), (int)dy.size(2),
                   (int)dy.size(3), 1, 1, 2, 2, 0, 0};
   TORCH_CHECK(tdl::conv_bf16_supported(g), "conv_dgrad_s2: unsupported geometry (C and K must be multiples of 64)");
-  auto dx = at::empty({dy.size(0), h, w, w_hwio.size(2)}, dy.options());
+  auto dx = fresh({dy.size(0), h, w, w_hwio.size(2)}, dy.options(), 2);
+  const int64_t M = (int64_t)g.N * g.OH * g.OW, bm = tdl::conv_dgrad_s2_row_tile(g);
+  DgradBn bn(bn_y, bn_x, bn_x2, dy, h, w, w_hwio.size(2), (M + bm - 1) / bm);
   tdl::conv_dgrad_s2_1x1_bf16(dy.data_ptr(), w_hwio.data_ptr(), dx.data_ptr(), g, cur_stream(),
-                              opt_residual(residual, dy, dy.size(0), h, w, w_hwio.size(2)));
-  return dx;
+                              opt_residual(residual, dy, dy.size(0), h, w, w_hwio.size(2)), bn.by, bn.bx, bn.p(),
+                              bn.bx2, bn.p2());
+  return bn.out(dx);
+}
+
+at::Tensor conv_dgrad_s2(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w, c10::optional<at::Tensor> residual) {
+  return conv_dgrad_s2_impl(dy, w_hwio, h, w, residual, c10::nullopt, c10::nullopt, c10::nullopt)[0];
+}
+
+std::vector<at::Tensor> conv_dgrad_s2_bn(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w,
+                                         c10::optional<at::Tensor> residual, at::Tensor bn_y, at::Tensor bn_x,
+                                         c10::optional<at::Tensor> bn_x2) {
+  return conv_dgrad_s2_impl(dy, w_hwio, h, w, residual, bn_y, bn_x, bn_x2);
 }
 
 // weight gradient: dw[KH,KW,C,K] (bf16, or added into the f32 `out` when given) from x[N,H,W,C] and
@@ -343,6 +398,70 @@ at::Tensor conv_wgrad(at::Tensor x, at::Tensor dy, int64_t kh, int64_t kw, int64
   auto dw = at::empty({kh, kw, x.size(3), dy.size(3)}, x.options());
   tdl::conv_wgrad_bf16(x.data_ptr(), dy.data_ptr(), ws.data_ptr<float>(), p, dw.data_ptr(), nullptr, false, g,
                        cur_stream());
+  return dw;
+}
+
+// small-channel stride-2 conv (ResNet stem, csrc/kernels/stem.hip).  x [N,H,W,C] (bf16 or f32,
+// C <= 4), w_hwio [KH,KW,C,K] bf16, zero padding (pt, pb, pl, pr) folded into the packed copy.
+// Returns (y [N,OH,OW,K] bf16, xp packed image for the backward[, part [P + ceil(P/64)][2][K]])
+std::vector<at::Tensor> stem_fwd(at::Tensor x, at::Tensor w_hwio, int64_t pt, int64_t pb, int64_t pl, int64_t pr,
+                                 int64_t sh, int64_t sw, bool stats) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() == 4 &&
+                  (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat),
+              "stem: x must be a contiguous NHWC bf16/f32 GPU tensor");
+  conv_check(w_hwio, "w");
+  TORCH_CHECK(w_hwio.dim() == 4 && w_hwio.size(2) == x.size(3), "stem: weights must be HWIO [KH,KW,C,K]");
+  const int N = (int)x.size(0), H = (int)x.size(1), W = (int)x.size(2), C = (int)x.size(3);
+  const int KH = (int)w_hwio.size(0), KW = (int)w_hwio.size(1), K = (int)w_hwio.size(3);
+  TORCH_CHECK(tdl::stem_supported(C, KH, KW, (int)sw, K) && sh >= 1 && pt >= 0 && pb >= 0 && pl >= 0 && pr >= 0,
+              "stem: unsupported geometry");
+  const int HP = H + (int)(pt + pb), WPv = W + (int)(pl + pr);
+  const int OH = (HP - KH) / (int)sh + 1, OW = (WPv - KW) / 2 + 1;
+  TORCH_CHECK(OH > 0 && OW > 0, "stem: empty output");
+  // packed width: every receptive field reads 8 columns (taps past KW are zero-weighted): 2(OW-1)+8
+  const int WP = std::max(WPv, 2 * (OW - 1) + 8);
+  const int HPp = std::max(HP, (OH - 1) * (int)sh + KH);
+  TORCH_CHECK((long long)N * HPp * WP * 4 < (1LL << 31), "stem: packed image too large");
+  auto xp = at::empty({N, HPp, WP, 4}, x.options().dtype(at::kBFloat16));
+  tdl::stem_pack(x.data_ptr(), x.scalar_type() == at::kBFloat16, xp.data_ptr(), N, H, W, C, HPp, WP, (int)pt, (int)pl,
+                 cur_stream());
+  auto wp = at::empty({K, KH, 32}, w_hwio.options());
+  tdl::stem_wpack(w_hwio.data_ptr(), wp.data_ptr(), KH, KW, C, K, cur_stream());
+  auto y = at::empty({N, OH, OW, K}, x.options().dtype(at::kBFloat16));
+  const int64_t M = (int64_t)N * OH * OW, bm = tdl::stem_fwd_row_tile(), P = (M + bm - 1) / bm;
+  at::Tensor part;
+  if (stats) part = fresh({P + (P + 63) / 64, 2, (int64_t)K}, x.options().dtype(at::kFloat));
+  tdl::stem_fwd(xp.data_ptr(), wp.data_ptr(), y.data_ptr(), stats ? part.data_ptr<float>() : nullptr, N, HPp, WP, OH,
+                OW, K, KH, (int)sh, cur_stream());
+  if (stats) return {y, xp, part};
+  return {y, xp};
+}
+
+// weight gradient of stem_fwd from its packed image: dW HWIO [KH,KW,C,K] bf16, or added into the f32
+// `out` (accumulate) / written to it
+at::Tensor stem_wgrad(at::Tensor xp, at::Tensor dy, int64_t kh, int64_t kw, int64_t c, int64_t sh,
+                      c10::optional<at::Tensor> out, bool accumulate) {
+  conv_check(xp, "xp");
+  conv_check(dy, "dy");
+  TORCH_CHECK(xp.dim() == 4 && xp.size(3) == 4 && dy.dim() == 4 && dy.size(0) == xp.size(0), "stem_wgrad: shapes");
+  const int N = (int)xp.size(0), HP = (int)xp.size(1), WP = (int)xp.size(2);
+  const int OH = (int)dy.size(1), OW = (int)dy.size(2), K = (int)dy.size(3);
+  TORCH_CHECK(tdl::stem_supported((int)c, (int)kh, (int)kw, 2, K) && (OH - 1) * sh + kh <= HP &&
+                  2 * (OW - 1) + 8 <= WP,
+              "stem_wgrad: geometry inconsistent with the packed image");
+  const int M = N * OH * OW;
+  auto ws = at::empty({tdl::stem_wgrad_ws_elems(M, K, (int)kh)}, dy.options().dtype(at::kFloat));
+  if (out.has_value()) {
+    auto& o = *out;
+    TORCH_CHECK(o.is_cuda() && o.is_contiguous() && o.scalar_type() == at::kFloat && o.numel() == kh * kw * c * K,
+                "stem_wgrad: out must be a contiguous f32 tensor of KH*KW*C*K elements");
+    tdl::stem_wgrad(xp.data_ptr(), dy.data_ptr(), ws.data_ptr<float>(), N, HP, WP, OH, OW, K, (int)kh, (int)kw, (int)c,
+                    (int)sh, o.data_ptr<float>(), nullptr, accumulate, cur_stream());
+    return o;
+  }
+  auto dw = at::empty({kh, kw, c, (int64_t)K}, dy.options());
+  tdl::stem_wgrad(xp.data_ptr(), dy.data_ptr(), ws.data_ptr<float>(), N, HP, WP, OH, OW, K, (int)kh, (int)kw, (int)c,
+                  (int)sh, nullptr, dw.data_ptr(), false, cur_stream());
   return dw;
 }
 
@@ -466,7 +585,14 @@ void register_ops(pybind11::module& m) {
   m.def("slab_cast_bf16", &slab_cast_bf16, "f32 -> bf16 copy of a whole weight slab (one launch)");
   m.def("bn_set_tuning", &tdl::bn_set_tuning, "BN kernel sweep hooks (max_parts, elem_blocks, elem_unroll; 0 = keep)");
   m.def("slab_transpose_bf16", &slab_transpose_bf16, "HWIO f32 conv kernels -> OHWI bf16, all in one launch");
-  m.def("conv_dgrad_bn", &conv_dgrad_bn, "stride-1 conv input gradient + fused BN->Add->ReLU backward (dz, part)");
+  m.def("conv_dgrad_bn", &conv_dgrad_bn, "stride-1 conv input gradient + fused BN->Add->ReLU backward (dz, part[, part2])",
+        pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("h"), pybind11::arg("wd"), pybind11::arg("pt"),
+        pybind11::arg("pl"), pybind11::arg("residual"), pybind11::arg("bn_y"), pybind11::arg("bn_x"),
+        pybind11::arg("bn_x2") = pybind11::none());
+  m.def("conv_dgrad_s2_bn", &conv_dgrad_s2_bn,
+        "1x1 stride-2 conv input gradient + fused BN->Add->ReLU backward (dz, part[, part2])", pybind11::arg("dy"),
+        pybind11::arg("w"), pybind11::arg("h"), pybind11::arg("wd"), pybind11::arg("residual"), pybind11::arg("bn_y"),
+        pybind11::arg("bn_x"), pybind11::arg("bn_x2") = pybind11::none());
   m.def("conv_dgrad_s2", &conv_dgrad_s2, "NHWC bf16 1x1 stride-2 convolution input gradient (MFMA)",
         pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("h"), pybind11::arg("wd"),
         pybind11::arg("residual") = pybind11::none());
@@ -477,6 +603,12 @@ void register_ops(pybind11::module& m) {
   m.def("conv_wgrad_plans", &conv_wgrad_plans, "weight-gradient candidate plans, best first: [[wmw, wnw, chunk, nsplit]]");
   m.def("conv_force_tile", &tdl::conv_force_tile, "conv tile sweep hook (0 = heuristic)");
   m.def("conv_force_depth", &tdl::conv_force_depth, "conv main-loop prefetch depth A/B hook (1 or 2)");
+  m.def("stem_fwd", &stem_fwd, "small-channel stride-2 conv (ResNet stem): (y, packed x[, BN part])",
+        pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("pt"), pybind11::arg("pb"), pybind11::arg("pl"),
+        pybind11::arg("pr"), pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("stats") = false);
+  m.def("stem_wgrad", &stem_wgrad, "stem conv weight gradient from the packed image", pybind11::arg("xp"),
+        pybind11::arg("dy"), pybind11::arg("kh"), pybind11::arg("kw"), pybind11::arg("c"), pybind11::arg("sh"),
+        pybind11::arg("out") = pybind11::none(), pybind11::arg("accumulate") = false);
   m.def("conv_fwd", &conv_fwd, "NHWC bf16 implicit-GEMM convolution forward (MFMA)");
   m.def("conv_fwd_stats", &conv_fwd_stats, "conv forward + batch-norm partial channel sums of its output");
   m.def("conv_dgrad", &conv_dgrad, "NHWC bf16 implicit-GEMM stride-1 convolution input gradient (MFMA)",

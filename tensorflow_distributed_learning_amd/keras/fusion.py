@@ -14,6 +14,8 @@ list; the plan rewrites, at execution time only (the layer graph, variables, che
 * ``BatchNormalization -> Add(other) -> ReLU``: the ResNet block tail, one fused pass that also
   produces the residual's gradient.
 * ``ZeroPadding2D -> MaxPooling2D('valid')``: one pooling pass with implicit zero padding.
+* ``ZeroPadding2D -> Conv2D`` with <= 4 input channels, 'valid', column stride 2 (the ResNet stem):
+  the padding goes into the stem kernel's packed image (ops/conv.py ``stem_conv2d_nhwc``).
 * a tensor read by a Conv2D and by one other node (the ResNet block input: the shortcut / the
   residual of the block tail, and the first 1x1 conv): the two backward contributions meet in a
   ``GradBox`` (ops/conv.py) and the conv's input-gradient kernel adds the other one in its
@@ -33,14 +35,19 @@ from . import layers as L
 
 
 class Group:
-    __slots__ = ("bn_node", "relu", "residual", "conv_layer", "out", "last", "conv_reader")
+    __slots__ = ("bn_node", "relu", "residual", "conv_layer", "out", "last", "conv_reader", "add_node", "res_bn")
 
-    def __init__(self, bn_node, relu, residual, conv_layer, out, last, conv_reader=False):
+    def __init__(self, bn_node, relu, residual, conv_layer, out, last, conv_reader=False, add_node=None):
         self.bn_node, self.relu, self.residual, self.conv_layer, self.out, self.last = (
             bn_node, relu, residual, conv_layer, out, last)
         # BN -> ReLU whose output is read by exactly one Conv2D: that conv's input gradient is the
         # group's whole output gradient, so its epilogue can run the group's backward reduction
         self.conv_reader = conv_reader
+        self.add_node = add_node  # the absorbed Add of a BN -> Add -> ReLU group
+        # the plain BN group (a projection shortcut's BN) whose output is this group's residual and
+        # is read by nothing else: its output gradient is this group's dz, so the conv epilogue that
+        # reduces this group's backward sums can reduce that BN's as well
+        self.res_bn = None
 
 
 class Plan:
@@ -48,7 +55,7 @@ class Plan:
         self.skip = set()        # node ids absorbed into a group that runs elsewhere
         self.conv_nobias = set()  # conv node ids whose bias is folded into their BN
         self.groups: Dict[int, Group] = {}  # id(last node) -> group
-        self.pool_pad: Dict[int, tuple] = {}  # id(max-pool node) -> (padding input, padding)
+        self.pool_pad: Dict[int, tuple] = {}  # id(max-pool / stem conv node) -> (padding input, padding)
         self.conv_box: Dict[int, int] = {}   # id(conv node) -> id(input tensor) of its GradBox
         self.taps: Dict[int, set] = {}       # id(node or group last node) -> ids of inputs read through a tap
 
@@ -92,6 +99,15 @@ def plan(nodes: List[L.Node], outputs) -> Plan:
             if prod is not None and isinstance(prod.layer, L.ZeroPadding2D) and only_consumer(x_t) is n:
                 p.pool_pad[id(n)] = (prod.inputs, prod.layer.padding)
                 p.skip.add(id(prod))
+    for n in nodes:  # ZeroPadding2D -> small-channel stride-2 'valid' Conv2D (the stem): padding folded in
+        if isinstance(n.layer, L.Conv2D) and n.layer.padding == "valid" and n.layer.strides[1] == 2 and \
+                n.layer.groups == 1 and tuple(n.layer.dilation_rate) == (1, 1) and max(n.layer.kernel_size) <= 8:
+            x_t = _single_tensor(n.inputs)
+            prod = producer.get(id(x_t)) if x_t is not None else None
+            if prod is not None and isinstance(prod.layer, L.ZeroPadding2D) and only_consumer(x_t) is n and \
+                    x_t.shape[-1] is not None and int(x_t.shape[-1]) <= 4:
+                p.pool_pad[id(n)] = (prod.inputs, prod.layer.padding)
+                p.skip.add(id(prod))
     for n in nodes:
         bn = n.layer
         if not (isinstance(bn, L.BatchNormalization) and bn.trainable and bn.axis in (-1, 3)):
@@ -106,7 +122,7 @@ def plan(nodes: List[L.Node], outputs) -> Plan:
                 prod.layer.activation is A.linear and prod.layer.trainable and only_consumer(x_t) is n:
             conv_layer = prod.layer
             p.conv_nobias.add(id(prod))
-        relu, residual, last, out = False, None, n, out_t
+        relu, residual, last, out, add_node = False, None, n, out_t, None
         c1 = only_consumer(out_t)
         if c1 is not None and _is_plain_relu(c1.layer):
             relu, last, out = True, c1, _single_tensor(c1.outputs)
@@ -117,13 +133,19 @@ def plan(nodes: List[L.Node], outputs) -> Plan:
             other = c1.inputs[1] if c1.inputs[0] is out_t else c1.inputs[0]
             if c2 is not None and _is_plain_relu(c2.layer) and other is not out_t and \
                     tuple(other.shape) == tuple(out_t.shape):
-                relu, residual, last, out = True, other, c2, _single_tensor(c2.outputs)
+                relu, residual, last, out, add_node = True, other, c2, _single_tensor(c2.outputs), c1
                 p.skip.add(id(c1))
         if last is not n:
             p.skip.add(id(n))
         reader = only_consumer(out) if relu and residual is None else None
         conv_reader = reader is not None and isinstance(reader.layer, L.Conv2D) and reader.inputs is out
-        p.groups[id(last)] = Group(n, relu, residual, conv_layer, out, last, conv_reader)
+        p.groups[id(last)] = Group(n, relu, residual, conv_layer, out, last, conv_reader, add_node)
+    by_out = {id(g.out): g for g in p.groups.values()}
+    for g in p.groups.values():
+        pg = by_out.get(id(g.residual)) if g.residual is not None else None
+        if pg is not None and not pg.relu and pg.residual is None and pg.last is pg.bn_node and \
+                only_consumer(g.residual) is g.add_node:
+            g.res_bn = pg
     if os.environ.get("TDL_FUSE_GRAD_SUM", "1") == "1":
         _plan_grad_sums(p, nodes, consumers, outs)
     return p
@@ -189,4 +211,6 @@ def run_group(g: Group, vals, training, taps=None, boxes=None):
         # a conv reading this group's output can fuse the group's backward reduction into its
         # input-gradient epilogue (ops/conv.py): it needs the BN input
         y._tdl_bn_src = x
+        if g.res_bn is not None:
+            y._tdl_bn_src2 = vals[id(g.res_bn.bn_node.inputs)]
     vals[id(g.out)] = y

@@ -322,10 +322,27 @@ class Conv2D(Layer):
                                     regularizer=self.bias_regularizer) if self.use_bias else None
         self.built = True
 
-    def call(self, x, training=None, _fold_bias=False, _grad_box=None, _bn_stats=False):
+    def call(self, x, training=None, _fold_bias=False, _grad_box=None, _bn_stats=False, _zero_pad=None):
         """``_fold_bias``: the functional executor folded this bias into the following training-mode
         BatchNormalization (keras/fusion.py), so the convolution runs without it.  ``_grad_box``:
-        the input's other consumer's gradient is summed into this conv's input gradient."""
+        the input's other consumer's gradient is summed into this conv's input gradient.
+        ``_zero_pad``: ((top, bottom), (left, right)) of a ZeroPadding2D folded in front (a <= 4-channel
+        stride-2 'valid' conv: the ResNet stem, csrc/kernels/stem.hip)."""
+        if _zero_pad is not None:
+            (pt, pb), (pl, pr) = _zero_pad
+            if self.padding == "valid" and _conv.stem_supported(x, self.kernel.value, self.strides, self.groups,
+                                                                self.dilation_rate):
+                gt = self.kernel.grad_target()
+                k_hwio = (self.kernel.compute_view(torch.bfloat16) if gt is not None else None)
+                if k_hwio is None:
+                    k_hwio = self.kernel.value.detach().to(torch.bfloat16) if gt is not None else \
+                        self.kernel.cast(torch.bfloat16)
+                y = _conv.stem_conv2d_nhwc(x, k_hwio, (pt, pb, pl, pr), self.strides, grad_out=gt, bn_stats=_bn_stats,
+                                           anchor=self.kernel.value if gt is not None else None)
+                if self.bias is not None and not _fold_bias:
+                    y = y + self.bias.value.to(y.dtype)
+                return self.activation(y)
+            x = F.pad(x, (0, 0, pl, pr, pt, pb))
         # (1x1 convs stay on MIOpen: routing them through hipBLASLt GEMMs measured slower on MI355X,
         #  scripts/probe_1x1_gemm.py)
         gt = None
@@ -358,7 +375,8 @@ class Conv2D(Layer):
             # hand-written implicit-GEMM MFMA kernels (csrc/kernels/conv.hip), autotuned against MIOpen
             y = _conv.conv2d_nhwc(x, k_hwio, self.strides, pad if pad else (0, 0), grad_out=gt,
                                   w_ohwi=self.kernel.compute_view_ohwi(x.dtype) if gt is not None else None,
-                                  grad_box=_grad_box, bn_stats=_bn_stats, bn_src=getattr(x, "_tdl_bn_src", None))
+                                  grad_box=_grad_box, bn_stats=_bn_stats, bn_src=getattr(x, "_tdl_bn_src", None),
+                                  bn_src2=getattr(x, "_tdl_bn_src2", None))
             if b is not None:
                 y = y + b
             return self.activation(y)

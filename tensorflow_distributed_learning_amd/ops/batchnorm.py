@@ -26,6 +26,7 @@ from . import hip
 
 
 FUSED_BWD = [0]  # backward calls that took their reduction from a conv epilogue (tests)
+FUSED_BWD_MODES = {0: 0, 1: 0, 2: 0}  # the same, by mode (0 plain, 1 relu, 2 add+relu)
 
 
 def supported(x: torch.Tensor) -> bool:
@@ -74,7 +75,10 @@ class _BatchNormTrain(torch.autograd.Function):
         C = hip()
         xc, gamma, st, y, conv_bias = ctx.saved_tensors
         has_g, has_b, has_r, has_cb = ctx.flags
-        part = getattr(dy, "_tdl_bn_bwd_part", None) if ctx.mode >= 1 else None
+        # precomputed reductions (ops/conv.py): a group's from the consuming conv's input-gradient
+        # epilogue; a plain BN's (mode 0) when its output gradient is such a group's dz
+        part = getattr(dy, "_tdl_bn_bwd_part", None)
+        part2 = getattr(dy, "_tdl_bn_bwd_part2", None) if ctx.mode == 2 else None
         dy = _aligned(dy.to(xc.dtype))
         go = ctx.grad_out or (None, None)
         fused = part is not None and dy.dtype == xc.dtype and dy.is_contiguous() and dy.data_ptr() % 16 == 0
@@ -82,12 +86,20 @@ class _BatchNormTrain(torch.autograd.Function):
         if fused:
             # dy is already this group's masked dz, reduced by the consuming conv's dgrad epilogue
             FUSED_BWD[0] += 1
+            FUSED_BWD_MODES[ctx.mode] += 1
             out = C.bn_backward(dy, xc, None, gamma if has_g else None, st, ctx.mode, go[0], go[1], part)
         else:
             out = C.bn_backward(dy, xc, y if ctx.mode == 2 else None, gamma if has_g else None, st, ctx.mode,
                                 go[0], go[1])
         dx, dgamma, dbeta = out[0], out[1], out[2]
         dres = out[3].to(ctx.res_dtype) if has_r else None
+        if fused and dres is not None:
+            # dres IS dy here, which carries this group's own part: hand the residual's producer a
+            # fresh view, with the sums the conv epilogue reduced for it (a plain projection-shortcut
+            # BN: part2) or none
+            dres = dres.view_as(dres)
+            if part2 is not None:
+                dres._tdl_bn_bwd_part = part2
         dcb = torch.zeros_like(conv_bias) if (has_cb and ctx.needs_input_grad[4]) else None
         return (dx, dgamma if ctx.needs_input_grad[1] else None, dbeta if ctx.needs_input_grad[2] else None, dres,
                 dcb, None, None, None, None, None, None, None)

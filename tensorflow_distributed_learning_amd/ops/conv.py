@@ -22,6 +22,10 @@ import torch.nn.functional as F
 from . import hip
 
 _FUSE_BN_BWD = [os.environ.get("TDL_FUSE_BN_BWD", "1") == "1"]
+# the two extensions of that fusion, separately switchable: the 1x1 stride-2 input gradient's epilogue,
+# and the projection-shortcut BN's sums (part2) beside the block-output group's
+_FUSE_BN_BWD_S2 = [os.environ.get("TDL_FUSE_BN_BWD_S2", "1") == "1"]
+_FUSE_BN_BWD_SHORTCUT = [os.environ.get("TDL_FUSE_BN_BWD_SHORTCUT", "1") == "1"]
 _choice: dict = {}  # (direction, shape key) -> True (hand-written kernel) / False (MIOpen)
 _times: dict = {}  # (direction, shape key) -> (hand-written ms, MIOpen ms) as measured by the autotuner
 
@@ -155,7 +159,8 @@ def _ref_fwd(x, w_oihw, stride, pad):
 
 class _Conv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, kernel, stride, pad, grad_out, w_ohwi=None, box=None, stats_out=None, bn_src=None):
+    def forward(ctx, x, kernel, stride, pad, grad_out, w_ohwi=None, box=None, stats_out=None, bn_src=None,
+                bn_src2=None):
         C = hip()
         x = x.contiguous()
         if x.data_ptr() % 16:
@@ -184,6 +189,8 @@ class _Conv(torch.autograd.Function):
         ctx.box = box
         ctx.bn_src = bn_src if (bn_src is not None and tuple(bn_src.shape) == tuple(x.shape)
                                 and bn_src.dtype == x.dtype) else None
+        ctx.bn_src2 = bn_src2 if (ctx.bn_src is not None and bn_src2 is not None
+                                  and tuple(bn_src2.shape) == tuple(x.shape) and bn_src2.dtype == x.dtype) else None
         if box is not None:
             box.n += 1
         return y
@@ -230,8 +237,8 @@ class _Conv(torch.autograd.Function):
             # the BN group reduction a read of dz, x, y and a write of dz
             # the BN-group fusion needs the complete gradient of x: the second GradBox participant,
             # or the only reader of x (no box)
-            fuse_bn = (ctx.bn_src is not None and (other is not None or ctx.box is None) and stride == (1, 1)
-                       and _FUSE_BN_BWD[0])
+            fuse_bn = (ctx.bn_src is not None and (other is not None or ctx.box is None) and hip_fn is not None
+                       and _FUSE_BN_BWD[0] and (stride == (1, 1) or _FUSE_BN_BWD_S2[0]))
             dx_bytes = x.numel() * x.element_size()
             saved = (2 * dx_bytes if other is not None else 0) + (2 * dx_bytes if fuse_bn else 0)
             key = (key + (other is not None, fuse_bn)) if hip_fn is not None else None
@@ -239,12 +246,22 @@ class _Conv(torch.autograd.Function):
                 src = ctx.bn_src
                 if fuse_bn:
                     # full gradient of the BN (-> Add) -> ReLU group output x: mask it and reduce it for
-                    # the group's BN backward in the same epilogue (ops/batchnorm.py uses the part)
-                    src = src.contiguous()
-                    if src.data_ptr() % 16:
-                        src = src.clone()
-                    dx, part = C.conv_dgrad_bn(dy, kc, x.shape[1], x.shape[2], pad[0], pad[1], other, x, src)
-                    dx._tdl_bn_bwd_part = part
+                    # the group's BN backward in the same epilogue (ops/batchnorm.py uses the part);
+                    # with bn_src2 also the reduction of the projection-shortcut BN feeding its Add
+                    src, src2 = _aligned(src), ctx.bn_src2 if _FUSE_BN_BWD_SHORTCUT[0] else None
+                    src2 = _aligned(src2) if src2 is not None else None
+                    if stride == (1, 1):
+                        out = C.conv_dgrad_bn(dy, kc, x.shape[1], x.shape[2], pad[0], pad[1], other, x, src, src2)
+                    else:
+                        out = C.conv_dgrad_s2_bn(dy, kc, x.shape[1], x.shape[2], other, x, src, src2)
+                    dx = out[0]
+                    dx._tdl_bn_bwd_part = out[1]
+                    if src2 is not None:
+                        dx._tdl_bn_bwd_part2 = out[2]
+                    if _DEBUG_PARTS:
+                        _check_parts(dx, src, out[1], "part")
+                        if src2 is not None:
+                            _check_parts(dx, src2, out[2], "part2")
                 else:
                     dx = hip_fn(other)
                 other = None
@@ -272,7 +289,30 @@ class _Conv(torch.autograd.Function):
             dx = dx + other.view_as(dx)
         if first:  # park this contribution for the other consumer's backward
             box.g, dx = dx, None
-        return dx, dw, None, None, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None, None, None
+
+
+_DEBUG_PARTS = os.environ.get("TDL_DEBUG_BN_PARTS") == "1"
+
+
+def _check_parts(dz, xb, part, what):
+    """TDL_DEBUG_BN_PARTS=1: an epilogue's BN sums vs PyTorch over the tensors (stderr)."""
+    import sys
+
+    C = dz.shape[-1]
+    P = part.shape[0]
+    while P > 1 and (P - 1) + (P - 1 + 63) // 64 >= part.shape[0]:
+        P -= 1
+    got = part[:P].double().sum(0)
+    d, x = dz.double().reshape(-1, C), xb.double().reshape(-1, C)
+    ref = torch.stack([d.sum(0), (d * x).sum(0)])
+    err = ((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30)).item()
+    print(f"[tdl parts] {what} {tuple(dz.shape)} rows {P}/{part.shape[0]} rel err {err:.3g}", file=sys.stderr, flush=True)
+
+
+def _aligned(t):
+    t = t.contiguous()
+    return t.clone() if t.data_ptr() % 16 else t
 
 
 def _miopen_bwd(dy_nchw, x_nchw, w_oihw, stride, pad, mask):
@@ -282,7 +322,7 @@ def _miopen_bwd(dy_nchw, x_nchw, w_oihw, stride, pad, mask):
 
 
 def conv2d_nhwc(x, kernel_hwio, stride=(1, 1), pad=(0, 0), grad_out=None, w_ohwi=None, grad_box=None,
-                bn_stats=False, bn_src=None):
+                bn_stats=False, bn_src=None, bn_src2=None):
     """y[N,OH,OW,K] = conv(x[N,H,W,C], kernel[KH,KW,C,K]) with symmetric zero padding ``pad = (ph, pw)``,
     bf16; the caller checked :func:`supported`.  ``grad_out``: f32 [KH,KW,C,K] tensor the weight
     gradient is added into (a trainer's gradient slab view; ``kernel_hwio`` then needs no autograd);
@@ -292,9 +332,71 @@ def conv2d_nhwc(x, kernel_hwio, stride=(1, 1), pad=(0, 0), grad_out=None, w_ohwi
     ``y._tdl_bn_part`` for the BN that consumes it (ops/batchnorm.py skips its statistics pass);
     ``bn_src``: x is the output relu(bn(bn_src) + r) of a fused BN group; when this conv's input
     gradient is the complete gradient of x (second GradBox participant), its epilogue also applies
-    the group's ReLU mask and reduces the group's BN backward sums."""
+    the group's ReLU mask and reduces the group's BN backward sums; ``bn_src2``: the input of the
+    plain (projection-shortcut) BN whose output is that group's residual: the same epilogue reduces
+    its backward sums too."""
     holder = [None] if bn_stats else None
-    y = _Conv.apply(x, kernel_hwio, tuple(stride), tuple(pad), grad_out, w_ohwi, grad_box, holder, bn_src)
+    y = _Conv.apply(x, kernel_hwio, tuple(stride), tuple(pad), grad_out, w_ohwi, grad_box, holder, bn_src, bn_src2)
+    if holder is not None and holder[0] is not None:
+        y._tdl_bn_part = holder[0]
+    return y
+
+
+def stem_supported(x: torch.Tensor, kernel_hwio: torch.Tensor, strides, groups=1, dilation=(1, 1)) -> bool:
+    """The small-channel stride-2 kernel (csrc/kernels/stem.hip): the ResNet stem, 3 -> 64 channels."""
+    kh, kw, cin, cout = kernel_hwio.shape
+    return (x.is_cuda and x.dtype in (torch.bfloat16, torch.float32) and x.dim() == 4 and groups == 1
+            and tuple(dilation) == (1, 1) and x.shape[-1] == cin and 1 <= cin <= 4 and 1 <= kh <= 8 and 1 <= kw <= 8
+            and int(strides[1]) == 2 and cout % 64 == 0 and mode() != "miopen")
+
+
+class _Stem(torch.autograd.Function):
+    """Small-channel stride-2 conv with its zero padding folded in (stem.hip): forward on the packed
+    NHWC4 image (kept for the weight gradient), weight gradient on MFMA with transposed LDS reads."""
+
+    @staticmethod
+    def forward(ctx, x, kernel, pads, stride, grad_out, holder, anchor=None):
+        C = hip()
+        x = _aligned(x)
+        kc = _aligned(kernel.to(torch.bfloat16))
+        out = C.stem_fwd(x, kc, pads[0], pads[1], pads[2], pads[3], stride[0], stride[1], holder is not None)
+        if holder is not None:
+            holder[0] = out[2]
+        ctx.save_for_backward(out[1], kernel, x if ctx.needs_input_grad[0] else None)
+        ctx.geo = (pads, stride)
+        ctx.grad_out = grad_out
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = hip()
+        xp, kernel, x = ctx.saved_tensors
+        pads, stride = ctx.geo
+        dy = _aligned(dy.to(torch.bfloat16))
+        kh, kw, cin, _ = kernel.shape
+        dw = dx = None
+        if ctx.grad_out is not None:  # f32 slab view: dW added straight into it
+            C.stem_wgrad(xp, dy, kh, kw, cin, stride[0], out=ctx.grad_out, accumulate=True)
+        elif ctx.needs_input_grad[1]:
+            dw = C.stem_wgrad(xp, dy, kh, kw, cin, stride[0]).to(kernel.dtype)
+        if ctx.needs_input_grad[0]:  # image gradient (not needed for training): library path
+            xpad = F.pad(x, (0, 0, pads[2], pads[3], pads[0], pads[1]))
+            w_oihw = kernel.to(dy.dtype).permute(3, 2, 0, 1)
+            g = _miopen_bwd(dy.permute(0, 3, 1, 2), xpad.to(dy.dtype).permute(0, 3, 1, 2), w_oihw, list(stride),
+                            [0, 0], [True, False, False])[0].permute(0, 2, 3, 1)
+            dx = g[:, pads[0]:g.shape[1] - pads[1], pads[2]:g.shape[2] - pads[3], :].to(x.dtype)
+        return dx, dw, None, None, None, None, None
+
+
+def stem_conv2d_nhwc(x, kernel_hwio, pads, stride, grad_out=None, bn_stats=False, anchor=None):
+    """y = conv(zero_pad(x, pads = (top, bottom, left, right)), kernel_hwio) for a <= 4-channel image,
+    column stride 2 (:func:`stem_supported`); ``grad_out`` / ``bn_stats`` as for :func:`conv2d_nhwc`.
+    ``anchor``: with ``grad_out``, the variable's leaf tensor, so that the backward runs although
+    neither the image nor the detached compute-dtype kernel needs a gradient (its gradient goes
+    into ``grad_out``; the anchor itself gets none)."""
+    holder = [None] if bn_stats else None
+    y = _Stem.apply(x, kernel_hwio, tuple(int(p) for p in pads), tuple(int(s) for s in stride), grad_out, holder,
+                    anchor)
     if holder is not None and holder[0] is not None:
         y._tdl_bn_part = holder[0]
     return y

@@ -39,6 +39,10 @@ def test_plan_shapes_resnet50():
     assert len(p.groups) == 53 and len(p.conv_nobias) == 53
     assert sum(g.residual is not None for g in p.groups.values()) == 16
     assert sum(g.relu and g.residual is None for g in p.groups.values()) == 33
+    # the 4 conv blocks: the block-output group also reduces its projection-shortcut BN's backward
+    res_bn = [g for g in p.groups.values() if g.res_bn is not None]
+    assert len(res_bn) == 4
+    assert all(not g.res_bn.relu and g.res_bn.residual is None for g in res_bn)
 
 
 def _run(m, x, fuse):

@@ -85,11 +85,19 @@ def test_direct_slab_gradients_match_autograd_accumulation():
 
 def test_fused_gradient_sums_match_autograd_adds():
     """Tensors read by a conv and one other node: the conv's input-gradient epilogue adds the other
-    contribution (keras/fusion.py grad boxes) instead of autograd's separate add."""
-    mf, hf = _train(True, grad_sum=True)
-    boxes = mf.__dict__["_grad_boxes"]
-    assert len(boxes) == 2 and all(b.n == 2 and b.g is None for b in boxes.values())
-    mu, hu = _train(True, grad_sum=False)
+    contribution (keras/fusion.py grad boxes) instead of autograd's separate add.  (The BN-group
+    reductions stay in the BN's own pass in both runs: reduced in the epilogue, their f32 summation
+    order differs, and bf16 activations turn that into visible weight differences after two steps.)"""
+    from tensorflow_distributed_learning_amd.ops import conv as CV
+
+    CV._FUSE_BN_BWD[0] = False
+    try:
+        mf, hf = _train(True, grad_sum=True)
+        boxes = mf.__dict__["_grad_boxes"]
+        assert len(boxes) == 2 and all(b.n == 2 and b.g is None for b in boxes.values())
+        mu, hu = _train(True, grad_sum=False)
+    finally:
+        CV._FUSE_BN_BWD[0] = True
     assert not mu.__dict__["_grad_boxes"]
     for v, a, b in zip(mf.weights, mf.get_weights(), mu.get_weights()):
         scale = max(float(np.abs(b).max()), 1e-3)
@@ -184,3 +192,108 @@ def test_fused_bn_group_backward_in_conv_epilogue():
         scale = max(float(np.abs(b).max()), 1e-3)
         np.testing.assert_allclose(a, b, atol=2e-2 * scale, rtol=2e-2, err_msg=v.name)
     np.testing.assert_allclose(hf.history["loss"], hu.history["loss"], rtol=1e-2)
+
+
+def test_fused_bn_backward_projection_shortcut_and_stride2():
+    """ResNet conv blocks: the projection-shortcut BN's backward sums come from the same conv
+    epilogue as the block output group's (part2), and a group read by two 1x1 stride-2 convs (the
+    next stage's conv block) is reduced in the stride-2 input-gradient epilogue; training matches
+    the unfused path."""
+    from tensorflow_distributed_learning_amd.ops import batchnorm as B
+    from tensorflow_distributed_learning_amd.ops import conv as CV
+
+    L = tdl.keras.layers
+
+    def bn_relu(t):
+        return L.Activation("relu")(L.BatchNormalization()(t))
+
+    def block(x, s=1, project=False):
+        y = bn_relu(L.Conv2D(64, 1, strides=s)(x))
+        y = bn_relu(L.Conv2D(64, 3, padding="same")(y))
+        y = L.BatchNormalization()(L.Conv2D(128, 1)(y))
+        sc = L.BatchNormalization()(L.Conv2D(128, 1, strides=s)(x)) if project else x
+        return L.Activation("relu")(L.Add()([y, sc]))
+
+    def model():
+        tdl.keras.utils.set_random_seed(11)
+        inp = L.Input(shape=(8, 8, 64))
+        x = bn_relu(L.Conv2D(64, 3, padding="same")(inp))
+        x = block(x, 1, True)
+        x = block(x)
+        x = block(x, 2, True)
+        x = block(x)
+        x = L.GlobalAveragePooling2D()(x)
+        return tdl.keras.Model(inp, L.Dense(16)(x))
+
+    def run(fuse):
+        CV._FUSE_BN_BWD[0] = fuse
+        old = {k: os.environ.get(k) for k in ("TDL_GRAPH_STEP", "TDL_CONV")}
+        os.environ.update({"TDL_GRAPH_STEP": "0", "TDL_CONV": "hip"})
+        try:
+            tdl.keras.backend.clear_session()
+            tdl.keras.mixed_precision.set_global_policy("mixed_bfloat16")
+            g = torch.Generator().manual_seed(0)
+            ds = tdl.data.Dataset.from_tensor_slices((torch.rand(128, 8, 8, 64, generator=g),
+                                                      torch.randint(0, 16, (128,), generator=g))).batch(32).repeat()
+            with tdl.distribute.MirroredStrategy(devices=["/gpu:0"]).scope():
+                m = model()
+                m.compile(loss=tdl.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+                          optimizer=tdl.keras.optimizers.SGD(learning_rate=0.05, momentum=0.9))
+            n0 = dict(B.FUSED_BWD_MODES)
+            h = m.fit(ds, epochs=1, steps_per_epoch=2, verbose=0)
+            return m, h, {k: B.FUSED_BWD_MODES[k] - n0[k] for k in n0}
+        finally:
+            CV._FUSE_BN_BWD[0] = True
+            tdl.keras.mixed_precision.set_global_policy("float32")
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+
+    mf, hf, nf = run(True)
+    mu, hu, nu = run(False)
+    # per step: both shortcut BNs (mode 0); the outputs of blocks 1-3 (block 2's is read by the two
+    # stride-2 convs of block 3); the 8 inner BN -> ReLU groups.  Two steps.
+    assert nf == {0: 4, 1: 16, 2: 6}, nf
+    assert nu == {0: 0, 1: 0, 2: 0}, nu
+    for v, a, b in zip(mf.weights, mf.get_weights(), mu.get_weights()):
+        scale = max(float(np.abs(b).max()), 1e-3)
+        np.testing.assert_allclose(a, b, atol=2e-2 * scale, rtol=2e-2, err_msg=v.name)
+    np.testing.assert_allclose(hf.history["loss"], hu.history["loss"], rtol=1e-2)
+
+
+def test_conv_dgrad_s2_bn_epilogue_matches_reference():
+    """conv_dgrad_s2_bn / conv_dgrad_bn with bn_x2: dz and every partial-sum row vs fp32 PyTorch."""
+    from tensorflow_distributed_learning_amd.ops import hip
+
+    C = hip()
+    g = torch.Generator(device="cpu").manual_seed(3)
+    N, H, W, Ci, K = 4, 14, 14, 128, 256
+    for s2 in (True, False):
+        k = (torch.randn(1 if s2 else 3, 1 if s2 else 3, Ci, K, generator=g) * 0.05).cuda().bfloat16()
+        OH = 7 if s2 else H
+        dy = torch.randn(N, OH, OH, K, generator=g).cuda().bfloat16()
+        r = torch.randn(N, H, W, Ci, generator=g).cuda().bfloat16()
+        by = torch.randn(N, H, W, Ci, generator=g).cuda().bfloat16()
+        bx = torch.randn(N, H, W, Ci, generator=g).cuda().bfloat16()
+        bx2 = torch.randn(N, H, W, Ci, generator=g).cuda().bfloat16()
+        if s2:
+            base = C.conv_dgrad_s2(dy, k, H, W, r)
+            dz, part, part2 = C.conv_dgrad_s2_bn(dy, k, H, W, r, by, bx, bx2)
+        else:
+            base = C.conv_dgrad(dy, k, H, W, 1, 1, r)
+            dz, part, part2 = C.conv_dgrad_bn(dy, k, H, W, 1, 1, r, by, bx, bx2)
+        ref = base.float() * (by.float() > 0)
+        assert torch.equal(dz.float(), ref.bfloat16().float())
+        rows = (N * OH * OH + 127) // 128
+        S = part[:rows, 0].sum(0)
+        np.testing.assert_allclose(S.cpu().numpy(), ref.bfloat16().float().sum((0, 1, 2)).cpu().numpy(),
+                                   rtol=1e-3, atol=1e-2)
+        Q = part[:rows, 1].sum(0)
+        np.testing.assert_allclose(Q.cpu().numpy(), (dz.float() * bx.float()).sum((0, 1, 2)).cpu().numpy(),
+                                   rtol=1e-3, atol=1e-2)
+        assert torch.equal(part2[:rows, 0], part[:rows, 0])
+        Q2 = part2[:rows, 1].sum(0)
+        np.testing.assert_allclose(Q2.cpu().numpy(), (dz.float() * bx2.float()).sum((0, 1, 2)).cpu().numpy(),
+                                   rtol=1e-3, atol=1e-2)
