@@ -10,7 +10,6 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import tensorflow_distributed_learning_amd as tdl  # noqa: E402
 from tensorflow_distributed_learning_amd.ops import conv as CV  # noqa: E402
 
-import test_slab_grad_gpu as T  # noqa: E402,F401
 
 L = tdl.keras.layers
 

@@ -118,6 +118,11 @@ def test_stem_autograd_and_model_fusion():
     assert any(isinstance(n.layer, L.Conv2D) and id(n) in plan.pool_pad for n in mf._nodes)
     mu, hu = run(False)
     for v, a, b in zip(mf.weights, mf.get_weights(), mu.get_weights()):
+        if v.name.startswith("conv2d") and v.name.endswith("bias:0"):
+            # folded into the BN in the fused plan: exactly zero gradient there, rounding noise (1e-5)
+            # through the unfused layers
+            assert float(np.abs(a).max()) == 0.0 and float(np.abs(b).max()) < 1e-3
+            continue
         scale = max(float(np.abs(b).max()), 1e-3)
         np.testing.assert_allclose(a, b, atol=3e-2 * scale, rtol=3e-2, err_msg=v.name)
     np.testing.assert_allclose(hf.history["loss"], hu.history["loss"], rtol=2e-2)
