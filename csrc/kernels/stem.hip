@@ -257,6 +257,21 @@ __global__ __launch_bounds__(256, 2) void k_stem_wgrad(StemWgrad a) {
   const long long p0 = (long long)sl * kWgPix;
   const long long p1 = min((long long)a.M, p0 + kWgPix);
 
+  // each thread stages fixed (pixel-in-chunk, kh, part) items; its pixels' (n, oh, ow) advance by
+  // kChunk per chunk without divisions (kChunk < OW wraps at most once... or loops)
+  int xpx[kXrLoads], xoff[kXrLoads], xn[kXrLoads], xoh[kXrLoads], xow[kXrLoads];
+#pragma unroll
+  for (int u = 0; u < kXrLoads; ++u) {
+    const int s = tid + 256 * u;
+    const int px = s < nx ? s / (KH * 4) : 0, rem = s < nx ? s - px * (KH * 4) : 0;
+    xpx[u] = s < nx ? px : -1;
+    xoff[u] = ((rem >> 2) * a.WP) * 4 + (rem & 3) * 8;  // kh rows down, part * 8 elements across
+    const long long m = p0 + px;
+    xow[u] = (int)(m % a.OW);
+    const long long t = m / a.OW;
+    xoh[u] = (int)(t % a.OH);
+    xn[u] = (int)(t / a.OH);
+  }
   u32x4 rd[kDyLoads], rx[kXrLoads];
   auto gload = [&](long long c0) {
 #pragma unroll
@@ -267,18 +282,18 @@ __global__ __launch_bounds__(256, 2) void k_stem_wgrad(StemWgrad a) {
     }
 #pragma unroll
     for (int u = 0; u < kXrLoads; ++u) {
-      const int s = tid + 256 * u;
       rx[u] = u32x4{0u, 0u, 0u, 0u};
-      if (s < nx) {
-        const int px = s / (KH * 4), rem = s - px * (KH * 4), kh = rem >> 2, part = rem & 3;
-        const long long m = c0 + px;
-        if (m < p1) {
-          const int ow = (int)(m % a.OW);
-          const long long t = m / a.OW;
-          const int oh = (int)(t % a.OH), n = (int)(t / a.OH);
-          const long long off =
-              (((long long)n * a.HP + (long long)oh * a.SH + kh) * a.WP + 2LL * ow) * 4 + part * 8;
-          rx[u] = *reinterpret_cast<const u32x4*>(a.xp + off);
+      if (xpx[u] >= 0 && c0 + xpx[u] < p1) {
+        const long long off = (((long long)xn[u] * a.HP + (long long)xoh[u] * a.SH) * a.WP + 2LL * xow[u]) * 4 + xoff[u];
+        rx[u] = *reinterpret_cast<const u32x4*>(a.xp + off);
+      }
+      // advance this item's pixel by one chunk
+      xow[u] += kChunk;
+      while (xow[u] >= a.OW) {
+        xow[u] -= a.OW;
+        if (++xoh[u] == a.OH) {
+          xoh[u] = 0;
+          ++xn[u];
         }
       }
     }
@@ -293,7 +308,7 @@ __global__ __launch_bounds__(256, 2) void k_stem_wgrad(StemWgrad a) {
     for (int u = 0; u < kXrLoads; ++u) {
       const int s = tid + 256 * u;
       if (s < nx) {
-        const int px = s / (KH * 4), rem = s - px * (KH * 4);
+        const int px = xpx[u], rem = s - px * (KH * 4);
         *reinterpret_cast<u32x4*>(xr + px * kXrLd + rem * 8) = rx[u];  // rem * 8 = kh * 32 + part * 8
       }
     }

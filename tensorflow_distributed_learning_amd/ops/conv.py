@@ -100,6 +100,11 @@ def _time(fn, reps=5) -> float:
     return sorted(ts)[reps // 2]
 
 
+# the hand-written kernel is kept unless the library is more than this much faster: single timings of
+# near-equal candidates flip from run to run (profiles/resnet50_steady_state_breakdown_r3b.txt had a
+# 3x3 wgrad on MIOpen that the bench run before had on the hand-written kernel), and a stable choice
+# keeps the step's kernel set -- and its numerics -- the same across runs
+_PREFER_HIP = float(os.environ.get("TDL_CONV_PREFER_HIP", "1.05"))
 _HBM_BYTES_PER_MS = 4.5e9  # streaming rate the BN/add kernels reach on MI355X (profiles/bn_tuning_sweep_r2.jsonl)
 
 
@@ -116,7 +121,7 @@ def _pick(key, hip_fn, ref_fn, saved_bytes: int = 0) -> bool:
         return False
     t_ref = _time(ref_fn) + saved_bytes / _HBM_BYTES_PER_MS
     t_hip = _time(hip_fn)
-    got = t_hip < t_ref
+    got = t_hip < t_ref * _PREFER_HIP
     _choice[key] = got
     _times[key] = (t_hip, t_ref)
     return got
@@ -138,11 +143,13 @@ def _pick_wgrad(key, C, x, dy, kh, kw, stride, pad, ref_fn):
     if torch.cuda.is_current_stream_capturing():
         return None
     t_ref = _time(ref_fn)
-    best, t_best = None, t_ref
+    best, t_best = None, float("inf")
     for p in plans:
         t = _time(lambda: C.conv_wgrad(x, dy, kh, kw, stride[0], stride[1], pad[0], pad[1], plan=p))
         if t < t_best:
             best, t_best = p, t
+    if not t_best < t_ref * _PREFER_HIP:
+        best = None
     _choice[key] = best
     _times[key] = (t_best, t_ref)
     return best
