@@ -25,7 +25,8 @@ int poison() {  // 1: partial-sum buffers, 2: and the gradient outputs
   return on;
 }
 at::Tensor fresh(at::IntArrayRef shape, const at::TensorOptions& o, int level = 1) {
-  return poison() >= level ? at::full(shape, std::numeric_limits<float>::quiet_NaN(), o) : at::empty(shape, o);
+  const bool fp = o.dtype() == at::kFloat || o.dtype() == at::kBFloat16 || o.dtype() == at::kHalf;
+  return (fp && poison() >= level) ? at::full(shape, std::numeric_limits<float>::quiet_NaN(), o) : at::empty(shape, o);
 }
 
 at::Tensor gather_rows(at::Tensor src, at::Tensor idx, double scale) {
@@ -36,7 +37,7 @@ at::Tensor gather_rows(at::Tensor src, at::Tensor idx, double scale) {
   const int64_t row_elems = src.numel() / std::max<int64_t>(src.size(0), 1);
   std::vector<int64_t> shape(src.sizes().begin(), src.sizes().end());
   shape[0] = rows;
-  auto out = at::empty(shape, src.options().dtype(at::kFloat));
+  auto out = fresh(shape, src.options().dtype(at::kFloat));
   if (src.scalar_type() == at::kFloat) {
     tdl::gather_rows_f32(src.data_ptr<float>(), idx.data_ptr<int>(), out.data_ptr<float>(), rows, row_elems,
                          (float)scale, cur_stream());
@@ -52,7 +53,7 @@ at::Tensor gather_rows(at::Tensor src, at::Tensor idx, double scale) {
 at::Tensor gather_labels(at::Tensor src, at::Tensor idx) {
   TORCH_CHECK(src.is_cuda() && idx.is_cuda() && src.scalar_type() == at::kInt && idx.scalar_type() == at::kInt,
               "gather_labels: int32 GPU tensors expected");
-  auto out = at::empty({idx.numel()}, src.options());
+  auto out = fresh({idx.numel()}, src.options());
   tdl::gather_i32(src.data_ptr<int>(), idx.data_ptr<int>(), out.data_ptr<int>(), idx.numel(), cur_stream());
   return out;
 }
@@ -114,9 +115,9 @@ std::vector<at::Tensor> bn_forward_train(at::Tensor x, c10::optional<at::Tensor>
     given = parts_rows(*part_in, C);
     part = *part_in;
   } else {
-    part = at::empty({(int64_t)plan.part_rows * 2 * C}, f);
+    part = fresh({(int64_t)plan.part_rows * 2 * C}, f);
   }
-  auto st = at::empty({4, C}, f);  // mean, invstd, scale, shift
+  auto st = fresh({4, C}, f);  // mean, invstd, scale, shift
   float* mm = const_cast<float*>(opt_f32(moving_mean));
   float* mv = const_cast<float*>(opt_f32(moving_var));
   TORCH_CHECK((mm == nullptr) == (mv == nullptr), "batch_norm: moving mean and variance go together");
@@ -125,7 +126,7 @@ std::vector<at::Tensor> bn_forward_train(at::Tensor x, c10::optional<at::Tensor>
   tdl::bn_forward_stats(x.data_ptr(), bn_dtype(x), M, (int)C, part.data_ptr<float>(), opt_f32(gamma), opt_f32(beta),
                         opt_f32(mean_off), sp, sp + C, sp + 2 * C, sp + 3 * C, mm, mv, (float)momentum, (float)eps, s,
                         given);
-  auto y = at::empty_like(x);
+  auto y = fresh(x.sizes(), x.options());
   tdl::bn_apply(x.data_ptr(), res, y.data_ptr(), bn_dtype(x), M, (int)C, sp + 2 * C, sp + 3 * C, relu ? 1 : 0, s);
   return {y, st};
 }
@@ -149,7 +150,7 @@ std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, c10::optional<a
     TORCH_CHECK(y.has_value() && y->defined(), "batch_norm backward mode 2 needs y");
     bn_check(*y);
     yp = y->data_ptr();
-    dz = at::empty_like(x);
+    dz = fresh(x.sizes(), x.options());
   } else if (mode == 2) {
     dz = dy;
   }
@@ -164,10 +165,10 @@ std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, c10::optional<a
     given = parts_rows(*part_in, C);
     part = *part_in;
   } else {
-    part = at::empty({(int64_t)plan.part_rows * 2 * C}, f);
+    part = fresh({(int64_t)plan.part_rows * 2 * C}, f);
   }
-  auto out = at::empty({5, C}, f);  // dgamma, dbeta, coef[3]
-  auto dx = at::empty_like(x);
+  auto out = fresh({5, C}, f);  // dgamma, dbeta, coef[3]
+  auto dx = fresh(x.sizes(), x.options());
   float* o = out.data_ptr<float>();
   const float* sp = st.data_ptr<float>();
   auto check_out = [&](const c10::optional<at::Tensor>& t) {
@@ -194,8 +195,8 @@ std::vector<at::Tensor> maxpool_fwd(at::Tensor x, int64_t kh, int64_t kw, int64_
   TORCH_CHECK(kh * kw < 255 && kh > 0 && kw > 0 && sh > 0 && sw > 0 && OH > 0 && OW > 0, "maxpool: bad geometry");
   tdl::PoolGeom g{(int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3), (int)OH, (int)OW,
                   (int)kh, (int)kw, (int)sh, (int)sw, (int)pt, (int)pl, pad_zero ? 1 : 0};
-  auto y = at::empty({x.size(0), OH, OW, x.size(3)}, x.options());
-  auto arg = at::empty({x.size(0), OH, OW, x.size(3)}, x.options().dtype(at::kByte));
+  auto y = fresh({x.size(0), OH, OW, x.size(3)}, x.options());
+  auto arg = fresh({x.size(0), OH, OW, x.size(3)}, x.options().dtype(at::kByte));
   tdl::maxpool_forward(x.data_ptr(), y.data_ptr(), arg.data_ptr<uint8_t>(), bn_dtype(x) == tdl::BnDType::kBF16, g,
                        cur_stream());
   return {y, arg};
@@ -209,7 +210,7 @@ at::Tensor maxpool_bwd(at::Tensor dy, at::Tensor arg, std::vector<int64_t> in_sh
   TORCH_CHECK(in_shape.size() == 4 && in_shape[3] == dy.size(3) && in_shape[0] == dy.size(0), "maxpool: bad shape");
   tdl::PoolGeom g{(int)in_shape[0], (int)in_shape[1], (int)in_shape[2], (int)in_shape[3], (int)dy.size(1),
                   (int)dy.size(2), (int)kh, (int)kw, (int)sh, (int)sw, (int)pt, (int)pl, 0};
-  auto dx = at::empty(in_shape, dy.options());
+  auto dx = fresh(in_shape, dy.options());
   tdl::maxpool_backward(dy.data_ptr(), arg.data_ptr<uint8_t>(), dx.data_ptr(), bn_dtype(dy) == tdl::BnDType::kBF16, g,
                         cur_stream());
   return dx;
@@ -237,7 +238,7 @@ at::Tensor conv_fwd(at::Tensor x, at::Tensor w_ohwi, int64_t oh, int64_t ow, int
   conv_check(w_ohwi, "w");
   TORCH_CHECK(w_ohwi.dim() == 4 && w_ohwi.size(3) == x.size(3), "conv_fwd: weights must be OHWI [K,KH,KW,C]");
   auto g = conv_geom(x, oh, ow, w_ohwi.size(0), w_ohwi.size(1), w_ohwi.size(2), sh, sw, pt, pl);
-  auto y = at::empty({x.size(0), oh, ow, w_ohwi.size(0)}, x.options());
+  auto y = fresh({x.size(0), oh, ow, w_ohwi.size(0)}, x.options());
   tdl::conv_fwd_bf16(x.data_ptr(), w_ohwi.data_ptr(), y.data_ptr(), g, cur_stream());
   return y;
 }
@@ -249,7 +250,7 @@ std::vector<at::Tensor> conv_fwd_stats(at::Tensor x, at::Tensor w_ohwi, int64_t 
   conv_check(w_ohwi, "w");
   TORCH_CHECK(w_ohwi.dim() == 4 && w_ohwi.size(3) == x.size(3), "conv_fwd: weights must be OHWI [K,KH,KW,C]");
   auto g = conv_geom(x, oh, ow, w_ohwi.size(0), w_ohwi.size(1), w_ohwi.size(2), sh, sw, pt, pl);
-  auto y = at::empty({x.size(0), oh, ow, w_ohwi.size(0)}, x.options());
+  auto y = fresh({x.size(0), oh, ow, w_ohwi.size(0)}, x.options());
   const int64_t M = (int64_t)g.N * g.OH * g.OW, bm = tdl::conv_fwd_row_tile(g);
   const int64_t P = (M + bm - 1) / bm;
   auto part = fresh({P + (P + 63) / 64, 2, (int64_t)g.K}, x.options().dtype(at::kFloat));
@@ -384,7 +385,7 @@ at::Tensor conv_wgrad(at::Tensor x, at::Tensor dy, int64_t kh, int64_t kw, int64
                 "conv_wgrad: bad plan");
     p = tdl::conv_wgrad_make_plan(g, wmw, wnw, (int)plan[2]);
   }
-  auto ws = at::empty({p.ws_elems}, x.options().dtype(at::kFloat));
+  auto ws = fresh({p.ws_elems}, x.options().dtype(at::kFloat));
   if (out.has_value()) {
     auto& o = *out;
     TORCH_CHECK(o.is_cuda() && o.is_contiguous() && o.scalar_type() == at::kFloat &&
@@ -395,7 +396,7 @@ at::Tensor conv_wgrad(at::Tensor x, at::Tensor dy, int64_t kh, int64_t kw, int64
                          accumulate, g, cur_stream());
     return o;
   }
-  auto dw = at::empty({kh, kw, x.size(3), dy.size(3)}, x.options());
+  auto dw = fresh({kh, kw, x.size(3), dy.size(3)}, x.options());
   tdl::conv_wgrad_bf16(x.data_ptr(), dy.data_ptr(), ws.data_ptr<float>(), p, dw.data_ptr(), nullptr, false, g,
                        cur_stream());
   return dw;
@@ -422,12 +423,12 @@ std::vector<at::Tensor> stem_fwd(at::Tensor x, at::Tensor w_hwio, int64_t pt, in
   const int WP = std::max(WPv, 2 * (OW - 1) + 8);
   const int HPp = std::max(HP, (OH - 1) * (int)sh + KH);
   TORCH_CHECK((long long)N * HPp * WP * 4 < (1LL << 31), "stem: packed image too large");
-  auto xp = at::empty({N, HPp, WP, 4}, x.options().dtype(at::kBFloat16));
+  auto xp = fresh({N, HPp, WP, 4}, x.options().dtype(at::kBFloat16));
   tdl::stem_pack(x.data_ptr(), x.scalar_type() == at::kBFloat16, xp.data_ptr(), N, H, W, C, HPp, WP, (int)pt, (int)pl,
                  cur_stream());
-  auto wp = at::empty({K, KH, 32}, w_hwio.options());
+  auto wp = fresh({K, KH, 32}, w_hwio.options());
   tdl::stem_wpack(w_hwio.data_ptr(), wp.data_ptr(), KH, KW, C, K, cur_stream());
-  auto y = at::empty({N, OH, OW, K}, x.options().dtype(at::kBFloat16));
+  auto y = fresh({N, OH, OW, K}, x.options().dtype(at::kBFloat16));
   const int64_t M = (int64_t)N * OH * OW, bm = tdl::stem_fwd_row_tile(), P = (M + bm - 1) / bm;
   at::Tensor part;
   if (stats) part = fresh({P + (P + 63) / 64, 2, (int64_t)K}, x.options().dtype(at::kFloat));
@@ -450,7 +451,7 @@ at::Tensor stem_wgrad(at::Tensor xp, at::Tensor dy, int64_t kh, int64_t kw, int6
                   2 * (OW - 1) + 8 <= WP,
               "stem_wgrad: geometry inconsistent with the packed image");
   const int M = N * OH * OW;
-  auto ws = at::empty({tdl::stem_wgrad_ws_elems(M, K, (int)kh)}, dy.options().dtype(at::kFloat));
+  auto ws = fresh({tdl::stem_wgrad_ws_elems(M, K, (int)kh)}, dy.options().dtype(at::kFloat));
   if (out.has_value()) {
     auto& o = *out;
     TORCH_CHECK(o.is_cuda() && o.is_contiguous() && o.scalar_type() == at::kFloat && o.numel() == kh * kw * c * K,
@@ -459,7 +460,7 @@ at::Tensor stem_wgrad(at::Tensor xp, at::Tensor dy, int64_t kh, int64_t kw, int6
                     (int)sh, o.data_ptr<float>(), nullptr, accumulate, cur_stream());
     return o;
   }
-  auto dw = at::empty({kh, kw, c, (int64_t)K}, dy.options());
+  auto dw = fresh({kh, kw, c, (int64_t)K}, dy.options());
   tdl::stem_wgrad(xp.data_ptr(), dy.data_ptr(), ws.data_ptr<float>(), N, HP, WP, OH, OW, K, (int)kh, (int)kw, (int)c,
                   (int)sh, nullptr, dw.data_ptr(), false, cur_stream());
   return dw;
@@ -529,7 +530,7 @@ at::Tensor gemm_bf16(at::Tensor a, int64_t ta, at::Tensor b, int64_t tb, c10::op
                    o.data_ptr<float>(), nullptr, o.stride(0), bp, (float)alpha, accumulate, cur_stream());
     return o;
   }
-  auto c = at::empty({M, N}, a.options());
+  auto c = fresh({M, N}, a.options());
   tdl::gemm_bf16((int)ta, (int)tb, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), (int)M, (int)N, (int)K,
                  nullptr, c.data_ptr(), N, bp, (float)alpha, false, cur_stream());
   return c;
@@ -538,7 +539,7 @@ at::Tensor gemm_bf16(at::Tensor a, int64_t ta, at::Tensor b, int64_t tb, c10::op
 at::Tensor gap_fwd(at::Tensor x) {
   conv_check(x, "gap: x");
   TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "gap: NHWC with C % 8 == 0");
-  auto y = at::empty({x.size(0), x.size(3)}, x.options());
+  auto y = fresh({x.size(0), x.size(3)}, x.options());
   tdl::gap_fwd_bf16(x.data_ptr(), y.data_ptr(), (int)x.size(0), (int)(x.size(1) * x.size(2)), (int)x.size(3),
                     cur_stream());
   return y;
@@ -547,7 +548,7 @@ at::Tensor gap_fwd(at::Tensor x) {
 at::Tensor gap_bwd(at::Tensor dy, int64_t h, int64_t w) {
   conv_check(dy, "gap: dy");
   TORCH_CHECK(dy.dim() == 2 && dy.size(1) % 8 == 0, "gap: dy [N][C], C % 8 == 0");
-  auto dx = at::empty({dy.size(0), h, w, dy.size(1)}, dy.options());
+  auto dx = fresh({dy.size(0), h, w, dy.size(1)}, dy.options());
   tdl::gap_bwd_bf16(dy.data_ptr(), dx.data_ptr(), (int)dy.size(0), (int)(h * w), (int)dy.size(1), cur_stream());
   return dx;
 }
@@ -555,8 +556,8 @@ std::vector<at::Tensor> xent_fwd(at::Tensor z, at::Tensor labels) {
   TORCH_CHECK(z.is_cuda() && z.is_contiguous() && z.scalar_type() == at::kFloat && z.dim() == 2, "xent: f32 [N][K] logits");
   TORCH_CHECK(labels.is_cuda() && labels.is_contiguous() && labels.scalar_type() == at::kLong &&
                   labels.numel() == z.size(0), "xent: int64 [N] labels");
-  auto loss = at::empty({z.size(0)}, z.options());
-  auto lse = at::empty({z.size(0)}, z.options());
+  auto loss = fresh({z.size(0)}, z.options());
+  auto lse = fresh({z.size(0)}, z.options());
   tdl::softmax_xent_fwd(z.data_ptr<float>(), reinterpret_cast<const long long*>(labels.data_ptr<int64_t>()), (int)z.size(0), (int)z.size(1),
                         loss.data_ptr<float>(), lse.data_ptr<float>(), cur_stream());
   return {loss, lse};
@@ -566,7 +567,7 @@ at::Tensor xent_bwd(at::Tensor z, at::Tensor labels, at::Tensor g) {
   TORCH_CHECK(z.is_cuda() && z.is_contiguous() && z.scalar_type() == at::kFloat && z.dim() == 2, "xent: f32 [N][K] logits");
   TORCH_CHECK(labels.is_contiguous() && labels.scalar_type() == at::kLong && labels.numel() == z.size(0), "xent: labels");
   TORCH_CHECK(g.is_cuda() && g.is_contiguous() && g.scalar_type() == at::kFloat && g.numel() == z.size(0), "xent: g");
-  auto dz = at::empty_like(z);
+  auto dz = fresh(z.sizes(), z.options());
   tdl::softmax_xent_bwd(z.data_ptr<float>(), reinterpret_cast<const long long*>(labels.data_ptr<int64_t>()), (int)z.size(0), (int)z.size(1),
                         g.data_ptr<float>(), dz.data_ptr<float>(), cur_stream());
   return dz;

@@ -74,8 +74,16 @@ class LazyLogs(dict):
         return True
 
 
+def _async_ok(t: torch.Tensor) -> bool:
+    """An asynchronous host->device copy is safe only from pinned memory (PyTorch's host allocator
+    keeps a pinned block until the copies reading it complete).  A pageable batch may be freed and
+    its memory reused by the next batch right after ``.to`` returns, while the copy still reads it."""
+    return t.is_cuda or t.is_pinned()
+
+
 def _to_device(batch, device):
-    return D.map_structure(lambda t: t.to(device, non_blocking=True) if isinstance(t, torch.Tensor) else t, batch)
+    return D.map_structure(lambda t: t.to(device, non_blocking=_async_ok(t)) if isinstance(t, torch.Tensor) else t,
+                           batch)
 
 
 def _split_xy(batch):
@@ -415,7 +423,7 @@ class GenericTrainer:
             self._graphs[key] = ent
         static, graph = ent
         for s_, t in zip(static, flat):
-            s_.copy_(t, non_blocking=True)
+            s_.copy_(t, non_blocking=_async_ok(t))
         self.optimizer._sync_lr()
         graph.replay()
         self.optimizer.iterations += 1

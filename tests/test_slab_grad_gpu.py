@@ -195,37 +195,35 @@ def test_fused_bn_group_backward_in_conv_epilogue():
     np.testing.assert_allclose(hf.history["loss"], hu.history["loss"], rtol=1e-2)
 
 
-def test_fused_bn_backward_projection_shortcut_and_stride2():
+def test_fused_bn_backward_projection_shortcut_and_stride2(tmp_path):
     """ResNet conv blocks: the projection-shortcut BN's backward sums come from the same conv
     epilogue as the block output group's (part2), and a group read by two 1x1 stride-2 convs (the
     next stage's conv block) is reduced in the stride-2 input-gradient epilogue; training matches
-    the unfused path (scripts/diag_bnfuse.py: the same model, cross-process and in-process)."""
-    from tensorflow_distributed_learning_amd.ops import batchnorm as B
-    from tensorflow_distributed_learning_amd.ops import conv as CV
+    the unfused path.  Each configuration trains in a fresh process (scripts/diag_bnfuse2.py) with
+    HIP_LAUNCH_BLOCKING=1: this small model's 2-step result differs between asynchronous and
+    launch-blocking execution by up to ~50 % in some BN betas, identically before this fusion
+    existed (commit df563a5; README "Known issues"), and in asynchronous mode it can come out either
+    way from run to run, which would mask what this test checks."""
+    import re
+    import subprocess
 
-    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "scripts"))
-    import diag_bnfuse as D
-
-    old = {k: os.environ.get(k) for k in ("TDL_GRAPH_STEP", "TDL_CONV")}
-    try:
-        mu = D.run(False, False, False, 2)
-        n0 = dict(B.FUSED_BWD_MODES)
-        mf = D.run(True, True, True, 2)
-        nf = {k: B.FUSED_BWD_MODES[k] - n0[k] for k in n0}
-    finally:
-        CV._FUSE_BN_BWD[0] = CV._FUSE_BN_BWD_S2[0] = CV._FUSE_BN_BWD_SHORTCUT[0] = True
-        tdl.keras.mixed_precision.set_global_policy("float32")
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "scripts", "diag_bnfuse2.py")
+    w, modes = {}, {}
+    for cfg in ("F", "T"):
+        out = str(tmp_path / f"w_{cfg}.npz")
+        env = dict(os.environ, HIP_LAUNCH_BLOCKING="1")
+        r = subprocess.run([sys.executable, script, cfg, out], capture_output=True, text=True, timeout=300, env=env)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        w[cfg] = np.load(out)
+        modes[cfg] = {int(k): int(v) for k, v in re.findall(r"(\d): (\d+)", r.stdout.split("fused_modes")[1].split("\n")[0])}
     # per step: both shortcut BNs (mode 0); the outputs of blocks 1-3 (block 2's is read by the two
     # stride-2 convs of block 3); the 8 inner BN -> ReLU groups.  Two steps.
-    assert nf == {0: 4, 1: 16, 2: 6}, nf
-    for v, a, b in zip(mf.weights, mf.get_weights(), mu.get_weights()):
+    assert modes["T"] == {0: 4, 1: 16, 2: 6}, modes
+    assert modes["F"] == {0: 0, 1: 0, 2: 0}, modes
+    for k in w["F"].files:
+        a, b = w["T"][k], w["F"][k]
         scale = max(float(np.abs(b).max()), 1e-3)
-        np.testing.assert_allclose(a, b, atol=2e-2 * scale, rtol=2e-2, err_msg=v.name)
+        np.testing.assert_allclose(a, b, atol=2e-2 * scale, rtol=2e-2, err_msg=k)
 
 
 def test_conv_dgrad_s2_bn_epilogue_matches_reference():
