@@ -69,6 +69,14 @@ WgradPlan conv_wgrad_make_plan(const ConvGeom& g, int wmw, int wnw, int nsplit);
 void conv_wgrad_bf16(const void* x, const void* dy, float* ws, const WgradPlan& p, void* dw_bf16, float* dw_f32,
                      bool accumulate, const ConvGeom& g, hipStream_t s);
 
+// Weight gradient of a 3x3 / stride 1 / pad 1 conv with C == 64 (wgrad3x3.hip): whole output rows per
+// workgroup, the 9 x 64 x 64 tile in registers, deterministic slice reduction.  ws: ..._ws_elems f32.
+bool conv_wgrad3x3_c64_supported(const ConvGeom& g);
+long long conv_wgrad3x3_c64_ws_elems(const ConvGeom& g);
+void conv_wgrad3x3_c64(const void* x, const void* dy, float* ws, void* dw_bf16, float* dw_f32, bool accumulate,
+                       const ConvGeom& g, hipStream_t s);
+void conv_wgrad3x3_set_rows(int rows);  // A/B hook: output rows per slice (0 = heuristic)
+
 // Tile-sweep hook: 0 = per-shape heuristic (default), 1 = 128x64, 2 = 128x128, 3 = 256x128.
 void conv_force_tile(int tile);
 // A/B hook: register prefetch depth of the implicit-GEMM main loop (1 or 2 tiles in flight)

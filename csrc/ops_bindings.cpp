@@ -375,6 +375,23 @@ at::Tensor conv_wgrad(at::Tensor x, at::Tensor dy, int64_t kh, int64_t kw, int64
   auto g = conv_geom(x, dy.size(1), dy.size(2), dy.size(3), kh, kw, sh, sw, pt, pl);
   TORCH_CHECK(tdl::conv_wgrad_supported(g), "conv_wgrad: N*OH*OW must be < 2^24");
   TORCH_CHECK(plan.empty() || plan.size() == 3, "conv_wgrad: plan = [wmw, wnw, nsplit]");
+  if (!plan.empty() && plan[0] == 0) {  // [0, 0, 0]: the row kernel of 3x3 / C = 64 convs (wgrad3x3.hip)
+    TORCH_CHECK(tdl::conv_wgrad3x3_c64_supported(g), "conv_wgrad: the 3x3 row kernel does not take this shape");
+    auto ws = fresh({tdl::conv_wgrad3x3_c64_ws_elems(g)}, x.options().dtype(at::kFloat));
+    if (out.has_value()) {
+      auto& o = *out;
+      TORCH_CHECK(o.is_cuda() && o.is_contiguous() && o.scalar_type() == at::kFloat &&
+                      o.numel() == kh * kw * x.size(3) * dy.size(3),
+                  "conv_wgrad: out must be a contiguous f32 tensor of KH*KW*C*K elements");
+      tdl::conv_wgrad3x3_c64(x.data_ptr(), dy.data_ptr(), ws.data_ptr<float>(), nullptr, o.data_ptr<float>(), accumulate,
+                             g, cur_stream());
+      return o;
+    }
+    auto dw = fresh({kh, kw, x.size(3), dy.size(3)}, x.options());
+    tdl::conv_wgrad3x3_c64(x.data_ptr(), dy.data_ptr(), ws.data_ptr<float>(), dw.data_ptr(), nullptr, false, g,
+                           cur_stream());
+    return dw;
+  }
   tdl::WgradPlan p;
   if (plan.empty()) {
     p = tdl::conv_wgrad_plans(g, 1).at(0);
@@ -473,6 +490,8 @@ std::vector<std::vector<int64_t>> conv_wgrad_plans(std::vector<int64_t> x_shape,
   tdl::ConvGeom g{(int)x_shape[0], (int)x_shape[1], (int)x_shape[2], (int)x_shape[3], (int)dy_shape[1],
                   (int)dy_shape[2], (int)dy_shape[3], (int)kh, (int)kw, (int)sh, (int)sw, (int)pt, (int)pl};
   std::vector<std::vector<int64_t>> out;
+  // the 3x3 / C = 64 row kernel first where it applies (it beats the split-K tiles on these shapes)
+  if (tdl::conv_wgrad3x3_c64_supported(g)) out.push_back({0, 0, 0, 0});
   for (const auto& p : tdl::conv_wgrad_plans(g, (int)max_plans)) out.push_back({p.wmw, p.wnw, p.chunk, p.nsplit});
   return out;
 }
@@ -603,6 +622,7 @@ void register_ops(pybind11::module& m) {
         pybind11::arg("accumulate") = false, pybind11::arg("plan") = std::vector<int64_t>{});
   m.def("conv_wgrad_plans", &conv_wgrad_plans, "weight-gradient candidate plans, best first: [[wmw, wnw, chunk, nsplit]]");
   m.def("conv_force_tile", &tdl::conv_force_tile, "conv tile sweep hook (0 = heuristic)");
+  m.def("conv_wgrad3x3_set_rows", &tdl::conv_wgrad3x3_set_rows, "3x3 row-kernel wgrad: output rows per slice (0 = auto)");
   m.def("conv_force_depth", &tdl::conv_force_depth, "conv main-loop prefetch depth A/B hook (1 or 2)");
   m.def("stem_fwd", &stem_fwd, "small-channel stride-2 conv (ResNet stem): (y, packed x[, BN part])",
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("pt"), pybind11::arg("pb"), pybind11::arg("pl"),

@@ -252,3 +252,29 @@ def test_conv2d_library_wgrad_reaches_slab(monkeypatch, with_box):
     finally:
         CV._choice.clear()
         CV._choice.update(saved)
+
+
+@pytest.mark.parametrize("shape", [(4, 14, 14, 64), (2, 56, 56, 128), (3, 9, 61, 64)])
+def test_wgrad3x3_row_kernel_matches_fp32(shape):
+    """The 3x3 / C = 64 row kernel (csrc/kernels/wgrad3x3.hip, plan [0, 0, 0]) vs fp32 PyTorch, bf16
+    out and added into an f32 slab, deterministic."""
+    from tensorflow_distributed_learning_amd.ops import hip
+
+    C = hip()
+    N, H, W, K = shape
+    g = torch.Generator(device="cpu").manual_seed(4)
+    x = torch.randn(N, H, W, 64, generator=g).cuda().bfloat16()
+    dy = torch.randn(N, H, W, K, generator=g).cuda().bfloat16()
+    plans = C.conv_wgrad_plans(list(x.shape), list(dy.shape), 3, 3, 1, 1, 1, 1, 2)
+    assert plans[0] == [0, 0, 0, 0]
+    w = torch.zeros(3, 3, 64, K, device="cuda", requires_grad=True)
+    y = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.permute(3, 2, 0, 1), padding=1)
+    y.backward(dy.float().permute(0, 3, 1, 2))
+    ref = w.grad
+    dw = C.conv_wgrad(x, dy, 3, 3, 1, 1, 1, 1, plan=[0, 0, 0])
+    scale = ref.abs().max().item()
+    assert (dw.float() - ref).abs().max().item() / scale < 1e-2
+    slab = torch.full(ref.shape, 0.25, device="cuda")
+    C.conv_wgrad(x, dy, 3, 3, 1, 1, 1, 1, out=slab, accumulate=True, plan=[0, 0, 0])
+    assert (slab - 0.25 - ref).abs().max().item() / scale < 1e-4
+    assert torch.equal(dw, C.conv_wgrad(x, dy, 3, 3, 1, 1, 1, 1, plan=[0, 0, 0]))
