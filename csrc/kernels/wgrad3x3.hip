@@ -190,9 +190,9 @@ void conv_wgrad3x3_set_rows(int rows) { g_w3_rows = rows; }
 
 static int w3_rows(const ConvGeom& g) {
   if (g_w3_rows > 0) return g_w3_rows;
-  // about 2 workgroups per CU (1 resident each: 148 KiB of partial tile in registers) over 256 CUs
+  // one workgroup per CU (1 resident each: the 9x64x64 partial tile lives in registers)
   const long long rows = (long long)g.N * g.H;
-  const long long target = 512LL / (g.K / 64);
+  const long long target = 256LL / (g.K / 64);  // one slice per CU: 56 rows at b=256 (rows 28: +8 %, 112: +70 %)
   return (int)std::max<long long>(1, (rows + target - 1) / target);
 }
 
