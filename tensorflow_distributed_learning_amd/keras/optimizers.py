@@ -28,6 +28,7 @@ class Optimizer:
         self._n = None
         self._device = None
         self.lr_dev: Optional[torch.Tensor] = None
+        self._lr_synced = None  # (value, lr_dev address) last written by _sync_lr
         unknown = set(kwargs) - {"decay", "amsgrad_legacy", "jit_compile", "is_legacy_optimizer",
                                  "use_ema", "ema_momentum", "ema_overwrite_frequency"}
         if unknown:
@@ -53,8 +54,13 @@ class Optimizer:
         return float(lr)
 
     def _sync_lr(self, step: Optional[int] = None):
+        # one fill kernel only when the value changes: a constant learning rate costs no launch in
+        # front of every graph replay (the device copy is written nowhere else)
         if self.lr_dev is not None:
-            self.lr_dev.fill_(self.current_lr(step))
+            v = self.current_lr(step)
+            if self._lr_synced != (v, self.lr_dev.data_ptr()):
+                self.lr_dev.fill_(v)
+                self._lr_synced = (v, self.lr_dev.data_ptr())
 
     # ------------------------------------------------------------------ slots
     def build(self, n: int, device: torch.device):
@@ -62,6 +68,7 @@ class Optimizer:
             return
         self._n, self._device = n, device
         self.lr_dev = torch.full((1,), self.current_lr(), dtype=torch.float32, device=device)
+        self._lr_synced = (self.current_lr(), self.lr_dev.data_ptr())
         for k in self._slot_names():
             old = self._slots.get(k)
             self._slots[k] = old.to(device) if (old is not None and old.numel() == n) else torch.zeros(
