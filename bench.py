@@ -138,8 +138,8 @@ def main():
     if done != K:
         raise SystemExit(f"bench: ran {done} steps instead of {K}")
     t = torch.tensor([dt], dtype=torch.float64, device=dev if comm.name == "rccl" else "cpu")
-    comm.all_reduce(t, "max")
-    dt = float(t.item())
+    per_rank = [float(v) for v in comm.all_gather(t).reshape(-1).tolist()]
+    dt = max(per_rank)
     logs = trainer.logs()  # also raises if an xGMI all-reduce timed out on this rank
     identical = consistency.replicas_identical(comm, trainer.W)
     ips = K * B / dt
@@ -174,7 +174,13 @@ def main():
                        "input_prefetch_executions": 1,
                        "allreduce_in_graph": bool(trainer.capture_comm and R > 1),
                        "replicas_identical": identical,
-                       "final_loss": round(logs["loss"], 4)},
+                       "final_loss": round(logs["loss"], 4),
+                       # per-rank timed-region spread (the MAX is reported), and why any faster path
+                       # was not taken on this job (self-tests, capture probes, xGMI set-up)
+                       "rank_ms_per_step": [round(v / K * 1e3, 5) for v in per_rank],
+                       "rank_spread_pct": round(100.0 * (max(per_rank) - min(per_rank)) / max(per_rank), 2),
+                       "fallbacks": list(getattr(trainer, "fallbacks", [])) + (
+                           [f"xgmi: {comm.xgmi_reason}"] if getattr(comm, "xgmi_reason", "") else [])},
         }), flush=True)
     strategy.shutdown()
     if not identical:

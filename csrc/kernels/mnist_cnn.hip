@@ -1373,8 +1373,14 @@ __device__ __forceinline__ void finalize_x_body(const MnistArgs& a, int apply_sg
   float* xdst = nullptr;
   int64_t half = 0;
   if (xchg) {
-    if (xgmi_failed(a.xa.err)) return;  // a peer already failed: no exchange, no update
     e = __builtin_amdgcn_readfirstlane(a.xa.epoch[j]) + 1u;
+    if (xgmi_failed(a.xa.err)) {
+      // a peer already failed: no exchange, no update, and G is left as the previous step wrote it.
+      // The epoch still advances (as in k_xgmi_oneshot / _twoshot), so that after a reset_error
+      // every rank's channel epochs stay in step and no rank reads the other parity half
+      if (tid == 0) a.xa.epoch[j] = e;
+      return;
+    }
     half = (int64_t)(e & 1u) * 2 * a.xa.cap;
     xdst = a.xa.p.buf[a.xa.rank] + half;
   }

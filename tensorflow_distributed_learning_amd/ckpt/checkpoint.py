@@ -82,6 +82,11 @@ def read_bundle(prefix: str, verify: bool = True) -> Dict[str, torch.Tensor]:
     with open(prefix + ".data-00000-of-00001", "rb") as f:
         data = f.read()
     for name, e in index["tensors"].items():
+        if e["dtype"] not in _DT_INV:
+            if name == "_CHECKPOINTABLE_OBJECT_GRAPH":
+                continue  # a TF2 object-graph proto (string tensor): not a variable
+            raise ValueError(f"{prefix}: tensor {name!r} has dtype {e['dtype']}, which this reader does not "
+                             "support (numeric tensors only)")
         raw = data[e["offset"] : e["offset"] + e["nbytes"]]
         if verify and crc32c(raw) != e["crc32c"]:
             raise ValueError(f"checksum mismatch for {name} in {prefix}")

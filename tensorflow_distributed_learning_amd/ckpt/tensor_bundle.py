@@ -32,6 +32,14 @@ BLOCK_SIZE = 4096  # target data block size before a new block is started (TF's 
 DT = {"float32": 1, "float64": 2, "int32": 3, "uint8": 4, "int16": 5, "int8": 6, "int64": 9, "bool": 10,
       "bfloat16": 14, "float16": 19}
 DT_INV = {v: k for k, v in DT.items()}
+# read-only: TF2 checkpoints carry _CHECKPOINTABLE_OBJECT_GRAPH as a DT_STRING tensor (the object
+# graph proto); bundles written here hold numeric tensors only (name-based loading: the files work
+# with tf.train.load_checkpoint / list_variables, not with a TF2 object-graph restore)
+DT_INV[7] = "string"
+
+
+def dtype_name(code: int) -> str:
+    return DT_INV.get(int(code), f"unsupported-dtype-{int(code)}")
 
 
 def mask_crc(c: int) -> int:
@@ -133,7 +141,7 @@ def parse_entry(buf: bytes) -> dict:
     for shp in f.get(2, [b""]):
         for dim in _parse(shp).get(2, []):
             shape.append(int(_parse(dim).get(1, [0])[0]))
-    return {"dtype": DT_INV[f.get(1, [0])[0]], "shape": shape, "shard_id": f.get(3, [0])[0],
+    return {"dtype": dtype_name(f.get(1, [0])[0]), "shape": shape, "shard_id": f.get(3, [0])[0],
             "offset": f.get(4, [0])[0], "size": f.get(5, [0])[0],
             "crc32c": unmask_crc(f[6][0]) if 6 in f else None}
 

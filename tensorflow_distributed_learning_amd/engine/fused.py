@@ -141,6 +141,7 @@ class FusedMnistTrainer:
         self._capture_comm = None
         self._comm_stream = None
         self.allreduce_mode = "local" if self.R == 1 else None
+        self.fallbacks = []  # why a faster path was not taken (bench.py reports them)
         # R > 1: the dense bucket's all-reduce on a side stream overlapping the conv backward is
         # opt-in; serial is the default: on one MI355X (2 replica processes sharing it) the forked
         # execution graph ran 350 us/step against 68.6 serial (profiles/mnist_side_stream_ab_r2.txt)
@@ -163,6 +164,8 @@ class FusedMnistTrainer:
                 self._capture_comm = False
             else:
                 self._capture_comm = bool(self.comm.capture_probe())
+                if not self._capture_comm:
+                    self.fallbacks.append("all-reduce not capturable into the execution graph (probe failed)")
         return self._capture_comm
 
     # ------------------------------------------------------------------ data
@@ -297,42 +300,71 @@ class FusedMnistTrainer:
         n = len(self.X)
         idx = ((torch.arange(b, dtype=torch.int64) * 7919 + self.rank * 104729) % n).to(torch.int32).to(dev)
         saved = (self.W.clone(), self.G.clone())
-        ok, why = True, ""
+        # phase 1, local work only: one step through the exchange.  Whatever happens here, every
+        # rank then reaches the same agreement collective (a rank that raised must not wander into
+        # a different collective than its peers)
+        ok, why, timed_out, w_x, g_local = True, "", False, None, None
         try:
             tst = M.FusedMnistTrainStep(self.X, self.Y, idx, self.W, self.G, self.layout, b, self.R,
                                         self.optimizer.lr_dev, torch.zeros(4, dtype=torch.float32, device=dev),
                                         global_batch=b * self.R)
-            if tst.fused_bwd:
-                tst.set_exchange(self._xchg, twoshot=self._xchg_twoshot)
-                torch.cuda.synchronize(dev)
-                tst.forward_backward(0)
-                tst.finalize(True, exchange=True)
-                torch.cuda.synchronize(dev)
-                tst.check()
-                if self._xchg.error():
-                    raise RuntimeError("exchange timed out")
-                w_x, g_local = self.W.clone(), self.G.clone()
-                self.comm.all_reduce(g_local, "sum")
-                lr = float(self.optimizer.lr_dev.item())
-                w_ref = saved[0] - lr * g_local
-                if os.environ.get("TDL_FAULT_XCHG_SELFTEST") == str(self.rank):  # fault injection (tests)
-                    w_ref = w_ref + 1.0
-                if not torch.allclose(w_x, w_ref, rtol=1e-5, atol=1e-7):
-                    ok, why = False, f"max |W - W_ref| = {float((w_x - w_ref).abs().max()):.3g}"
-                if not consistency.replicas_identical(self.comm, w_x):
-                    ok, why = False, "replicas differ"
+            if not tst.fused_bwd:
+                raise RuntimeError("fused backward unavailable")
+            tst.set_exchange(self._xchg, twoshot=self._xchg_twoshot)
+            torch.cuda.synchronize(dev)
+            if os.environ.get("TDL_FAULT_XCHG_SELFTEST_RAISE") == str(self.rank):  # fault injection (tests)
+                raise RuntimeError("injected self-test failure before the exchange")
+            tst.forward_backward(0)
+            tst.finalize(True, exchange=True)
+            torch.cuda.synchronize(dev)
+            timed_out = bool(self._xchg.error())
+            if timed_out:
+                raise RuntimeError("exchange timed out")
+            tst.check()
+            w_x, g_local = self.W.clone(), self.G.clone()
             del tst
         except Exception as e:  # noqa: BLE001 - any failure means the serial path
             ok, why = False, f"{type(e).__name__}: {e}"
+            timed_out = timed_out or bool(self._xchg.error())
+        # agreement on the control plane (never through the xGMI kernel: its device may now carry a
+        # sticky error word): [step ok everywhere, no rank timed out]
+        ok_all, no_timeout = self._agree_flags([ok, not timed_out])
+        if not no_timeout:
+            # a bounded wait expired: the error word disables every xGMI kernel on that device, so
+            # the serial all-reduce could not run there either -- fail the job on every rank
+            self.W.copy_(saved[0])
+            raise RuntimeError("exchange-in-finalize self-test: a peer did not arrive at the xGMI exchange "
+                               f"({why or 'on another rank'}); the device fabric or a peer is broken")
+        if ok_all:
+            # phase 2, every rank: the reference reduction and the cross-replica identity check
+            self.comm.all_reduce(g_local, "sum")
+            lr = float(self.optimizer.lr_dev.item())
+            w_ref = saved[0] - lr * g_local
+            if os.environ.get("TDL_FAULT_XCHG_SELFTEST") == str(self.rank):  # fault injection (tests)
+                w_ref = w_ref + 1.0
+            if not torch.allclose(w_x, w_ref, rtol=1e-5, atol=1e-7):
+                ok, why = False, f"max |W - W_ref| = {float((w_x - w_ref).abs().max()):.3g}"
+            if not consistency.replicas_identical(self.comm, w_x):
+                ok, why = False, "replicas differ"
+            ok_all = self._agree_flags([ok])[0]
         self.W.copy_(saved[0])
         self.G.copy_(saved[1])
-        f = torch.tensor([1.0 if ok else 0.0], device=dev if self.comm.name == "rccl" else "cpu")
-        self.comm.all_reduce(f, "min")
-        agreed = bool(f.item() > 0.5)
-        if not agreed and self.rank == 0:
-            warnings.warn(f"exchange-in-finalize self-test failed ({why or 'on another rank'}); "
-                          "using the serial gradient all-reduce")
-        return agreed
+        if not ok_all:
+            self.fallbacks.append(f"exchange-in-finalize self-test failed ({why or 'on another rank'})")
+            if self.rank == 0:
+                warnings.warn(f"exchange-in-finalize self-test failed ({why or 'on another rank'}); "
+                              "using the serial gradient all-reduce")
+        return ok_all
+
+    def _agree_flags(self, flags) -> list:
+        """MIN over ranks of boolean flags through the process group itself (not the communicator's
+        xGMI fast path)."""
+        import torch.distributed as dist
+
+        on = self.device if self.comm.name == "rccl" else torch.device("cpu")
+        f = torch.tensor([1.0 if x else 0.0 for x in flags], device=on)
+        dist.all_reduce(f, op=dist.ReduceOp.MIN)
+        return [bool(v > 0.5) for v in f.tolist()]
 
     def _update(self, lo: int = 0, hi: Optional[int] = None):
         from .. import ops

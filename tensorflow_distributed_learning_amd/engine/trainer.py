@@ -166,6 +166,10 @@ class GenericTrainer:
         # metric accumulators start from zero for callers that drive run_train() directly
         # (fit() resets them per epoch; scripts/bench_resnet50.py did not, and reported stale state)
         self.reset_metrics()
+        if self.device.type == "cuda":
+            from ..ops import conv as _conv
+
+            _conv.bind_communicator(self.comm)  # rank 0 makes the autotuning decisions for all replicas
         if self.device.type == "cuda" and os.environ.get("TDL_CONV_AUTOTUNE", "1") == "1":
             # like TF's cuDNN autotuning (TF_CUDNN_USE_AUTOTUNE=1): MIOpen find-mode search of the
             # conv solvers per shape on first use (+12% ResNet-50 step rate on MI355X)
@@ -342,12 +346,24 @@ class GenericTrainer:
                 loss, per_ex, y_pred = self._forward_loss(x, y, sw, global_n)
         finally:
             V.CAST_ACCUMULATE[0] -= 1
+        from ..utils import checksums as _ck
+
+        if _ck.enabled():
+            _ck.record("input:x", x)
+            _ck.record("input:y", y)
+            _ck.record("loss", loss)
         with trace_range("tdl.backward"):
             loss.backward()
+        if _ck.enabled():
+            for v, gv in zip(self.model._trainable_vars, self.model._layout.views(G)):
+                _ck.record("slab_grad:" + v.name, gv)
         for b in (self.model.__dict__.get("_grad_boxes") or {}).values():
             if b.g is not None:  # a parked gradient contribution nobody collected
                 raise RuntimeError("fused gradient sum lost a contribution (keras/fusion.py grad boxes)")
-        if self.comm.world_size > 1:
+        from ..utils import fault
+
+        skip = self.comm.world_size > 1 and fault.maybe_skip_collective(self.comm.rank, int(self.optimizer.iterations))
+        if self.comm.world_size > 1 and not skip:
             with trace_range("tdl.allreduce"):
                 if self._buckets is not None:
                     for w in self._works:
@@ -369,6 +385,8 @@ class GenericTrainer:
                     self.comm.all_reduce(G, "sum")
         with torch.no_grad(), trace_range("tdl.optimizer"):
             self.optimizer.apply_flat(self.W, G, sync_lr=sync_lr)
+            if _ck.enabled():
+                _ck.record("slab_W", self.W)
             self.loss_tracker.update_state(per_ex.detach())
             yp = y_pred.detach()
             for m in self.metrics:

@@ -254,6 +254,7 @@ class Dense(Layer):
         self.built = True
 
     def call(self, x, training=None):
+        x = _autocast_input(x)
         if _dense.dense_supported(x, self.units):
             # bf16 on the GPU: hand-written MFMA GEMMs (ops/dense.py), gradients straight into the
             # trainer's slab when it is bound
@@ -263,7 +264,7 @@ class Dense(Layer):
                 w = self.kernel.compute_view(x.dtype)
                 w = w if w is not None else self.kernel.value.detach().to(x.dtype)
                 b = self.bias.value.detach() if self.bias is not None else None
-                return self.activation(_dense.dense_bf16(x, w, b, (gw, gb)))
+                return self.activation(_dense.dense_bf16(x, w, b, (gw, gb), anchor=self.kernel.value))
             b = self.bias.value if self.bias is not None else None
             return self.activation(_dense.dense_bf16(x, self.kernel.cast(x.dtype), b))
         y = torch.matmul(x, self.kernel.cast(x.dtype))
@@ -278,6 +279,20 @@ class Dense(Layer):
         return dict(super().get_config(), units=self.units, activation=_act.serialize(self.activation),
                     use_bias=self.use_bias, kernel_initializer=_init.serialize(self.kernel_initializer),
                     bias_initializer=_init.serialize(self.bias_initializer))
+
+
+def _autocast_input(x):
+    """Keras mixed precision: a layer casts its floating-point inputs to its compute dtype.  Under
+    the ``mixed_bfloat16`` policy (bf16 autocast on the GPU) an f32 batch straight from the input
+    pipeline therefore reaches the first Conv2D as bf16 and runs on the hand-written kernels.
+    Without this cast it went to MIOpen under autocast, whose find-mode solver choice depends on
+    timing: the first layer's output -- and, amplified over BN steps, the whole training run --
+    then differed between runs and between asynchronous and HIP_LAUNCH_BLOCKING=1 execution
+    (scripts/diag_checksums.py, profiles/generic_determinism_r4.txt)."""
+    if (isinstance(x, torch.Tensor) and x.is_cuda and x.dtype == torch.float32 and torch.is_autocast_enabled("cuda")
+            and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+        return x.to(torch.bfloat16)
+    return x
 
 
 def _same_pads(in_size, k, s, d=1):
@@ -343,8 +358,7 @@ class Conv2D(Layer):
                     y = y + self.bias.value.to(y.dtype)
                 return self.activation(y)
             x = F.pad(x, (0, 0, pl, pr, pt, pb))
-        # (1x1 convs stay on MIOpen: routing them through hipBLASLt GEMMs measured slower on MI355X,
-        #  scripts/probe_1x1_gemm.py)
+        x = _autocast_input(x)
         gt = None
         if _conv.supported(x, self.kernel.value, self.groups, self.dilation_rate):
             gt = self.kernel.grad_target()
@@ -376,7 +390,8 @@ class Conv2D(Layer):
             y = _conv.conv2d_nhwc(x, k_hwio, self.strides, pad if pad else (0, 0), grad_out=gt,
                                   w_ohwi=self.kernel.compute_view_ohwi(x.dtype) if gt is not None else None,
                                   grad_box=_grad_box, bn_stats=_bn_stats, bn_src=getattr(x, "_tdl_bn_src", None),
-                                  bn_src2=getattr(x, "_tdl_bn_src2", None))
+                                  bn_src2=getattr(x, "_tdl_bn_src2", None),
+                                  anchor=self.kernel.value if gt is not None else None)
             if b is not None:
                 y = y + b
             return self.activation(y)

@@ -128,6 +128,9 @@ class Model(Layer):
                 fp = None
         boxes = {}  # id(tensor) -> GradBox of its two consumers' backward contributions
         self.__dict__["_grad_boxes"] = boxes
+        from ..utils import checksums as _ck
+
+        ck = _ck.enabled()
         for n in self._nodes:
             if fp is not None:
                 nid = id(n)
@@ -138,6 +141,10 @@ class Model(Layer):
                     from .fusion import run_group
 
                     run_group(g, vals, training, fp.taps.get(nid), boxes)
+                    if ck:
+                        tag = f"group:{g.bn_node.layer.name}"
+                        _ck.record(tag, vals[id(g.out)])
+                        _ck.hook_grad(tag, vals[id(g.out)])
                     continue
             kw = {k: v for k, v in n.kwargs.items() if k != "training"}
             src = n.inputs
@@ -161,6 +168,10 @@ class Model(Layer):
             else:
                 args = _map(lambda t: vals[id(t)], src)
             out = n.layer(args, training=training, **kw)
+            if ck:
+                _ck.record_tree(f"node:{n.layer.name}", out)
+                if isinstance(out, torch.Tensor):
+                    _ck.hook_grad(f"node:{n.layer.name}", out)
             if isinstance(n.outputs, list):
                 for t, o in zip(n.outputs, out):
                     vals[id(t)] = o
@@ -394,6 +405,8 @@ class Model(Layer):
         handler.new_iterator()
         exhausted = False
         logs = {}
+        from ..utils import fault as _fault
+
         for epoch in range(initial_epoch, epochs):
             self._current_epoch = epoch
             trainer.reset_metrics()
@@ -419,7 +432,9 @@ class Model(Layer):
                 if self.stop_training:
                     break
             cb_list.params["seen_steps"] = done
+            _fault.note_progress(busy=True)  # the log read waits on the device and on peers
             logs = dict(trainer.logs())
+            _fault.note_progress(busy=False)  # callbacks (chief checkpoints, validation) run now
             if validation_data is not None and (epoch + 1) % validation_freq == 0:
                 val = self.evaluate(validation_data if isinstance(validation_data, D.Dataset) else
                                     validation_data[0], None if isinstance(validation_data, D.Dataset) else
@@ -438,6 +453,7 @@ class Model(Layer):
             if self.stop_training:
                 break
         trainer.finish()
+        _fault.note_progress(busy=False)
         if hasattr(handler, "close"):  # stop an index producer, commit the epochs it consumed
             handler.close()
         if os.environ.get("TDL_CHECK_REPLICAS", "1") == "1":
@@ -796,6 +812,7 @@ def _run_guarded(trainer, handler, n, strategy, model=None):
     from ..utils.tracing import trace_range
 
     wd = getattr(strategy.extended, "watchdog", None)
+    fault.note_progress(busy=True)
     try:
         with trace_range(f"tdl.execution[{n} steps]"):
             got = trainer.run_train(handler, n)
@@ -808,6 +825,7 @@ def _run_guarded(trainer, handler, n, strategy, model=None):
                 wd.acknowledged = True
                 raise fault.PeerLostError(f"{wd.reason} (collective failed: {e})") from e
         raise
+    fault.note_progress(count=int(trainer.optimizer.iterations))
     fault.check()
     fault.maybe_inject(strategy.extended.rank, int(trainer.optimizer.iterations))
     if model is not None:

@@ -108,6 +108,41 @@ _PREFER_HIP = float(os.environ.get("TDL_CONV_PREFER_HIP", "1.05"))
 _HBM_BYTES_PER_MS = 4.5e9  # streaming rate the BN/add kernels reach on MI355X (profiles/bn_tuning_sweep_r2.jsonl)
 
 
+# the job's communicator while a multi-replica trainer runs (engine/trainer.py binds it): rank 0
+# makes every autotuning decision and broadcasts it, so that all replicas run the same kernel set
+# (the same numerics, the same step time) instead of timing candidates each on its own
+_COMM = [None]
+_FALLBACK_LOGGED: set = set()
+
+
+def bind_communicator(comm) -> None:
+    _COMM[0] = comm if comm is not None and getattr(comm, "world_size", 1) > 1 else None
+
+
+def _capture_fallback(key) -> None:
+    """A shape first met inside a graph capture cannot be timed (nor agreed on collectively): it
+    runs on the library path.  Say so once per shape instead of going silent."""
+    if key not in _FALLBACK_LOGGED:
+        _FALLBACK_LOGGED.add(key)
+        import warnings
+
+        warnings.warn(f"conv autotuner: {key[0]} shape {key[1:]} first seen inside a hipGraph capture; "
+                      "using MIOpen for it (run one eager step of every shape before capturing)")
+
+
+def _agree(local_decide, encode, decode):
+    """Rank 0 decides (``local_decide``), every rank gets rank 0's decision.  Collective: every
+    replica reaches the same key at the same point of the same model's first eager step."""
+    comm = _COMM[0]
+    if comm is None:
+        return local_decide()
+    v = local_decide() if comm.rank == 0 else None
+    on = comm.device if getattr(comm, "name", "") == "rccl" else torch.device("cpu")
+    t = torch.tensor(encode(v) if v is not None else [0, 0, 0, 0], dtype=torch.int64, device=on)
+    comm.broadcast(t, 0)
+    return decode(t.tolist())
+
+
 def _pick(key, hip_fn, ref_fn, saved_bytes: int = 0) -> bool:
     """``saved_bytes``: HBM traffic of the passes the hand-written kernel's fused epilogue removes
     (BN statistics, gradient sums) that the library path would still run; credited to it."""
@@ -118,12 +153,17 @@ def _pick(key, hip_fn, ref_fn, saved_bytes: int = 0) -> bool:
     if got is not None:
         return got
     if torch.cuda.is_current_stream_capturing():
+        _capture_fallback(key)
         return False
-    t_ref = _time(ref_fn) + saved_bytes / _HBM_BYTES_PER_MS
-    t_hip = _time(hip_fn)
-    got = t_hip < t_ref * _PREFER_HIP
+
+    def decide():
+        t_ref = _time(ref_fn) + saved_bytes / _HBM_BYTES_PER_MS
+        t_hip = _time(hip_fn)
+        _times[key] = (t_hip, t_ref)
+        return t_hip < t_ref * _PREFER_HIP
+
+    got = _agree(decide, lambda v: [int(v), 0, 0, 0], lambda a: bool(a[0]))
     _choice[key] = got
-    _times[key] = (t_hip, t_ref)
     return got
 
 
@@ -141,17 +181,22 @@ def _pick_wgrad(key, C, x, dy, kh, kw, stride, pad, ref_fn):
         _choice[key] = plans[0]
         return plans[0]
     if torch.cuda.is_current_stream_capturing():
+        _capture_fallback(key)
         return None
-    t_ref = _time(ref_fn)
-    best, t_best = None, float("inf")
-    for p in plans:
-        t = _time(lambda: C.conv_wgrad(x, dy, kh, kw, stride[0], stride[1], pad[0], pad[1], plan=p))
-        if t < t_best:
-            best, t_best = p, t
-    if not t_best < t_ref * _PREFER_HIP:
-        best = None
+
+    def decide():
+        t_ref = _time(ref_fn)
+        best, t_best = None, float("inf")
+        for p in plans:
+            t = _time(lambda: C.conv_wgrad(x, dy, kh, kw, stride[0], stride[1], pad[0], pad[1], plan=p))
+            if t < t_best:
+                best, t_best = p, t
+        _times[key] = (t_best, t_ref)
+        return best if t_best < t_ref * _PREFER_HIP else None
+
+    best = _agree(decide, lambda v: [1] + [int(u) for u in v] if v is not None else [0, 0, 0, 0],
+                  lambda a: [int(u) for u in a[1:]] if a[0] else None)
     _choice[key] = best
-    _times[key] = (t_best, t_ref)
     return best
 
 
@@ -167,7 +212,7 @@ def _ref_fwd(x, w_oihw, stride, pad):
 class _Conv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, kernel, stride, pad, grad_out, w_ohwi=None, box=None, stats_out=None, bn_src=None,
-                bn_src2=None):
+                bn_src2=None, anchor=None):
         C = hip()
         x = x.contiguous()
         if x.data_ptr() % 16:
@@ -296,7 +341,7 @@ class _Conv(torch.autograd.Function):
             dx = dx + other.view_as(dx)
         if first:  # park this contribution for the other consumer's backward
             box.g, dx = dx, None
-        return dx, dw, None, None, None, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None, None, None, None
 
 
 _DEBUG_PARTS = os.environ.get("TDL_DEBUG_BN_PARTS") == "1"
@@ -329,7 +374,7 @@ def _miopen_bwd(dy_nchw, x_nchw, w_oihw, stride, pad, mask):
 
 
 def conv2d_nhwc(x, kernel_hwio, stride=(1, 1), pad=(0, 0), grad_out=None, w_ohwi=None, grad_box=None,
-                bn_stats=False, bn_src=None, bn_src2=None):
+                bn_stats=False, bn_src=None, bn_src2=None, anchor=None):
     """y[N,OH,OW,K] = conv(x[N,H,W,C], kernel[KH,KW,C,K]) with symmetric zero padding ``pad = (ph, pw)``,
     bf16; the caller checked :func:`supported`.  ``grad_out``: f32 [KH,KW,C,K] tensor the weight
     gradient is added into (a trainer's gradient slab view; ``kernel_hwio`` then needs no autograd);
@@ -341,9 +386,12 @@ def conv2d_nhwc(x, kernel_hwio, stride=(1, 1), pad=(0, 0), grad_out=None, w_ohwi
     gradient is the complete gradient of x (second GradBox participant), its epilogue also applies
     the group's ReLU mask and reduces the group's BN backward sums; ``bn_src2``: the input of the
     plain (projection-shortcut) BN whose output is that group's residual: the same epilogue reduces
-    its backward sums too."""
+    its backward sums too.  ``anchor``: with ``grad_out``, the variable's leaf tensor, so that the
+    backward runs although neither the input (the first layer's batch) nor the detached compute-dtype
+    kernel needs a gradient (the kernel's gradient goes into ``grad_out``; the anchor gets none)."""
     holder = [None] if bn_stats else None
-    y = _Conv.apply(x, kernel_hwio, tuple(stride), tuple(pad), grad_out, w_ohwi, grad_box, holder, bn_src, bn_src2)
+    y = _Conv.apply(x, kernel_hwio, tuple(stride), tuple(pad), grad_out, w_ohwi, grad_box, holder, bn_src, bn_src2,
+                    anchor)
     if holder is not None and holder[0] is not None:
         y._tdl_bn_part = holder[0]
     return y

@@ -49,7 +49,7 @@ def dense_supported(x: torch.Tensor, units: int) -> bool:
 
 class _Dense(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, targets):
+    def forward(ctx, x, w, b, targets, anchor=None):
         C = hip()
         x = _aligned(x)
         wc = _aligned(w)
@@ -78,13 +78,15 @@ class _Dense(torch.autograd.Function):
                 gb_t.add_(s)
             elif ctx.needs_input_grad[2]:
                 db = s
-        return dx, dw, db, None
+        return dx, dw, db, None, None
 
 
-def dense_bf16(x, w, b=None, targets=None):
+def dense_bf16(x, w, b=None, targets=None, anchor=None):
     """``x [N, in] bf16 @ w [in, out] bf16 (+ b f32)`` -> bf16 [N, out].  ``targets = (dW, db)``:
-    f32 slab views the gradients are added into (``w`` / ``b`` then need no autograd)."""
-    return _Dense.apply(x, w, b, targets)
+    f32 slab views the gradients are added into (``w`` / ``b`` then need no autograd).  ``anchor``:
+    with targets, the kernel variable's leaf, so that the backward runs when nothing else needs a
+    gradient (a first layer reading the input batch)."""
+    return _Dense.apply(x, w, b, targets, anchor)
 
 
 class _SoftmaxXent(torch.autograd.Function):

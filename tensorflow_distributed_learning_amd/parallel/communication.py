@@ -12,8 +12,23 @@ accepted.  Mapping on this framework:
 from __future__ import annotations
 
 import enum
+import os
 from dataclasses import dataclass
 from typing import Optional
+
+
+def default_timeout() -> float:
+    """Seconds a collective may wait for its peers before the job fails (process-group timeout,
+    the xGMI kernels' bounded waits, the progress watchdog).  TF's collectives wait for ever; a
+    synchronous job whose peer is live but out of step should end in about two minutes, not the
+    30 of torch's default.  ``TDL_COLLECTIVE_TIMEOUT`` overrides; ``CommunicationOptions.timeout_seconds``
+    overrides per strategy."""
+    return float(os.environ.get("TDL_COLLECTIVE_TIMEOUT", "120"))
+
+
+def collective_timeout(opts) -> float:
+    t = getattr(opts, "timeout_seconds", None)
+    return float(t) if t else default_timeout()
 
 
 class CommunicationImplementation(enum.Enum):

@@ -129,8 +129,12 @@ class TorchCommunicator(Communicator):
     """torch.distributed process group (``nccl`` = RCCL over xGMI, or ``gloo``)."""
 
     def __init__(self, backend: str, rank: int, world_size: int, device: torch.device, store=None,
-                 timeout: float = 1800.0, init: bool = True):
+                 timeout: Optional[float] = None, init: bool = True):
         super().__init__(rank, world_size, device)
+        from .communication import default_timeout
+
+        timeout = float(timeout or default_timeout())
+        self.timeout = timeout
         self.backend = backend
         self.name = "rccl" if backend == "nccl" else backend
         self.capturable = backend == "nccl"
@@ -150,9 +154,10 @@ class TorchCommunicator(Communicator):
             self._owns_group = True
         self._avg_native = backend == "nccl"
         self.xgmi = None  # parallel/xgmi.py one-shot path for small f32 messages (single node)
+        self.xgmi_reason = ""  # why the xGMI path was dropped (bench.py reports it)
         self.algorithm = "ring" if backend == "gloo" else "rccl"
 
-    def enable_xgmi(self) -> bool:
+    def enable_xgmi(self, timeout: Optional[float] = None) -> bool:
         """Route small f32 sum/mean all-reduces through the xGMI one-shot kernel when every rank
         is on this node (collective; the self-test runs on the first prepared channel).  Over a
         gloo group (replica processes sharing one GPU, where RCCL cannot run) the kernel is the
@@ -164,7 +169,8 @@ class TorchCommunicator(Communicator):
         if not xgmi.single_node():
             return False
         ctrl = self.device if self.backend == "nccl" else torch.device("cpu")
-        self.xgmi = xgmi.XgmiAllReduce(self.rank, self.world_size, self.device, ctrl_device=ctrl)
+        self.xgmi = xgmi.XgmiAllReduce(self.rank, self.world_size, self.device, ctrl_device=ctrl,
+                                       timeout=timeout or self.timeout)
         # over gloo the kernel is the only device data plane: messages above its limit go in chunks
         self.xgmi.chunked = self.backend != "nccl"
         return True
@@ -178,6 +184,7 @@ class TorchCommunicator(Communicator):
                 self.algorithm = ("xgmi-twoshot+" if two else "xgmi-oneshot+") + \
                     ("rccl" if self.backend == "nccl" else self.backend)
             else:
+                self.xgmi_reason = self.xgmi.reason or "disabled"
                 self.xgmi = None
 
     def all_reduce_sgd(self, g, w, lr):

@@ -30,6 +30,8 @@ from .communication import (
     CollectiveCommunication,
     CommunicationImplementation,
     CommunicationOptions,
+    collective_timeout,
+    default_timeout,
     normalize_options,
 )
 from .communicator import Communicator, LocalCommunicator, RingCommunicator, TorchCommunicator
@@ -323,10 +325,11 @@ class _DefaultStrategy(Strategy):
 
 # ------------------------------------------------------------------------------------------------
 def _select_communicator(impl: CommunicationImplementation, device: torch.device, rank: int, world: int,
-                         store=None, host_hint: str = "127.0.0.1", timeout: float = 1800.0,
+                         store=None, host_hint: str = "127.0.0.1", timeout: Optional[float] = None,
                          prefer_native_ring: bool = True) -> Communicator:
     if world == 1:
         return LocalCommunicator(device)
+    timeout = float(timeout or default_timeout())
     gpu = device.type == "cuda"
     if impl == CommunicationImplementation.NCCL and not gpu:
         raise ValueError("CollectiveCommunication.NCCL (RCCL) requires GPU replicas; this replica is on the CPU")
@@ -354,11 +357,11 @@ def _select_communicator(impl: CommunicationImplementation, device: torch.device
             dist.init_process_group("gloo", rank=rank, world_size=world)
         comm = TorchCommunicator("gloo", rank, world, device, store=None if dist.is_initialized() else store,
                                  timeout=timeout)
-        comm.enable_xgmi()
+        comm.enable_xgmi(timeout)
         return comm
     comm = TorchCommunicator("nccl", rank, world, device, store=store, timeout=timeout)
     if impl != CommunicationImplementation.NCCL:  # AUTO: topology/size-aware algorithm choice
-        comm.enable_xgmi()
+        comm.enable_xgmi(timeout)
     return comm
 
 
@@ -405,7 +408,7 @@ class MirroredStrategy(Strategy):
             if dev.type == "cuda":
                 torch.cuda.set_device(dev)
             comm = _select_communicator(opts.implementation, dev, launched["rank"], launched["world_size"],
-                                        timeout=opts.timeout_seconds or 1800.0)
+                                        timeout=collective_timeout(opts))
             ext = StrategyExtended(self, dev, launched["rank"], launched["world_size"], lr, comm, opts)
         super().__init__(ext)
         if ext.world_size > 1:
@@ -466,7 +469,7 @@ class MultiWorkerMirroredStrategy(Strategy):
             local = _LocalPlacement.resolve(launched, gpus_per_worker)
             rank, world, lr, dev = local
             comm = _select_communicator(opts.implementation, dev, rank, world,
-                                        timeout=opts.timeout_seconds or 1800.0) if world > 1 else LocalCommunicator(dev)
+                                        timeout=collective_timeout(opts)) if world > 1 else LocalCommunicator(dev)
             if world > 1:
                 from ..cluster.liveness import start_for_process_group
 
@@ -488,7 +491,7 @@ class MultiWorkerMirroredStrategy(Strategy):
             rank, world = layout.rank, layout.world_size
             host_hint = cfg.task_address[0] if cfg.task_address else "127.0.0.1"
             comm = _select_communicator(opts.implementation, dev, rank, world, store=rendezvous.store,
-                                        host_hint=host_hint, timeout=opts.timeout_seconds or 1800.0)
+                                        host_hint=host_hint, timeout=collective_timeout(opts))
         ext = StrategyExtended(self, dev, rank, world, lr, comm, opts, tf_config=cfg, rendezvous=rendezvous)
         ext.watchdog = watchdog
         super().__init__(ext, cluster_resolver=resolver)

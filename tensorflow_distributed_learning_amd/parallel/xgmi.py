@@ -46,7 +46,8 @@ def choose_algo(numel: int, world: int) -> int:
 class XgmiAllReduce:
     """Channel manager of one process group (every rank on this node, one GPU each)."""
 
-    def __init__(self, rank: int, world: int, device: torch.device, group=None, ctrl_device=None):
+    def __init__(self, rank: int, world: int, device: torch.device, group=None, ctrl_device=None,
+                 timeout: Optional[float] = None):
         from .. import ops
 
         self.C = ops.hip()
@@ -55,8 +56,13 @@ class XgmiAllReduce:
         self.ctrl = torch.device(ctrl_device) if ctrl_device is not None else self.device
         # bounded in-kernel waits: a peer that does not arrive within this many seconds sets the
         # device's error word; every later exchange then returns at entry and the host raises at the
-        # next health check (log read / execution boundary)
-        self.timeout = float(os.environ.get("TDL_XGMI_TIMEOUT", "60"))
+        # next health check (log read / execution boundary).  Default: the job's collective timeout
+        # (the process group's), so a slow but live peer is no more fatal here than under RCCL
+        if timeout is None:
+            from .communication import default_timeout
+
+            timeout = default_timeout()
+        self.timeout = float(os.environ.get("TDL_XGMI_TIMEOUT", timeout))
         self.limit = max_bytes() // 4
         self._chans: Dict[int, object] = {}
         self._selftest_chans = []
@@ -245,13 +251,27 @@ class XgmiAllReduce:
             ch.all_reduce_sgd(gf[o:o + c], wf[o:o + c], lr, 1.0)
         return True
 
+    def _any_channel(self):
+        for group in (list(self._chans.values()), self._dedicated, self._selftest_chans):
+            if group:
+                return group[0]
+        return None
+
+    def error(self) -> bool:
+        """Whether any xGMI kernel on this device timed out waiting for a peer (host sync; one
+        error word per device, shared by every channel: any channel reads it)."""
+        ch = self._any_channel()
+        return bool(ch is not None and ch.error())
+
     def check(self) -> None:
         """Raise if any kernel of this rank timed out waiting for a peer (host sync)."""
-        for n, ch in self._chans.items():  # (one error word per device, shared by every channel)
-            if ch.error():
-                raise RuntimeError(f"xgmi all-reduce: a peer did not arrive within {self.timeout:.0f} s "
-                                   f"(channel of {n} elements); the job's ranks are out of step or one died")
-            break
+        if self.error():
+            raise RuntimeError(f"xgmi all-reduce: a peer did not arrive within {self.timeout:.0f} s; "
+                               "the job's ranks are out of step or one died")
+
+    def disable(self, reason: str) -> None:
+        """Stop routing collectives through the kernel (every rank must call this at the same point)."""
+        self.ok, self.reason = False, reason
 
     def close(self) -> None:
         self._chans.clear()

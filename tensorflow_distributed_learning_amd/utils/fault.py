@@ -80,6 +80,34 @@ def maybe_corrupt(rank: int, step: int, slab) -> bool:
     return True
 
 
+def maybe_skip_collective(rank: int, step: int) -> bool:
+    """Fault injection hook: ``TDL_FAULT_SKIP_ALLREDUCE_AT_STEP="rank:step"`` makes that rank leave
+    out its gradient all-reduce once (a live rank out of step with its peers: the hung-collective
+    case the progress watchdog and the collective timeouts must end)."""
+    spec = os.environ.get("TDL_FAULT_SKIP_ALLREDUCE_AT_STEP")
+    if not spec:
+        return False
+    r, s = (int(v) for v in spec.split(":"))
+    if r != rank or step != s:
+        return False
+    sys.stderr.write(f"[tdl] fault injection: rank {rank} skips its gradient all-reduce at step {step}\n")
+    sys.stderr.flush()
+    return True
+
+
+# this rank's training progress, published by its watchdog thread: [executions done, busy flag].
+# busy = the host is inside a training execution or its log read (waiting on the device or on
+# peers); a rank that stays busy without progressing for ``stall_after`` seconds is stuck
+_PROGRESS = [0, False]
+
+
+def note_progress(count: Optional[int] = None, busy: Optional[bool] = None) -> None:
+    if count is not None:
+        _PROGRESS[0] = int(count)
+    if busy is not None:
+        _PROGRESS[1] = bool(busy)
+
+
 def check() -> None:
     """Raise :class:`PeerLostError` if the job has been aborted."""
     w = _ACTIVE
@@ -91,13 +119,21 @@ def check() -> None:
 class PeerWatchdog:
     """Per-rank failure detector over the rendezvous store (see module docstring)."""
 
-    def __init__(self, rendezvous, interval: float = 0.5, stale_after: float = 60.0, grace: float = 30.0):
+    def __init__(self, rendezvous, interval: float = 0.5, stale_after: float = 60.0, grace: float = 30.0,
+                 stall_after: Optional[float] = None):
         from .. import ops
+        from ..parallel.communication import default_timeout
 
         self.rdv = rendezvous
         self.interval = float(interval)
         self.stale_after = float(stale_after)
         self.grace = float(grace)
+        # a live rank (heartbeat fine) stuck inside an execution: a collective a peer never joins,
+        # or a device wait that never ends (an all-reduce inside a replayed hipGraph is invisible
+        # to the process group's own timeout)
+        self.stall_after = float(os.environ.get("TDL_STALL_TIMEOUT", stall_after or default_timeout()))
+        self._published = None
+        self._seen = {}  # chief: rank -> (progress record, monotonic time it last changed)
         self.reason: Optional[str] = None
         self.acknowledged = False
         self._stop = threading.Event()
@@ -134,7 +170,40 @@ class PeerWatchdog:
         stale = self.rdv.dead_peers(self.stale_after)
         if stale:
             return f"no heartbeat from {', '.join(sorted('rank ' + c[3:] for c in stale))} for {self.stale_after:.0f}s"
-        return None
+        return self._stall_scan()
+
+    def _publish_progress(self):
+        rec = f"{_PROGRESS[0]} {int(_PROGRESS[1])}"
+        if rec != self._published:
+            self._client.set(f"progress/{self.rank}", rec.encode())
+            self._published = rec
+
+    def _stall_scan(self) -> Optional[str]:
+        """Chief: ranks busy in an execution whose progress record has not changed for
+        ``stall_after`` seconds."""
+        if self.stall_after <= 0:
+            return None
+        now = time.monotonic()
+        stuck, counts = [], {}
+        for r in range(self.world):
+            key = f"progress/{r}"
+            if not self._client.check([key]):
+                continue
+            rec = bytes(self._client.get(key)).decode()
+            prev = self._seen.get(r)
+            if prev is None or prev[0] != rec:
+                self._seen[r] = (rec, now)
+                prev = self._seen[r]
+            n, busy = rec.split()
+            counts[r] = int(n)
+            if busy == "1" and now - prev[1] > self.stall_after:
+                stuck.append(r)
+        if not stuck:
+            return None
+        where = ", ".join(f"rank {r} at execution {counts[r]}" for r in stuck)
+        others = ", ".join(f"rank {r}: {c}" for r, c in sorted(counts.items()) if r not in stuck)
+        return (f"no training progress for {self.stall_after:.0f}s on {where} (heartbeats alive: a collective a peer "
+                f"never joined, or a hung device wait){'; ' + others if others else ''}")
 
     def _abort(self, reason: str):
         if self.reason is None:
@@ -147,6 +216,7 @@ class PeerWatchdog:
         while not self._stop.wait(self.interval):
             if self.reason is None:
                 try:
+                    self._publish_progress()
                     if self.rdv.server is not None:
                         why = self._chief_scan()
                         if why is not None:

@@ -210,3 +210,30 @@ def test_unsupervised_ranks_detect_a_dead_peer(tmp_path):
         assert rc != 0, e[-2000:]
         assert "rank 1" in e or "PeerLost" in e or "peer" in e.lower(), e[-2000:]
     assert time.time() - t0 < 60
+
+
+def test_live_rank_out_of_step_ends_the_job(tmp_path):
+    """A LIVE rank that leaves out one gradient all-reduce (heartbeats keep coming): the ranks'
+    collectives no longer pair up, and the progress watchdog (utils/fault.py, a rank busy in an
+    execution without progress for TDL_STALL_TIMEOUT) or the collective timeout must end every
+    rank non-zero -- no 30-minute hang."""
+    script = tmp_path / "job.py"
+    script.write_text(textwrap.dedent(MIRRORED.replace('"/cpu:2"], ', '], ')))
+    port = _ports(1)[0]
+    procs = []
+    for r in range(2):
+        env = _cpu_env(TDL_FAULT_SKIP_ALLREDUCE_AT_STEP="1:6", RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r),
+                       LOCAL_WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TDL_LAUNCHED="1",
+                       TDL_STALL_TIMEOUT="8", TDL_COLLECTIVE_TIMEOUT="40")
+        procs.append(subprocess.Popen([sys.executable, str(script), str(tmp_path)], cwd=ROOT, env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    _pids(tmp_path, 2)
+    t0 = time.time()
+    outs = _finish(procs, timeout=150)
+    assert "skips its gradient all-reduce" in outs[1][2]
+    for r in range(2):
+        rc, _, e = outs[r]
+        assert rc != 0, e[-2000:]
+    assert any("no training progress" in e or "replica" in e.lower() or "timed out" in e.lower()
+               for _, _, e in outs), [e[-1500:] for _, _, e in outs]
+    assert time.time() - t0 < 90

@@ -50,7 +50,8 @@ w = np.concatenate([v.ravel() for v in m.get_weights()]).astype(np.float64)
 rank = strategy.extended.rank
 np.save(os.path.join(out, f"w{rank}_{R}.npy"), w)
 comm = strategy.extended.communicator
-json.dump({"loss": hist.history["loss"], "engine": tr.kind, "comm": comm.name,
+from tensorflow_distributed_learning_amd.ops import conv as CV
+json.dump({"choices": sorted([str(k), v] for k, v in CV.choices().items()), "loss": hist.history["loss"], "engine": tr.kind, "comm": comm.name,
            "algorithm": getattr(comm, "algorithm", comm.name), "buckets": tr.plan.n_buckets,
            "bucketed": tr._buckets is not None, "graphs": len(tr._graphs), "fired": len(getattr(tr, "_works", [])),
            "task": [strategy.extended.task_type, strategy.extended.task_id]},
@@ -58,10 +59,10 @@ json.dump({"loss": hist.history["loss"], "engine": tr.kind, "comm": comm.name,
 """
 
 
-def _run(tmp_path, args):
+def _run(tmp_path, args, conv="hip"):
     s = tmp_path / "job.py"
     s.write_text(textwrap.dedent(BODY))
-    env = dict(os.environ, PYTHONPATH=ROOT, TDL_SHARE_GPU="1", TDL_CONV="hip")
+    env = dict(os.environ, PYTHONPATH=ROOT, TDL_SHARE_GPU="1", TDL_CONV=conv)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "TF_CONFIG"):
         env.pop(k, None)
     r = subprocess.run([sys.executable, "-m", "tensorflow_distributed_learning_amd.launch"] + args + [str(s), str(tmp_path)],
@@ -98,3 +99,15 @@ def test_generic_config5_layout_two_workers_two_replicas(tmp_path, single):
     _run(tmp_path, ["--local-workers", "2", "--gpus-per-worker", "2"])
     res = _check(tmp_path, 4, single)
     assert [r["task"] for r in res] == [["worker", 0], ["worker", 0], ["worker", 1], ["worker", 1]]
+
+
+def test_autotune_decisions_identical_on_every_rank(tmp_path, single):
+    """TDL_CONV=auto with two replicas: rank 0 times the candidates and broadcasts every decision
+    (ops/conv.py _agree), so both replicas record the same kernel choice for every (direction,
+    shape) and stay bit-identical."""
+    _run(tmp_path, ["--nproc-per-node", "2"], conv="auto")
+    res = [json.load(open(tmp_path / f"r{i}_2.json")) for i in range(2)]
+    assert res[0]["choices"], "the autotuner made no decision"
+    assert res[0]["choices"] == res[1]["choices"]
+    ws = [np.load(tmp_path / f"w{i}_2.npy") for i in range(2)]
+    assert np.array_equal(ws[0], ws[1]), "replicas diverged"

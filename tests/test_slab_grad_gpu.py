@@ -195,39 +195,71 @@ def test_fused_bn_group_backward_in_conv_epilogue():
     np.testing.assert_allclose(hf.history["loss"], hu.history["loss"], rtol=1e-2)
 
 
-def test_fused_bn_backward_projection_shortcut_and_stride2(tmp_path):
+def _diag_run(cfg, steps):
+    """scripts/diag_bnfuse.py's ResNet-style model (projection shortcuts, stride-2 blocks, bf16,
+    SGD momentum), ``steps`` eager steps in this process: (weights, BN fused-backward modes used)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "scripts"))
+    from diag_bnfuse import run
+
+    from tensorflow_distributed_learning_amd.ops import batchnorm as B
+    from tensorflow_distributed_learning_amd.ops import conv as CV
+
+    old = {k: os.environ.get(k) for k in ("TDL_GRAPH_STEP", "TDL_CONV")}
+    m0 = dict(B.FUSED_BWD_MODES)
+    try:
+        m = run(*{"F": (False, False, False), "T": (True, True, True)}[cfg], steps)
+        modes = {k: B.FUSED_BWD_MODES[k] - m0[k] for k in m0}
+        return [np.array(w) for w in m.get_weights()], modes
+    finally:
+        CV._FUSE_BN_BWD[0] = CV._FUSE_BN_BWD_S2[0] = CV._FUSE_BN_BWD_SHORTCUT[0] = True
+        tdl.keras.mixed_precision.set_global_policy("float32")
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def test_fused_bn_backward_projection_shortcut_and_stride2():
     """ResNet conv blocks: the projection-shortcut BN's backward sums come from the same conv
     epilogue as the block output group's (part2), and a group read by two 1x1 stride-2 convs (the
     next stage's conv block) is reduced in the stride-2 input-gradient epilogue; training matches
-    the unfused path.  Each configuration trains in a fresh process (scripts/diag_bnfuse2.py) with
-    HIP_LAUNCH_BLOCKING=1: this small model's 2-step result differs between asynchronous and
-    launch-blocking execution by up to ~50 % in some BN betas, identically before this fusion
-    existed (commit df563a5; README "Known issues"), and in asynchronous mode it can come out either
-    way from run to run, which would mask what this test checks."""
-    import re
-    import subprocess
-
-    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "scripts", "diag_bnfuse2.py")
-    w, modes = {}, {}
-    for cfg in ("F", "T"):
-        out = str(tmp_path / f"w_{cfg}.npz")
-        env = dict(os.environ, HIP_LAUNCH_BLOCKING="1")
-        r = subprocess.run([sys.executable, script, cfg, out, "1"], capture_output=True, text=True, timeout=300,
-                           env=env)
-        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-        w[cfg] = np.load(out)
-        modes[cfg] = {int(k): int(v) for k, v in re.findall(r"(\d): (\d+)", r.stdout.split("fused_modes")[1].split("\n")[0])}
+    the unfused path.  Both configurations run in this process, asynchronously (the round-3
+    async-vs-launch-blocking difference was the first conv on MIOpen, keras/layers.py
+    _autocast_input)."""
+    wf, mf = _diag_run("F", 1)
+    wt, mt = _diag_run("T", 1)
     # one step: both shortcut BNs (mode 0); the outputs of blocks 1-3 (block 2's is read by the two
     # stride-2 convs of block 3); the 8 inner BN -> ReLU groups
-    assert modes["T"] == {0: 2, 1: 8, 2: 3}, modes
-    assert modes["F"] == {0: 0, 1: 0, 2: 0}, modes
+    assert mt == {0: 2, 1: 8, 2: 3}, mt
+    assert mf == {0: 0, 1: 0, 2: 0}, mf
     # (one SGD step: the epilogue sums run in another f32 order, and over more steps bf16
     # activations amplify that into tens of percent on the tiny BN betas of this model; one step
     # bounds the gradients themselves, at the direct-slab test's 5e-2)
-    for k in w["F"].files:
-        a, b = w["T"][k], w["F"][k]
+    for a, b in zip(wt, wf):
         scale = max(float(np.abs(b).max()), 1e-3)
-        np.testing.assert_allclose(a, b, atol=5e-2 * scale, rtol=2e-2, err_msg=k)
+        np.testing.assert_allclose(a, b, atol=5e-2 * scale, rtol=2e-2)
+
+
+def test_generic_engine_async_matches_launch_blocking_bitwise(tmp_path):
+    """Regression pin for the round-3 'async vs HIP_LAUNCH_BLOCKING=1' divergence: two momentum
+    steps of the BN-heavy model, fused BN backward on, asynchronous in this process (twice) and
+    launch-blocking in a subprocess, give bit-identical weights."""
+    import subprocess
+
+    a1, _ = _diag_run("T", 2)
+    a2, _ = _diag_run("T", 2)
+    out = str(tmp_path / "w_blocking.npz")
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "scripts", "diag_bnfuse2.py")
+    r = subprocess.run([sys.executable, script, "T", out, "2"], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, HIP_LAUNCH_BLOCKING="1"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    z = np.load(out)
+    b = [z[f"arr_{i}"] for i in range(len(z.files))]
+    assert len(a1) == len(a2) == len(b)
+    for i, (x, y, w) in enumerate(zip(a1, a2, b)):
+        assert np.array_equal(x, y), f"weight {i}: two asynchronous runs differ"
+        assert np.array_equal(x, w), f"weight {i}: asynchronous vs launch-blocking differ, max {np.abs(x - w).max()}"
 
 
 def test_conv_dgrad_s2_bn_epilogue_matches_reference():

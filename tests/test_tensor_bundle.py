@@ -65,3 +65,25 @@ def test_corruption_detected_and_json_index_still_read(tmp_path, monkeypatch):
     ck.write_bundle(prefix, {"a": torch.ones(8)})
     assert not TB.is_table(prefix + ".index")
     assert torch.equal(ck.read_bundle(prefix)["a"], torch.ones(8))
+
+
+def test_string_entries_listed_and_object_graph_skipped(tmp_path):
+    """TF2 bundles carry _CHECKPOINTABLE_OBJECT_GRAPH as a DT_STRING (7) tensor: list_variables
+    shows it, read_bundle skips it, and any other string tensor is refused by name."""
+    prefix = str(tmp_path / "tf2")
+    ck.write_bundle(prefix, {"dense/kernel": torch.ones(2, 3)})
+    kv = TB.read_table(prefix + ".index")
+    data_len = len(open(prefix + ".data-00000-of-00001", "rb").read())
+    blob = b"\x0a\x03obj"
+
+    def string_entry():
+        return TB._field_varint(1, 7) + TB._field_varint(4, data_len) + TB._field_varint(5, len(blob)) + \
+            TB._field_fixed32(6, TB.mask_crc(crc32c(blob)))
+    with open(prefix + ".data-00000-of-00001", "ab") as f:
+        f.write(blob)
+    TB.write_table(prefix + ".index", kv + [(b"_CHECKPOINTABLE_OBJECT_GRAPH", string_entry())])
+    assert dict(ck.list_variables(prefix))["_CHECKPOINTABLE_OBJECT_GRAPH"] == ()
+    assert set(ck.read_bundle(prefix)) == {"dense/kernel"}
+    TB.write_table(prefix + ".index", kv + [(b"vocab", string_entry())])
+    with pytest.raises(ValueError, match="vocab"):
+        ck.read_bundle(prefix)
