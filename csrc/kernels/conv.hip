@@ -120,6 +120,154 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return (uint16_t)(u >> 16);
 }
 
+// Epilogue shared by the conv kernels: the f32 accumulators (wave tile WTM x WTN at (wrow0, wcol0) of
+// the BM x BN workgroup tile, acc[i][j] = 16x16 subtile, lane = 4 adjacent channels of one pixel) are
+// rounded to bf16 into LDS ([BM][BN + 8], the operand LDS is free by now), then written back as 16-byte
+// row segments with the variant's fused operations (residual, BN statistics / BN-group backward sums,
+// stride-2 scatter).  Every thread of the workgroup must call it (it has workgroup barriers).
+template <int BM, int BN, int NT, int EK, int WTM, int WTN, int LDS_ELEMS>
+__device__ __forceinline__ void conv_epilogue(const Igemm& a, const f4v (&acc)[WTM / 16][WTN / 16], uint16_t* lds,
+                                              int tm, int tn, int wrow0, int wcol0) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  constexpr int OUT_LD = BN + 8;
+  constexpr int SEG = BN / 8;              // 16-B segments per row
+  constexpr int EPI = BM * SEG / NT;       // segments per thread
+  static_assert(BM * SEG % NT == 0, "epilogue segments must divide evenly");
+  // residual (gradient sum): all of this thread's loads issued here, before the LDS round trip, so
+  // their latency overlaps it instead of serialising the store loop
+  u32x4 rv[EK == 2 ? 1 : EPI];
+  if (EK != 2 && a.res) {
+#pragma unroll
+    for (int e = 0; e < EPI; ++e) {
+      const int s = tid + e * NT, row = s / SEG, seg = s % SEG, m = tm * BM + row;
+      rv[e] = m < a.M ? *reinterpret_cast<const u32x4*>(a.res + (long long)m * a.K + tn * BN + seg * 8)
+                      : u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+  static_assert(BM * OUT_LD <= LDS_ELEMS, "epilogue tile must fit the operand LDS");
+  // (operands are swapped in the MFMA, so a lane holds 4 consecutive channels of one pixel: one 8-B write)
+#pragma unroll
+  for (int i = 0; i < WTM / 16; ++i)
+#pragma unroll
+    for (int j = 0; j < WTN / 16; ++j) {
+      const uint32_t lo = f2bf(acc[i][j][0]) | ((uint32_t)f2bf(acc[i][j][1]) << 16);
+      const uint32_t hi = f2bf(acc[i][j][2]) | ((uint32_t)f2bf(acc[i][j][3]) << 16);
+      *reinterpret_cast<uint2*>(lds + (wrow0 + i * 16 + (lane & 15)) * OUT_LD + wcol0 + j * 16 + (lane >> 4) * 4) =
+          make_uint2(lo, hi);
+    }
+  // BN-backward fusion operands (the accumulators are dead now: registers to spare)
+  constexpr int BNE = EK == 1 ? EPI : 1;
+  u32x4 ry[BNE], rx[BNE], rx2[BNE];
+  if constexpr (EK == 1) {
+#pragma unroll
+    for (int e = 0; e < EPI; ++e) {
+      const int s = tid + e * NT, row = s / SEG, seg = s % SEG, m = tm * BM + row;
+      const long long o = (long long)m * a.K + tn * BN + seg * 8;
+      const bool in = m < a.M;
+      ry[e] = in ? *reinterpret_cast<const u32x4*>(a.bn_y + o) : u32x4{0u, 0u, 0u, 0u};
+      rx[e] = in ? *reinterpret_cast<const u32x4*>(a.bn_x + o) : u32x4{0u, 0u, 0u, 0u};
+      rx2[e] = (in && a.bn_x2) ? *reinterpret_cast<const u32x4*>(a.bn_x2 + o) : u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+  __syncthreads();
+  static_assert(NT % SEG == 0, "a thread keeps one 8-channel segment across its rows");
+  // per-tile channel sums: (y, y^2) of the forward output, or (dz, dz * xb) [and dz * xb2] of a fused
+  // BN group backward
+  float* sums = a.stats ? a.stats : (EK != 0 ? a.bn_part : nullptr);
+  float* sums2 = (EK != 0 && a.bn_part) ? a.bn_part2 : nullptr;
+  float cs[8], cq[8], cq2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) cs[j] = cq[j] = cq2[j] = 0.f;
+  if constexpr (EK != 2) {
+#pragma unroll
+    for (int e = 0; e < EPI; ++e) {
+      const int s = tid + e * NT, row = s / SEG, seg = s % SEG;
+      const int m = tm * BM + row;
+      if (m < a.M) {
+        const long long o = (long long)m * a.K + tn * BN + seg * 8;
+        u32x4 v = *reinterpret_cast<const u32x4*>(lds + row * OUT_LD + seg * 8);
+        if (a.res) v = add_bf16x8(v, rv[e]);
+        if constexpr (EK == 1) v = relu_mask_bf16x8(v, ry[e]);
+        *reinterpret_cast<u32x4*>(a.y + o) = v;
+        if (sums) accum_bf16x8(v, EK == 1 ? rx[e] : v, cs, cq);
+        if constexpr (EK == 1)
+          if (sums2) dot_bf16x8(v, rx2[e], cq2);
+      }
+    }
+  } else {
+    for (int s = tid; s < BM * SEG; s += NT) {
+      const int row = s / SEG, seg = s % SEG;
+      const int m = tm * BM + row;
+      if (m >= a.M) continue;
+      const int ow = m % a.OW, t = m / a.OW, oh = t % a.OH, n = t / a.OH;
+      const int h = 2 * oh, w = 2 * ow;
+      const long long off = (((long long)n * a.XH + h) * a.XW + w) * a.K + tn * BN + seg * 8;
+      const long long rs = (long long)a.XW * a.K;
+      const bool w1 = w + 1 < a.XW, h1 = h + 1 < a.XH;
+      // the 2x2 block of dx pixels this output row owns: (2oh, 2ow) gets the computed gradient, the
+      // other three only the other contribution (or zeros)
+      const bool ok[4] = {true, w1, h1, w1 && h1};
+      const long long po[4] = {off, off + a.K, off + rs, off + rs + a.K};
+      const u32x4 z{0u, 0u, 0u, 0u};
+      u32x4 p[4];
+      // every load of the block issued before any math
+#pragma unroll
+      for (int q = 0; q < 4; ++q) p[q] = (a.res && ok[q]) ? *reinterpret_cast<const u32x4*>(a.res + po[q]) : z;
+      u32x4 by[4], bx[4], bx2[4];
+      if (a.bn_part) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          by[q] = ok[q] ? *reinterpret_cast<const u32x4*>(a.bn_y + po[q]) : z;
+          bx[q] = ok[q] ? *reinterpret_cast<const u32x4*>(a.bn_x + po[q]) : z;
+          bx2[q] = (ok[q] && a.bn_x2) ? *reinterpret_cast<const u32x4*>(a.bn_x2 + po[q]) : z;
+        }
+      }
+      const u32x4 v = *reinterpret_cast<const u32x4*>(lds + row * OUT_LD + seg * 8);
+      p[0] = a.res ? add_bf16x8(v, p[0]) : v;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (!ok[q]) continue;
+        if (a.bn_part) {
+          p[q] = relu_mask_bf16x8(p[q], by[q]);
+          accum_bf16x8(p[q], bx[q], cs, cq);
+          if (sums2) dot_bf16x8(p[q], bx2[q], cq2);
+        }
+        *reinterpret_cast<u32x4*>(a.y + po[q]) = p[q];
+      }
+    }
+  }
+  if (sums) {
+    // fixed-order reduction over the NT / SEG threads of each segment, through the (now free) LDS
+    constexpr int TPS = NT / SEG;  // threads per segment
+    static_assert(3 * TPS * BN * 4 <= LDS_ELEMS * 2, "stats scratch must fit the operand LDS");
+    
+    __syncthreads();  // every thread has read its tile rows
+    float* red = reinterpret_cast<float*>(lds);
+    const int seg = tid % SEG, grp = tid / SEG;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[grp * BN + seg * 8 + j] = cs[j];
+      red[TPS * BN + grp * BN + seg * 8 + j] = cq[j];
+      if (sums2) red[2 * TPS * BN + grp * BN + seg * 8 + j] = cq2[j];
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += NT) {
+      float S = 0.f, Q = 0.f, Q2 = 0.f;
+      for (int g2 = 0; g2 < TPS; ++g2) {
+        S += red[g2 * BN + c];
+        Q += red[TPS * BN + g2 * BN + c];
+        if (sums2) Q2 += red[2 * TPS * BN + g2 * BN + c];
+      }
+      sums[((long long)tm * 2) * a.K + tn * BN + c] = S;
+      sums[((long long)tm * 2 + 1) * a.K + tn * BN + c] = Q;
+      if (sums2) {
+        sums2[((long long)tm * 2) * a.K + tn * BN + c] = S;
+        sums2[((long long)tm * 2 + 1) * a.K + tn * BN + c] = Q2;
+      }
+    }
+  }
+}
+
 // EK selects the epilogue a variant carries (registers: the VGPR peak of the heaviest epilogue sets the
 // occupancy of the whole kernel, so the plain variant must not pay for the fused ones): 0 plain
 // (+ residual, + BN statistics), 1 fused BN-group backward, 2 stride-2 scatter (+ residual, + BN group)
@@ -273,142 +421,150 @@ __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
   }
 
   // epilogue: bf16 tile into LDS ([BM][BN + 8]), then 16-B row segments to global
-  constexpr int OUT_LD = BN + 8;
-  constexpr int SEG = BN / 8;              // 16-B segments per row
-  constexpr int EPI = BM * SEG / NT;       // segments per thread
-  static_assert(BM * SEG % NT == 0, "epilogue segments must divide evenly");
-  // residual (gradient sum): all of this thread's loads issued here, before the LDS round trip, so
-  // their latency overlaps it instead of serialising the store loop
-  u32x4 rv[EK == 2 ? 1 : EPI];
-  if (EK != 2 && a.res) {
+  conv_epilogue<BM, BN, NT, EK, 64, WN, 2 * (BM + BN) * LDS_ROW>(a, acc, lds, tm, tn, wm * 64, wn * WN);
+}
+
+// ---------------------------------------------------------------------------------------------
+// v2 main loop: 8 waves (512 threads), BM x BN x 64 tiles, a 3-stage LDS ring filled by LDS-DMA
+// (buffer_load_dwordx4 ... lds: no register staging, no ds_write pass), tile t+2's loads in flight
+// while tile t computes, ONE raw barrier per k-tile (counted vmcnt, never 0 in the loop).  The
+// LDS image is the v1 one (128-B rows, 16-B chunks XOR-swizzled by row): an LDS-DMA writes 64 lanes x
+// 16 B linearly, so the swizzle goes on the SOURCE address -- lane L of a wave-instruction covering
+// rows 8g .. 8g+7 writes slot L % 8 of row 8g + L / 8 and therefore fetches chunk (L % 8) ^ swz(row)
+// (cdna_hip_programming.md rule 21).  Out-of-image taps read voffset 0x80000000: the buffer's
+// range check lands zeros in LDS, exactly as the v1 loader's register zeros.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+constexpr int kV2Stages = 3;
+
+template <int BM, int BN>
+constexpr int v2_lds_elems() { return kV2Stages * (BM + BN) * LDS_ROW; }
+
+template <int BM, int BN, int WGM, int WGN, int EK>
+__global__ __launch_bounds__(512, 1) void k_conv_glds(Igemm a) {
+  constexpr int NT = 512;
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;  // wave tile
+  constexpr int MI = WTM / 16, NJ = WTN / 16;
+  constexpr int STAGE = (BM + BN) * LDS_ROW;      // bf16 elements per ring stage
+  constexpr int A_LD = BM / 64;                   // LDS-DMA wave-instructions (8 rows each) per thread, A
+  constexpr int B_LD = BN / 64;                   //                                              ..., B
+  static_assert(WGM * WGN == 8 && BM % 64 == 0 && BN % 64 == 0 && MI >= 1 && NJ >= 1, "v2 geometry");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[v2_lds_elems<BM, BN>()];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int ntn = a.K / BN;
+  const int tn = wg % ntn, tm = wg / ntn;
+
+  const long long bias = ((long long)a.PT * a.W + a.PL) * a.C;
+  const auto x_rsrc = buf_rsrc(a.x - bias, (unsigned)(((long long)a.N * a.H * a.W * a.C + bias) * 2));
+  const auto w_rsrc = buf_rsrc(a.w, (unsigned)((long long)a.KH * a.KW * a.C * a.K * 2));
+  // this lane's row inside each of its row groups, and the (source-swizzled) chunk it fetches
+  const int lrow = lane >> 3;
+  int a_vo[A_LD];
+  uint32_t a_tap[A_LD];
 #pragma unroll
-    for (int e = 0; e < EPI; ++e) {
-      const int s = tid + e * NT, row = s / SEG, seg = s % SEG, m = tm * BM + row;
-      rv[e] = m < a.M ? *reinterpret_cast<const u32x4*>(a.res + (long long)m * a.K + tn * BN + seg * 8)
-                      : u32x4{0u, 0u, 0u, 0u};
-    }
-  }
-  static_assert(BM * OUT_LD <= 2 * (BM + BN) * LDS_ROW, "epilogue tile must fit the operand LDS");
-  // (operands are swapped in the MFMA, so a lane holds 4 consecutive channels of one pixel: one 8-B write)
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < NS; ++j) {
-      const uint32_t lo = f2bf(acc[i][j][0]) | ((uint32_t)f2bf(acc[i][j][1]) << 16);
-      const uint32_t hi = f2bf(acc[i][j][2]) | ((uint32_t)f2bf(acc[i][j][3]) << 16);
-      *reinterpret_cast<uint2*>(lds + (wm * 64 + i * 16 + (lane & 15)) * OUT_LD + wn * WN + j * 16 + (lane >> 4) * 4) =
-          make_uint2(lo, hi);
-    }
-  // BN-backward fusion operands (the accumulators are dead now: registers to spare)
-  constexpr int BNE = EK == 1 ? EPI : 1;
-  u32x4 ry[BNE], rx[BNE], rx2[BNE];
-  if constexpr (EK == 1) {
-#pragma unroll
-    for (int e = 0; e < EPI; ++e) {
-      const int s = tid + e * NT, row = s / SEG, seg = s % SEG, m = tm * BM + row;
-      const long long o = (long long)m * a.K + tn * BN + seg * 8;
-      const bool in = m < a.M;
-      ry[e] = in ? *reinterpret_cast<const u32x4*>(a.bn_y + o) : u32x4{0u, 0u, 0u, 0u};
-      rx[e] = in ? *reinterpret_cast<const u32x4*>(a.bn_x + o) : u32x4{0u, 0u, 0u, 0u};
-      rx2[e] = (in && a.bn_x2) ? *reinterpret_cast<const u32x4*>(a.bn_x2 + o) : u32x4{0u, 0u, 0u, 0u};
-    }
-  }
-  __syncthreads();
-  static_assert(NT % SEG == 0, "a thread keeps one 8-channel segment across its rows");
-  // per-tile channel sums: (y, y^2) of the forward output, or (dz, dz * xb) [and dz * xb2] of a fused
-  // BN group backward
-  float* sums = a.stats ? a.stats : (EK != 0 ? a.bn_part : nullptr);
-  float* sums2 = (EK != 0 && a.bn_part) ? a.bn_part2 : nullptr;
-  float cs[8], cq[8], cq2[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) cs[j] = cq[j] = cq2[j] = 0.f;
-  if constexpr (EK != 2) {
-#pragma unroll
-    for (int e = 0; e < EPI; ++e) {
-      const int s = tid + e * NT, row = s / SEG, seg = s % SEG;
-      const int m = tm * BM + row;
-      if (m < a.M) {
-        const long long o = (long long)m * a.K + tn * BN + seg * 8;
-        u32x4 v = *reinterpret_cast<const u32x4*>(lds + row * OUT_LD + seg * 8);
-        if (a.res) v = add_bf16x8(v, rv[e]);
-        if constexpr (EK == 1) v = relu_mask_bf16x8(v, ry[e]);
-        *reinterpret_cast<u32x4*>(a.y + o) = v;
-        if (sums) accum_bf16x8(v, EK == 1 ? rx[e] : v, cs, cq);
-        if constexpr (EK == 1)
-          if (sums2) dot_bf16x8(v, rx2[e], cq2);
-      }
-    }
-  } else {
-    for (int s = tid; s < BM * SEG; s += NT) {
-      const int row = s / SEG, seg = s % SEG;
-      const int m = tm * BM + row;
-      if (m >= a.M) continue;
+  for (int i = 0; i < A_LD; ++i) {
+    const int row = (i * 8 + wave) * 8 + lrow;  // row group i*8 + wave
+    const int chunk = (lane & 7) ^ swz(row);
+    const int m = tm * BM + row;
+    a_tap[i] = 0u;
+    a_vo[i] = 0;
+    if (m < a.M) {
       const int ow = m % a.OW, t = m / a.OW, oh = t % a.OH, n = t / a.OH;
-      const int h = 2 * oh, w = 2 * ow;
-      const long long off = (((long long)n * a.XH + h) * a.XW + w) * a.K + tn * BN + seg * 8;
-      const long long rs = (long long)a.XW * a.K;
-      const bool w1 = w + 1 < a.XW, h1 = h + 1 < a.XH;
-      // the 2x2 block of dx pixels this output row owns: (2oh, 2ow) gets the computed gradient, the
-      // other three only the other contribution (or zeros)
-      const bool ok[4] = {true, w1, h1, w1 && h1};
-      const long long po[4] = {off, off + a.K, off + rs, off + rs + a.K};
-      const u32x4 z{0u, 0u, 0u, 0u};
-      u32x4 p[4];
-      // every load of the block issued before any math
-#pragma unroll
-      for (int q = 0; q < 4; ++q) p[q] = (a.res && ok[q]) ? *reinterpret_cast<const u32x4*>(a.res + po[q]) : z;
-      u32x4 by[4], bx[4], bx2[4];
-      if (a.bn_part) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          by[q] = ok[q] ? *reinterpret_cast<const u32x4*>(a.bn_y + po[q]) : z;
-          bx[q] = ok[q] ? *reinterpret_cast<const u32x4*>(a.bn_x + po[q]) : z;
-          bx2[q] = (ok[q] && a.bn_x2) ? *reinterpret_cast<const u32x4*>(a.bn_x2 + po[q]) : z;
-        }
-      }
-      const u32x4 v = *reinterpret_cast<const u32x4*>(lds + row * OUT_LD + seg * 8);
-      p[0] = a.res ? add_bf16x8(v, p[0]) : v;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (!ok[q]) continue;
-        if (a.bn_part) {
-          p[q] = relu_mask_bf16x8(p[q], by[q]);
-          accum_bf16x8(p[q], bx[q], cs, cq);
-          if (sums2) dot_bf16x8(p[q], bx2[q], cq2);
-        }
-        *reinterpret_cast<u32x4*>(a.y + po[q]) = p[q];
-      }
+      const int ih = oh * a.SH - a.PT, iw = ow * a.SW - a.PL;
+      a_vo[i] = (int)(((((long long)n * a.H + ih) * a.W + iw) * a.C + chunk * 8 + bias) * 2);
+      for (int kh = 0; kh < a.KH; ++kh)
+        for (int kw = 0; kw < a.KW; ++kw)
+          if ((unsigned)(ih + kh) < (unsigned)a.H && (unsigned)(iw + kw) < (unsigned)a.W) a_tap[i] |= 1u << (kh * a.KW + kw);
     }
   }
-  if (sums) {
-    // fixed-order reduction over the NT / SEG threads of each segment, through the (now free) LDS
-    constexpr int TPS = NT / SEG;  // threads per segment
-    static_assert(3 * TPS * BN * 4 <= 2 * (BM + BN) * LDS_ROW * 2, "stats scratch must fit the operand LDS");
-    __syncthreads();  // every thread has read its tile rows
-    float* red = reinterpret_cast<float*>(lds);
-    const int seg = tid % SEG, grp = tid / SEG;
+  int b_vo[B_LD];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      red[grp * BN + seg * 8 + j] = cs[j];
-      red[TPS * BN + grp * BN + seg * 8 + j] = cq[j];
-      if (sums2) red[2 * TPS * BN + grp * BN + seg * 8 + j] = cq2[j];
-    }
-    __syncthreads();
-    for (int c = tid; c < BN; c += NT) {
-      float S = 0.f, Q = 0.f, Q2 = 0.f;
-      for (int g2 = 0; g2 < TPS; ++g2) {
-        S += red[g2 * BN + c];
-        Q += red[TPS * BN + g2 * BN + c];
-        if (sums2) Q2 += red[2 * TPS * BN + g2 * BN + c];
-      }
-      sums[((long long)tm * 2) * a.K + tn * BN + c] = S;
-      sums[((long long)tm * 2 + 1) * a.K + tn * BN + c] = Q;
-      if (sums2) {
-        sums2[((long long)tm * 2) * a.K + tn * BN + c] = S;
-        sums2[((long long)tm * 2 + 1) * a.K + tn * BN + c] = Q2;
-      }
-    }
+  for (int i = 0; i < B_LD; ++i) {
+    const int row = (i * 8 + wave) * 8 + lrow;
+    const int chunk = (lane & 7) ^ swz(row);
+    b_vo[i] = (int)(((long long)(tn * BN + row) * a.w_col + chunk * 8) * 2);
   }
+
+  const int ctiles = a.C / BK;
+  const int ntiles = a.KH * a.KW * ctiles;
+  int n_c = 0, n_kw = 0, n_kh = 0;
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  auto issue = [&](int stage) {
+    const int c0 = n_c * BK, kw = n_kw, kh = n_kh;
+    if (++n_c == ctiles) {
+      n_c = 0;
+      if (++n_kw == a.KW) {
+        n_kw = 0;
+        ++n_kh;
+      }
+    }
+    const int tap = kh * a.KW + kw;
+    const int soff_a = (int)((((long long)kh * a.W + kw) * a.C + c0) * 2);
+    uint16_t* base = lds + stage * STAGE;
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+      const int vo = ((a_tap[i] >> tap) & 1u) ? a_vo[i] : (int)0x80000000;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(x_rsrc, (lds_ptr_t)(base + (i * 8 + wave) * 8 * LDS_ROW), 16, vo,
+                                               soff_a, 0, 0);
+    }
+    const int wkh = a.flip ? a.KH - 1 - kh : kh, wkw = a.flip ? a.KW - 1 - kw : kw;
+    const int soff_b = (int)((wkh * a.w_kh + wkw * a.w_kw + c0) * 2);
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(w_rsrc, (lds_ptr_t)(base + (BM + (i * 8 + wave) * 8) * LDS_ROW), 16,
+                                               b_vo[i], soff_b, 0, 0);
+  };
+
+  f4v acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  const int frow = lane & 15;
+  const int fk0 = ((lane >> 4) ^ swz(frow)) * 8, fk1 = (((lane >> 4) | 4) ^ swz(frow)) * 8;
+  auto compute = [&](int stage) {
+    const uint16_t* la = lds + stage * STAGE + (wm * WTM + frow) * LDS_ROW;
+    const uint16_t* lb = lds + stage * STAGE + (BM + wn * WTN + frow) * LDS_ROW;
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      const int fk = kk ? fk1 : fk0;
+      bf16x8 fa[MI], fb[NJ];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(la + i * 16 * LDS_ROW + fk);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(lb + j * 16 * LDS_ROW + fk);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  issue(0);
+  if (ntiles > 1) issue(1);
+  int st = 0;
+  for (int t = 0; t < ntiles; ++t) {
+    // tile t landed (this thread's loads: all but tile t+1's), every wave past tile t-1's reads
+    if (t + 1 < ntiles)
+      wait_vmcnt_barrier<A_LD + B_LD>();
+    else
+      wait_vmcnt_barrier<0>();
+    if (t + 2 < ntiles) issue(st == 0 ? 2 : st - 1);  // stage (t + 2) % 3 == stage (t - 1) % 3
+    compute(st);
+    st = st == 2 ? 0 : st + 1;
+  }
+  __syncthreads();  // every wave done reading the ring: the epilogue reuses it
+  conv_epilogue<BM, BN, NT, EK, WTM, WTN, v2_lds_elems<BM, BN>()>(a, acc, lds, tm, tn, wm * WTM, wn * WTN);
 }
 
 int g_depth = 2;  // register prefetch depth (tiles in flight); conv_force_depth for A/B sweeps
@@ -433,12 +589,35 @@ void launch_tile(const Igemm& a, hipStream_t s) {
 }
 
 int g_forced_tile = 0;  // 0: heuristic below; 1: 128 x 64, 2: 128 x 128, 3: 256 x 128 (tile sweeps)
+int g_impl = 2;         // 1: v1 register-staged kernel only; 2: the LDS-DMA ring kernel where it applies
+
+template <int BM, int BN, int WGM, int WGN>
+void launch_v2(const Igemm& a, hipStream_t s) {
+  const dim3 grid((a.M + BM - 1) / BM * (a.K / BN)), block(512);
+  if (a.scatter)
+    hipLaunchKernelGGL((k_conv_glds<BM, BN, WGM, WGN, 2>), grid, block, 0, s, a);
+  else if (a.bn_part)
+    hipLaunchKernelGGL((k_conv_glds<BM, BN, WGM, WGN, 1>), grid, block, 0, s, a);
+  else
+    hipLaunchKernelGGL((k_conv_glds<BM, BN, WGM, WGN, 0>), grid, block, 0, s, a);
+}
+
+// v2 (256-row tiles) where the grid still fills the chip: at least one workgroup per CU
+bool use_v2(int M, int K) {
+  if (g_impl != 2 || g_forced_tile != 0) return false;
+  const long long wgs = (long long)(M + 255) / 256 * (K % 128 == 0 ? K / 128 : K / 64);
+  return wgs >= 256;
+}
 
 // Tile choice, from the sweep over the ResNet-50 b=256 convolutions (profiles/conv_tile_sweep_r1.jsonl):
 // 128 x 128 wins every shape with K % 128 == 0, including the 7x7 ones whose grid is under two
 // workgroups per CU (the 64-column tile's extra LDS traffic per MFMA costs more than the idle CUs);
 // 256 x 128 loses 5-20 % everywhere.  The 64-column tile only serves K == 64 * odd.
 void launch(const Igemm& a, hipStream_t s) {
+  if (use_v2(a.M, a.K)) {
+    if (a.K % 128 == 0) return launch_v2<256, 128, 4, 2>(a, s);
+    return launch_v2<256, 64, 4, 2>(a, s);
+  }
   if (g_forced_tile == 3 && a.K % 128 == 0) return launch_tile<256, 128>(a, s);
   if (g_forced_tile == 1 || a.K % 128 != 0) return launch_tile<128, 64>(a, s);
   launch_tile<128, 128>(a, s);
@@ -447,6 +626,7 @@ void launch(const Igemm& a, hipStream_t s) {
 }  // namespace
 
 void conv_force_tile(int tile) { g_forced_tile = tile; }
+void conv_force_impl(int impl) { g_impl = impl == 1 ? 1 : 2; }
 void conv_force_depth(int depth) { g_depth = depth == 1 ? 1 : 2; }
 
 bool conv_bf16_supported(const ConvGeom& g) {
@@ -462,14 +642,21 @@ bool conv_bf16_supported(const ConvGeom& g) {
          (long long)g.KH * g.KW * g.C * g.K < two_gib_elems;
 }
 
+// the row tile launch() picks (the BN partial-sum rows of an epilogue are per row tile)
 int conv_fwd_row_tile(const ConvGeom& g) {
-  // the tile launch() picks for the forward (128 rows in every variant but the sweep-only 256)
+  if (use_v2(g.N * g.OH * g.OW, g.K)) return 256;
   return (g_forced_tile == 3 && g.K % 128 == 0) ? 256 : 128;
 }
 
-int conv_dgrad_row_tile(const ConvGeom& g) { return (g_forced_tile == 3 && g.C % 128 == 0) ? 256 : 128; }
+int conv_dgrad_row_tile(const ConvGeom& g) {
+  if (use_v2(g.N * g.H * g.W, g.C)) return 256;
+  return (g_forced_tile == 3 && g.C % 128 == 0) ? 256 : 128;
+}
 
-int conv_dgrad_s2_row_tile(const ConvGeom& g) { return (g_forced_tile == 3 && g.C % 128 == 0) ? 256 : 128; }
+int conv_dgrad_s2_row_tile(const ConvGeom& g) {
+  if (use_v2(g.N * g.OH * g.OW, g.C)) return 256;
+  return (g_forced_tile == 3 && g.C % 128 == 0) ? 256 : 128;
+}
 
 void conv_fwd_bf16(const void* x, const void* w_ohwi, void* y, const ConvGeom& g, hipStream_t s, float* stats) {
   Igemm a{static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w_ohwi), static_cast<uint16_t*>(y),

@@ -25,6 +25,7 @@
 // blockIdx -> (slice, tile) is XCD-aware: the tiles of one slice (which read the same dy and x
 // pixels) run on one XCD and share its L2.
 #include "kernels/conv.h"
+#include "kernels/common.h"
 
 #include <algorithm>
 #include <cmath>
@@ -225,6 +226,148 @@ __global__ __launch_bounds__(64 * WMW * WNW) __attribute__((amdgpu_waves_per_eu(
     }
 }
 
+// v2: 8 waves (2 per SIMD, one workgroup per CU), a 3-stage LDS ring filled by LDS-DMA
+// (buffer_load_dwordx4 ... lds), stage st+2's loads in flight while stage st computes, one raw
+// barrier per stage.  Wave w stages pixel rows 8w .. 8w+7 of EVERY sub-image (one 1-KiB LDS-DMA
+// wave-instruction each), so a lane decomposes its pixel once per stage for all of its loads.  The
+// LDS image is the v1 one (fswz-swizzled 128-B rows), produced by swizzling the SOURCE chunk: lane L
+// writes slot L % 8 of its row, so it fetches chunk (L % 8) ^ fswz(row).  Padding taps and pixels
+// past the slice read voffset 0x80000000: the buffer range check lands zeros.
+template <int N>
+__device__ __forceinline__ void wg_wait_vmcnt_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+constexpr int kWgStages = 3;
+
+template <int WMW, int WNW>
+__global__ __launch_bounds__(512, 1) void k_conv_wgrad_glds(Wgrad a) {
+  constexpr int SA = WMW, SBn = WNW, NSUB = SA + SBn;
+  constexpr int STAGE = NSUB * SUB;
+  static_assert(WMW * WNW == 8, "8 waves");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[kWgStages * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WNW, wn = wave % WNW;
+
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = orig & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int ntk = a.K / (64 * WMW), ntc = (a.TC + 64 * WNW - 1) / (64 * WNW), ntiles = ntk * ntc;
+  const int split = wg / ntiles, tile = wg % ntiles;
+  const int tk = tile % ntk, ttc = tile / ntk;
+  const int k0 = tk * 64 * WMW, tc0 = ttc * 64 * WNW;
+  const int mbeg = split * a.chunk;
+  const int mend = min(a.M, mbeg + a.chunk);
+  const int nst = (mend - mbeg + RB - 1) / RB;
+
+  const auto dy_rsrc = buf_rsrc(a.dy, (unsigned)((long long)a.M * a.K * 2));
+  const auto x_rsrc = buf_rsrc(a.x, (unsigned)((long long)a.N * a.H * a.W * a.C * 2));
+  const int row = wave * 8 + (lane >> 3);                   // this lane's pixel row of every sub-image
+  const int chunk8 = ((lane & 7) ^ fswz(row)) * 8;         // source-swizzled chunk (elements)
+  int b_kh[SBn], b_kw[SBn], b_off[SBn];
+  bool b_live[SBn];
+#pragma unroll
+  for (int j = 0; j < SBn; ++j) {
+    const int tc = tc0 + 64 * j;
+    b_live[j] = tc < a.TC;
+    const int tap = tc / a.C, c0 = tc - tap * a.C;
+    b_kh[j] = tap / a.KW;
+    b_kw[j] = tap - b_kh[j] * a.KW;
+    b_off[j] = (b_kh[j] * a.W + b_kw[j]) * a.C + c0 + chunk8;
+  }
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  auto issue = [&](int st, int stage) {
+    const int m = mbeg + st * RB + row;
+    const bool live = m < mend;
+    uint16_t* base = lds + stage * STAGE + wave * 8 * 64;
+#pragma unroll
+    for (int j = 0; j < SA; ++j) {
+      const int vo = live ? (int)(((long long)m * a.K + k0 + 64 * j + chunk8) * 2) : (int)0x80000000;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(dy_rsrc, (lds_ptr_t)(base + j * SUB), 16, vo, 0, 0, 0);
+    }
+    if (a.direct) {
+#pragma unroll
+      for (int j = 0; j < SBn; ++j) {
+        const int vo = (live && b_live[j]) ? (int)(((long long)m * a.C + b_off[j]) * 2) : (int)0x80000000;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(x_rsrc, (lds_ptr_t)(base + (SA + j) * SUB), 16, vo, 0, 0, 0);
+      }
+    } else {
+      int ow, oh;
+      const int t = fdiv(live ? m : 0, a.OW, a.inv_ow, ow);
+      const int n = fdiv(t, a.OH, a.inv_oh, oh);
+      const int ih0 = oh * a.SH - a.PT, iw0 = ow * a.SW - a.PL;
+      const int pbase = ((n * a.H + ih0) * a.W + iw0) * a.C;
+#pragma unroll
+      for (int j = 0; j < SBn; ++j) {
+        const int ih = ih0 + b_kh[j], iw = iw0 + b_kw[j];
+        const bool ok = live && b_live[j] && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        const int vo = ok ? (pbase + b_off[j]) * 2 : (int)0x80000000;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(x_rsrc, (lds_ptr_t)(base + (SA + j) * SUB), 16, vo, 0, 0, 0);
+      }
+    }
+  };
+
+  const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+  const int trow = 8 * g + qq;
+  const int tsw = fswz(trow);
+  auto tr_off = [&](int col0) { return trow * 64 + (((col0 >> 3) + (pp >> 1)) ^ tsw) * 8 + (pp & 1) * 4; };
+  const int a_sub = wm * SUB, b_sub = (SA + wn) * SUB;
+
+  f4v acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  if (nst > 0) issue(0, 0);
+  if (nst > 1) issue(1, 1);
+  int stg = 0;
+  for (int st = 0; st < nst; ++st) {
+    if (st + 1 < nst)
+      wg_wait_vmcnt_barrier<NSUB>();
+    else
+      wg_wait_vmcnt_barrier<0>();
+    if (st + 2 < nst) issue(st + 2, stg == 0 ? 2 : stg - 1);
+    const uint16_t* base = lds + stg * STAGE;
+#pragma unroll
+    for (int kk = 0; kk < RB; kk += 32) {
+      bf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint16_t* p = base + a_sub + tr_off(16 * i) + kk * 64;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p + 4 * 64));
+        fa[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint16_t* p = base + b_sub + tr_off(16 * j) + kk * 64;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p + 4 * 64));
+        fb[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    stg = stg == 2 ? 0 : stg + 1;
+  }
+
+  if (tc0 + 64 * wn >= a.TC) return;
+  float* ws = a.ws + (long long)split * a.TC * a.K;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = k0 + wm * 64 + i * 16 + 4 * g;
+      const int tc = tc0 + wn * 64 + j * 16 + (lane & 15);
+      *reinterpret_cast<f4v*>(ws + (long long)tc * a.K + k) = acc[i][j];
+    }
+}
+
 // dW = sum of the S partial slabs in a fixed order: wave w of the block sums slices w, w + G, ...
 // (4 independent chains), then wave 0 adds the G wave sums in order.  Out: HWIO bf16, or f32
 // (+= when accumulate).
@@ -278,8 +421,14 @@ void launch_wgrad(const Wgrad& a, hipStream_t s) {
   hipLaunchKernelGGL((k_conv_wgrad<WMW, WNW>), dim3(tiles * a.nsplit), dim3(64 * WMW * WNW), lds, s, a);
 }
 
-// tile shapes (waves along k, waves along tc)
-constexpr int kTiles[][2] = {{1, 1}, {1, 2}, {2, 1}, {2, 2}, {1, 4}, {4, 1}};
+template <int WMW, int WNW>
+void launch_wgrad_glds(const Wgrad& a, hipStream_t s) {
+  const int tiles = (a.K / (64 * WMW)) * ((a.TC + 64 * WNW - 1) / (64 * WNW));
+  hipLaunchKernelGGL((k_conv_wgrad_glds<WMW, WNW>), dim3(tiles * a.nsplit), dim3(512), 0, s, a);
+}
+
+// tile shapes (waves along k, waves along tc); the 8-wave ones are the LDS-DMA ring kernel
+constexpr int kTiles[][2] = {{1, 1}, {1, 2}, {2, 1}, {2, 2}, {1, 4}, {4, 1}, {2, 4}, {4, 2}};
 
 }  // namespace
 
@@ -320,10 +469,11 @@ std::vector<WgradPlan> conv_wgrad_plans(const ConvGeom& g, int max_plans) {
     const int ntc = (TC + btc - 1) / btc;
     if ((ntc * btc - TC) * 4 > ntc * btc) continue;  // > 25 % of the tc columns padding
     const int tiles = (g.K / bmk) * ntc;
-    const int lds_kb = 2 * (wmw + wnw) * 8;
+    const bool ring = wmw * wnw == 8;  // LDS-DMA ring kernel: one 144-KiB workgroup per CU
+    const int lds_kb = (ring ? 3 : 2) * (wmw + wnw) * 8;
     const int per_cu = std::max(1, std::min(160 / lds_kb, 8 / (wmw * wnw)));  // <= 2 waves per SIMD
     const double macs = (double)M * tiles * bmk * btc;
-    const double t_mma = macs * 2.0 / 1.0e15 * 1e6;
+    const double t_mma = macs * 2.0 / (ring ? 1.3e15 : 1.0e15) * 1e6;
     // dy re-read per tc tile, x per k tile (taps of one pixel neighbourhood hit L2: count once per tile)
     const double bytes = (double)M * 2.0 * ((double)g.K * ntc + (double)std::min(TC, btc) * ntc * (g.K / bmk));
     const double t_mem = bytes / 5.0e12 * 1e6;
@@ -368,6 +518,8 @@ void conv_wgrad_bf16(const void* x, const void* dy, float* ws, const WgradPlan& 
     case 18: launch_wgrad<2, 2>(a, s); break;
     case 12: launch_wgrad<1, 4>(a, s); break;
     case 33: launch_wgrad<4, 1>(a, s); break;
+    case 20: launch_wgrad_glds<2, 4>(a, s); break;
+    case 34: launch_wgrad_glds<4, 2>(a, s); break;
     default: return;
   }
   const long long n4 = (long long)a.TC * a.K / 4;

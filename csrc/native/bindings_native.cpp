@@ -183,7 +183,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         r.all_gather(ip, op, nb);
       })
       .def("barrier", &tdl::RingComm::barrier, py::call_guard<py::gil_scoped_release>())
-      .def("close", &tdl::RingComm::close);
+      .def("close", &tdl::RingComm::close)
+      .def("abort", &tdl::RingComm::abort);
 
   m.def("buffered_shuffle", &buffered_shuffle, py::arg("src"), py::arg("buffer_size"), py::arg("seed"),
         py::call_guard<py::gil_scoped_release>());

@@ -9,6 +9,8 @@
 // ends with bit-identical results.
 #include "ring.h"
 
+#include <sys/socket.h>
+
 #include <algorithm>
 #include <cmath>
 #include <vector>
@@ -76,6 +78,12 @@ void RingComm::close() {
       ::close(*fd);
       *fd = -1;
     }
+  }
+}
+
+void RingComm::abort() {
+  for (int fd : {right_fd_, left_fd_}) {
+    if (fd >= 0) ::shutdown(fd, SHUT_RDWR);
   }
 }
 

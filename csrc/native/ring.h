@@ -24,6 +24,9 @@ class RingComm {
   void all_gather(const void* in, void* out, int64_t nbytes_per_rank);
   void barrier();
   void close();
+  // Unblock a collective running on another thread (its poll/recv sees the shut-down sockets and
+  // throws): the job watchdog's abort.  The descriptors stay open until close().
+  void abort();
 
  private:
   void exchange(const char* sbuf, size_t sn, char* rbuf, size_t rn, char* reduce_dst, DType dt, RedOp op);

@@ -397,7 +397,8 @@ at::Tensor conv_wgrad(at::Tensor x, at::Tensor dy, int64_t kh, int64_t kw, int64
     p = tdl::conv_wgrad_plans(g, 1).at(0);
   } else {
     const int wmw = (int)plan[0], wnw = (int)plan[1];
-    TORCH_CHECK((wmw == 1 || wmw == 2 || wmw == 4) && (wnw == 1 || wnw == 2 || wnw == 4) && wmw * wnw <= 4 &&
+    TORCH_CHECK((wmw == 1 || wmw == 2 || wmw == 4) && (wnw == 1 || wnw == 2 || wnw == 4) &&
+                    (wmw * wnw <= 4 || (wmw * wnw == 8 && wmw != wnw)) &&
                     g.K % (64 * wmw) == 0 && plan[2] >= 1,
                 "conv_wgrad: bad plan");
     p = tdl::conv_wgrad_make_plan(g, wmw, wnw, (int)plan[2]);
@@ -622,6 +623,7 @@ void register_ops(pybind11::module& m) {
         pybind11::arg("accumulate") = false, pybind11::arg("plan") = std::vector<int64_t>{});
   m.def("conv_wgrad_plans", &conv_wgrad_plans, "weight-gradient candidate plans, best first: [[wmw, wnw, chunk, nsplit]]");
   m.def("conv_force_tile", &tdl::conv_force_tile, "conv tile sweep hook (0 = heuristic)");
+  m.def("conv_force_impl", &tdl::conv_force_impl, "conv main loop A/B hook: 1 = v1 register staged, 2 = LDS-DMA ring");
   m.def("conv_wgrad3x3_set_rows", &tdl::conv_wgrad3x3_set_rows, "3x3 row-kernel wgrad: output rows per slice (0 = auto)");
   m.def("conv_force_depth", &tdl::conv_force_depth, "conv main-loop prefetch depth A/B hook (1 or 2)");
   m.def("stem_fwd", &stem_fwd, "small-channel stride-2 conv (ResNet stem): (y, packed x[, BN part])",

@@ -143,7 +143,11 @@ def main():
                                    if getattr(strategy.extended, "tf_config", None) else 1),
                        "engine": trainer.kind, "communicator": comm.name,
                        "allreduce": getattr(comm, "algorithm", comm.name),
-                       "bucket_plan": (trainer.plan.as_dict() if getattr(trainer, "plan", None) else None),
+                       # what ran (no modelled terms): bucket count / size / wire dtype of the all-reduce
+                       "buckets": ({"n": trainer.plan.n_buckets if trainer._buckets is not None else 1,
+                                    "bytes": trainer.plan.bucket_bytes, "wire_dtype": trainer.plan.wire_dtype,
+                                    "overlapped_with_backward": trainer._buckets is not None}
+                                   if R > 1 and getattr(trainer, "plan", None) else None),
                        "replicas_identical": identical, "final_loss": round(logs["loss"], 4)},
         }), flush=True)
     if strategy.extended.rank == 0:

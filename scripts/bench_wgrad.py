@@ -59,11 +59,12 @@ def main():
 
         plans = C.conv_wgrad_plans(list(x.shape), list(dy.shape), KH, KH, s, s, p, p, a.candidates)
         ref = mi([False, True, False])[1].permute(2, 3, 1, 0).float()
-        times = []
+        times, errs = [], []
         for pl in plans:
             hw = lambda: C.conv_wgrad(x, dy, KH, KH, s, s, p, p, plan=[pl[0], pl[1], pl[3]])  # noqa: E731
-            err = float((hw().float() - ref).abs().max() / ref.abs().max())
+            errs.append(float((hw().float() - ref).abs().max() / ref.abs().max()))
             times.append(round(t(hw), 1))
+        err = max(errs)
         t_m = t(lambda: mi([False, True, False]))
         i = min(range(len(times)), key=times.__getitem__)
         t_h = times[i]

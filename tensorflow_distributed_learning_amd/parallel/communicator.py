@@ -82,6 +82,11 @@ class Communicator:
     def shutdown(self) -> None:
         pass
 
+    def abort(self) -> None:
+        """Unblock this rank's collectives after a job fault (called from the watchdog thread, so
+        that a rank stuck in a collective raises instead of waiting for its timeout).  Best effort;
+        the communicator is unusable afterwards."""
+
     def __repr__(self):
         return f"{type(self).__name__}(rank={self.rank}, world_size={self.world_size}, device={self.device})"
 
@@ -319,6 +324,18 @@ class TorchCommunicator(Communicator):
         self._capture_ok = ok
         return ok
 
+    def abort(self):
+        """RCCL: ncclCommAbort on every communicator of the job (torch's process-group abort), which
+        makes a collective blocked in RCCL return an error on this rank.  gloo has no abort (its own
+        timeout applies)."""
+        if self.backend == "nccl" and dist.is_initialized():
+            try:
+                from torch.distributed import distributed_c10d as c10d
+
+                c10d._abort_process_group()
+            except Exception:  # noqa: BLE001 - best effort from the watchdog thread
+                pass
+
     def shutdown(self):
         if self.xgmi is not None:
             try:
@@ -447,6 +464,9 @@ class RingCommunicator(Communicator):
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
         self._ring.barrier()
+
+    def abort(self):
+        self._ring.abort()
 
     def shutdown(self):
         self._ring.close()

@@ -415,6 +415,8 @@ class MirroredStrategy(Strategy):
             from ..cluster.liveness import start_for_process_group
 
             ext.watchdog = start_for_process_group(ext.rank, ext.world_size)
+            if ext.watchdog is not None:
+                ext.watchdog.on_abort = ext.communicator.abort
             ext.communicator.barrier()
 
 
@@ -500,6 +502,8 @@ class MultiWorkerMirroredStrategy(Strategy):
 
             ext.watchdog = PeerWatchdog(rendezvous, stale_after=float(os.environ.get("TDL_HEARTBEAT_TIMEOUT", "60")),
                                         grace=float(os.environ.get("TDL_ABORT_GRACE", "30"))).start()
+        if ext.watchdog is not None:
+            ext.watchdog.on_abort = comm.abort
         if world > 1:
             comm.barrier()
 

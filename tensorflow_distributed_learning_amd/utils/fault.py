@@ -134,6 +134,7 @@ class PeerWatchdog:
         self.stall_after = float(os.environ.get("TDL_STALL_TIMEOUT", stall_after or default_timeout()))
         self._published = None
         self._seen = {}  # chief: rank -> (progress record, monotonic time it last changed)
+        self.on_abort = None  # e.g. the communicator's abort (strategy.py sets it)
         self.reason: Optional[str] = None
         self.acknowledged = False
         self._stop = threading.Event()
@@ -210,6 +211,11 @@ class PeerWatchdog:
             self.reason = reason
             sys.stderr.write(f"[tdl] rank {self.rank}: aborting multi-worker job: {reason}\n")
             sys.stderr.flush()
+            if self.on_abort is not None:  # unblock a collective this rank may be stuck in
+                try:
+                    self.on_abort()
+                except Exception:  # noqa: BLE001 - best effort; the grace-period exit follows
+                    pass
 
     def _run(self):
         aborted_at = None

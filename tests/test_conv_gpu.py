@@ -76,7 +76,7 @@ def test_conv2d_layer_on_hip_kernels(monkeypatch):
     yr.backward(dy.float())
     torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=2e-2)
     torch.testing.assert_close(x.grad.float(), xr.grad, atol=4e-2, rtol=2e-2)
-    torch.testing.assert_close(kk.grad, kr.grad, atol=0.5, rtol=3e-2)
+    torch.testing.assert_close(kk.grad, kr.grad, atol=2e-2 * float(kr.grad.abs().max()), rtol=3e-2)
 
 
 @pytest.mark.parametrize("shape", [(64, 16, 16, 64, 512, 1, 1, 1, 0), (64, 16, 16, 128, 512, 3, 3, 1, 1),
@@ -243,10 +243,10 @@ def test_conv2d_library_wgrad_reaches_slab(monkeypatch, with_box):
         else:
             y.backward(dy)
         dx_ref, dw_ref = _ref_grads(x, k, 1, 1, dy)
-        torch.testing.assert_close(gout, dw_ref, atol=0.5, rtol=3e-2)
+        torch.testing.assert_close(gout, dw_ref, atol=2e-2 * float(dw_ref.abs().max()), rtol=3e-2)
         if with_box:
             dx2_ref, dw2_ref = _ref_grads(x, k2, 1, 1, dy2)
-            torch.testing.assert_close(gout2, dw2_ref, atol=0.5, rtol=3e-2)
+            torch.testing.assert_close(gout2, dw2_ref, atol=2e-2 * float(dw2_ref.abs().max()), rtol=3e-2)
             dx_ref = dx_ref + dx2_ref
         torch.testing.assert_close(xg.grad.float(), dx_ref, atol=8e-2, rtol=3e-2)
     finally:
