@@ -30,6 +30,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uns
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
 }
 
+// LDS-DMA: one 16-B chunk per lane from a raw buffer straight into LDS (buffer_load_dwordx4 ... lds).
+// The 64 lanes of the wave write 1 KiB linearly from `wave_dst` (wave-uniform): lane L lands at
+// wave_dst + 16 L bytes.  Out-of-range voffsets (e.g. 0x80000000) land zeros.
+__device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, uint16_t* wave_dst, int voffset, int soffset) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)wave_dst, 16, voffset,
+                                           soffset, 0, 0);
+}
+
 // 16-byte WRITE-THROUGH (sc1, aux 16) store: the bytes reach memory past this XCD's L2, so a
 // consumer workgroup on any XCD reads them with sc1 loads after the producer's vmcnt(0) drain and
 // an agent-scope counter/flag (MI355X_MICROARCH.md, inter-workgroup visibility).

@@ -497,7 +497,6 @@ __global__ __launch_bounds__(512, 1) void k_conv_glds(Igemm a) {
   const int ctiles = a.C / BK;
   const int ntiles = a.KH * a.KW * ctiles;
   int n_c = 0, n_kw = 0, n_kh = 0;
-  typedef __attribute__((address_space(3))) void* lds_ptr_t;
   auto issue = [&](int stage) {
     const int c0 = n_c * BK, kw = n_kw, kh = n_kh;
     if (++n_c == ctiles) {
@@ -513,15 +512,13 @@ __global__ __launch_bounds__(512, 1) void k_conv_glds(Igemm a) {
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
       const int vo = ((a_tap[i] >> tap) & 1u) ? a_vo[i] : (int)0x80000000;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(x_rsrc, (lds_ptr_t)(base + (i * 8 + wave) * 8 * LDS_ROW), 16, vo,
-                                               soff_a, 0, 0);
+      lds_dma16(x_rsrc, base + (i * 8 + wave) * 8 * LDS_ROW, vo, soff_a);
     }
     const int wkh = a.flip ? a.KH - 1 - kh : kh, wkw = a.flip ? a.KW - 1 - kw : kw;
     const int soff_b = (int)((wkh * a.w_kh + wkw * a.w_kw + c0) * 2);
 #pragma unroll
     for (int i = 0; i < B_LD; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(w_rsrc, (lds_ptr_t)(base + (BM + (i * 8 + wave) * 8) * LDS_ROW), 16,
-                                               b_vo[i], soff_b, 0, 0);
+      lds_dma16(w_rsrc, base + (BM + (i * 8 + wave) * 8) * LDS_ROW, b_vo[i], soff_b);
   };
 
   f4v acc[MI][NJ];

@@ -277,7 +277,6 @@ __global__ __launch_bounds__(512, 1) void k_conv_wgrad_glds(Wgrad a) {
     b_kw[j] = tap - b_kh[j] * a.KW;
     b_off[j] = (b_kh[j] * a.W + b_kw[j]) * a.C + c0 + chunk8;
   }
-  typedef __attribute__((address_space(3))) void* lds_ptr_t;
   auto issue = [&](int st, int stage) {
     const int m = mbeg + st * RB + row;
     const bool live = m < mend;
@@ -285,13 +284,13 @@ __global__ __launch_bounds__(512, 1) void k_conv_wgrad_glds(Wgrad a) {
 #pragma unroll
     for (int j = 0; j < SA; ++j) {
       const int vo = live ? (int)(((long long)m * a.K + k0 + 64 * j + chunk8) * 2) : (int)0x80000000;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(dy_rsrc, (lds_ptr_t)(base + j * SUB), 16, vo, 0, 0, 0);
+      lds_dma16(dy_rsrc, base + j * SUB, vo, 0);
     }
     if (a.direct) {
 #pragma unroll
       for (int j = 0; j < SBn; ++j) {
         const int vo = (live && b_live[j]) ? (int)(((long long)m * a.C + b_off[j]) * 2) : (int)0x80000000;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(x_rsrc, (lds_ptr_t)(base + (SA + j) * SUB), 16, vo, 0, 0, 0);
+        lds_dma16(x_rsrc, base + (SA + j) * SUB, vo, 0);
       }
     } else {
       int ow, oh;
@@ -304,7 +303,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_wgrad_glds(Wgrad a) {
         const int ih = ih0 + b_kh[j], iw = iw0 + b_kw[j];
         const bool ok = live && b_live[j] && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
         const int vo = ok ? (pbase + b_off[j]) * 2 : (int)0x80000000;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(x_rsrc, (lds_ptr_t)(base + (SA + j) * SUB), 16, vo, 0, 0, 0);
+        lds_dma16(x_rsrc, base + (SA + j) * SUB, vo, 0);
       }
     }
   };

@@ -294,7 +294,11 @@ class GenericTrainer:
                 self._counts[b] -= 1
                 if self._counts[b] == 0:
                     s, e = self._bucket_ranges[b]
-                    if self._wire_bufs is None:
+                    if getattr(self, "_skip_comm", False):  # fault injection: this rank leaves it out
+                        from ..parallel.communicator import _Done
+
+                        self._works.append(_Done())
+                    elif self._wire_bufs is None:
                         self._works.append(self.comm.all_reduce_async(self.G[s:e], "sum"))
                     else:
                         buf = self._wire_bufs[b]
@@ -327,6 +331,11 @@ class GenericTrainer:
 
     def train_step(self, batch, global_n: int, sync_lr: bool = True):
         x, y, sw = _split_xy(_to_device(batch, self.device))
+        from ..utils import fault
+
+        # fault injection (tests): this rank leaves out this step's gradient all-reduce
+        self._skip_comm = self.comm.world_size > 1 and fault.maybe_skip_collective(self.comm.rank,
+                                                                                   int(self.optimizer.iterations))
         G = self.G
         G.zero_()
         if self._buckets is not None:
@@ -360,10 +369,7 @@ class GenericTrainer:
         for b in (self.model.__dict__.get("_grad_boxes") or {}).values():
             if b.g is not None:  # a parked gradient contribution nobody collected
                 raise RuntimeError("fused gradient sum lost a contribution (keras/fusion.py grad boxes)")
-        from ..utils import fault
-
-        skip = self.comm.world_size > 1 and fault.maybe_skip_collective(self.comm.rank, int(self.optimizer.iterations))
-        if self.comm.world_size > 1 and not skip:
+        if self.comm.world_size > 1 and not self._skip_comm:
             with trace_range("tdl.allreduce"):
                 if self._buckets is not None:
                     for w in self._works:

@@ -161,3 +161,37 @@ def test_corrupted_replica_is_caught(tmp_path, mode):
         assert np.array_equal(np.load(tmp_path / "w0.npy"), np.load(tmp_path / "w1.npy"))
     else:
         assert a["status"] == b["status"] == "raised", (a, b)
+
+
+def test_live_rank_out_of_step_ends_the_job(tmp_path):
+    """A LIVE replica leaves out one gradient all-reduce (the xGMI bucket exchanges of the generic
+    engine on the shared GPU): its peer waits in the exchange kernel while both keep heartbeating.
+    The progress watchdog (utils/fault.py) and the bounded collective waits must end EVERY rank
+    non-zero -- within 150 s, not the 30 minutes of an unbounded collective."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = str(s.getsockname()[1])
+    s.close()
+    procs = []
+    for r in range(2):
+        env = _env(TDL_FAULT_SKIP_ALLREDUCE_AT_STEP="1:1", JOB_EPOCHS="50", JOB_REPLICAS="2", RANK=str(r),
+                   WORLD_SIZE="2", LOCAL_RANK=str(r), LOCAL_WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=port,
+                   TDL_LAUNCHED="1", TDL_DISABLE_FUSED="1", TDL_GRAPH_STEP="0", TDL_STALL_TIMEOUT="20",
+                   TDL_COLLECTIVE_TIMEOUT="40")
+        procs.append(subprocess.Popen([sys.executable, str(_script(tmp_path)), str(tmp_path)], cwd=ROOT, env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    _pids(tmp_path, 2)
+    t0 = time.time()
+    outs = []
+    for p in procs:
+        try:
+            o, e = p.communicate(timeout=170)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise AssertionError("a rank hung after the out-of-step fault")
+        outs.append((p.returncode, e))
+    assert "skips its gradient all-reduce" in outs[1][1], outs[1][1][-3000:]
+    for r in range(2):
+        assert outs[r][0] != 0, outs[r][1][-3000:]
+    assert time.time() - t0 < 150
