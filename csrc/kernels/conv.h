@@ -79,8 +79,9 @@ void conv_wgrad3x3_set_rows(int rows);  // A/B hook: output rows per slice (0 = 
 
 // Tile-sweep hook: 0 = per-shape heuristic (default), 1 = 128x64, 2 = 128x128, 3 = 256x128.
 void conv_force_tile(int tile);
-// A/B hook: 1 = the v1 register-staged kernel everywhere, 2 = the LDS-DMA ring kernel (default) where
-// its 256-row tiles still give >= one workgroup per CU
+// A/B hook: 1 = the v1 register-staged kernel everywhere, 2 (default) = the LDS-DMA ring kernel where
+// it measured faster (>= 32 k-tiles, >= one workgroup per CU), 3 = the ring kernel wherever its
+// 256-row tiles give >= one workgroup per CU (tests, sweeps)
 void conv_force_impl(int impl);
 // A/B hook: register prefetch depth of the implicit-GEMM main loop (1 or 2 tiles in flight)
 void conv_force_depth(int depth);

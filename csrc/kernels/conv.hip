@@ -586,7 +586,7 @@ void launch_tile(const Igemm& a, hipStream_t s) {
 }
 
 int g_forced_tile = 0;  // 0: heuristic below; 1: 128 x 64, 2: 128 x 128, 3: 256 x 128 (tile sweeps)
-int g_impl = 2;         // 1: v1 register-staged kernel only; 2: the LDS-DMA ring kernel where it applies
+int g_impl = 2;  // 1: v1 only; 2: the LDS-DMA ring kernel where it measured faster; 3: wherever it fits
 
 template <int BM, int BN, int WGM, int WGN>
 void launch_v2(const Igemm& a, hipStream_t s) {
@@ -599,9 +599,13 @@ void launch_v2(const Igemm& a, hipStream_t s) {
     hipLaunchKernelGGL((k_conv_glds<BM, BN, WGM, WGN, 0>), grid, block, 0, s, a);
 }
 
-// v2 (256-row tiles) where the grid still fills the chip: at least one workgroup per CU
-bool use_v2(int M, int K) {
-  if (g_impl != 2 || g_forced_tile != 0) return false;
+// v2 (256-row tiles, one 8-wave workgroup per CU) where it measured faster than v1
+// (profiles/conv_v2_r4.txt): long reductions (>= 32 k-tiles: the 3x3 convs at 14x14 / 7x7 and
+// the 1024 / 2048-channel 1x1 ones) with a grid that still fills the chip.  With 9-18 k-tiles the
+// ring's fill and drain and the unoverlapped epilogue of the single workgroup per CU cost more
+// than the LDS-DMA saves (v1 keeps two workgroups per CU).  Outputs are bit-identical either way.
+bool use_v2(int M, int K, int ktiles) {
+  if (g_impl == 1 || g_forced_tile != 0 || (g_impl == 2 && ktiles < 32)) return false;
   const long long wgs = (long long)(M + 255) / 256 * (K % 128 == 0 ? K / 128 : K / 64);
   return wgs >= 256;
 }
@@ -611,7 +615,7 @@ bool use_v2(int M, int K) {
 // workgroups per CU (the 64-column tile's extra LDS traffic per MFMA costs more than the idle CUs);
 // 256 x 128 loses 5-20 % everywhere.  The 64-column tile only serves K == 64 * odd.
 void launch(const Igemm& a, hipStream_t s) {
-  if (use_v2(a.M, a.K)) {
+  if (use_v2(a.M, a.K, a.KH * a.KW * (a.C / BK))) {
     if (a.K % 128 == 0) return launch_v2<256, 128, 4, 2>(a, s);
     return launch_v2<256, 64, 4, 2>(a, s);
   }
@@ -623,7 +627,7 @@ void launch(const Igemm& a, hipStream_t s) {
 }  // namespace
 
 void conv_force_tile(int tile) { g_forced_tile = tile; }
-void conv_force_impl(int impl) { g_impl = impl == 1 ? 1 : 2; }
+void conv_force_impl(int impl) { g_impl = (impl == 1 || impl == 3) ? impl : 2; }
 void conv_force_depth(int depth) { g_depth = depth == 1 ? 1 : 2; }
 
 bool conv_bf16_supported(const ConvGeom& g) {
@@ -641,17 +645,17 @@ bool conv_bf16_supported(const ConvGeom& g) {
 
 // the row tile launch() picks (the BN partial-sum rows of an epilogue are per row tile)
 int conv_fwd_row_tile(const ConvGeom& g) {
-  if (use_v2(g.N * g.OH * g.OW, g.K)) return 256;
+  if (use_v2(g.N * g.OH * g.OW, g.K, g.KH * g.KW * (g.C / BK))) return 256;
   return (g_forced_tile == 3 && g.K % 128 == 0) ? 256 : 128;
 }
 
 int conv_dgrad_row_tile(const ConvGeom& g) {
-  if (use_v2(g.N * g.H * g.W, g.C)) return 256;
+  if (use_v2(g.N * g.H * g.W, g.C, g.KH * g.KW * (g.K / BK))) return 256;
   return (g_forced_tile == 3 && g.C % 128 == 0) ? 256 : 128;
 }
 
 int conv_dgrad_s2_row_tile(const ConvGeom& g) {
-  if (use_v2(g.N * g.OH * g.OW, g.C)) return 256;
+  if (use_v2(g.N * g.OH * g.OW, g.C, g.K / BK)) return 256;
   return (g_forced_tile == 3 && g.C % 128 == 0) ? 256 : 128;
 }
 

@@ -472,7 +472,10 @@ std::vector<WgradPlan> conv_wgrad_plans(const ConvGeom& g, int max_plans) {
     const int lds_kb = (ring ? 3 : 2) * (wmw + wnw) * 8;
     const int per_cu = std::max(1, std::min(160 / lds_kb, 8 / (wmw * wnw)));  // <= 2 waves per SIMD
     const double macs = (double)M * tiles * bmk * btc;
-    const double t_mma = macs * 2.0 / (ring ? 1.3e15 : 1.0e15) * 1e6;
+    // measured (profiles/conv_v2_r4.txt): the ring kernel wins on 3x3 and strided 1x1 shapes and
+    // loses on stride-1 1x1 ones (the v1 2x2-wave tile), where its rate is scaled down
+    const bool direct = g.KH == 1 && g.KW == 1 && g.SH == 1 && g.SW == 1 && g.PT == 0 && g.PL == 0;
+    const double t_mma = macs * 2.0 / (ring ? (direct ? 0.85e15 : 1.3e15) : 1.0e15) * 1e6;
     // dy re-read per tc tile, x per k tile (taps of one pixel neighbourhood hit L2: count once per tile)
     const double bytes = (double)M * 2.0 * ((double)g.K * ntc + (double)std::min(TC, btc) * ntc * (g.K / bmk));
     const double t_mem = bytes / 5.0e12 * 1e6;
@@ -491,12 +494,24 @@ std::vector<WgradPlan> conv_wgrad_plans(const ConvGeom& g, int max_plans) {
     }
   }
   std::sort(c.begin(), c.end(), [](const Cand& x, const Cand& y) { return x.t < y.t; });
-  std::vector<WgradPlan> out;
+  // best first, but both kernel families (v1 register-staged, 8-wave LDS-DMA ring) among the first
+  // candidates: the model ranks them only roughly, the autotuner's timing decides
+  std::vector<WgradPlan> fam[2];
   for (const auto& e : c) {
+    auto& f = fam[e.p.wmw * e.p.wnw == 8 ? 1 : 0];
     bool dup = false;
-    for (const auto& o : out) dup |= (o.wmw == e.p.wmw && o.wnw == e.p.wnw && o.nsplit == e.p.nsplit);
-    if (!dup) out.push_back(e.p);
-    if ((int)out.size() >= max_plans) break;
+    for (const auto& o : f) dup |= (o.wmw == e.p.wmw && o.wnw == e.p.wnw && o.nsplit == e.p.nsplit);
+    if (!dup) f.push_back(e.p);
+  }
+  std::vector<WgradPlan> out;
+  size_t i0 = 0, i1 = 0;
+  const bool ring_first = !c.empty() && c.front().p.wmw * c.front().p.wnw == 8;
+  while ((int)out.size() < max_plans && (i0 < fam[0].size() || i1 < fam[1].size())) {
+    const bool take_ring = (out.size() % 2 == 0) == ring_first;
+    if ((take_ring && i1 < fam[1].size()) || i0 >= fam[0].size())
+      out.push_back(fam[1][i1++]);
+    else
+      out.push_back(fam[0][i0++]);
   }
   return out;
 }

@@ -50,7 +50,7 @@ def sweep(C, fn):
     """Times of the v1 (register-staged, 128-row tiles) and v2 (LDS-DMA ring, 256-row tiles where
     the grid fills the chip) main loops."""
     out = []
-    for impl in (1, 2):
+    for impl in (1, 3):
         C.conv_force_impl(impl)
         out.append(round(t(fn), 1))
     C.conv_force_impl(2)
