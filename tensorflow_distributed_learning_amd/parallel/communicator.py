@@ -259,9 +259,10 @@ class TorchCommunicator(Communicator):
         return t
 
     def all_gather(self, t):
-        out = torch.empty((self.world_size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, t.contiguous())
-        return out
+        # flat output (gloo's all-gather-into-tensor takes only a [world * numel] buffer), then viewed
+        out = torch.empty(self.world_size * t.numel(), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.contiguous().view(-1))
+        return out.view((self.world_size,) + tuple(t.shape))
 
     def barrier(self):
         if self.backend == "nccl" and self.device.type == "cuda":

@@ -36,6 +36,9 @@ def test_bench_two_replicas_self_launched_shared_gpu():
     assert d["config"]["allreduce"] == "xgmi-oneshot+gloo"
     assert d["config"]["allreduce_in_graph"] is True
     assert d["config"]["replicas_identical"] is True
+    # per-rank timed regions (the MAX is the reported time) and the fallbacks taken (none here)
+    assert len(d["config"]["rank_ms_per_step"]) == 2 and max(d["config"]["rank_ms_per_step"]) == d["ms_per_step"]
+    assert d["config"]["rank_spread_pct"] >= 0 and d["config"]["fallbacks"] == [], d["config"]
 
 
 def test_bench_three_replicas_two_shot_shared_gpu():
