@@ -94,7 +94,7 @@ def build_hip_ext(nproc, verbose=False):
         if _stale(src, obj, hdr):
             jobs.append(([hipcc, "-c", "-x", "hip", f"--offload-arch={ARCH}", "-fno-gpu-rdc", *common, *extra, src, "-o", obj], obj))
     host_defs = ["-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DTORCH_API_INCLUDE_EXTENSION_H", "-DTORCH_EXTENSION_NAME=_C"]
-    for src in [os.path.join(CSRC, n) for n in ("bindings.cpp", "ops_bindings.cpp", "comm_bindings.cpp")]:
+    for src in [os.path.join(CSRC, n) for n in ("bindings.cpp", "ops_bindings.cpp", "comm_bindings.cpp", "rccl_comm.cpp")]:
         obj = os.path.join(odir, os.path.basename(src) + ".o")
         objs.append(obj)
         if _stale(src, obj, hdr):

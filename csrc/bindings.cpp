@@ -269,6 +269,7 @@ void sgd_momentum(at::Tensor w, at::Tensor g, at::Tensor v, at::Tensor lr, doubl
 
 void register_ops(pybind11::module& m);
 void register_comm(pybind11::module& m);
+void register_rccl(pybind11::module& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels of tensorflow_distributed_learning_amd";
@@ -299,4 +300,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sgd_momentum", &sgd_momentum);
   register_ops(m);
   register_comm(m);
+  register_rccl(m);
 }

@@ -1,0 +1,236 @@
+// Owned RCCL communicator (see rccl_comm.h) + its Python bindings.
+#include "rccl_comm.h"
+
+#include <dlfcn.h>
+#include <torch/extension.h>
+
+#include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPStream.h>
+
+#include <atomic>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+
+namespace tdl_host {
+
+namespace {
+constexpr int kIdBytes = 128;  // NCCL_UNIQUE_ID_BYTES
+struct UniqueId {
+  char internal[kIdBytes];
+};
+typedef int Result;  // ncclResult_t: 0 success, 7 in progress
+typedef void* Comm;  // ncclComm_t
+
+// ncclDataType_t / ncclRedOp_t values of rccl.h (stable across RCCL releases)
+int nccl_dtype(int d) {
+  switch (d) {
+    case 0: return 7;  // ncclFloat32
+    case 1: return 9;  // ncclBfloat16
+    case 2: return 6;  // ncclFloat16
+    case 3: return 8;  // ncclFloat64
+    case 4: return 2;  // ncclInt32
+    case 5: return 4;  // ncclInt64
+    case 6: return 1;  // ncclUint8
+  }
+  throw std::invalid_argument("rccl: unsupported dtype code " + std::to_string(d));
+}
+int nccl_op(int o) {
+  if (o < 0 || o > 4) throw std::invalid_argument("rccl: unsupported reduction op " + std::to_string(o));
+  return o;  // ncclSum 0, ncclProd 1, ncclMax 2, ncclMin 3, ncclAvg 4
+}
+}  // namespace
+
+struct RcclApi {
+  Result (*GetVersion)(int*);
+  Result (*GetUniqueId)(UniqueId*);
+  Result (*CommInitRank)(Comm*, int, UniqueId, int);
+  Result (*CommDestroy)(Comm);
+  Result (*CommAbort)(Comm);
+  Result (*CommGetAsyncError)(Comm, Result*);
+  const char* (*GetErrorString)(Result);
+  Result (*AllReduce)(const void*, void*, size_t, int, int, Comm, hipStream_t);
+  Result (*Broadcast)(const void*, void*, size_t, int, int, Comm, hipStream_t);
+  Result (*AllGather)(const void*, void*, size_t, int, Comm, hipStream_t);
+  Result (*ReduceScatter)(const void*, void*, size_t, int, int, Comm, hipStream_t);
+  Result (*GroupStart)();
+  Result (*GroupEnd)();
+
+  static const RcclApi& get() {
+    static RcclApi api;
+    static std::once_flag once;
+    std::call_once(once, [] { api.load(); });
+    return api;
+  }
+
+ private:
+  void* sym(void* h, const char* name) {
+    void* p = dlsym(h, name);
+    if (p == nullptr) throw std::runtime_error(std::string("rccl: symbol ") + name + " not found");
+    return p;
+  }
+  void load() {
+    // the RCCL torch already loaded (its ProcessGroupNCCL links it): never a second copy
+    void* h = dlopen("librccl.so", RTLD_NOW | RTLD_NOLOAD);
+    if (h == nullptr) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    if (h == nullptr) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+    if (h == nullptr) throw std::runtime_error(std::string("rccl: cannot load librccl.so: ") + dlerror());
+    GetVersion = reinterpret_cast<decltype(GetVersion)>(sym(h, "ncclGetVersion"));
+    GetUniqueId = reinterpret_cast<decltype(GetUniqueId)>(sym(h, "ncclGetUniqueId"));
+    CommInitRank = reinterpret_cast<decltype(CommInitRank)>(sym(h, "ncclCommInitRank"));
+    CommDestroy = reinterpret_cast<decltype(CommDestroy)>(sym(h, "ncclCommDestroy"));
+    CommAbort = reinterpret_cast<decltype(CommAbort)>(sym(h, "ncclCommAbort"));
+    CommGetAsyncError = reinterpret_cast<decltype(CommGetAsyncError)>(sym(h, "ncclCommGetAsyncError"));
+    GetErrorString = reinterpret_cast<decltype(GetErrorString)>(sym(h, "ncclGetErrorString"));
+    AllReduce = reinterpret_cast<decltype(AllReduce)>(sym(h, "ncclAllReduce"));
+    Broadcast = reinterpret_cast<decltype(Broadcast)>(sym(h, "ncclBroadcast"));
+    AllGather = reinterpret_cast<decltype(AllGather)>(sym(h, "ncclAllGather"));
+    ReduceScatter = reinterpret_cast<decltype(ReduceScatter)>(sym(h, "ncclReduceScatter"));
+    GroupStart = reinterpret_cast<decltype(GroupStart)>(sym(h, "ncclGroupStart"));
+    GroupEnd = reinterpret_cast<decltype(GroupEnd)>(sym(h, "ncclGroupEnd"));
+  }
+};
+
+RcclComm::RcclComm(const std::string& uid, int rank, int world, int device)
+    : api_(RcclApi::get()), rank_(rank), world_(world), device_(device) {
+  if ((int)uid.size() != kIdBytes) throw std::invalid_argument("rccl: unique id must be 128 bytes");
+  if (world < 1 || rank < 0 || rank >= world) throw std::invalid_argument("rccl: bad rank / world");
+  UniqueId id;
+  std::memcpy(id.internal, uid.data(), kIdBytes);
+  c10::hip::HIPGuard guard((c10::DeviceIndex)device);
+  check(api_.CommInitRank(&comm_, world, id, rank), "ncclCommInitRank");
+}
+
+RcclComm::~RcclComm() {
+  if (comm_ != nullptr && !aborted_) (void)api_.CommDestroy(comm_);
+}
+
+std::string RcclComm::unique_id() {
+  UniqueId id;
+  const auto& api = RcclApi::get();
+  const Result r = api.GetUniqueId(&id);
+  if (r != 0) throw std::runtime_error(std::string("rccl: ncclGetUniqueId failed: ") + api.GetErrorString(r));
+  return std::string(id.internal, kIdBytes);
+}
+
+int RcclComm::version() {
+  int v = 0;
+  RcclApi::get().GetVersion(&v);
+  return v;
+}
+
+void RcclComm::check(int r, const char* what) const {
+  if (r != 0 && r != 7) throw std::runtime_error(std::string("rccl: ") + what + " failed: " + api_.GetErrorString(r));
+}
+
+void RcclComm::all_reduce(void* sb, void* rb, size_t n, int dt, int op, hipStream_t s) {
+  if (aborted_) throw std::runtime_error("rccl: communicator was aborted");
+  check(api_.AllReduce(sb, rb, n, nccl_dtype(dt), nccl_op(op), comm_, s), "ncclAllReduce");
+}
+void RcclComm::broadcast(void* sb, void* rb, size_t n, int dt, int root, hipStream_t s) {
+  if (aborted_) throw std::runtime_error("rccl: communicator was aborted");
+  check(api_.Broadcast(sb, rb, n, nccl_dtype(dt), root, comm_, s), "ncclBroadcast");
+}
+void RcclComm::all_gather(void* sb, void* rb, size_t n, int dt, hipStream_t s) {
+  if (aborted_) throw std::runtime_error("rccl: communicator was aborted");
+  check(api_.AllGather(sb, rb, n, nccl_dtype(dt), comm_, s), "ncclAllGather");
+}
+void RcclComm::reduce_scatter(void* sb, void* rb, size_t n, int dt, int op, hipStream_t s) {
+  if (aborted_) throw std::runtime_error("rccl: communicator was aborted");
+  check(api_.ReduceScatter(sb, rb, n, nccl_dtype(dt), nccl_op(op), comm_, s), "ncclReduceScatter");
+}
+void RcclComm::group_start() { check(api_.GroupStart(), "ncclGroupStart"); }
+void RcclComm::group_end() { check(api_.GroupEnd(), "ncclGroupEnd"); }
+
+int RcclComm::async_error() {
+  if (aborted_) return -1;
+  Result e = 0;
+  const Result r = api_.CommGetAsyncError(comm_, &e);
+  if (r != 0) return r;
+  return (e == 0 || e == 7) ? 0 : e;
+}
+
+std::string RcclComm::error_string(int code) const {
+  if (code < 0) return "communicator aborted";
+  return api_.GetErrorString(code);
+}
+
+void RcclComm::abort() {
+  if (aborted_ || comm_ == nullptr) return;
+  aborted_ = true;
+  (void)api_.CommAbort(comm_);
+}
+
+}  // namespace tdl_host
+
+namespace {
+using tdl_host::RcclComm;
+
+int dtype_code(const at::Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return 0;
+    case at::kBFloat16: return 1;
+    case at::kHalf: return 2;
+    case at::kDouble: return 3;
+    case at::kInt: return 4;
+    case at::kLong: return 5;
+    case at::kByte: return 6;
+    default: TORCH_CHECK(false, "rccl: unsupported tensor dtype ", t.scalar_type());
+  }
+}
+
+void check_t(const at::Tensor& t, const RcclComm& c, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "rccl: ", what, " must be a contiguous GPU tensor");
+  (void)c;
+}
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+}  // namespace
+
+void register_rccl(pybind11::module& m) {
+  pybind11::class_<RcclComm>(m, "RcclComm")
+      .def(pybind11::init([](pybind11::bytes uid, int rank, int world, int device) {
+             return new RcclComm(std::string(uid), rank, world, device);
+           }),
+           pybind11::arg("unique_id"), pybind11::arg("rank"), pybind11::arg("world"), pybind11::arg("device"),
+           pybind11::call_guard<pybind11::gil_scoped_release>())
+      .def_static("unique_id", []() { return pybind11::bytes(RcclComm::unique_id()); })
+      .def_static("version", &RcclComm::version)
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("world", &RcclComm::world)
+      .def("all_reduce",
+           [](RcclComm& c, at::Tensor t, int op) {
+             check_t(t, c, "tensor");
+             c.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), dtype_code(t), op, stream());
+           },
+           pybind11::arg("tensor"), pybind11::arg("op") = 0)
+      .def("broadcast",
+           [](RcclComm& c, at::Tensor t, int root) {
+             check_t(t, c, "tensor");
+             c.broadcast(t.data_ptr(), t.data_ptr(), t.numel(), dtype_code(t), root, stream());
+           },
+           pybind11::arg("tensor"), pybind11::arg("root") = 0)
+      .def("all_gather",
+           [](RcclComm& c, at::Tensor out, at::Tensor in) {
+             check_t(out, c, "out");
+             check_t(in, c, "in");
+             TORCH_CHECK(out.numel() == in.numel() * c.world() && out.scalar_type() == in.scalar_type(),
+                         "rccl: all_gather out must hold world x in");
+             c.all_gather(in.data_ptr(), out.data_ptr(), in.numel(), dtype_code(in), stream());
+           })
+      .def("reduce_scatter",
+           [](RcclComm& c, at::Tensor out, at::Tensor in, int op) {
+             check_t(out, c, "out");
+             check_t(in, c, "in");
+             TORCH_CHECK(in.numel() == out.numel() * c.world() && out.scalar_type() == in.scalar_type(),
+                         "rccl: reduce_scatter in must hold world x out");
+             c.reduce_scatter(in.data_ptr(), out.data_ptr(), out.numel(), dtype_code(in), op, stream());
+           },
+           pybind11::arg("out"), pybind11::arg("in"), pybind11::arg("op") = 0)
+      .def("group_start", &RcclComm::group_start)
+      .def("group_end", &RcclComm::group_end)
+      .def("async_error", &RcclComm::async_error)
+      .def("error_string", &RcclComm::error_string)
+      .def("abort", &RcclComm::abort, pybind11::call_guard<pybind11::gil_scoped_release>())
+      .def_property_readonly("aborted", &RcclComm::aborted);
+}

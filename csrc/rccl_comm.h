@@ -1,0 +1,60 @@
+// Owned RCCL communicator (Communicator over ncclCommInitRank / ncclAllReduce /
+// ncclBroadcast / ncclGroupStart+End / ncclCommGetAsyncError / ncclCommAbort), one rank per GPU.
+//
+// torch.distributed's "nccl" process group is RCCL too, but it owns the communicator: its error
+// handling is a watchdog thread with a 10-minute default and a process teardown.  This class gives
+// the framework the communicator itself: collectives enqueued on the caller's HIP stream (so they
+// record into hipGraphs like any kernel), a non-blocking async-error query for the job watchdog,
+// and ncclCommAbort from any thread, which makes a collective that waits for a dead or out-of-step
+// peer return instead of hanging the GPU queue.
+//
+// The RCCL entry points are resolved at run time from the librccl the process already has loaded
+// (torch's own copy, RCCL 2.26 at the time of writing -- SURVEY.md §7.4 risk 3: two RCCL builds in
+// one process must not be mixed), so only ABI-stable API of RCCL >= 2.18 is used: no config structs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+namespace tdl_host {
+
+struct RcclApi;
+
+class RcclComm {
+ public:
+  // unique_id: the 128 bytes rank 0 got from unique_id() and shared with every rank
+  RcclComm(const std::string& unique_id, int rank, int world, int device);
+  ~RcclComm();
+
+  static std::string unique_id();  // ncclGetUniqueId (rank 0)
+  static int version();            // ncclGetVersion of the resolved library
+
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+
+  // dtype: 0 f32, 1 bf16, 2 f16, 3 f64, 4 i32, 5 i64, 6 u8; op: 0 sum, 1 prod, 2 max, 3 min, 4 avg
+  void all_reduce(void* sendbuf, void* recvbuf, size_t count, int dtype, int op, hipStream_t s);
+  void broadcast(void* sendbuf, void* recvbuf, size_t count, int dtype, int root, hipStream_t s);
+  void all_gather(void* sendbuf, void* recvbuf, size_t sendcount, int dtype, hipStream_t s);
+  void reduce_scatter(void* sendbuf, void* recvbuf, size_t recvcount, int dtype, int op, hipStream_t s);
+  void group_start();
+  void group_end();
+
+  // ncclCommGetAsyncError: 0 = fine (ncclSuccess / ncclInProgress), otherwise the RCCL error code
+  int async_error();
+  std::string error_string(int code) const;
+  // ncclCommAbort: unblocks every pending collective of this communicator; safe from another
+  // thread; the communicator is unusable afterwards
+  void abort();
+  bool aborted() const { return aborted_; }
+
+ private:
+  void check(int r, const char* what) const;
+  const RcclApi& api_;
+  void* comm_ = nullptr;
+  int rank_, world_, device_;
+  bool aborted_ = false;
+};
+
+}  // namespace tdl_host

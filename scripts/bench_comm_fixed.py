@@ -4,7 +4,9 @@ constants in parallel/bucketing.py with measured ones).
 
     python scripts/bench_comm_fixed.py > profiles/comm_fixed_costs_r4.jsonl
 
-(A world-1 RCCL "all-reduce" launches nothing and measures nothing: no such rows.)
+(A world-1 RCCL "all-reduce" launches nothing and measures nothing: no such rows.)  The round-3
+single-sample 28.5 us for the 64 KiB two-shot was a cold first call: with interleaved repeats its
+median is 6.8 us and that sample shows up as the max (profiles/comm_fixed_costs_r4.jsonl).
 
 * ``xgmi_oneshot`` / ``xgmi_twoshot`` at R = 2 and 4: the xGMI all-reduce kernel between R
   processes that share the one GPU (IPC-mapped exchange buffers, flags, fences, rank-order sums):
@@ -64,7 +66,10 @@ def xgmi_worker(rank: int, R: int, port: str):
     dist.init_process_group("gloo", rank=rank, world_size=R, init_method=f"tcp://127.0.0.1:{port}")
     C = ops.hip()
     cases = []
-    for nbytes in SIZES:
+    # R replica processes share the ONE GPU: every launch's workgroups spin until the same workgroup
+    # of each peer arrives, so all R launches must be resident at once -- at R = 4 only the small
+    # channels fit (the 1-4 MiB ones time out: 256-1024 spinning workgroups per process)
+    for nbytes in (SIZES if R <= 2 else [b for b in SIZES if b <= (256 << 10)]):
         n = nbytes // 4
         for algo in (0, 1):
             ch = C.XgmiChannel(rank, R, n, 0, 60.0, algo)

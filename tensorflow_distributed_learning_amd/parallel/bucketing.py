@@ -25,9 +25,9 @@ from typing import Optional
 
 XGMI_LINK_GBPS = 153.6       # per direction, per link (MI355X_MICROARCH.md)
 XGMI_LINKS = 7               # point-to-point links per GPU (8-GPU full mesh)
-# Per-call fixed costs.  MEASURED on one MI355X (profiles/comm_fixed_costs_r3.jsonl,
-# scripts/bench_comm_fixed.py): the xGMI one-shot kernel between 2 replica processes sharing the GPU
-# costs 4.7 us at 64 KiB (flags, fences, launch; no fabric hop).  RCCL's per-call latency is NOT
+# Per-call fixed costs.  MEASURED on one MI355X (profiles/comm_fixed_costs_r4.jsonl,
+# scripts/bench_comm_fixed.py, median of 7 interleaved repeats): the xGMI one-shot kernel between 2
+# replica processes sharing the GPU costs 4.7 us at 64 KiB (flags, fences, launch; no fabric hop).  RCCL's per-call latency is NOT
 # measurable on a one-GPU box (a world-1 RCCL all-reduce launches nothing: 0.07 us) and stays the
 # modelled 25 us for 2(R-1) dependent ring hops on one node.  The link term is modelled too.
 XGMI_CALL_US = 4.7           # measured (see above)
@@ -61,7 +61,7 @@ class BucketPlan:
         d["cost_model"] = {
             "per_bucket_us": "modelled",
             "call_latency_us": XGMI_CALL_US if xg else RCCL_CALL_LATENCY_US,
-            "call_latency_source": "measured (profiles/comm_fixed_costs_r3.jsonl)" if xg else "modelled",
+            "call_latency_source": "measured (profiles/comm_fixed_costs_r4.jsonl)" if xg else "modelled",
             "fabric": f"modelled: {XGMI_LINK_GBPS} GB/s per xGMI link x efficiency {LINK_EFFICIENCY}",
         }
         return d

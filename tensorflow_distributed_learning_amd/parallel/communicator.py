@@ -353,6 +353,170 @@ class TorchCommunicator(Communicator):
             self._owns_group = False
 
 
+class NativeRcclCommunicator(TorchCommunicator):
+    """The framework's OWN RCCL communicator (csrc/rccl_comm.cpp): device
+    collectives go straight to ncclAllReduce / ncclBroadcast / ncclAllGather on the caller's HIP
+    stream (capturable into hipGraphs), the communicator's asynchronous errors are polled by
+    :meth:`check_health`, and :meth:`abort` is ncclCommAbort (from the job watchdog's thread: a rank
+    stuck in a collective returns instead of hanging the GPU queue).  A gloo process group carries
+    the control plane (unique-id exchange, host tensors, barriers).  The xGMI kernel path for small
+    single-node messages works on top of it as on the torch RCCL group (``enable_xgmi``).
+
+    Selected with ``TDL_NATIVE_RCCL=1`` for GPU replicas (``CollectiveCommunication.NCCL`` / ``AUTO``)."""
+
+    def __init__(self, rank: int, world_size: int, device: torch.device, store=None,
+                 timeout: Optional[float] = None):
+        super().__init__("gloo", rank, world_size, device, store=store, timeout=timeout)
+        self.name = "rccl"
+        self.capturable = True
+        self._avg_native = True
+        self.algorithm = "rccl-native"
+        from torch.distributed import distributed_c10d as c10d
+
+        C = ops.hip()
+        kv = c10d._get_default_store()
+        key = "tdl/rccl/unique_id"
+        if rank == 0:
+            kv.set(key, C.RcclComm.unique_id())
+        uid = kv.get(key)
+        torch.cuda.set_device(self.device)
+        self.rccl = C.RcclComm(bytes(uid), rank, world_size, self.device.index or 0)
+        self.rccl_version = int(C.RcclComm.version())
+
+    def enable_xgmi(self, timeout: Optional[float] = None) -> bool:
+        ok = super().enable_xgmi(timeout)
+        if ok and self.xgmi is not None:
+            self.xgmi.chunked = False  # large messages belong to RCCL's rings, as on the torch group
+        return ok
+
+    def prepare_all_reduce(self, *numels):
+        super().prepare_all_reduce(*numels)
+        self.algorithm = self.algorithm.replace("+gloo", "+rccl-native")
+
+    # ---- device data plane ------------------------------------------------------------------
+    _OPC = {"sum": 0, "prod": 1, "max": 2, "min": 3, "mean": 4}
+
+    def all_reduce(self, t, op="sum"):
+        if not t.is_cuda:
+            return super().all_reduce(t, op)
+        if self.xgmi is not None and self.xgmi.all_reduce(t, op):
+            return t
+        if op not in self._OPC:
+            raise ValueError(f"unknown reduce op {op}")
+        if op == "mean" and not t.is_floating_point():
+            raise ValueError("mean all-reduce of an integer tensor")
+        self.rccl.all_reduce(t if t.is_contiguous() else t.contiguous(), self._OPC[op])
+        return t
+
+    def all_reduce_async(self, t, op="sum"):
+        if not t.is_cuda:
+            return super().all_reduce_async(t, op)
+        if self.xgmi is not None and op in ("sum", "mean") and self.xgmi.applicable(t) and \
+                self.xgmi.has_channel(t.numel()):
+            return _SideStreamWork(self, t, op)
+        return _RcclSideWork(self, t, op)
+
+    def broadcast(self, t, src=0):
+        if not t.is_cuda:
+            return super().broadcast(t, src)
+        self.rccl.broadcast(t, int(src))
+        return t
+
+    def all_gather(self, t):
+        if not t.is_cuda:
+            return super().all_gather(t)
+        out = torch.empty(self.world_size * t.numel(), dtype=t.dtype, device=t.device)
+        self.rccl.all_gather(out, t.contiguous().view(-1))
+        return out.view((self.world_size,) + tuple(t.shape))
+
+    def barrier(self):
+        torch.cuda.synchronize(self.device)
+        dist.barrier()
+
+    def _no_host_collective_in_capture(self, t):
+        if not t.is_cuda:
+            super()._no_host_collective_in_capture(t)
+
+    def device_bucket_capable(self, numels) -> bool:
+        return True
+
+    def capture_probe(self) -> bool:
+        """Collectively: an RCCL all-reduce recorded into a hipGraph replays correctly on every
+        rank (agreement on the gloo control plane, so every rank takes the same path)."""
+        if getattr(self, "_capture_ok", None) is not None:
+            return self._capture_ok
+        dev = self.device
+        t = torch.full((64,), float(self.rank + 1), device=dev)
+        ok = True
+        try:
+            self.rccl.all_reduce(t, 0)
+            torch.cuda.synchronize(dev)
+            s = torch.cuda.Stream(dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                self.rccl.all_reduce(t, 0)
+            torch.cuda.synchronize(dev)
+        except Exception:  # noqa: BLE001 - capture unsupported: eager collectives
+            ok = False
+        f = torch.tensor([1.0 if ok else 0.0])
+        dist.all_reduce(f, op=dist.ReduceOp.MIN)
+        ok = bool(f.item() > 0.5)
+        if ok:
+            t.fill_(float(self.rank + 1))
+            g.replay()
+            torch.cuda.synchronize(dev)
+            want = float(self.world_size * (self.world_size + 1) // 2)
+            f.fill_(1.0 if bool(torch.all(t == want)) else 0.0)
+            dist.all_reduce(f, op=dist.ReduceOp.MIN)
+            ok = bool(f.item() > 0.5)
+        self._capture_ok = ok
+        return ok
+
+    # ---- failure handling ------------------------------------------------------------------
+    def check_health(self):
+        super().check_health()
+        e = self.rccl.async_error()
+        if e != 0:
+            raise RuntimeError(f"rccl: asynchronous communicator error: {self.rccl.error_string(e)}")
+
+    def abort(self):
+        """ncclCommAbort: every pending collective of this communicator returns (watchdog thread)."""
+        try:
+            self.rccl.abort()
+        except Exception:  # noqa: BLE001 - best effort
+            pass
+
+    def shutdown(self):
+        if not self.rccl.aborted:
+            try:
+                torch.cuda.synchronize(self.device)
+            except Exception:  # noqa: BLE001
+                pass
+        super().shutdown()
+
+
+class _RcclSideWork:
+    """An RCCL all-reduce enqueued on the communicator's side stream (forked from the current one):
+    it overlaps the rest of the backward on the GPU; ``wait()`` joins it back."""
+
+    def __init__(self, comm, t, op):
+        dev = t.device
+        if getattr(comm, "_side", None) is None:
+            comm._side = torch.cuda.Stream(dev)
+        side = comm._side
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            comm.all_reduce(t, op)
+        self._side, self._dev = side, dev
+
+    def wait(self):
+        torch.cuda.current_stream(self._dev).wait_stream(self._side)
+
+    def is_completed(self):
+        return self._side.query()
+
+
 class _SideStreamWork:
     """An all-reduce issued on the communicator's side stream (forked from the caller's current
     stream); ``wait()`` joins it back into the stream current at wait time."""

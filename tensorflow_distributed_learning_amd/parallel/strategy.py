@@ -359,7 +359,13 @@ def _select_communicator(impl: CommunicationImplementation, device: torch.device
                                  timeout=timeout)
         comm.enable_xgmi(timeout)
         return comm
-    comm = TorchCommunicator("nccl", rank, world, device, store=store, timeout=timeout)
+    if os.environ.get("TDL_NATIVE_RCCL") == "1":
+        # the framework's own RCCL communicator (csrc/rccl_comm.cpp: async-error query, abort)
+        from .communicator import NativeRcclCommunicator
+
+        comm = NativeRcclCommunicator(rank, world, device, store=store, timeout=timeout)
+    else:
+        comm = TorchCommunicator("nccl", rank, world, device, store=store, timeout=timeout)
     if impl != CommunicationImplementation.NCCL:  # AUTO: topology/size-aware algorithm choice
         comm.enable_xgmi(timeout)
     return comm

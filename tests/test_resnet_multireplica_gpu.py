@@ -31,7 +31,7 @@ def test_resnet50_two_replicas():
     d = _run(["--gpus", "2", "--batch", "16", "--steps", "4", "--warmup", "3"])
     c = d["config"]
     assert d["n_gpus"] == 2 and c["replicas_identical"] and c["allreduce"].startswith("xgmi"), c
-    assert c["bucket_plan"]["n_buckets"] > 1, c
+    assert c["buckets"]["n"] > 1 and c["buckets"]["overlapped_with_backward"], c
 
 
 def test_resnet50_config5_two_workers_two_replicas():
