@@ -271,15 +271,24 @@ __device__ __forceinline__ void conv_epilogue(const Igemm& a, const f4v (&acc)[W
 // EK selects the epilogue a variant carries (registers: the VGPR peak of the heaviest epilogue sets the
 // occupancy of the whole kernel, so the plain variant must not pay for the fused ones): 0 plain
 // (+ residual, + BN statistics), 1 fused BN-group backward, 2 stride-2 scatter (+ residual, + BN group)
+// DEPTH 0: one LDS stage, no prefetch, up to 4 workgroups per CU -- for reductions of 1-2 k-tiles
+// (the small-channel 1x1 convs), where no main loop exists to pipeline and the time is the load
+// latency and the epilogue, which more resident workgroups overlap with each other
+template <int BM, int BN, int DEPTH>
+constexpr int v1_lds_elems() {
+  return DEPTH == 0 ? ((BM + BN) * LDS_ROW > BM * (BN + 8) ? (BM + BN) * LDS_ROW : BM * (BN + 8))
+                    : 2 * (BM + BN) * LDS_ROW;
+}
+
 template <int BM, int BN, int DEPTH, int EK>
-__global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
+__global__ __launch_bounds__(BM * 2, DEPTH == 0 ? 4 : 2) void k_conv_igemm(Igemm a) {
   constexpr int NT = BM * 2;         // threads: (BM / 64) x 2 waves, each 64 x BN/2
   constexpr int RP = NT / 8;         // tile rows per staging pass (8 x 16-B chunks per 128-B row)
   constexpr int WN = BN / 2;         // columns per wave
   constexpr int NS = WN / 16;        // 16-wide column subtiles per wave
   constexpr int A_LD = BM * BK / 8 / NT;  // 16-B A chunks per thread per tile (4)
   constexpr int B_LD = BN * BK / 8 / NT;  // 16-B B chunks per thread per tile
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * (BM + BN) * LDS_ROW];
+  __shared__ __attribute__((aligned(16))) uint16_t lds[v1_lds_elems<BM, BN, DEPTH>()];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -389,7 +398,16 @@ __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
     }
   };
 
-  if (DEPTH == 1) {
+  if (DEPTH == 0) {
+    for (int t = 0; t < ntiles; ++t) {
+      gload(ra[0], rb[0]);
+      if (t) __syncthreads();  // every wave done reading the previous tile
+      sstore(0, ra[0], rb[0]);
+      __syncthreads();
+      compute(0);
+    }
+    __syncthreads();  // the epilogue reuses the operand LDS
+  } else if (DEPTH == 1) {
     gload(ra[0], rb[0]);
     sstore(0, ra[0], rb[0]);
     __syncthreads();
@@ -421,7 +439,7 @@ __global__ __launch_bounds__(BM * 2, 2) void k_conv_igemm(Igemm a) {
   }
 
   // epilogue: bf16 tile into LDS ([BM][BN + 8]), then 16-B row segments to global
-  conv_epilogue<BM, BN, NT, EK, 64, WN, 2 * (BM + BN) * LDS_ROW>(a, acc, lds, tm, tn, wm * 64, wn * WN);
+  conv_epilogue<BM, BN, NT, EK, 64, WN, v1_lds_elems<BM, BN, DEPTH>()>(a, acc, lds, tm, tn, wm * 64, wn * WN);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -564,22 +582,33 @@ __global__ __launch_bounds__(512, 1) void k_conv_glds(Igemm a) {
   conv_epilogue<BM, BN, NT, EK, WTM, WTN, v2_lds_elems<BM, BN>()>(a, acc, lds, tm, tn, wm * WTM, wn * WTN);
 }
 
-int g_depth = 2;  // register prefetch depth (tiles in flight); conv_force_depth for A/B sweeps
+int g_depth = 2;  // register prefetch depth (tiles in flight); conv_force_depth for A/B sweeps (0: single stage)
+bool g_short_single = true;  // 1-2 k-tile reductions: the single-stage, 4-workgroups-per-CU variant
 
 template <int BM, int BN, int DEPTH>
 void launch_epi(const Igemm& a, hipStream_t s) {
   const dim3 grid((a.M + BM - 1) / BM * (a.K / BN)), block(BM * 2);
-  if (a.scatter)
-    hipLaunchKernelGGL((k_conv_igemm<BM, BN, DEPTH, 2>), grid, block, 0, s, a);
-  else if (a.bn_part)
-    hipLaunchKernelGGL((k_conv_igemm<BM, BN, DEPTH, 1>), grid, block, 0, s, a);
-  else
-    hipLaunchKernelGGL((k_conv_igemm<BM, BN, DEPTH, 0>), grid, block, 0, s, a);
+  if constexpr (DEPTH == 0) {  // plain epilogue only (launch_tile)
+    hipLaunchKernelGGL((k_conv_igemm<BM, BN, 0, 0>), grid, block, 0, s, a);
+  } else {
+    if (a.scatter)
+      hipLaunchKernelGGL((k_conv_igemm<BM, BN, DEPTH, 2>), grid, block, 0, s, a);
+    else if (a.bn_part)
+      hipLaunchKernelGGL((k_conv_igemm<BM, BN, DEPTH, 1>), grid, block, 0, s, a);
+    else
+      hipLaunchKernelGGL((k_conv_igemm<BM, BN, DEPTH, 0>), grid, block, 0, s, a);
+  }
 }
 
 template <int BM, int BN>
 void launch_tile(const Igemm& a, hipStream_t s) {
-  if (g_depth == 1)
+  const int ktiles = a.KH * a.KW * (a.C / BK);
+  // (plain epilogue only: the fused BN-backward epilogues do not fit the 128-VGPR budget of 4
+  // workgroups per CU without spilling)
+  const bool plain = !a.scatter && a.bn_part == nullptr;
+  if (plain && (g_depth == 0 || (g_depth == 2 && g_short_single && ktiles <= 2)))
+    launch_epi<BM, BN, 0>(a, s);
+  else if (g_depth == 1)
     launch_epi<BM, BN, 1>(a, s);
   else
     launch_epi<BM, BN, 2>(a, s);
@@ -628,7 +657,12 @@ void launch(const Igemm& a, hipStream_t s) {
 
 void conv_force_tile(int tile) { g_forced_tile = tile; }
 void conv_force_impl(int impl) { g_impl = (impl == 1 || impl == 3) ? impl : 2; }
-void conv_force_depth(int depth) { g_depth = depth == 1 ? 1 : 2; }
+void conv_force_depth(int depth) {
+  // 0: single stage everywhere, 1 / 2: register prefetch depth (3: depth 2 without the short-
+  // reduction single-stage variant)
+  g_depth = depth == 0 ? 0 : (depth == 1 ? 1 : 2);
+  g_short_single = depth != 3;
+}
 
 bool conv_bf16_supported(const ConvGeom& g) {
   // byte offsets of every operand and output within 2 GiB (32-bit buffer offsets), <= 32 taps

@@ -189,8 +189,10 @@ hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
 void register_rccl(pybind11::module& m) {
   pybind11::class_<RcclComm>(m, "RcclComm")
-      .def(pybind11::init([](pybind11::bytes uid, int rank, int world, int device) {
-             return new RcclComm(std::string(uid), rank, world, device);
+      // the id arrives as std::string (converted while the GIL is held): the constructor runs with
+      // the GIL released, so no Python object may be owned by this lambda
+      .def(pybind11::init([](const std::string& uid, int rank, int world, int device) {
+             return new RcclComm(uid, rank, world, device);
            }),
            pybind11::arg("unique_id"), pybind11::arg("rank"), pybind11::arg("world"), pybind11::arg("device"),
            pybind11::call_guard<pybind11::gil_scoped_release>())

@@ -278,3 +278,35 @@ def test_wgrad3x3_row_kernel_matches_fp32(shape):
     C.conv_wgrad(x, dy, 3, 3, 1, 1, 1, 1, out=slab, accumulate=True, plan=[0, 0, 0])
     assert (slab - 0.25 - ref).abs().max().item() / scale < 1e-4
     assert torch.equal(dw, C.conv_wgrad(x, dy, 3, 3, 1, 1, 1, 1, plan=[0, 0, 0]))
+
+
+@pytest.mark.parametrize("shape", [(3, 7, 7, 128, 256, 1, 1, 1, 0), (8, 28, 28, 64, 256, 1, 1, 1, 0),
+                                   (2, 14, 14, 64, 64, 3, 3, 1, 1)])
+def test_conv_main_loop_variants_bitwise(shape):
+    """Every main-loop variant of the v1 kernel (single LDS stage with 4 workgroups per CU, register
+    prefetch depth 1 and 2, and the default selection that takes the single stage for 1-2 k-tile
+    reductions) issues the same MFMAs in the same order: outputs and BN partial sums agree bitwise,
+    and match the fp32 reference."""
+    from tensorflow_distributed_learning_amd.ops import hip
+
+    C = hip()
+    N, H, W, Ci, K, KH, KW, s, p = shape
+    x, k = _mk(shape, "cuda:0")
+    w = k.permute(3, 0, 1, 2).contiguous()
+    ref = _ref_fwd(x, k, s, p)
+    OH, OW = ref.shape[1], ref.shape[2]
+    outs = []
+    try:
+        C.conv_force_impl(1)
+        for depth in (0, 1, 3, 2):
+            C.conv_force_depth(depth)
+            outs.append((C.conv_fwd(x, w, OH, OW, s, s, p, p),) + tuple(C.conv_fwd_stats(x, w, OH, OW, s, s, p, p)))
+    finally:
+        C.conv_force_depth(2)
+        C.conv_force_impl(2)
+    torch.testing.assert_close(outs[0][0].float(), ref, atol=3e-2, rtol=2e-2)
+    for o in outs[1:]:
+        assert torch.equal(o[0], outs[0][0]) and torch.equal(o[1], outs[0][1])
+        R = o[2].shape[0]  # partial rows [P + ceil(P / 64)]: the trailing scratch rows are not outputs
+        P = next(q for q in range(R + 1) if q + (q + 63) // 64 == R)
+        assert torch.equal(o[2][:P], outs[0][2][:P])
