@@ -271,7 +271,8 @@ __device__ __forceinline__ void conv_epilogue(const Igemm& a, const f4v (&acc)[W
 // EK selects the epilogue a variant carries (registers: the VGPR peak of the heaviest epilogue sets the
 // occupancy of the whole kernel, so the plain variant must not pay for the fused ones): 0 plain
 // (+ residual, + BN statistics), 1 fused BN-group backward, 2 stride-2 scatter (+ residual, + BN group)
-// DEPTH 0: one LDS stage, no prefetch, up to 4 workgroups per CU -- for reductions of 1-2 k-tiles
+// DEPTH 0: one LDS stage, no prefetch, 4 waves per SIMD (two 256x128 workgroups per CU instead of one:
+// <= 128 VGPRs, 55 KB LDS each) -- for reductions of 1-2 k-tiles
 // (the small-channel 1x1 convs), where no main loop exists to pipeline and the time is the load
 // latency and the epilogue, which more resident workgroups overlap with each other
 template <int BM, int BN, int DEPTH>

@@ -283,7 +283,7 @@ def test_wgrad3x3_row_kernel_matches_fp32(shape):
 @pytest.mark.parametrize("shape", [(3, 7, 7, 128, 256, 1, 1, 1, 0), (8, 28, 28, 64, 256, 1, 1, 1, 0),
                                    (2, 14, 14, 64, 64, 3, 3, 1, 1)])
 def test_conv_main_loop_variants_bitwise(shape):
-    """Every main-loop variant of the v1 kernel (single LDS stage with 4 workgroups per CU, register
+    """Every main-loop variant of the v1 kernel (single LDS stage at 4 waves per SIMD, register
     prefetch depth 1 and 2, and the default selection that takes the single stage for 1-2 k-tile
     reductions) issues the same MFMAs in the same order: outputs and BN partial sums agree bitwise,
     and match the fp32 reference."""
