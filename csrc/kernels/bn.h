@@ -20,6 +20,8 @@ struct BnPlan {
 BnPlan bn_plan(int64_t M, int C);
 // sweep hooks: partial-pass workgroup cap, elementwise-pass grid cap, vectors per thread (1 or 2)
 void bn_set_tuning(int max_parts, int elem_blocks, int elem_unroll);
+// elementwise kernel family (A/B hook): 0 grid-stride, 1 blocked with 2 / 4 / 8 vectors per thread
+void bn_set_elementwise(int kind, int vectors_per_thread);
 
 // forward: part [parts][2][C] scratch; mean/invstd [C] out; scale/shift [C] out (x*scale+shift);
 // moving stats updated in place (momentum m: moving = moving*m + batch*(1-m), variance unbiased);

@@ -21,6 +21,11 @@ constexpr int kUnroll = 4;
 int g_max_parts = 512;
 int g_elem_blocks = 256 * 16;
 int g_elem_unroll = 1;  // 2 measured 1-4 % slower (scripts/bench_bn.py, profiles/bn_tuning_sweep_r2.jsonl)
+// elementwise kernel family: 0 grid-stride (one vector per thread per tensor in flight, LDS channel
+// tables), 1 blocked (g_elem_vpt vectors per thread per tensor in flight, channels in registers)
+int g_elem_kind = 1;
+int g_elem_vpt = 4;
+int g_blk_blocks = 8192;  // grid cap of the blocked kernels (measured best, profiles/bn_blocked_sweep_r4.jsonl)
 constexpr int kFinPhases = 16;  // partial-row phases per channel in the finalize kernels (1024 threads)
 
 __device__ __forceinline__ float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
@@ -354,6 +359,152 @@ __global__ __launch_bounds__(256) void k_bn_dx(const void* __restrict__ dy, cons
   }
 }
 
+// Blocked elementwise passes (bf16, C a power of two <= 2048).  A workgroup streams chunks of 256*V
+// consecutive 16-B vectors, thread t owning vectors t, t + 256, ... of a chunk: the V loads per
+// tensor are all issued before any math (2V x 16 B in flight per thread), and since C divides
+// 2048 = 256 vectors x 8 channels a thread's 8 channels are the same in every chunk, so its
+// scale/shift (dx coefficients) sit in registers instead of an LDS table read per vector.  bf16
+// packing is v_cvt_pk_bf16_f32 (round to nearest even, as f2bf).
+__device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
+  uint32_t r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+  return r;
+}
+
+__device__ __forceinline__ void unpack8(const uint4& u, float* o) {
+  o[0] = bf_lo(u.x); o[1] = bf_hi(u.x); o[2] = bf_lo(u.y); o[3] = bf_hi(u.y);
+  o[4] = bf_lo(u.z); o[5] = bf_hi(u.z); o[6] = bf_lo(u.w); o[7] = bf_hi(u.w);
+}
+
+__device__ __forceinline__ uint4 pack8(const float* v) {
+  return uint4{pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]), pk_bf16(v[4], v[5]), pk_bf16(v[6], v[7])};
+}
+
+template <int V>
+__global__ __launch_bounds__(256) void k_bn_apply_blk(const uint4* __restrict__ x, const uint4* __restrict__ res,
+                                                      uint4* __restrict__ y, int64_t n8, int C,
+                                                      const float* __restrict__ scale,
+                                                      const float* __restrict__ shift, int relu) {
+  const int c0 = (threadIdx.x * 8) & (C - 1);
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = scale[c0 + j];
+    sh[j] = shift[c0 + j];
+  }
+  const int64_t nch = (n8 + 256 * V - 1) / (256 * V);
+  for (int64_t ch = blockIdx.x; ch < nch; ch += gridDim.x) {
+    const int64_t v0 = ch * (256 * V) + threadIdx.x;
+    uint4 xu[V], ru[V];
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+      if (v0 + u * 256 < n8) {
+        xu[u] = x[v0 + u * 256];
+        if (res != nullptr) ru[u] = res[v0 + u * 256];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+      if (v0 + u * 256 >= n8) break;
+      float o[8], r[8];
+      unpack8(xu[u], o);
+      if (res != nullptr) unpack8(ru[u], r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        o[j] = fmaf(o[j], sc[j], sh[j]);
+        if (res != nullptr) o[j] += r[j];
+        if (relu) o[j] = fmaxf(o[j], 0.f);
+      }
+      y[v0 + u * 256] = pack8(o);
+    }
+  }
+}
+
+template <bool MASK, int V>
+__global__ __launch_bounds__(256) void k_bn_dx_blk(const uint4* __restrict__ dy, const uint4* __restrict__ x,
+                                                   uint4* __restrict__ dx, int64_t n8, int C,
+                                                   const float* __restrict__ coef, const float* __restrict__ scale,
+                                                   const float* __restrict__ shift) {
+  const int c0 = (threadIdx.x * 8) & (C - 1);
+  float cA[8], cB[8], cD[8], cS[8], cT[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    cA[j] = coef[c0 + j];
+    cB[j] = coef[C + c0 + j];
+    cD[j] = coef[2 * C + c0 + j];
+    cS[j] = MASK ? scale[c0 + j] : 0.f;
+    cT[j] = MASK ? shift[c0 + j] : 0.f;
+  }
+  const int64_t nch = (n8 + 256 * V - 1) / (256 * V);
+  for (int64_t ch = blockIdx.x; ch < nch; ch += gridDim.x) {
+    const int64_t v0 = ch * (256 * V) + threadIdx.x;
+    uint4 gu[V], xu[V];
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+      if (v0 + u * 256 < n8) {
+        gu[u] = dy[v0 + u * 256];
+        xu[u] = x[v0 + u * 256];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+      if (v0 + u * 256 >= n8) break;
+      float g[8], xv[8];
+      unpack8(gu[u], g);
+      unpack8(xu[u], xv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (MASK && !(fmaf(xv[j], cS[j], cT[j]) > 0.f)) g[j] = 0.f;
+        g[j] = fmaf(cA[j], g[j], fmaf(cB[j], xv[j], cD[j]));
+      }
+      dx[v0 + u * 256] = pack8(g);
+    }
+  }
+}
+
+bool blocked_ok(BnDType dt, int C) { return g_elem_kind == 1 && dt == BnDType::kBF16 && C >= 8 && C <= 2048 && (C & (C - 1)) == 0; }
+
+int blocked_grid(int64_t n8) {
+  const int64_t nch = (n8 + 256 * g_elem_vpt - 1) / (256 * g_elem_vpt);
+  return (int)std::min<int64_t>(std::max<int64_t>(nch, 1), g_blk_blocks);
+}
+
+template <int V>
+void launch_apply_blk(const void* x, const void* res, void* y, int64_t n8, int C, const float* scale,
+                      const float* shift, int relu, hipStream_t s) {
+  hipLaunchKernelGGL((k_bn_apply_blk<V>), dim3(blocked_grid(n8)), dim3(256), 0, s, static_cast<const uint4*>(x),
+                     static_cast<const uint4*>(res), static_cast<uint4*>(y), n8, C, scale, shift, relu);
+}
+
+template <bool MASK, int V>
+void launch_dx_blk(const void* dy, const void* x, void* dx, int64_t n8, int C, const float* coef, const float* scale,
+                   const float* shift, hipStream_t s) {
+  hipLaunchKernelGGL((k_bn_dx_blk<MASK, V>), dim3(blocked_grid(n8)), dim3(256), 0, s, static_cast<const uint4*>(dy),
+                     static_cast<const uint4*>(x), static_cast<uint4*>(dx), n8, C, coef, scale, shift);
+}
+
+// dispatch on the per-thread depth (2, 4 or 8 vectors per tensor)
+void apply_blk(const void* x, const void* res, void* y, int64_t n8, int C, const float* scale, const float* shift,
+               int relu, hipStream_t s) {
+  if (g_elem_vpt == 2)
+    launch_apply_blk<2>(x, res, y, n8, C, scale, shift, relu, s);
+  else if (g_elem_vpt == 8)
+    launch_apply_blk<8>(x, res, y, n8, C, scale, shift, relu, s);
+  else
+    launch_apply_blk<4>(x, res, y, n8, C, scale, shift, relu, s);
+}
+
+template <bool MASK>
+void dx_blk(const void* dy, const void* x, void* dx, int64_t n8, int C, const float* coef, const float* scale,
+            const float* shift, hipStream_t s) {
+  if (g_elem_vpt == 2)
+    launch_dx_blk<MASK, 2>(dy, x, dx, n8, C, coef, scale, shift, s);
+  else if (g_elem_vpt == 8)
+    launch_dx_blk<MASK, 8>(dy, x, dx, n8, C, coef, scale, shift, s);
+  else
+    launch_dx_blk<MASK, 4>(dy, x, dx, n8, C, coef, scale, shift, s);
+}
+
 int elementwise_grid(int64_t n8) {
   const int64_t b = (n8 + 255) / 256;
   return (int)std::min<int64_t>(b, g_elem_blocks);
@@ -363,8 +514,13 @@ int elementwise_grid(int64_t n8) {
 
 void bn_set_tuning(int max_parts, int elem_blocks, int elem_unroll) {
   if (max_parts > 0) g_max_parts = max_parts;
-  if (elem_blocks > 0) g_elem_blocks = elem_blocks;
+  if (elem_blocks > 0) g_elem_blocks = g_blk_blocks = elem_blocks;
   if (elem_unroll == 1 || elem_unroll == 2) g_elem_unroll = elem_unroll;
+}
+
+void bn_set_elementwise(int kind, int vectors_per_thread) {
+  g_elem_kind = kind == 0 ? 0 : 1;
+  if (vectors_per_thread == 2 || vectors_per_thread == 4 || vectors_per_thread == 8) g_elem_vpt = vectors_per_thread;
 }
 
 BnPlan bn_plan(int64_t M, int C) {
@@ -408,6 +564,10 @@ void bn_forward_stats(const void* x, BnDType dt, int64_t M, int C, float* part, 
 void bn_apply(const void* x, const void* residual, void* y, BnDType dt, int64_t M, int C, const float* scale,
               const float* shift, int relu, hipStream_t s) {
   const int64_t n8 = M * C / 8;
+  if (blocked_ok(dt, C)) {
+    apply_blk(x, residual, y, n8, C, scale, shift, relu, s);
+    return;
+  }
   const dim3 g(elementwise_grid(n8)), b(256);
   if (dt == BnDType::kBF16) {
     if (g_elem_unroll == 2)
@@ -433,8 +593,11 @@ static void bn_backward_t(const void* dy, const void* x, const void* y, void* dz
     hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), dim3(64 * kFinPhases), 0, s, pr, P, M, C, gamma, mean,
                        invstd, dgamma, dbeta, coef, acc);
     const int64_t n8 = M * C / 8;
-    hipLaunchKernelGGL((k_bn_dx<D, false, 1>), dim3(elementwise_grid(n8)), blk, 0, s, dy, x, dx, n8, C, coef, nullptr,
-                       nullptr);
+    if (blocked_ok(D, C))
+      dx_blk<false>(dy, x, dx, n8, C, coef, nullptr, nullptr, s);
+    else
+      hipLaunchKernelGGL((k_bn_dx<D, false, 1>), dim3(elementwise_grid(n8)), blk, 0, s, dy, x, dx, n8, C, coef,
+                         nullptr, nullptr);
     return;
   }
   if (mode == 0)
@@ -450,6 +613,13 @@ static void bn_backward_t(const void* dy, const void* x, const void* y, void* dz
   hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), dim3(64 * kFinPhases), 0, s, pr, P, M, C, gamma, mean, invstd,
                      dgamma, dbeta, coef, acc);
   const int64_t n8 = M * C / 8;
+  if (blocked_ok(D, C)) {
+    if (mode == 1)
+      dx_blk<true>(dy, x, dx, n8, C, coef, scale, shift, s);
+    else
+      dx_blk<false>(mode == 2 ? dz : dy, x, dx, n8, C, coef, nullptr, nullptr, s);
+    return;
+  }
   const dim3 ge(elementwise_grid(n8));
   const bool u2 = g_elem_unroll == 2 && D == BnDType::kBF16;
   if (mode == 1) {

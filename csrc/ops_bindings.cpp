@@ -605,6 +605,8 @@ void register_ops(pybind11::module& m) {
   m.def("gap_bwd", &gap_bwd, "NHWC bf16 global average pooling backward");
   m.def("slab_cast_bf16", &slab_cast_bf16, "f32 -> bf16 copy of a whole weight slab (one launch)");
   m.def("bn_set_tuning", &tdl::bn_set_tuning, "BN kernel sweep hooks (max_parts, elem_blocks, elem_unroll; 0 = keep)");
+  m.def("bn_set_elementwise", &tdl::bn_set_elementwise,
+        "BN elementwise kernel family A/B hook (kind 0 grid-stride / 1 blocked, vectors per thread 2/4/8)");
   m.def("slab_transpose_bf16", &slab_transpose_bf16, "HWIO f32 conv kernels -> OHWI bf16, all in one launch");
   m.def("conv_dgrad_bn", &conv_dgrad_bn, "stride-1 conv input gradient + fused BN->Add->ReLU backward (dz, part[, part2])",
         pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("h"), pybind11::arg("wd"), pybind11::arg("pt"),

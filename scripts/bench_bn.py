@@ -1,6 +1,7 @@
 """Effective HBM bandwidth of the NHWC batch-norm kernels (csrc/kernels/bn.hip) on the ResNet-50
 b=256 shapes, over a sweep of the tuning knobs (partial-pass workgroups, elementwise grid, vectors per
-thread), with a plain device copy as the reference ceiling.  One JSON line per (config, shape)."""
+thread, elementwise kernel family: 0 grid-stride, 1 blocked), with a plain device copy as the reference
+ceiling.  One JSON line per shape."""
 import json
 import sys
 
@@ -11,7 +12,9 @@ from tensorflow_distributed_learning_amd.ops import hip  # noqa: E402
 
 SHAPES = [(802816, 64), (802816, 256), (200704, 128), (200704, 512), (50176, 256), (50176, 1024), (12544, 512),
           (12544, 2048), (3211264, 64)]
-CONFIGS = [(512, 4096, 1), (1024, 4096, 2), (2048, 4096, 2), (2048, 8192, 2), (4096, 4096, 2), (2048, 2048, 1)]
+# (max_parts, elem_blocks, elem_unroll, kind, vectors per thread)
+CONFIGS = [(512, 4096, 1, 0, 4), (512, 4096, 1, 1, 2), (512, 4096, 1, 1, 4), (512, 4096, 1, 1, 8),
+           (512, 8192, 1, 1, 4), (512, 2048, 1, 1, 4), (512, 1024, 1, 1, 8)]
 
 
 def t(fn, reps=10):
@@ -40,7 +43,8 @@ def main():
         tc = t(lambda: y.copy_(x))
         rec = {"shape": [M, Ch], "copy_TBps": round(2 * nb / tc / 1e6, 2)}
         for cfg in CONFIGS:
-            C.bn_set_tuning(*cfg)
+            C.bn_set_tuning(*cfg[:3])
+            C.bn_set_elementwise(*cfg[3:])
             yf, st = C.bn_forward_train(x, g, b, mm, mv, 0.99, 1e-3, True, None, None)
             t_f = t(lambda: C.bn_forward_train(x, g, b, mm, mv, 0.99, 1e-3, True, None, None))
             t_fr = t(lambda: C.bn_forward_train(x, g, b, mm, mv, 0.99, 1e-3, True, r, None))
@@ -54,6 +58,9 @@ def main():
             tot[key] = tot.get(key, 0.0) + t_f + t_fr + t_b1 + t_b2
         print(json.dumps(rec), flush=True)
     print(json.dumps({"total_us_per_config": {k: round(v, 1) for k, v in tot.items()}}))
+    C.bn_set_tuning(512, 4096, 1)  # the defaults (the blocked kernels' grid cap back to 8192 below)
+    C.bn_set_elementwise(1, 4)
+    C.bn_set_tuning(0, 8192, 0)
 
 
 if __name__ == "__main__":

@@ -176,3 +176,41 @@ def test_maxpool_nhwc_matches_torch(dtype, geo):
     y.backward(dy)
     yr.backward(dy.float())
     torch.testing.assert_close(xa.grad.float(), xb.grad, atol=1e-2 if dtype == torch.bfloat16 else 1e-6, rtol=1e-2)
+
+
+@pytest.mark.parametrize("shape", [(16, 56, 56, 64), (3, 7, 7, 2048), (5, 9, 9, 256), (1, 3, 5, 8)])
+def test_bn_elementwise_blocked_matches_grid_stride_bitwise(shape):
+    """The blocked elementwise kernels (channels in registers, several vectors per thread in flight,
+    ragged last chunk) compute bit-identical apply / dx to the grid-stride ones, for every backward
+    mode and with a residual."""
+    from tensorflow_distributed_learning_amd.ops import hip
+
+    Ck = hip()
+    torch.manual_seed(2)
+    dev = torch.device("cuda:0")
+    C = shape[-1]
+    x = (torch.randn(shape, device=dev) * 2 + 0.5).bfloat16()
+    r = torch.randn(shape, device=dev).bfloat16()
+    dy = torch.randn(shape, device=dev).bfloat16()
+    g, b = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev)
+
+    def run():
+        mm, mv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        y0, st = Ck.bn_forward_train(x, g, b, mm, mv, 0.9, 1e-3, True, None, None)
+        y1, _ = Ck.bn_forward_train(x, g, b, mm, mv, 0.9, 1e-3, False, r, None)
+        outs = [y0, y1]
+        for mode in (0, 1, 2):
+            outs += [t for t in Ck.bn_backward(dy, x, y0 if mode == 2 else None, g, st, mode) if t is not None]
+        return outs
+
+    try:
+        Ck.bn_set_elementwise(0, 4)
+        ref = run()
+        for vpt in (2, 4, 8):
+            Ck.bn_set_elementwise(1, vpt)
+            got = run()
+            assert len(got) == len(ref)
+            for a, e in zip(got, ref):
+                assert torch.equal(a, e)
+    finally:
+        Ck.bn_set_elementwise(1, 4)
