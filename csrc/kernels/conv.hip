@@ -125,7 +125,9 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
 // rounded to bf16 into LDS ([BM][BN + 8], the operand LDS is free by now), then written back as 16-byte
 // row segments with the variant's fused operations (residual, BN statistics / BN-group backward sums,
 // stride-2 scatter).  Every thread of the workgroup must call it (it has workgroup barriers).
-template <int BM, int BN, int NT, int EK, int WTM, int WTN, int LDS_ELEMS>
+// LOWREG (the 4-waves-per-SIMD variants, <= 128 VGPRs): the BN-group backward epilogue loads its
+// residual and BN operands in chunks of EPI / 4 segments right before their use instead of all up front.
+template <int BM, int BN, int NT, int EK, int WTM, int WTN, int LDS_ELEMS, bool LOWREG = false>
 __device__ __forceinline__ void conv_epilogue(const Igemm& a, const f4v (&acc)[WTM / 16][WTN / 16], uint16_t* lds,
                                               int tm, int tn, int wrow0, int wcol0) {
   const int tid = threadIdx.x, lane = tid & 63;
@@ -135,8 +137,9 @@ __device__ __forceinline__ void conv_epilogue(const Igemm& a, const f4v (&acc)[W
   static_assert(BM * SEG % NT == 0, "epilogue segments must divide evenly");
   // residual (gradient sum): all of this thread's loads issued here, before the LDS round trip, so
   // their latency overlaps it instead of serialising the store loop
+  constexpr int EC = (LOWREG && EK == 1) ? (EPI >= 4 ? EPI / 4 : 1) : EPI;  // segments per operand chunk
   u32x4 rv[EK == 2 ? 1 : EPI];
-  if (EK != 2 && a.res) {
+  if (EK != 2 && a.res && EC == EPI) {
 #pragma unroll
     for (int e = 0; e < EPI; ++e) {
       const int s = tid + e * NT, row = s / SEG, seg = s % SEG, m = tm * BM + row;
@@ -158,17 +161,32 @@ __device__ __forceinline__ void conv_epilogue(const Igemm& a, const f4v (&acc)[W
   // BN-backward fusion operands (the accumulators are dead now: registers to spare)
   constexpr int BNE = EK == 1 ? EPI : 1;
   u32x4 ry[BNE], rx[BNE], rx2[BNE];
-  if constexpr (EK == 1) {
+  // the BN-group operands of segments [e0, e0 + EC) (all of them up front unless LOWREG)
+  auto load_bn = [&](int e0) {
+    if constexpr (EK == 1) {
 #pragma unroll
-    for (int e = 0; e < EPI; ++e) {
-      const int s = tid + e * NT, row = s / SEG, seg = s % SEG, m = tm * BM + row;
-      const long long o = (long long)m * a.K + tn * BN + seg * 8;
-      const bool in = m < a.M;
-      ry[e] = in ? *reinterpret_cast<const u32x4*>(a.bn_y + o) : u32x4{0u, 0u, 0u, 0u};
-      rx[e] = in ? *reinterpret_cast<const u32x4*>(a.bn_x + o) : u32x4{0u, 0u, 0u, 0u};
-      rx2[e] = (in && a.bn_x2) ? *reinterpret_cast<const u32x4*>(a.bn_x2 + o) : u32x4{0u, 0u, 0u, 0u};
+      for (int e = e0; e < e0 + EC; ++e) {
+        const int s = tid + e * NT, row = s / SEG, seg = s % SEG, m = tm * BM + row;
+        const long long o = (long long)m * a.K + tn * BN + seg * 8;
+        const bool in = m < a.M;
+        ry[e] = in ? *reinterpret_cast<const u32x4*>(a.bn_y + o) : u32x4{0u, 0u, 0u, 0u};
+        rx[e] = in ? *reinterpret_cast<const u32x4*>(a.bn_x + o) : u32x4{0u, 0u, 0u, 0u};
+        rx2[e] = (in && a.bn_x2) ? *reinterpret_cast<const u32x4*>(a.bn_x2 + o) : u32x4{0u, 0u, 0u, 0u};
+        if (EC != EPI && a.res)
+          rv[e] = in ? *reinterpret_cast<const u32x4*>(a.res + o) : u32x4{0u, 0u, 0u, 0u};
+      }
+    } else if (EC != EPI && EK == 0) {
+      if (a.res) {
+#pragma unroll
+        for (int e = e0; e < e0 + EC; ++e) {
+          const int s = tid + e * NT, row = s / SEG, seg = s % SEG, m = tm * BM + row;
+          rv[e] = m < a.M ? *reinterpret_cast<const u32x4*>(a.res + (long long)m * a.K + tn * BN + seg * 8)
+                          : u32x4{0u, 0u, 0u, 0u};
+        }
+      }
     }
-  }
+  };
+  if (EC == EPI) load_bn(0);
   __syncthreads();
   static_assert(NT % SEG == 0, "a thread keeps one 8-channel segment across its rows");
   // per-tile channel sums: (y, y^2) of the forward output, or (dz, dz * xb) [and dz * xb2] of a fused
@@ -181,6 +199,7 @@ __device__ __forceinline__ void conv_epilogue(const Igemm& a, const f4v (&acc)[W
   if constexpr (EK != 2) {
 #pragma unroll
     for (int e = 0; e < EPI; ++e) {
+      if (EC != EPI && e % EC == 0) load_bn(e);
       const int s = tid + e * NT, row = s / SEG, seg = s % SEG;
       const int m = tm * BM + row;
       if (m < a.M) {
@@ -271,18 +290,20 @@ __device__ __forceinline__ void conv_epilogue(const Igemm& a, const f4v (&acc)[W
 // EK selects the epilogue a variant carries (registers: the VGPR peak of the heaviest epilogue sets the
 // occupancy of the whole kernel, so the plain variant must not pay for the fused ones): 0 plain
 // (+ residual, + BN statistics), 1 fused BN-group backward, 2 stride-2 scatter (+ residual, + BN group)
-// DEPTH 0: one LDS stage, no prefetch, 4 waves per SIMD (two 256x128 workgroups per CU instead of one:
-// <= 128 VGPRs, 55 KB LDS each) -- for reductions of 1-2 k-tiles
-// (the small-channel 1x1 convs), where no main loop exists to pipeline and the time is the load
-// latency and the epilogue, which more resident workgroups overlap with each other
+// DEPTH 0 (the default, see launch_tile): one LDS stage, no prefetch, 4 waves per SIMD (four 128x128
+// workgroups per CU instead of two: <= 128 VGPRs, 37 KB LDS each); the resident workgroups hide each
+// other's load latency and epilogues.
+// DEPTH 3: one LDS stage with one tile of register prefetch, 3 waves per SIMD (<= 168 VGPRs; plain
+// and scatter epilogues): the next tile's loads fly during this tile's MFMAs, and three workgroups
+// per CU instead of the two that double-buffered LDS allows.
 template <int BM, int BN, int DEPTH>
 constexpr int v1_lds_elems() {
-  return DEPTH == 0 ? ((BM + BN) * LDS_ROW > BM * (BN + 8) ? (BM + BN) * LDS_ROW : BM * (BN + 8))
-                    : 2 * (BM + BN) * LDS_ROW;
+  return (DEPTH == 0 || DEPTH == 3) ? ((BM + BN) * LDS_ROW > BM * (BN + 8) ? (BM + BN) * LDS_ROW : BM * (BN + 8))
+                                    : 2 * (BM + BN) * LDS_ROW;
 }
 
 template <int BM, int BN, int DEPTH, int EK>
-__global__ __launch_bounds__(BM * 2, DEPTH == 0 ? 4 : 2) void k_conv_igemm(Igemm a) {
+__global__ __launch_bounds__(BM * 2, DEPTH == 0 ? 4 : (DEPTH == 3 ? 3 : 2)) void k_conv_igemm(Igemm a) {
   constexpr int NT = BM * 2;         // threads: (BM / 64) x 2 waves, each 64 x BN/2
   constexpr int RP = NT / 8;         // tile rows per staging pass (8 x 16-B chunks per 128-B row)
   constexpr int WN = BN / 2;         // columns per wave
@@ -408,6 +429,16 @@ __global__ __launch_bounds__(BM * 2, DEPTH == 0 ? 4 : 2) void k_conv_igemm(Igemm
       compute(0);
     }
     __syncthreads();  // the epilogue reuses the operand LDS
+  } else if (DEPTH == 3) {
+    gload(ra[0], rb[0]);
+    for (int t = 0; t < ntiles; ++t) {
+      if (t) __syncthreads();  // every wave done reading tile t - 1
+      sstore(0, ra[0], rb[0]);
+      __syncthreads();
+      if (t + 1 < ntiles) gload(ra[0], rb[0]);  // in flight during this tile's MFMAs
+      compute(0);
+    }
+    __syncthreads();
   } else if (DEPTH == 1) {
     gload(ra[0], rb[0]);
     sstore(0, ra[0], rb[0]);
@@ -440,7 +471,8 @@ __global__ __launch_bounds__(BM * 2, DEPTH == 0 ? 4 : 2) void k_conv_igemm(Igemm
   }
 
   // epilogue: bf16 tile into LDS ([BM][BN + 8]), then 16-B row segments to global
-  conv_epilogue<BM, BN, NT, EK, 64, WN, v1_lds_elems<BM, BN, DEPTH>()>(a, acc, lds, tm, tn, wm * 64, wn * WN);
+  conv_epilogue<BM, BN, NT, EK, 64, WN, v1_lds_elems<BM, BN, DEPTH>(), DEPTH == 0>(a, acc, lds, tm, tn, wm * 64,
+                                                                                 wn * WN);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -583,32 +615,35 @@ __global__ __launch_bounds__(512, 1) void k_conv_glds(Igemm a) {
   conv_epilogue<BM, BN, NT, EK, WTM, WTN, v2_lds_elems<BM, BN>()>(a, acc, lds, tm, tn, wm * WTM, wn * WTN);
 }
 
-int g_depth = 2;  // register prefetch depth (tiles in flight); conv_force_depth for A/B sweeps (0: single stage)
-bool g_short_single = true;  // 1-2 k-tile reductions: the single-stage, 4-workgroups-per-CU variant
+int g_depth = 2;  // main-loop variant; conv_force_depth for A/B sweeps
+bool g_single = true;  // default: the single-stage, 4-waves-per-SIMD variant for every reduction length
 
 template <int BM, int BN, int DEPTH>
 void launch_epi(const Igemm& a, hipStream_t s) {
   const dim3 grid((a.M + BM - 1) / BM * (a.K / BN)), block(BM * 2);
-  if constexpr (DEPTH == 0) {  // plain epilogue only (launch_tile)
-    hipLaunchKernelGGL((k_conv_igemm<BM, BN, 0, 0>), grid, block, 0, s, a);
-  } else {
-    if (a.scatter)
-      hipLaunchKernelGGL((k_conv_igemm<BM, BN, DEPTH, 2>), grid, block, 0, s, a);
-    else if (a.bn_part)
-      hipLaunchKernelGGL((k_conv_igemm<BM, BN, DEPTH, 1>), grid, block, 0, s, a);
+  {
+    if (a.scatter)  // (the scatter epilogue spills at 128 VGPRs: depth 0 takes the 3-waves-per-SIMD variant)
+      hipLaunchKernelGGL((k_conv_igemm<BM, BN, DEPTH == 0 ? 3 : DEPTH, 2>), grid, block, 0, s, a);
+    else if (a.bn_part)  // (DEPTH 3's fused BN-group backward epilogue spills at 168 VGPRs: depth 2)
+      hipLaunchKernelGGL((k_conv_igemm<BM, BN, DEPTH == 3 ? 2 : DEPTH, 1>), grid, block, 0, s, a);
     else
       hipLaunchKernelGGL((k_conv_igemm<BM, BN, DEPTH, 0>), grid, block, 0, s, a);
   }
 }
 
+// Main-loop variant, from the A/B over the Keras ResNet-50 b=256 convolutions
+// (profiles/conv_main_loop_ab_r4.txt): four resident 128x128 workgroups per CU without any
+// software pipelining (DEPTH 0) beat two double-buffered ones with two tiles of register prefetch
+// (DEPTH 2) on every shape, 1x1 and 3x3, short and long reductions (e.g. 28x28 3x3 fwd 95.6 -> 73.4
+// us, 14x14 1024->256 1x1 fwd 46.2 -> 40.3): the other workgroups' MFMAs hide a workgroup's load
+// latency and its epilogue better than its own prefetch does.  The single LDS stage with register
+// prefetch at three per CU (DEPTH 3) lands in between.
 template <int BM, int BN>
 void launch_tile(const Igemm& a, hipStream_t s) {
-  const int ktiles = a.KH * a.KW * (a.C / BK);
-  // (plain epilogue only: the fused BN-backward epilogues do not fit the 128-VGPR budget of 4
-  // workgroups per CU without spilling)
-  const bool plain = !a.scatter && a.bn_part == nullptr;
-  if (plain && (g_depth == 0 || (g_depth == 2 && g_short_single && ktiles <= 2)))
+  if (g_depth == 0 || (g_depth == 2 && g_single))
     launch_epi<BM, BN, 0>(a, s);
+  else if (g_depth == 3)
+    launch_epi<BM, BN, 3>(a, s);
   else if (g_depth == 1)
     launch_epi<BM, BN, 1>(a, s);
   else
@@ -630,12 +665,12 @@ void launch_v2(const Igemm& a, hipStream_t s) {
 }
 
 // v2 (256-row tiles, one 8-wave workgroup per CU) where it measured faster than v1
-// (profiles/conv_v2_r4.txt): long reductions (>= 32 k-tiles: the 3x3 convs at 14x14 / 7x7 and
-// the 1024 / 2048-channel 1x1 ones) with a grid that still fills the chip.  With 9-18 k-tiles the
-// ring's fill and drain and the unoverlapped epilogue of the single workgroup per CU cost more
-// than the LDS-DMA saves (v1 keeps two workgroups per CU).  Outputs are bit-identical either way.
-bool use_v2(int M, int K, int ktiles) {
-  if (g_impl == 1 || g_forced_tile != 0 || (g_impl == 2 && ktiles < 32)) return false;
+// (profiles/conv_v2_r4.txt, profiles/conv_main_loop_ab_r4.txt): 1x1 convs with long reductions
+// (>= 32 k-tiles: 2048 input channels) and a grid that still fills the chip, by 2-4 %.  Against the
+// 4-workgroups-per-CU v1 it loses everywhere else, the 3x3 convs at 14x14 / 7x7 included.  Outputs
+// are bit-identical either way.
+bool use_v2(int M, int K, int ktiles, int taps) {
+  if (g_impl == 1 || g_forced_tile != 0 || (g_impl == 2 && (ktiles < 32 || (taps != 1 && g_single)))) return false;
   const long long wgs = (long long)(M + 255) / 256 * (K % 128 == 0 ? K / 128 : K / 64);
   return wgs >= 256;
 }
@@ -645,7 +680,7 @@ bool use_v2(int M, int K, int ktiles) {
 // workgroups per CU (the 64-column tile's extra LDS traffic per MFMA costs more than the idle CUs);
 // 256 x 128 loses 5-20 % everywhere.  The 64-column tile only serves K == 64 * odd.
 void launch(const Igemm& a, hipStream_t s) {
-  if (use_v2(a.M, a.K, a.KH * a.KW * (a.C / BK))) {
+  if (use_v2(a.M, a.K, a.KH * a.KW * (a.C / BK), a.KH * a.KW)) {
     if (a.K % 128 == 0) return launch_v2<256, 128, 4, 2>(a, s);
     return launch_v2<256, 64, 4, 2>(a, s);
   }
@@ -659,10 +694,11 @@ void launch(const Igemm& a, hipStream_t s) {
 void conv_force_tile(int tile) { g_forced_tile = tile; }
 void conv_force_impl(int impl) { g_impl = (impl == 1 || impl == 3) ? impl : 2; }
 void conv_force_depth(int depth) {
-  // 0: single stage everywhere, 1 / 2: register prefetch depth (3: depth 2 without the short-
-  // reduction single-stage variant)
-  g_depth = depth == 0 ? 0 : (depth == 1 ? 1 : 2);
-  g_short_single = depth != 3;
+  // 0: single stage everywhere, 1 / 2: register prefetch depth 1 / the default selection (single
+  // stage), 3: depth 2 everywhere (the selection before round 4's A/B, v2 for every long reduction),
+  // 4: single LDS stage + register prefetch everywhere
+  g_depth = depth == 0 ? 0 : (depth == 1 ? 1 : (depth == 4 ? 3 : 2));
+  g_single = depth != 3;
 }
 
 bool conv_bf16_supported(const ConvGeom& g) {
@@ -680,17 +716,17 @@ bool conv_bf16_supported(const ConvGeom& g) {
 
 // the row tile launch() picks (the BN partial-sum rows of an epilogue are per row tile)
 int conv_fwd_row_tile(const ConvGeom& g) {
-  if (use_v2(g.N * g.OH * g.OW, g.K, g.KH * g.KW * (g.C / BK))) return 256;
+  if (use_v2(g.N * g.OH * g.OW, g.K, g.KH * g.KW * (g.C / BK), g.KH * g.KW)) return 256;
   return (g_forced_tile == 3 && g.K % 128 == 0) ? 256 : 128;
 }
 
 int conv_dgrad_row_tile(const ConvGeom& g) {
-  if (use_v2(g.N * g.H * g.W, g.C, g.KH * g.KW * (g.K / BK))) return 256;
+  if (use_v2(g.N * g.H * g.W, g.C, g.KH * g.KW * (g.K / BK), g.KH * g.KW)) return 256;
   return (g_forced_tile == 3 && g.C % 128 == 0) ? 256 : 128;
 }
 
 int conv_dgrad_s2_row_tile(const ConvGeom& g) {
-  if (use_v2(g.N * g.OH * g.OW, g.C, g.K / BK)) return 256;
+  if (use_v2(g.N * g.OH * g.OW, g.C, g.K / BK, 1)) return 256;
   return (g_forced_tile == 3 && g.C % 128 == 0) ? 256 : 128;
 }
 

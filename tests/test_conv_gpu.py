@@ -283,7 +283,8 @@ def test_wgrad3x3_row_kernel_matches_fp32(shape):
 @pytest.mark.parametrize("shape", [(3, 7, 7, 128, 256, 1, 1, 1, 0), (8, 28, 28, 64, 256, 1, 1, 1, 0),
                                    (2, 14, 14, 64, 64, 3, 3, 1, 1)])
 def test_conv_main_loop_variants_bitwise(shape):
-    """Every main-loop variant of the v1 kernel (single LDS stage at 4 waves per SIMD, register
+    """Every main-loop variant of the v1 kernel (single LDS stage at 4 waves per SIMD, single stage with
+    register prefetch at 3, register
     prefetch depth 1 and 2, and the default selection that takes the single stage for 1-2 k-tile
     reductions) issues the same MFMAs in the same order: outputs and BN partial sums agree bitwise,
     and match the fp32 reference."""
@@ -298,7 +299,7 @@ def test_conv_main_loop_variants_bitwise(shape):
     outs = []
     try:
         C.conv_force_impl(1)
-        for depth in (0, 1, 3, 2):
+        for depth in (0, 1, 3, 4, 2):
             C.conv_force_depth(depth)
             outs.append((C.conv_fwd(x, w, OH, OW, s, s, p, p),) + tuple(C.conv_fwd_stats(x, w, OH, OW, s, s, p, p)))
     finally:
