@@ -86,5 +86,8 @@ void conv_force_impl(int impl);
 // A/B hook: main loop of the implicit-GEMM kernel: 0 single LDS stage (4 waves per SIMD), 1 / 2
 // register prefetch depth (default 2, single stage for 1-2 k-tile reductions), 3 depth 2 always
 void conv_force_depth(int depth);
+// A/B hook: the register-staged weight-gradient kernel with one LDS stage at 3 waves per SIMD
+// or double-buffered with register prefetch at 2 (default)
+void conv_wgrad_force_single(bool single);
 
 }  // namespace tdl

@@ -489,21 +489,24 @@ __device__ __forceinline__ void wait_vmcnt_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
-constexpr int kV2Stages = 3;
+// STAGES 1 (the "dma1" variant): 4 waves, one LDS stage, no prefetch, 4 waves per SIMD -- the v1
+// DEPTH 0 schedule with the operands landing in LDS by DMA instead of registers + ds_write_b128.
+template <int BM, int BN, int STAGES>
+constexpr int v2_lds_elems() {
+  return STAGES * (BM + BN) * LDS_ROW > BM * (BN + 8) ? STAGES * (BM + BN) * LDS_ROW : BM * (BN + 8);
+}
 
-template <int BM, int BN>
-constexpr int v2_lds_elems() { return kV2Stages * (BM + BN) * LDS_ROW; }
-
-template <int BM, int BN, int WGM, int WGN, int EK>
-__global__ __launch_bounds__(512, 1) void k_conv_glds(Igemm a) {
-  constexpr int NT = 512;
+template <int BM, int BN, int WGM, int WGN, int EK, int STAGES, int MINW>
+__global__ __launch_bounds__(64 * WGM * WGN, MINW) void k_conv_glds(Igemm a) {
+  constexpr int NW = WGM * WGN, NT = 64 * NW;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;  // wave tile
   constexpr int MI = WTM / 16, NJ = WTN / 16;
   constexpr int STAGE = (BM + BN) * LDS_ROW;      // bf16 elements per ring stage
-  constexpr int A_LD = BM / 64;                   // LDS-DMA wave-instructions (8 rows each) per thread, A
-  constexpr int B_LD = BN / 64;                   //                                              ..., B
-  static_assert(WGM * WGN == 8 && BM % 64 == 0 && BN % 64 == 0 && MI >= 1 && NJ >= 1, "v2 geometry");
-  __shared__ __attribute__((aligned(16))) uint16_t lds[v2_lds_elems<BM, BN>()];
+  constexpr int A_LD = BM / (8 * NW);             // LDS-DMA wave-instructions (8 rows each) per thread, A
+  constexpr int B_LD = BN / (8 * NW);             //                                              ..., B
+  static_assert((STAGES == 3 || STAGES == 1) && BM % (8 * NW) == 0 && BN % (8 * NW) == 0 && MI >= 1 && NJ >= 1,
+                "v2 geometry");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[v2_lds_elems<BM, BN, STAGES>()];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
@@ -523,7 +526,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_glds(Igemm a) {
   uint32_t a_tap[A_LD];
 #pragma unroll
   for (int i = 0; i < A_LD; ++i) {
-    const int row = (i * 8 + wave) * 8 + lrow;  // row group i*8 + wave
+    const int row = (i * NW + wave) * 8 + lrow;  // row group i*NW + wave
     const int chunk = (lane & 7) ^ swz(row);
     const int m = tm * BM + row;
     a_tap[i] = 0u;
@@ -540,7 +543,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_glds(Igemm a) {
   int b_vo[B_LD];
 #pragma unroll
   for (int i = 0; i < B_LD; ++i) {
-    const int row = (i * 8 + wave) * 8 + lrow;
+    const int row = (i * NW + wave) * 8 + lrow;
     const int chunk = (lane & 7) ^ swz(row);
     b_vo[i] = (int)(((long long)(tn * BN + row) * a.w_col + chunk * 8) * 2);
   }
@@ -563,13 +566,13 @@ __global__ __launch_bounds__(512, 1) void k_conv_glds(Igemm a) {
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
       const int vo = ((a_tap[i] >> tap) & 1u) ? a_vo[i] : (int)0x80000000;
-      lds_dma16(x_rsrc, base + (i * 8 + wave) * 8 * LDS_ROW, vo, soff_a);
+      lds_dma16(x_rsrc, base + (i * NW + wave) * 8 * LDS_ROW, vo, soff_a);
     }
     const int wkh = a.flip ? a.KH - 1 - kh : kh, wkw = a.flip ? a.KW - 1 - kw : kw;
     const int soff_b = (int)((wkh * a.w_kh + wkw * a.w_kw + c0) * 2);
 #pragma unroll
     for (int i = 0; i < B_LD; ++i)
-      lds_dma16(w_rsrc, base + (BM + (i * 8 + wave) * 8) * LDS_ROW, b_vo[i], soff_b);
+      lds_dma16(w_rsrc, base + (BM + (i * NW + wave) * 8) * LDS_ROW, b_vo[i], soff_b);
   };
 
   f4v acc[MI][NJ];
@@ -598,21 +601,31 @@ __global__ __launch_bounds__(512, 1) void k_conv_glds(Igemm a) {
     }
   };
 
-  issue(0);
-  if (ntiles > 1) issue(1);
-  int st = 0;
-  for (int t = 0; t < ntiles; ++t) {
-    // tile t landed (this thread's loads: all but tile t+1's), every wave past tile t-1's reads
-    if (t + 1 < ntiles)
-      wait_vmcnt_barrier<A_LD + B_LD>();
-    else
-      wait_vmcnt_barrier<0>();
-    if (t + 2 < ntiles) issue(st == 0 ? 2 : st - 1);  // stage (t + 2) % 3 == stage (t - 1) % 3
-    compute(st);
-    st = st == 2 ? 0 : st + 1;
+  if constexpr (STAGES == 1) {
+    for (int t = 0; t < ntiles; ++t) {
+      if (t) __syncthreads();  // every wave done reading tile t - 1
+      issue(0);
+      wait_vmcnt_barrier<0>();  // tile t landed, for every wave
+      compute(0);
+    }
+  } else {
+    issue(0);
+    if (ntiles > 1) issue(1);
+    int st = 0;
+    for (int t = 0; t < ntiles; ++t) {
+      // tile t landed (this thread's loads: all but tile t+1's), every wave past tile t-1's reads
+      if (t + 1 < ntiles)
+        wait_vmcnt_barrier<A_LD + B_LD>();
+      else
+        wait_vmcnt_barrier<0>();
+      if (t + 2 < ntiles) issue(st == 0 ? 2 : st - 1);  // stage (t + 2) % 3 == stage (t - 1) % 3
+      compute(st);
+      st = st == 2 ? 0 : st + 1;
+    }
   }
   __syncthreads();  // every wave done reading the ring: the epilogue reuses it
-  conv_epilogue<BM, BN, NT, EK, WTM, WTN, v2_lds_elems<BM, BN>()>(a, acc, lds, tm, tn, wm * WTM, wn * WTN);
+  conv_epilogue<BM, BN, NT, EK, WTM, WTN, v2_lds_elems<BM, BN, STAGES>(), STAGES == 1>(a, acc, lds, tm, tn, wm * WTM,
+                                                                                       wn * WTN);
 }
 
 int g_depth = 2;  // main-loop variant; conv_force_depth for A/B sweeps
@@ -651,17 +664,18 @@ void launch_tile(const Igemm& a, hipStream_t s) {
 }
 
 int g_forced_tile = 0;  // 0: heuristic below; 1: 128 x 64, 2: 128 x 128, 3: 256 x 128 (tile sweeps)
-int g_impl = 2;  // 1: v1 only; 2: the LDS-DMA ring kernel where it measured faster; 3: wherever it fits
+int g_impl = 2;  // 1: v1 only; 2: the LDS-DMA ring kernel where it measured faster; 3: wherever it fits;
+                 // 4 / 5: the single-stage LDS-DMA kernel (dma1) at 4 / 3 waves per SIMD wherever v1 runs
 
-template <int BM, int BN, int WGM, int WGN>
+template <int BM, int BN, int WGM, int WGN, int STAGES = 3, int MINW = 1>
 void launch_v2(const Igemm& a, hipStream_t s) {
-  const dim3 grid((a.M + BM - 1) / BM * (a.K / BN)), block(512);
+  const dim3 grid((a.M + BM - 1) / BM * (a.K / BN)), block(64 * WGM * WGN);
   if (a.scatter)
-    hipLaunchKernelGGL((k_conv_glds<BM, BN, WGM, WGN, 2>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((k_conv_glds<BM, BN, WGM, WGN, 2, STAGES, MINW>), grid, block, 0, s, a);
   else if (a.bn_part)
-    hipLaunchKernelGGL((k_conv_glds<BM, BN, WGM, WGN, 1>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((k_conv_glds<BM, BN, WGM, WGN, 1, STAGES, MINW>), grid, block, 0, s, a);
   else
-    hipLaunchKernelGGL((k_conv_glds<BM, BN, WGM, WGN, 0>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((k_conv_glds<BM, BN, WGM, WGN, 0, STAGES, MINW>), grid, block, 0, s, a);
 }
 
 // v2 (256-row tiles, one 8-wave workgroup per CU) where it measured faster than v1
@@ -670,7 +684,7 @@ void launch_v2(const Igemm& a, hipStream_t s) {
 // 4-workgroups-per-CU v1 it loses everywhere else, the 3x3 convs at 14x14 / 7x7 included.  Outputs
 // are bit-identical either way.
 bool use_v2(int M, int K, int ktiles, int taps) {
-  if (g_impl == 1 || g_forced_tile != 0 || (g_impl == 2 && (ktiles < 32 || (taps != 1 && g_single)))) return false;
+  if (g_impl == 1 || g_impl >= 4 || g_forced_tile != 0 || (g_impl == 2 && (ktiles < 32 || (taps != 1 && g_single)))) return false;
   const long long wgs = (long long)(M + 255) / 256 * (K % 128 == 0 ? K / 128 : K / 64);
   return wgs >= 256;
 }
@@ -684,6 +698,11 @@ void launch(const Igemm& a, hipStream_t s) {
     if (a.K % 128 == 0) return launch_v2<256, 128, 4, 2>(a, s);
     return launch_v2<256, 64, 4, 2>(a, s);
   }
+  if (g_impl >= 4 && g_forced_tile == 0) {  // dma1 at 4 (impl 4) or 3 (impl 5) waves per SIMD
+    if (a.K % 128 == 0)
+      return g_impl == 4 ? launch_v2<128, 128, 2, 2, 1, 4>(a, s) : launch_v2<128, 128, 2, 2, 1, 3>(a, s);
+    return g_impl == 4 ? launch_v2<128, 64, 2, 2, 1, 4>(a, s) : launch_v2<128, 64, 2, 2, 1, 3>(a, s);
+  }
   if (g_forced_tile == 3 && a.K % 128 == 0) return launch_tile<256, 128>(a, s);
   if (g_forced_tile == 1 || a.K % 128 != 0) return launch_tile<128, 64>(a, s);
   launch_tile<128, 128>(a, s);
@@ -692,7 +711,7 @@ void launch(const Igemm& a, hipStream_t s) {
 }  // namespace
 
 void conv_force_tile(int tile) { g_forced_tile = tile; }
-void conv_force_impl(int impl) { g_impl = (impl == 1 || impl == 3) ? impl : 2; }
+void conv_force_impl(int impl) { g_impl = (impl == 1 || impl == 3 || impl == 4 || impl == 5) ? impl : 2; }
 void conv_force_depth(int depth) {
   // 0: single stage everywhere, 1 / 2: register prefetch depth 1 / the default selection (single
   // stage), 3: depth 2 everywhere (the selection before round 4's A/B, v2 for every long reduction),

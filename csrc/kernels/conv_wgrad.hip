@@ -77,8 +77,12 @@ __device__ __forceinline__ int fdiv(int n, int d, float inv, int& rem) {
 // Workgroup = WMW x WNW waves, each wave a 64 (k) x 64 (tc) tile of 4 x 4 16x16x32 MFMAs; the
 // workgroup tile is (64 WMW) x (64 WNW) and its LDS stage is WMW + WNW sub-images of 64 pixels x
 // 64 channels.  Columns past TC (a partial last tc tile) are staged as zeros and not stored.
-template <int WMW, int WNW>
-__global__ __launch_bounds__(64 * WMW * WNW) __attribute__((amdgpu_waves_per_eu(2))) void k_conv_wgrad(Wgrad a) {
+// SINGLE: one LDS stage and no register prefetch, 3 waves per SIMD (<= 168 VGPRs; at 4 the staging
+// registers spill): the other
+// resident workgroups hide a workgroup's load latency (the conv.hip DEPTH 0 finding).
+template <int WMW, int WNW, bool SINGLE>
+__global__ __launch_bounds__(64 * WMW * WNW) __attribute__((amdgpu_waves_per_eu(SINGLE ? 3 : 2))) void k_conv_wgrad(
+    Wgrad a) {
   constexpr int NW = WMW * WNW, NT = 64 * NW;
   constexpr int SA = WMW, SBn = WNW;
   constexpr int RPT = 8 / NW;                 // staged rows per thread per sub-image
@@ -178,14 +182,21 @@ __global__ __launch_bounds__(64 * WMW * WNW) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
 
-  if (nst > 0) {
+  if (!SINGLE && nst > 0) {
     gload(0);
     sstore(0);
   }
-  __syncthreads();
+  if (!SINGLE) __syncthreads();
   for (int st = 0; st < nst; ++st) {
-    const int buf = st & 1;
-    if (st + 1 < nst) gload(st + 1);
+    const int buf = SINGLE ? 0 : st & 1;
+    if (SINGLE) {
+      gload(st);
+      if (st) __syncthreads();  // every wave done reading stage st - 1
+      sstore(0);
+      __syncthreads();
+    } else if (st + 1 < nst) {
+      gload(st + 1);
+    }
     const uint16_t* base = lds + buf * STAGE;
 #pragma unroll
     for (int kk = 0; kk < RB; kk += 32) {
@@ -209,8 +220,10 @@ __global__ __launch_bounds__(64 * WMW * WNW) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
-    if (st + 1 < nst) sstore(buf ^ 1);
-    __syncthreads();
+    if (!SINGLE) {
+      if (st + 1 < nst) sstore(buf ^ 1);
+      __syncthreads();
+    }
   }
 
   // partial tile: lane holds k = 4 * (lane >> 4) .. + 3 of column tc = lane & 15 in each 16 x 16 block
@@ -408,16 +421,27 @@ __global__ __launch_bounds__(1024) void k_wgrad_reduce(const float* ws, long lon
   }
 }
 
-template <int WMW, int WNW>
-void launch_wgrad(const Wgrad& a, hipStream_t s) {
-  constexpr int lds = 2 * (WMW + WNW) * SUB * 2;
+bool g_wgrad_single = false;  // conv_wgrad_force_single (A/B hook)
+
+template <int WMW, int WNW, bool SINGLE>
+void launch_wgrad_t(const Wgrad& a, hipStream_t s) {
+  constexpr int lds = (SINGLE ? 1 : 2) * (WMW + WNW) * SUB * 2;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_conv_wgrad<WMW, WNW>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    (void)hipFuncSetAttribute((const void*)k_conv_wgrad<WMW, WNW, SINGLE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              lds);
     attr = true;
   }
   const int tiles = (a.K / (64 * WMW)) * ((a.TC + 64 * WNW - 1) / (64 * WNW));
-  hipLaunchKernelGGL((k_conv_wgrad<WMW, WNW>), dim3(tiles * a.nsplit), dim3(64 * WMW * WNW), lds, s, a);
+  hipLaunchKernelGGL((k_conv_wgrad<WMW, WNW, SINGLE>), dim3(tiles * a.nsplit), dim3(64 * WMW * WNW), lds, s, a);
+}
+
+template <int WMW, int WNW>
+void launch_wgrad(const Wgrad& a, hipStream_t s) {
+  if (g_wgrad_single)
+    launch_wgrad_t<WMW, WNW, true>(a, s);
+  else
+    launch_wgrad_t<WMW, WNW, false>(a, s);
 }
 
 template <int WMW, int WNW>
@@ -430,6 +454,8 @@ void launch_wgrad_glds(const Wgrad& a, hipStream_t s) {
 constexpr int kTiles[][2] = {{1, 1}, {1, 2}, {2, 1}, {2, 2}, {1, 4}, {4, 1}, {2, 4}, {4, 2}};
 
 }  // namespace
+
+void conv_wgrad_force_single(bool single) { g_wgrad_single = single; }
 
 bool conv_wgrad_supported(const ConvGeom& g) {
   return conv_bf16_supported(g) && (long long)g.N * g.OH * g.OW < (1ll << 24);
@@ -469,8 +495,10 @@ std::vector<WgradPlan> conv_wgrad_plans(const ConvGeom& g, int max_plans) {
     if ((ntc * btc - TC) * 4 > ntc * btc) continue;  // > 25 % of the tc columns padding
     const int tiles = (g.K / bmk) * ntc;
     const bool ring = wmw * wnw == 8;  // LDS-DMA ring kernel: one 144-KiB workgroup per CU
-    const int lds_kb = (ring ? 3 : 2) * (wmw + wnw) * 8;
-    const int per_cu = std::max(1, std::min(160 / lds_kb, 8 / (wmw * wnw)));  // <= 2 waves per SIMD
+    const bool single = !ring && g_wgrad_single;
+    const int lds_kb = (ring ? 3 : (single ? 1 : 2)) * (wmw + wnw) * 8;
+    // <= 2 waves per SIMD (3 for the single-stage v1 kernel)
+    const int per_cu = std::max(1, std::min(160 / lds_kb, (single ? 12 : 8) / (wmw * wnw)));
     const double macs = (double)M * tiles * bmk * btc;
     // measured (profiles/conv_v2_r4.txt): the ring kernel wins on 3x3 and strided 1x1 shapes and
     // loses on stride-1 1x1 ones (the v1 2x2-wave tile), where its rate is scaled down

@@ -47,13 +47,14 @@ def t(fn, reps=20):
 
 
 def sweep(C, fn):
-    """Times of the v1 (register-staged, 128-row tiles) and v2 (LDS-DMA ring, 256-row tiles where
-    the grid fills the chip) main loops, and of the default selection without the single-stage
+    """Times of the v1 (register-staged, 128-row tiles), v2 (LDS-DMA ring, 256-row tiles where
+    the grid fills the chip) and dma1 (single-stage LDS-DMA, 128-row tiles, at 4 and 3 waves per
+    SIMD) main loops, and of the default selection without the single-stage
     variant for 1-2 k-tile reductions (conv_force_depth(3)), of the single stage everywhere
     (conv_force_depth(0), plain epilogues) and of the single LDS stage with register prefetch at 3
     workgroups per CU everywhere (conv_force_depth(4))."""
     out = []
-    for impl in (1, 3):
+    for impl in (1, 3, 4, 5):
         C.conv_force_impl(impl)
         out.append(round(t(fn), 1))
     C.conv_force_impl(2)
@@ -83,7 +84,7 @@ def main():
         t_m = t(lambda: F.conv2d(xc, w_oihw, None, s, p))
         byt = 2.0 * B * (H * W * Ci + OH * OW * K)
         floor = max(flop / 1.2e15, byt / 5e12) * 1e6
-        print(json.dumps({"dir": "fwd", "shape": [B, H, W, Ci, K, KH, s, p], "rel_err": round(err, 5), "hip_us": round(t_h, 1), "v1_v2_d3_d0_d4_us": tiles,
+        print(json.dumps({"dir": "fwd", "shape": [B, H, W, Ci, K, KH, s, p], "rel_err": round(err, 5), "hip_us": round(t_h, 1), "v1_v2_dma4_dma3_d3_d0_d4_us": tiles,
                           "miopen_us": round(t_m, 1), "hip_tflops": round(flop / t_h / 1e6, 1),
                           "speedup": round(t_m / t_h, 3), "floor_us": round(floor, 1),
                           "calls": SHAPES_KERAS.get((H, W, Ci, K, KH, s, p), 0)}), flush=True)
@@ -99,7 +100,7 @@ def main():
             tiles = sweep(C, lambda: C.conv_dgrad(dy, kc, H, W, p, p))
             t_m = t(lambda: torch.ops.aten.convolution_backward(dyc, xc, w_oihw, None, [s, s], [p, p], [1, 1], False,
                                                                 [0, 0], 1, [True, False, False]))
-            print(json.dumps({"dir": "dgrad", "shape": [B, H, W, Ci, K, KH, s, p], "rel_err": round(err, 5), "hip_us": round(t_h, 1), "v1_v2_d3_d0_d4_us": tiles,
+            print(json.dumps({"dir": "dgrad", "shape": [B, H, W, Ci, K, KH, s, p], "rel_err": round(err, 5), "hip_us": round(t_h, 1), "v1_v2_dma4_dma3_d3_d0_d4_us": tiles,
                               "miopen_us": round(t_m, 1), "hip_tflops": round(flop / t_h / 1e6, 1),
                               "speedup": round(t_m / t_h, 3), "floor_us": round(floor, 1),
                               "calls": SHAPES_KERAS.get((H, W, Ci, K, KH, s, p), 0)}), flush=True)

@@ -38,8 +38,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--candidates", type=int, default=8, help="model plans timed per shape")
+    ap.add_argument("--single", type=int, default=0, help="register-staged kernel: 1 single LDS stage, 0 double-buffered")
     a = ap.parse_args()
     C = hip()
+    C.conv_wgrad_force_single(bool(a.single))
     dev = "cuda:0"
     B = a.batch
     torch.backends.cudnn.benchmark = True
@@ -83,7 +85,8 @@ def main():
             print(json.dumps({"dir": "dgrad_s2", "shape": [B, H, W, Ci, K, KH, s, p], "rel_err": round(err, 5),
                               "hip_us": round(t_h, 1), "miopen_us": round(t_m, 1),
                               "hip_tflops": round(flop / t_h / 1e6, 1), "speedup": round(t_m / t_h, 3)}), flush=True)
-    print(json.dumps({"wgrad_total_us_best_of": round(tot_h, 1), "wgrad_total_us_miopen": round(tot_m, 1)}))
+    print(json.dumps({"wgrad_total_us_best_of": round(tot_h, 1), "wgrad_total_us_miopen": round(tot_m, 1),
+                      "single": a.single}))
 
 
 if __name__ == "__main__":

@@ -10,5 +10,5 @@ timeout -k 10 500 python -u scripts/bench_conv.py 256 keras > $O/bench_conv.json
 grep -v amdgpu.ids $O/bench_conv.jsonl | python -c "
 import json,sys
 for l in sys.stdin:
-    d=json.loads(l); print(d['dir'], d['shape'][1:], d['hip_us'], d['v1_v2_d3_d0_d4_us'], d['miopen_us'], d['calls'])"
+    d=json.loads(l); print(d['dir'], d['shape'][1:], d['hip_us'], d['v1_v2_dma4_dma3_d3_d0_d4_us'], d['miopen_us'], d['calls'])"
 echo done

@@ -311,3 +311,28 @@ def test_conv_main_loop_variants_bitwise(shape):
         R = o[2].shape[0]  # partial rows [P + ceil(P / 64)]: the trailing scratch rows are not outputs
         P = next(q for q in range(R + 1) if q + (q + 63) // 64 == R)
         assert torch.equal(o[2][:P], outs[0][2][:P])
+
+
+@pytest.mark.parametrize("shape", [(4, 14, 14, 64, 128, 3, 3, 1, 1), (8, 28, 28, 128, 64, 1, 1, 1, 0),
+                                   (4, 9, 11, 128, 256, 1, 1, 2, 0)])
+def test_conv_wgrad_single_stage_matches_double_buffered_bitwise(shape):
+    """The register-staged weight-gradient kernel with one LDS stage and the double-buffered one
+    accumulate the same MFMAs in the same order: bit-identical for every v1 tile shape."""
+    from tensorflow_distributed_learning_amd.ops import hip
+
+    C = hip()
+    N, H, W, Ci, K, KH, KW, s, p = shape
+    x, k = _mk(shape, "cuda:0")
+    OH, OW = (H + 2 * p - KH) // s + 1, (W + 2 * p - KW) // s + 1
+    dy = torch.randn(N, OH, OW, K, device="cuda:0").bfloat16()
+    for wmw, wnw in ((1, 1), (2, 2), (1, 2), (2, 1)):
+        if K % (64 * wmw):
+            continue
+        outs = []
+        try:
+            for single in (True, False):
+                C.conv_wgrad_force_single(single)
+                outs.append(C.conv_wgrad(x, dy, KH, KW, s, s, p, p, plan=[wmw, wnw, 3]))
+        finally:
+            C.conv_wgrad_force_single(False)
+        assert torch.equal(outs[0], outs[1]), (wmw, wnw)

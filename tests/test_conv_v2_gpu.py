@@ -1,4 +1,5 @@
-"""The LDS-DMA ring conv kernel (csrc/kernels/conv.hip k_conv_glds, 256-row tiles) against the v1
+"""The LDS-DMA conv kernels (csrc/kernels/conv.hip k_conv_glds: the 3-stage ring with 256-row tiles,
+and the single-stage dma1 variant with 128-row tiles at 4 and 3 waves per SIMD) against the v1
 register-staged kernel and fp32 PyTorch, on shapes large enough for the launcher to pick it: the
 same per-output MFMA chain over the same k-tile order, so outputs are bit-identical to v1; the BN
 partial sums (per 256-row tile instead of 128) agree in total."""
@@ -18,10 +19,21 @@ def C():
     c.conv_force_impl(2)
 
 
+ALT = [3]
+
+
+@pytest.fixture(autouse=True, params=[3, 4, 5], ids=["ring", "dma1_w4", "dma1_w3"])
+def _alt_impl(request):
+    ALT[0] = request.param
+    yield
+
+
 def _both(C, fn):
     C.conv_force_impl(1)
     a = fn()
-    C.conv_force_impl(3)  # the ring kernel wherever it fits (the default picks it only for long reductions)
+    # 3: the ring kernel wherever it fits (the default picks it only for long 1x1 reductions);
+    # 4 / 5: the single-stage LDS-DMA kernel
+    C.conv_force_impl(ALT[0])
     b = fn()
     C.conv_force_impl(2)
     return a, b
