@@ -127,7 +127,7 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
 // stride-2 scatter).  Every thread of the workgroup must call it (it has workgroup barriers).
 // LOWREG (the 4-waves-per-SIMD variants, <= 128 VGPRs): the BN-group backward epilogue loads its
 // residual and BN operands in chunks of EPI / 4 segments right before their use instead of all up front.
-template <int BM, int BN, int NT, int EK, int WTM, int WTN, int LDS_ELEMS, bool LOWREG = false>
+template <int BM, int BN, int NT, int EK, int WTM, int WTN, int LDS_ELEMS, int LOWREG = 0>
 __device__ __forceinline__ void conv_epilogue(const Igemm& a, const f4v (&acc)[WTM / 16][WTN / 16], uint16_t* lds,
                                               int tm, int tn, int wrow0, int wcol0) {
   const int tid = threadIdx.x, lane = tid & 63;
@@ -137,7 +137,8 @@ __device__ __forceinline__ void conv_epilogue(const Igemm& a, const f4v (&acc)[W
   static_assert(BM * SEG % NT == 0, "epilogue segments must divide evenly");
   // residual (gradient sum): all of this thread's loads issued here, before the LDS round trip, so
   // their latency overlaps it instead of serialising the store loop
-  constexpr int EC = (LOWREG && EK == 1) ? (EPI >= 4 ? EPI / 4 : 1) : EPI;  // segments per operand chunk
+  // segments per operand chunk (LOWREG 1: the BN-group backward epilogue only, 2: every epilogue)
+  constexpr int EC = ((LOWREG == 1 && EK == 1) || (LOWREG == 2 && EK != 2)) ? (EPI >= 4 ? EPI / 4 : 1) : EPI;
   u32x4 rv[EK == 2 ? 1 : EPI];
   if (EK != 2 && a.res && EC == EPI) {
 #pragma unroll
@@ -471,8 +472,8 @@ __global__ __launch_bounds__(BM * 2, DEPTH == 0 ? 4 : (DEPTH == 3 ? 3 : 2)) void
   }
 
   // epilogue: bf16 tile into LDS ([BM][BN + 8]), then 16-B row segments to global
-  conv_epilogue<BM, BN, NT, EK, 64, WN, v1_lds_elems<BM, BN, DEPTH>(), DEPTH == 0>(a, acc, lds, tm, tn, wm * 64,
-                                                                                 wn * WN);
+  conv_epilogue<BM, BN, NT, EK, 64, WN, v1_lds_elems<BM, BN, DEPTH>(), DEPTH == 0 ? 1 : 0>(a, acc, lds, tm, tn,
+                                                                                         wm * 64, wn * WN);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -624,8 +625,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, MINW) void k_conv_glds(Igemm a) {
     }
   }
   __syncthreads();  // every wave done reading the ring: the epilogue reuses it
-  conv_epilogue<BM, BN, NT, EK, WTM, WTN, v2_lds_elems<BM, BN, STAGES>(), STAGES == 1>(a, acc, lds, tm, tn, wm * WTM,
-                                                                                       wn * WTN);
+  conv_epilogue<BM, BN, NT, EK, WTM, WTN, v2_lds_elems<BM, BN, STAGES>(), STAGES == 1 ? 2 : 0>(a, acc, lds, tm, tn,
+                                                                                             wm * WTM, wn * WTN);
 }
 
 int g_depth = 2;  // main-loop variant; conv_force_depth for A/B sweeps
@@ -678,15 +679,28 @@ void launch_v2(const Igemm& a, hipStream_t s) {
     hipLaunchKernelGGL((k_conv_glds<BM, BN, WGM, WGN, 0, STAGES, MINW>), grid, block, 0, s, a);
 }
 
-// v2 (256-row tiles, one 8-wave workgroup per CU) where it measured faster than v1
-// (profiles/conv_v2_r4.txt, profiles/conv_main_loop_ab_r4.txt): 1x1 convs with long reductions
-// (>= 32 k-tiles: 2048 input channels) and a grid that still fills the chip, by 2-4 %.  Against the
-// 4-workgroups-per-CU v1 it loses everywhere else, the 3x3 convs at 14x14 / 7x7 included.  Outputs
-// are bit-identical either way.
+// v2 (256-row tiles, one 8-wave workgroup per CU, 3-stage LDS-DMA ring): only when forced (impl 3)
+// or under the pre-round-4 selection (conv_force_depth(3): >= 32 k-tiles).  The default never takes
+// it: dma1 and the single-stage v1 beat it on every shape (profiles/conv_dma1_ab_r4.txt).
 bool use_v2(int M, int K, int ktiles, int taps) {
-  if (g_impl == 1 || g_impl >= 4 || g_forced_tile != 0 || (g_impl == 2 && (ktiles < 32 || (taps != 1 && g_single)))) return false;
+  (void)taps;
+  if (g_forced_tile != 0 || !(g_impl == 3 || (g_impl == 2 && !g_single && ktiles >= 32))) return false;
   const long long wgs = (long long)(M + 255) / 256 * (K % 128 == 0 ? K / 128 : K / 64);
   return wgs >= 256;
+}
+
+// dma1 (the single-stage LDS-DMA kernel, 4 waves of 64x64, 4 waves per SIMD) for the 3x3 convs and
+// the stride-2 scatter dgrads with >= 9 k-tiles and 128-column tiles: 6-11 % faster there in the
+// ResNet-50 step than the register-staged single-stage v1 (no VGPR staging, no ds_write pass: the
+// operands land in LDS by DMA).  The per-shape bench also favoured it for 1x1 convs with >= 16
+// k-tiles, but inside the step (fused BN epilogues, neighbouring kernels) those and the 64-column
+// tiles ran 2-7 % slower (profiles/conv_dma1_ab_r4.txt, resnet50_steady_state_breakdown_r4_dma1.txt).
+// Bit-identical either way.
+bool use_dma1(const Igemm& a) {
+  if (g_forced_tile != 0) return false;
+  if (g_impl >= 4) return true;
+  const int ktiles = a.KH * a.KW * (a.C / BK);
+  return g_impl == 2 && g_single && ktiles >= 9 && a.K % 128 == 0 && (a.KH * a.KW > 1 || a.scatter);
 }
 
 // Tile choice, from the sweep over the ResNet-50 b=256 convolutions (profiles/conv_tile_sweep_r1.jsonl):
@@ -698,10 +712,10 @@ void launch(const Igemm& a, hipStream_t s) {
     if (a.K % 128 == 0) return launch_v2<256, 128, 4, 2>(a, s);
     return launch_v2<256, 64, 4, 2>(a, s);
   }
-  if (g_impl >= 4 && g_forced_tile == 0) {  // dma1 at 4 (impl 4) or 3 (impl 5) waves per SIMD
+  if (use_dma1(a)) {  // dma1 at 4 (default, impl 4) or 3 (impl 5) waves per SIMD
     if (a.K % 128 == 0)
-      return g_impl == 4 ? launch_v2<128, 128, 2, 2, 1, 4>(a, s) : launch_v2<128, 128, 2, 2, 1, 3>(a, s);
-    return g_impl == 4 ? launch_v2<128, 64, 2, 2, 1, 4>(a, s) : launch_v2<128, 64, 2, 2, 1, 3>(a, s);
+      return g_impl != 5 ? launch_v2<128, 128, 2, 2, 1, 4>(a, s) : launch_v2<128, 128, 2, 2, 1, 3>(a, s);
+    return g_impl != 5 ? launch_v2<128, 64, 2, 2, 1, 4>(a, s) : launch_v2<128, 64, 2, 2, 1, 3>(a, s);
   }
   if (g_forced_tile == 3 && a.K % 128 == 0) return launch_tile<256, 128>(a, s);
   if (g_forced_tile == 1 || a.K % 128 != 0) return launch_tile<128, 64>(a, s);

@@ -15,5 +15,7 @@ struct PoolGeom {
 
 void maxpool_forward(const void* x, void* y, uint8_t* arg, bool bf16, const PoolGeom& g, hipStream_t s);
 void maxpool_backward(const void* dy, const uint8_t* arg, void* dx, bool bf16, const PoolGeom& g, hipStream_t s);
+// A/B hook: the generic window loops (default) or the unrolled kernels for 3x3 stride-2 pooling
+void maxpool_force_generic(bool generic);
 
 }  // namespace tdl

@@ -48,7 +48,10 @@ __device__ __forceinline__ void st8(void* p, int64_t e, const float* v) {
   }
 }
 
-template <bool BF>
+// K3S2: the 3x3 stride-2 window of ResNet (compile-time loops: every tap's load issued before the
+// compares, and at most 2 x 2 windows per input element in the backward, all four loads at once).
+// Same compare / sum order as the generic loops: bit-identical results.
+template <bool BF, bool K3S2>
 __global__ __launch_bounds__(256) void k_maxpool_fwd(const void* __restrict__ x, void* __restrict__ y,
                                                      uint8_t* __restrict__ arg, PoolGeom g) {
   const int G = g.C >> 3;
@@ -67,7 +70,34 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd(const void* __restrict__ x,
       best[j] = -INFINITY;
       am[j] = 255;
     }
-    for (int i = 0; i < g.kh; ++i) {
+    if constexpr (K3S2) {
+      float v[9][8];
+      bool in[9];
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const int h = oh * 2 - g.pt + i, w = ow * 2 - g.pl + k, q = i * 3 + k;
+          in[q] = h >= 0 && h < g.H && w >= 0 && w < g.W;
+          if (in[q]) {
+            ld8<BF>(x, (((int64_t)n * g.H + h) * g.W + w) * g.C + cg * 8, v[q]);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[q][j] = g.pad_zero ? 0.f : -INFINITY;
+          }
+        }
+#pragma unroll
+      for (int q = 0; q < 9; ++q) {
+        if (!in[q] && !g.pad_zero) continue;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (v[q][j] > best[j]) {
+            best[j] = v[q][j];
+            am[j] = in[q] ? (uint32_t)q : 255u;
+          }
+      }
+    }
+    for (int i = 0; i < (K3S2 ? 0 : g.kh); ++i) {
       const int h = oh * g.sh - g.pt + i;
       for (int k = 0; k < g.kw; ++k) {
         const int w = ow * g.sw - g.pl + k;
@@ -98,7 +128,7 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd(const void* __restrict__ x,
   }
 }
 
-template <bool BF>
+template <bool BF, bool K3S2>
 __global__ __launch_bounds__(256) void k_maxpool_bwd(const void* __restrict__ dy, const uint8_t* __restrict__ arg,
                                                      void* __restrict__ dx, PoolGeom g) {
   const int G = g.C >> 3;
@@ -118,7 +148,33 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd(const void* __restrict__ dy
     float acc[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-    for (int oh = oh0; oh <= oh1; ++oh)
+    if constexpr (K3S2) {  // oh1 - oh0 <= 1 and ow1 - ow0 <= 1
+      uint2 a[4];
+      float d[4][8];
+      bool ok[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int oh = oh0 + (q >> 1), ow = ow0 + (q & 1);
+        ok[q] = oh <= oh1 && ow <= ow1;
+        if (ok[q]) {
+          const int64_t o = (((int64_t)n * g.OH + oh) * g.OW + ow) * g.C + cg * 8;
+          a[q] = *reinterpret_cast<const uint2*>(arg + o);
+          ld8<BF>(dy, o, d[q]);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (!ok[q]) continue;
+        const int oh = oh0 + (q >> 1), ow = ow0 + (q & 1);
+        const uint32_t pos = (uint32_t)((hp - oh * 2) * 3 + (wp - ow * 2));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t aj = ((j < 4 ? a[q].x : a[q].y) >> (8 * (j & 3))) & 0xffu;
+          if (aj == pos) acc[j] += d[q][j];
+        }
+      }
+    }
+    for (int oh = oh0; oh <= (K3S2 ? -1 : oh1); ++oh)
       for (int ow = ow0; ow <= ow1; ++ow) {
         const uint32_t pos = (uint32_t)((hp - oh * g.sh) * g.kw + (wp - ow * g.sw));
         const int64_t o = (((int64_t)n * g.OH + oh) * g.OW + ow) * g.C + cg * 8;
@@ -137,22 +193,45 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd(const void* __restrict__ dy
 
 int grid_for(int64_t n) { return (int)std::min<int64_t>((n + 255) / 256, 256 * 32); }
 
+// maxpool_force_generic (A/B hook).  Default: the generic loops -- the unrolled 3x3 stride-2 kernels
+// measured slower in the ResNet-50 step (fwd 143 -> 237 us, bwd 226 -> 266 us: 9 loads of 16 B per
+// thread in flight cost occupancy, resnet50_steady_state_breakdown_r4_dma1.txt)
+bool g_pool_k3s2 = false;
+
+bool k3s2(const PoolGeom& g) { return g_pool_k3s2 && g.kh == 3 && g.kw == 3 && g.sh == 2 && g.sw == 2; }
+
 }  // namespace
+
+void maxpool_force_generic(bool generic) { g_pool_k3s2 = !generic; }
 
 void maxpool_forward(const void* x, void* y, uint8_t* arg, bool bf16, const PoolGeom& g, hipStream_t s) {
   const int64_t n = (int64_t)g.N * g.OH * g.OW * (g.C / 8);
-  if (bf16)
-    hipLaunchKernelGGL(k_maxpool_fwd<true>, dim3(grid_for(n)), dim3(256), 0, s, x, y, arg, g);
-  else
-    hipLaunchKernelGGL(k_maxpool_fwd<false>, dim3(grid_for(n)), dim3(256), 0, s, x, y, arg, g);
+  const dim3 gr(grid_for(n)), b(256);
+  if (k3s2(g)) {
+    if (bf16)
+      hipLaunchKernelGGL((k_maxpool_fwd<true, true>), gr, b, 0, s, x, y, arg, g);
+    else
+      hipLaunchKernelGGL((k_maxpool_fwd<false, true>), gr, b, 0, s, x, y, arg, g);
+  } else if (bf16) {
+    hipLaunchKernelGGL((k_maxpool_fwd<true, false>), gr, b, 0, s, x, y, arg, g);
+  } else {
+    hipLaunchKernelGGL((k_maxpool_fwd<false, false>), gr, b, 0, s, x, y, arg, g);
+  }
 }
 
 void maxpool_backward(const void* dy, const uint8_t* arg, void* dx, bool bf16, const PoolGeom& g, hipStream_t s) {
   const int64_t n = (int64_t)g.N * g.H * g.W * (g.C / 8);
-  if (bf16)
-    hipLaunchKernelGGL(k_maxpool_bwd<true>, dim3(grid_for(n)), dim3(256), 0, s, dy, arg, dx, g);
-  else
-    hipLaunchKernelGGL(k_maxpool_bwd<false>, dim3(grid_for(n)), dim3(256), 0, s, dy, arg, dx, g);
+  const dim3 gr(grid_for(n)), b(256);
+  if (k3s2(g)) {
+    if (bf16)
+      hipLaunchKernelGGL((k_maxpool_bwd<true, true>), gr, b, 0, s, dy, arg, dx, g);
+    else
+      hipLaunchKernelGGL((k_maxpool_bwd<false, true>), gr, b, 0, s, dy, arg, dx, g);
+  } else if (bf16) {
+    hipLaunchKernelGGL((k_maxpool_bwd<true, false>), gr, b, 0, s, dy, arg, dx, g);
+  } else {
+    hipLaunchKernelGGL((k_maxpool_bwd<false, false>), gr, b, 0, s, dy, arg, dx, g);
+  }
 }
 
 }  // namespace tdl

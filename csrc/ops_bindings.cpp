@@ -629,6 +629,8 @@ void register_ops(pybind11::module& m) {
   m.def("conv_wgrad3x3_set_rows", &tdl::conv_wgrad3x3_set_rows, "3x3 row-kernel wgrad: output rows per slice (0 = auto)");
   m.def("conv_wgrad_force_single", &tdl::conv_wgrad_force_single,
         "weight-gradient A/B hook: single LDS stage at 3 waves/SIMD (True) or double-buffered (False, default)");
+  m.def("maxpool_force_generic", &tdl::maxpool_force_generic,
+        "max-pool A/B hook: generic window loops (True, default) or the unrolled 3x3 stride-2 kernels (False)");
   m.def("conv_force_depth", &tdl::conv_force_depth, "conv main-loop A/B hook: 0 single stage, 1/2 prefetch depth, 3 depth 2 without the short-reduction single-stage variant");
   m.def("stem_fwd", &stem_fwd, "small-channel stride-2 conv (ResNet stem): (y, packed x[, BN part])",
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("pt"), pybind11::arg("pb"), pybind11::arg("pl"),

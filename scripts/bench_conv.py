@@ -58,10 +58,12 @@ def sweep(C, fn):
         C.conv_force_impl(impl)
         out.append(round(t(fn), 1))
     C.conv_force_impl(2)
-    for d in (3, 0, 4):
+    for d in (3, 0, 4):  # d3: the pre-round-4 default selection; d0 / d4: v1 variants everywhere
+        C.conv_force_impl(2 if d == 3 else 1)
         C.conv_force_depth(d)
         out.append(round(t(fn), 1))
     C.conv_force_depth(2)
+    C.conv_force_impl(2)
     return out
 
 

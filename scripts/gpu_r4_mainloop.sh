@@ -5,7 +5,7 @@ set -o pipefail
 O=gpurun_out/r4ml
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_conv_gpu.py tests/test_conv_v2_gpu.py -x -v --timeout 200 --timeout-method thread > $O/tests.log 2>&1 || { echo "TESTS FAILED"; tail -60 $O/tests.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_conv_gpu.py tests/test_conv_v2_gpu.py tests/test_bn_gpu.py -x -v --timeout 200 --timeout-method thread > $O/tests.log 2>&1 || { echo "TESTS FAILED"; tail -60 $O/tests.log; exit 1; }
 tail -3 $O/tests.log
 timeout -k 10 500 python -u scripts/bench_conv.py 256 keras > $O/bench_conv.jsonl 2>&1 || { echo "BENCH FAILED"; tail -30 $O/bench_conv.jsonl; exit 1; }
 grep -v amdgpu.ids $O/bench_conv.jsonl | python -c "

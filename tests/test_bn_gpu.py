@@ -214,3 +214,31 @@ def test_bn_elementwise_blocked_matches_grid_stride_bitwise(shape):
                 assert torch.equal(a, e)
     finally:
         Ck.bn_set_elementwise(1, 4)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("geo", [(1, 1, True), (0, 0, False), (1, 1, False)])
+@pytest.mark.parametrize("hw", [(17, 15), (112, 112)])
+def test_maxpool_3x3s2_unrolled_matches_generic_bitwise(dtype, geo, hw):
+    """The unrolled 3x3 stride-2 max-pool kernels give the generic loops' outputs, argmax and input
+    gradient bit for bit (same compare and sum order), with zero and -inf padding."""
+    from tensorflow_distributed_learning_amd.ops import hip
+
+    C = hip()
+    pt, pl, pad_zero = geo
+    H, W = hw
+    torch.manual_seed(3)
+    x = torch.randn(2, H, W, 64, device="cuda:0").to(dtype)
+    OH, OW = (H + 2 * pt - 3) // 2 + 1, (W + 2 * pl - 3) // 2 + 1
+    dy = torch.randn(2, OH, OW, 64, device="cuda:0").to(dtype)
+    outs = []
+    try:
+        for generic in (True, False):
+            C.maxpool_force_generic(generic)
+            y, arg = C.maxpool_fwd(x, 3, 3, 2, 2, pt, pl, OH, OW, pad_zero)
+            dx = C.maxpool_bwd(dy, arg, list(x.shape), 3, 3, 2, 2, pt, pl)
+            outs.append((y, arg, dx))
+    finally:
+        C.maxpool_force_generic(True)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

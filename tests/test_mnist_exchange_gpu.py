@@ -199,3 +199,19 @@ def test_bench_two_replicas_exchange_in_finalize_twoshot(tmp_path):
     d, _ = _bench2({"TDL_FX_TWOSHOT_MIN_R": "2"})
     cfg = d["config"]
     assert cfg["allreduce"] == "xgmi-in-finalize-twoshot" and cfg["replicas_identical"], cfg
+
+
+def test_bench_exchange_selftest_one_rank_raises_fails_every_rank(tmp_path):
+    """A rank whose self-test raises BEFORE the exchange (injected: TDL_FAULT_XCHG_SELFTEST_RAISE=1)
+    leaves its peer waiting in the xGMI exchange until the bounded wait expires (TDL_XGMI_TIMEOUT=30).
+    Both ranks then reach the same agreement collective, see the timeout and fail the job with the
+    same diagnosis instead of hanging or reducing garbage (the peer's device carries the sticky error
+    word, so no fallback can run there)."""
+    env = dict(os.environ, PYTHONPATH=ROOT, TDL_SHARE_GPU="1", TDL_MNIST_DP2_FWD="1", TDL_XGMI_TIMEOUT="30",
+               TDL_FAULT_XCHG_SELFTEST_RAISE="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "TF_CONFIG", "TDL_LAUNCHED", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--per-replica-batch", "16", "--steps", "10",
+                        "--warmup", "2"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode != 0, r.stdout[-2000:]
+    assert "did not arrive at the xGMI exchange" in r.stderr + r.stdout, (r.stdout + r.stderr)[-4000:]
