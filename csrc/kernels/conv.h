@@ -39,9 +39,12 @@ int conv_fwd_row_tile(const ConvGeom& g);
 // bn_part2 (with bn_x2, shaped like dx; needs bn_part): the group's residual is the output of a plain
 // BN (projection shortcut) with input bn_x2 and no other reader: bn_part2 := per-tile sums of dz and
 // dz * bn_x2, that BN's backward reduction
+// bn_ss (scale[C], shift[C] of a plain BN -> ReLU group's forward; then bn_y may be null): the mask is
+// recomputed as [bn_x * scale + shift > 0] instead of read from bn_y
 void conv_dgrad_bf16(const void* dy, const void* w_hwio, void* dx, const ConvGeom& g, hipStream_t s,
                      const void* residual = nullptr, const void* bn_y = nullptr, const void* bn_x = nullptr,
-                     float* bn_part = nullptr, const void* bn_x2 = nullptr, float* bn_part2 = nullptr);
+                     float* bn_part = nullptr, const void* bn_x2 = nullptr, float* bn_part2 = nullptr,
+                     const float* bn_ss = nullptr);
 int conv_dgrad_row_tile(const ConvGeom& g);
 
 // Input gradient of a 1x1, stride-2, unpadded convolution (the strided shortcut / first 1x1 of a
@@ -51,7 +54,8 @@ int conv_dgrad_row_tile(const ConvGeom& g);
 // N*OH*OW dy pixels, conv_dgrad_s2_row_tile)
 void conv_dgrad_s2_1x1_bf16(const void* dy, const void* w_hwio, void* dx, const ConvGeom& g, hipStream_t s,
                             const void* residual = nullptr, const void* bn_y = nullptr, const void* bn_x = nullptr,
-                            float* bn_part = nullptr, const void* bn_x2 = nullptr, float* bn_part2 = nullptr);
+                            float* bn_part = nullptr, const void* bn_x2 = nullptr, float* bn_part2 = nullptr,
+                            const float* bn_ss = nullptr);
 int conv_dgrad_s2_row_tile(const ConvGeom& g);
 
 // Weight gradient, split-K over output pixels with a deterministic partial-slab reduction.

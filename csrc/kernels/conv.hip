@@ -63,6 +63,10 @@ struct Igemm {
   // bn_part2 [row tiles][2][K] gets the per-tile channel sums of dz and dz * bn_x2 (its input)
   const uint16_t* bn_x2;
   float* bn_part2;
+  // optional, with bn_part and no bn_y: the group is a plain BN -> ReLU, and the ReLU mask is
+  // recomputed from bn_x as [bn_x * scale + shift > 0] (bn_ss = scale[K], shift[K] of its forward):
+  // one tensor read less than loading the group output
+  const float* bn_ss;
 };
 
 // per-channel sums of 8 packed bf16 values v: s += v, q += v * w (w also 8 packed bf16)
@@ -99,6 +103,20 @@ __device__ __forceinline__ u32x4 relu_mask_bf16x8(u32x4 v, u32x4 y) {
   return o;
 }
 
+// dz lanes where the recomputed group output relu(x * scale + shift) is zero: x 8 packed bf16 of the
+// BN input, the same f32 fma as the BN apply pass
+__device__ __forceinline__ u32x4 relu_mask_affine_bf16x8(u32x4 v, u32x4 x, const float* sc, const float* sh) {
+  u32x4 o;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float lo = __uint_as_float(x[k] << 16), hi = __uint_as_float(x[k] & 0xffff0000u);
+    const uint32_t mlo = fmaf(lo, sc[2 * k], sh[2 * k]) > 0.f ? 0x0000ffffu : 0u;
+    const uint32_t mhi = fmaf(hi, sc[2 * k + 1], sh[2 * k + 1]) > 0.f ? 0xffff0000u : 0u;
+    o[k] = v[k] & (mlo | mhi);
+  }
+  return o;
+}
+
 // a + b for 8 packed bf16 values (f32 add, round to nearest even)
 __device__ __forceinline__ u32x4 add_bf16x8(u32x4 a, u32x4 b) {
   u32x4 o;
@@ -127,6 +145,7 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
 // stride-2 scatter).  Every thread of the workgroup must call it (it has workgroup barriers).
 // LOWREG (the 4-waves-per-SIMD variants, <= 128 VGPRs): the BN-group backward epilogue loads its
 // residual and BN operands in chunks of EPI / 4 segments right before their use instead of all up front.
+// EK 3: the BN-group backward of EK 1 with the ReLU mask recomputed from the BN input (bn_ss).
 template <int BM, int BN, int NT, int EK, int WTM, int WTN, int LDS_ELEMS, int LOWREG = 0>
 __device__ __forceinline__ void conv_epilogue(const Igemm& a, const f4v (&acc)[WTM / 16][WTN / 16], uint16_t* lds,
                                               int tm, int tn, int wrow0, int wcol0) {
@@ -138,7 +157,8 @@ __device__ __forceinline__ void conv_epilogue(const Igemm& a, const f4v (&acc)[W
   // residual (gradient sum): all of this thread's loads issued here, before the LDS round trip, so
   // their latency overlaps it instead of serialising the store loop
   // segments per operand chunk (LOWREG 1: the BN-group backward epilogue only, 2: every epilogue)
-  constexpr int EC = ((LOWREG == 1 && EK == 1) || (LOWREG == 2 && EK != 2)) ? (EPI >= 4 ? EPI / 4 : 1) : EPI;
+  constexpr bool BNB = EK == 1 || EK == 3;  // fused BN-group backward
+  constexpr int EC = ((LOWREG == 1 && BNB) || (LOWREG == 2 && EK != 2)) ? (EPI >= 4 ? EPI / 4 : 1) : EPI;
   u32x4 rv[EK == 2 ? 1 : EPI];
   if (EK != 2 && a.res && EC == EPI) {
 #pragma unroll
@@ -160,17 +180,27 @@ __device__ __forceinline__ void conv_epilogue(const Igemm& a, const f4v (&acc)[W
           make_uint2(lo, hi);
     }
   // BN-backward fusion operands (the accumulators are dead now: registers to spare)
-  constexpr int BNE = EK == 1 ? EPI : 1;
-  u32x4 ry[BNE], rx[BNE], rx2[BNE];
+  constexpr int BNE = BNB ? EPI : 1;
+  u32x4 ry[EK == 1 ? EPI : 1], rx[BNE], rx2[BNE];
+  // EK 3: this thread's 8 channels (one segment column for all its rows) of the mask's scale / shift
+  float msc[EK == 3 ? 8 : 1], msh[EK == 3 ? 8 : 1];
+  if constexpr (EK == 3) {
+    const int c0 = tn * BN + (tid % SEG) * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      msc[j] = a.bn_ss[c0 + j];
+      msh[j] = a.bn_ss[a.K + c0 + j];
+    }
+  }
   // the BN-group operands of segments [e0, e0 + EC) (all of them up front unless LOWREG)
   auto load_bn = [&](int e0) {
-    if constexpr (EK == 1) {
+    if constexpr (BNB) {
 #pragma unroll
       for (int e = e0; e < e0 + EC; ++e) {
         const int s = tid + e * NT, row = s / SEG, seg = s % SEG, m = tm * BM + row;
         const long long o = (long long)m * a.K + tn * BN + seg * 8;
         const bool in = m < a.M;
-        ry[e] = in ? *reinterpret_cast<const u32x4*>(a.bn_y + o) : u32x4{0u, 0u, 0u, 0u};
+        if constexpr (EK == 1) ry[e] = in ? *reinterpret_cast<const u32x4*>(a.bn_y + o) : u32x4{0u, 0u, 0u, 0u};
         rx[e] = in ? *reinterpret_cast<const u32x4*>(a.bn_x + o) : u32x4{0u, 0u, 0u, 0u};
         rx2[e] = (in && a.bn_x2) ? *reinterpret_cast<const u32x4*>(a.bn_x2 + o) : u32x4{0u, 0u, 0u, 0u};
         if (EC != EPI && a.res)
@@ -208,9 +238,10 @@ __device__ __forceinline__ void conv_epilogue(const Igemm& a, const f4v (&acc)[W
         u32x4 v = *reinterpret_cast<const u32x4*>(lds + row * OUT_LD + seg * 8);
         if (a.res) v = add_bf16x8(v, rv[e]);
         if constexpr (EK == 1) v = relu_mask_bf16x8(v, ry[e]);
+        if constexpr (EK == 3) v = relu_mask_affine_bf16x8(v, rx[e], msc, msh);
         *reinterpret_cast<u32x4*>(a.y + o) = v;
-        if (sums) accum_bf16x8(v, EK == 1 ? rx[e] : v, cs, cq);
-        if constexpr (EK == 1)
+        if (sums) accum_bf16x8(v, BNB ? rx[e] : v, cs, cq);
+        if constexpr (BNB)
           if (sums2) dot_bf16x8(v, rx2[e], cq2);
       }
     }
@@ -237,7 +268,7 @@ __device__ __forceinline__ void conv_epilogue(const Igemm& a, const f4v (&acc)[W
       if (a.bn_part) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          by[q] = ok[q] ? *reinterpret_cast<const u32x4*>(a.bn_y + po[q]) : z;
+          by[q] = (ok[q] && a.bn_y) ? *reinterpret_cast<const u32x4*>(a.bn_y + po[q]) : z;
           bx[q] = ok[q] ? *reinterpret_cast<const u32x4*>(a.bn_x + po[q]) : z;
           bx2[q] = (ok[q] && a.bn_x2) ? *reinterpret_cast<const u32x4*>(a.bn_x2 + po[q]) : z;
         }
@@ -248,7 +279,18 @@ __device__ __forceinline__ void conv_epilogue(const Igemm& a, const f4v (&acc)[W
       for (int q = 0; q < 4; ++q) {
         if (!ok[q]) continue;
         if (a.bn_part) {
-          p[q] = relu_mask_bf16x8(p[q], by[q]);
+          if (a.bn_ss) {
+            const int c0 = tn * BN + seg * 8;
+            float sc[8], sh[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              sc[j] = a.bn_ss[c0 + j];
+              sh[j] = a.bn_ss[a.K + c0 + j];
+            }
+            p[q] = relu_mask_affine_bf16x8(p[q], bx[q], sc, sh);
+          } else {
+            p[q] = relu_mask_bf16x8(p[q], by[q]);
+          }
           accum_bf16x8(p[q], bx[q], cs, cq);
           if (sums2) dot_bf16x8(p[q], bx2[q], cq2);
         }
@@ -638,7 +680,9 @@ void launch_epi(const Igemm& a, hipStream_t s) {
   {
     if (a.scatter)  // (the scatter epilogue spills at 128 VGPRs: depth 0 takes the 3-waves-per-SIMD variant)
       hipLaunchKernelGGL((k_conv_igemm<BM, BN, DEPTH == 0 ? 3 : DEPTH, 2>), grid, block, 0, s, a);
-    else if (a.bn_part)  // (DEPTH 3's fused BN-group backward epilogue spills at 168 VGPRs: depth 2)
+    else if (a.bn_part && a.bn_ss)  // (DEPTH 3's fused BN-group backward epilogue spills at 168 VGPRs: depth 2)
+      hipLaunchKernelGGL((k_conv_igemm<BM, BN, DEPTH == 3 ? 2 : DEPTH, 3>), grid, block, 0, s, a);
+    else if (a.bn_part)
       hipLaunchKernelGGL((k_conv_igemm<BM, BN, DEPTH == 3 ? 2 : DEPTH, 1>), grid, block, 0, s, a);
     else
       hipLaunchKernelGGL((k_conv_igemm<BM, BN, DEPTH, 0>), grid, block, 0, s, a);
@@ -673,6 +717,8 @@ void launch_v2(const Igemm& a, hipStream_t s) {
   const dim3 grid((a.M + BM - 1) / BM * (a.K / BN)), block(64 * WGM * WGN);
   if (a.scatter)
     hipLaunchKernelGGL((k_conv_glds<BM, BN, WGM, WGN, 2, STAGES, MINW>), grid, block, 0, s, a);
+  else if (a.bn_part && a.bn_ss)
+    hipLaunchKernelGGL((k_conv_glds<BM, BN, WGM, WGN, 3, STAGES, MINW>), grid, block, 0, s, a);
   else if (a.bn_part)
     hipLaunchKernelGGL((k_conv_glds<BM, BN, WGM, WGN, 1, STAGES, MINW>), grid, block, 0, s, a);
   else
@@ -773,27 +819,27 @@ void conv_fwd_bf16(const void* x, const void* w_ohwi, void* y, const ConvGeom& g
 
 void conv_dgrad_bf16(const void* dy, const void* w_hwio, void* dx, const ConvGeom& g, hipStream_t s,
                      const void* residual, const void* bn_y, const void* bn_x, float* bn_part, const void* bn_x2,
-                     float* bn_part2) {
+                     float* bn_part2, const float* bn_ss) {
   // image = dy [N][OH][OW][K] (reduction channels K), output = dx [N][H][W][C] (columns C), stride 1,
   // mirrored taps with padding KH-1-PT / KW-1-PL
   Igemm a{static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w_hwio), static_cast<uint16_t*>(dx),
           g.N, g.OH, g.OW, g.K, g.H, g.W, g.C, g.KH, g.KW, 1, 1, g.KH - 1 - g.PT, g.KW - 1 - g.PL, 1,
           (long long)g.K, (long long)g.KW * g.C * g.K, (long long)g.C * g.K, g.N * g.H * g.W, 0, 0, 0,
           static_cast<const uint16_t*>(residual), nullptr, static_cast<const uint16_t*>(bn_y),
-          static_cast<const uint16_t*>(bn_x), bn_part, static_cast<const uint16_t*>(bn_x2), bn_part2};
+          static_cast<const uint16_t*>(bn_x), bn_part, static_cast<const uint16_t*>(bn_x2), bn_part2, bn_ss};
   launch(a, s);
 }
 
 void conv_dgrad_s2_1x1_bf16(const void* dy, const void* w_hwio, void* dx, const ConvGeom& g, hipStream_t s,
                             const void* residual, const void* bn_y, const void* bn_x, float* bn_part,
-                            const void* bn_x2, float* bn_part2) {
+                            const void* bn_x2, float* bn_part2, const float* bn_ss) {
   // a 1x1 stride-1 "convolution" of dy [N][OH][OW][K] with the HWIO rows [C][K] (columns C, reduction K),
   // scattered to the even pixels of dx [N][H][W][C]
   Igemm a{static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w_hwio), static_cast<uint16_t*>(dx),
           g.N, g.OH, g.OW, g.K, g.OH, g.OW, g.C, 1, 1, 1, 1, 0, 0, 0,
           (long long)g.K, 0, 0, g.N * g.OH * g.OW, 2, g.H, g.W, static_cast<const uint16_t*>(residual), nullptr,
           static_cast<const uint16_t*>(bn_y), static_cast<const uint16_t*>(bn_x), bn_part,
-          static_cast<const uint16_t*>(bn_x2), bn_part2};
+          static_cast<const uint16_t*>(bn_x2), bn_part2, bn_ss};
   launch(a, s);
 }
 

@@ -272,52 +272,63 @@ const void* opt_residual(const c10::optional<at::Tensor>& r, const at::Tensor& l
 std::vector<at::Tensor> conv_dgrad_impl(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w, int64_t pt,
                                         int64_t pl, c10::optional<at::Tensor> residual,
                                         c10::optional<at::Tensor> bn_y, c10::optional<at::Tensor> bn_x,
-                                        c10::optional<at::Tensor> bn_x2);
+                                        c10::optional<at::Tensor> bn_x2, c10::optional<at::Tensor> bn_stats);
 
 // BN-group fusion operands of an input gradient (see conv.h): (bn_y, bn_x[, bn_x2]) tensors shaped
 // like dx, and the part buffers [P + ceil(P/64)][2][C] for P row tiles
+// bn_stats: the [4][C] statistics (mean, invstd, scale, shift) of a plain BN -> ReLU group's forward:
+// the mask is recomputed from bn_x (bn_y may then be absent)
 struct DgradBn {
   const void *by = nullptr, *bx = nullptr, *bx2 = nullptr;
+  const float* ss = nullptr;
   at::Tensor part, part2;
   DgradBn(const c10::optional<at::Tensor>& bn_y, const c10::optional<at::Tensor>& bn_x,
-          const c10::optional<at::Tensor>& bn_x2, const at::Tensor& dy, int64_t h, int64_t w, int64_t c,
-          int64_t P) {
+          const c10::optional<at::Tensor>& bn_x2, const c10::optional<at::Tensor>& bn_stats, const at::Tensor& dy,
+          int64_t h, int64_t w, int64_t c, int64_t P) {
     by = opt_residual(bn_y, dy, dy.size(0), h, w, c);
     bx = opt_residual(bn_x, dy, dy.size(0), h, w, c);
     bx2 = opt_residual(bn_x2, dy, dy.size(0), h, w, c);
-    TORCH_CHECK((by == nullptr) == (bx == nullptr), "conv_dgrad: bn_y and bn_x go together");
-    TORCH_CHECK(bx2 == nullptr || by != nullptr, "conv_dgrad: bn_x2 needs bn_y / bn_x");
+    if (bn_stats.has_value() && bn_stats->defined()) {
+      TORCH_CHECK(bn_stats->is_cuda() && bn_stats->is_contiguous() && bn_stats->scalar_type() == at::kFloat &&
+                      bn_stats->numel() == 4 * c,
+                  "conv_dgrad: bn_stats must be the f32 [4][C] statistics of the group's BN");
+      ss = bn_stats->data_ptr<float>() + 2 * c;  // scale[C], shift[C]
+    }
+    TORCH_CHECK((by != nullptr || ss != nullptr) == (bx != nullptr), "conv_dgrad: bn_y (or bn_stats) and bn_x go together");
+    TORCH_CHECK(bx2 == nullptr || bx != nullptr, "conv_dgrad: bn_x2 needs bn_x");
     auto f = dy.options().dtype(at::kFloat);
-    if (by) part = fresh({P + (P + 63) / 64, 2, c}, f);
+    if (bx) part = fresh({P + (P + 63) / 64, 2, c}, f);
     if (bx2) part2 = fresh({P + (P + 63) / 64, 2, c}, f);
   }
-  float* p() { return by ? part.data_ptr<float>() : nullptr; }
+  float* p() { return bx ? part.data_ptr<float>() : nullptr; }
   float* p2() { return bx2 ? part2.data_ptr<float>() : nullptr; }
   std::vector<at::Tensor> out(const at::Tensor& dx) {
     if (bx2) return {dx, part, part2};
-    if (by) return {dx, part};
+    if (bx) return {dx, part};
     return {dx};
   }
 };
 
 at::Tensor conv_dgrad(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w, int64_t pt, int64_t pl,
                       c10::optional<at::Tensor> residual) {
-  return conv_dgrad_impl(dy, w_hwio, h, w, pt, pl, residual, c10::nullopt, c10::nullopt, c10::nullopt)[0];
+  return conv_dgrad_impl(dy, w_hwio, h, w, pt, pl, residual, c10::nullopt, c10::nullopt, c10::nullopt, c10::nullopt)[0];
 }
 
 // input gradient with the fused backward of the BN -> Add -> ReLU group that produced the conv's
 // input bn_y from bn_x: returns (dz, part[P + ceil(P/64)][2][C][, part2]); bn_x2: the input of the
-// plain BN whose output is the group's residual (part2: its backward sums)
+// plain BN whose output is the group's residual (part2: its backward sums); bn_stats instead of bn_y:
+// a plain BN -> ReLU group, mask recomputed from bn_x
 std::vector<at::Tensor> conv_dgrad_bn(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w, int64_t pt, int64_t pl,
-                                      c10::optional<at::Tensor> residual, at::Tensor bn_y, at::Tensor bn_x,
-                                      c10::optional<at::Tensor> bn_x2) {
-  return conv_dgrad_impl(dy, w_hwio, h, w, pt, pl, residual, bn_y, bn_x, bn_x2);
+                                      c10::optional<at::Tensor> residual, c10::optional<at::Tensor> bn_y,
+                                      at::Tensor bn_x, c10::optional<at::Tensor> bn_x2,
+                                      c10::optional<at::Tensor> bn_stats) {
+  return conv_dgrad_impl(dy, w_hwio, h, w, pt, pl, residual, bn_y, bn_x, bn_x2, bn_stats);
 }
 
 std::vector<at::Tensor> conv_dgrad_impl(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w, int64_t pt,
                                         int64_t pl, c10::optional<at::Tensor> residual,
                                         c10::optional<at::Tensor> bn_y, c10::optional<at::Tensor> bn_x,
-                                        c10::optional<at::Tensor> bn_x2) {
+                                        c10::optional<at::Tensor> bn_x2, c10::optional<at::Tensor> bn_stats) {
   conv_check(dy, "dy");
   conv_check(w_hwio, "w");
   TORCH_CHECK(w_hwio.dim() == 4 && w_hwio.size(3) == dy.size(3), "conv_dgrad: weights must be HWIO [KH,KW,C,K]");
@@ -326,17 +337,18 @@ std::vector<at::Tensor> conv_dgrad_impl(at::Tensor dy, at::Tensor w_hwio, int64_
   TORCH_CHECK(tdl::conv_bf16_supported(g), "conv_dgrad: unsupported geometry (C and K must be multiples of 64)");
   auto dx = fresh({dy.size(0), h, w, w_hwio.size(2)}, dy.options(), 2);
   const int64_t M = (int64_t)g.N * g.H * g.W, bm = tdl::conv_dgrad_row_tile(g);
-  DgradBn bn(bn_y, bn_x, bn_x2, dy, h, w, w_hwio.size(2), (M + bm - 1) / bm);
+  DgradBn bn(bn_y, bn_x, bn_x2, bn_stats, dy, h, w, w_hwio.size(2), (M + bm - 1) / bm);
   tdl::conv_dgrad_bf16(dy.data_ptr(), w_hwio.data_ptr(), dx.data_ptr(), g, cur_stream(),
                        opt_residual(residual, dy, dy.size(0), h, w, w_hwio.size(2)), bn.by, bn.bx, bn.p(), bn.bx2,
-                       bn.p2());
+                       bn.p2(), bn.ss);
   return bn.out(dx);
 }
 // input gradient of a 1x1 stride-2 unpadded conv: dx[N,H,W,C] from dy[N,OH,OW,K] and w_hwio[1,1,C,K];
 // with bn_y / bn_x[ / bn_x2] the fused BN-group backward as in conv_dgrad_bn: (dz, part[, part2])
 std::vector<at::Tensor> conv_dgrad_s2_impl(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w,
                                            c10::optional<at::Tensor> residual, c10::optional<at::Tensor> bn_y,
-                                           c10::optional<at::Tensor> bn_x, c10::optional<at::Tensor> bn_x2) {
+                                           c10::optional<at::Tensor> bn_x, c10::optional<at::Tensor> bn_x2,
+                                           c10::optional<at::Tensor> bn_stats) {
   conv_check(dy, "dy");
   conv_check(w_hwio, "w");
   TORCH_CHECK(w_hwio.dim() == 4 && w_hwio.size(0) == 1 && w_hwio.size(1) == 1 && w_hwio.size(3) == dy.size(3),
@@ -348,21 +360,22 @@ std::vector<at::Tensor> conv_dgrad_s2_impl(at::Tensor dy, at::Tensor w_hwio, int
   TORCH_CHECK(tdl::conv_bf16_supported(g), "conv_dgrad_s2: unsupported geometry (C and K must be multiples of 64)");
   auto dx = fresh({dy.size(0), h, w, w_hwio.size(2)}, dy.options(), 2);
   const int64_t M = (int64_t)g.N * g.OH * g.OW, bm = tdl::conv_dgrad_s2_row_tile(g);
-  DgradBn bn(bn_y, bn_x, bn_x2, dy, h, w, w_hwio.size(2), (M + bm - 1) / bm);
+  DgradBn bn(bn_y, bn_x, bn_x2, bn_stats, dy, h, w, w_hwio.size(2), (M + bm - 1) / bm);
   tdl::conv_dgrad_s2_1x1_bf16(dy.data_ptr(), w_hwio.data_ptr(), dx.data_ptr(), g, cur_stream(),
                               opt_residual(residual, dy, dy.size(0), h, w, w_hwio.size(2)), bn.by, bn.bx, bn.p(),
-                              bn.bx2, bn.p2());
+                              bn.bx2, bn.p2(), bn.ss);
   return bn.out(dx);
 }
 
 at::Tensor conv_dgrad_s2(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w, c10::optional<at::Tensor> residual) {
-  return conv_dgrad_s2_impl(dy, w_hwio, h, w, residual, c10::nullopt, c10::nullopt, c10::nullopt)[0];
+  return conv_dgrad_s2_impl(dy, w_hwio, h, w, residual, c10::nullopt, c10::nullopt, c10::nullopt, c10::nullopt)[0];
 }
 
 std::vector<at::Tensor> conv_dgrad_s2_bn(at::Tensor dy, at::Tensor w_hwio, int64_t h, int64_t w,
-                                         c10::optional<at::Tensor> residual, at::Tensor bn_y, at::Tensor bn_x,
-                                         c10::optional<at::Tensor> bn_x2) {
-  return conv_dgrad_s2_impl(dy, w_hwio, h, w, residual, bn_y, bn_x, bn_x2);
+                                         c10::optional<at::Tensor> residual, c10::optional<at::Tensor> bn_y,
+                                         at::Tensor bn_x, c10::optional<at::Tensor> bn_x2,
+                                         c10::optional<at::Tensor> bn_stats) {
+  return conv_dgrad_s2_impl(dy, w_hwio, h, w, residual, bn_y, bn_x, bn_x2, bn_stats);
 }
 
 // weight gradient: dw[KH,KW,C,K] (bf16, or added into the f32 `out` when given) from x[N,H,W,C] and
@@ -611,11 +624,11 @@ void register_ops(pybind11::module& m) {
   m.def("conv_dgrad_bn", &conv_dgrad_bn, "stride-1 conv input gradient + fused BN->Add->ReLU backward (dz, part[, part2])",
         pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("h"), pybind11::arg("wd"), pybind11::arg("pt"),
         pybind11::arg("pl"), pybind11::arg("residual"), pybind11::arg("bn_y"), pybind11::arg("bn_x"),
-        pybind11::arg("bn_x2") = pybind11::none());
+        pybind11::arg("bn_x2") = pybind11::none(), pybind11::arg("bn_stats") = pybind11::none());
   m.def("conv_dgrad_s2_bn", &conv_dgrad_s2_bn,
         "1x1 stride-2 conv input gradient + fused BN->Add->ReLU backward (dz, part[, part2])", pybind11::arg("dy"),
         pybind11::arg("w"), pybind11::arg("h"), pybind11::arg("wd"), pybind11::arg("residual"), pybind11::arg("bn_y"),
-        pybind11::arg("bn_x"), pybind11::arg("bn_x2") = pybind11::none());
+        pybind11::arg("bn_x"), pybind11::arg("bn_x2") = pybind11::none(), pybind11::arg("bn_stats") = pybind11::none());
   m.def("conv_dgrad_s2", &conv_dgrad_s2, "NHWC bf16 1x1 stride-2 convolution input gradient (MFMA)",
         pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("h"), pybind11::arg("wd"),
         pybind11::arg("residual") = pybind11::none());

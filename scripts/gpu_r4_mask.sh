@@ -1,0 +1,9 @@
+#!/bin/bash
+# Round 4: BN-ReLU mask from the BN statistics in the dgrad epilogue -- tests, then the ResNet-50 window.
+set -o pipefail
+O=gpurun_out/r4mask
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_slab_grad_gpu.py tests/test_conv_gpu.py tests/test_conv_v2_gpu.py tests/test_bn_gpu.py -x -v --timeout 200 --timeout-method thread > $O/tests.log 2>&1 || { echo "TESTS FAILED"; tail -60 $O/tests.log; exit 1; }
+tail -3 $O/tests.log
+bash scripts/gpu_resnet_window.sh rnw_mask

@@ -203,14 +203,18 @@ def run_group(g: Group, vals, training, taps=None, boxes=None):
         # the folded bias's gradient is exactly zero: with a gradient slab bound, leave its (zeroed)
         # slab entries alone instead of accumulating zeros
         cb = cbv.value.detach() if cbv.grad_target() is not None else cbv.value
+    st = [] if (g.relu and r is None) else None
     y = batch_norm_train(x, bn.gamma.value if bn.gamma is not None else None,
                          bn.beta.value if bn.beta is not None else None, bn.moving_mean.value,
                          bn.moving_variance.value, bn.momentum, bn.epsilon, relu=g.relu, residual=r, conv_bias=cb,
-                         grad_out=bn._grad_targets(), part=getattr(x, "_tdl_bn_part", None))
+                         grad_out=bn._grad_targets(), part=getattr(x, "_tdl_bn_part", None), stats_out=st)
     if g.relu and (r is not None or g.conv_reader) and y.is_cuda:
         # a conv reading this group's output can fuse the group's backward reduction into its
-        # input-gradient epilogue (ops/conv.py): it needs the BN input
+        # input-gradient epilogue (ops/conv.py): it needs the BN input, and for a plain BN -> ReLU
+        # group the batch statistics, from which the epilogue recomputes the ReLU mask (no read of y)
         y._tdl_bn_src = x
+        if st:
+            y._tdl_bn_stats = st[0]
         if g.res_bn is not None:
             y._tdl_bn_src2 = vals[id(g.res_bn.bn_node.inputs)]
     vals[id(g.out)] = y

@@ -391,6 +391,7 @@ class Conv2D(Layer):
                                   w_ohwi=self.kernel.compute_view_ohwi(x.dtype) if gt is not None else None,
                                   grad_box=_grad_box, bn_stats=_bn_stats, bn_src=getattr(x, "_tdl_bn_src", None),
                                   bn_src2=getattr(x, "_tdl_bn_src2", None),
+                                  bn_stats_src=getattr(x, "_tdl_bn_stats", None),
                                   anchor=self.kernel.value if gt is not None else None)
             if b is not None:
                 y = y + b

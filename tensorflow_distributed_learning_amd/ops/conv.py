@@ -26,6 +26,8 @@ _FUSE_BN_BWD = [os.environ.get("TDL_FUSE_BN_BWD", "1") == "1"]
 # and the projection-shortcut BN's sums (part2) beside the block-output group's
 _FUSE_BN_BWD_S2 = [os.environ.get("TDL_FUSE_BN_BWD_S2", "1") == "1"]
 _FUSE_BN_BWD_SHORTCUT = [os.environ.get("TDL_FUSE_BN_BWD_SHORTCUT", "1") == "1"]
+# a plain BN -> ReLU group's mask recomputed from its BN input and statistics (one read less)
+_FUSE_BN_MASK_STATS = [os.environ.get("TDL_FUSE_BN_MASK_STATS", "1") == "1"]
 _choice: dict = {}  # (direction, shape key) -> True (hand-written kernel) / False (MIOpen)
 _times: dict = {}  # (direction, shape key) -> (hand-written ms, MIOpen ms) as measured by the autotuner
 
@@ -212,7 +214,7 @@ def _ref_fwd(x, w_oihw, stride, pad):
 class _Conv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, kernel, stride, pad, grad_out, w_ohwi=None, box=None, stats_out=None, bn_src=None,
-                bn_src2=None, anchor=None):
+                bn_src2=None, anchor=None, bn_stats_src=None):
         C = hip()
         x = x.contiguous()
         if x.data_ptr() % 16:
@@ -243,6 +245,10 @@ class _Conv(torch.autograd.Function):
                                 and bn_src.dtype == x.dtype) else None
         ctx.bn_src2 = bn_src2 if (ctx.bn_src is not None and bn_src2 is not None
                                   and tuple(bn_src2.shape) == tuple(x.shape) and bn_src2.dtype == x.dtype) else None
+        # a plain BN -> ReLU group's [4][C] statistics: the dgrad epilogue recomputes the mask from bn_src
+        ctx.bn_stats_src = bn_stats_src if (ctx.bn_src is not None and ctx.bn_src2 is None and _FUSE_BN_MASK_STATS[0]
+                                            and bn_stats_src is not None
+                                            and bn_stats_src.numel() == 4 * x.shape[-1]) else None
         if box is not None:
             box.n += 1
         return y
@@ -302,10 +308,13 @@ class _Conv(torch.autograd.Function):
                     # with bn_src2 also the reduction of the projection-shortcut BN feeding its Add
                     src, src2 = _aligned(src), ctx.bn_src2 if _FUSE_BN_BWD_SHORTCUT[0] else None
                     src2 = _aligned(src2) if src2 is not None else None
+                    # plain BN -> ReLU group: no read of x for the mask (recomputed from src and the stats)
+                    st = ctx.bn_stats_src
+                    xm = x if st is None else None
                     if stride == (1, 1):
-                        out = C.conv_dgrad_bn(dy, kc, x.shape[1], x.shape[2], pad[0], pad[1], other, x, src, src2)
+                        out = C.conv_dgrad_bn(dy, kc, x.shape[1], x.shape[2], pad[0], pad[1], other, xm, src, src2, st)
                     else:
-                        out = C.conv_dgrad_s2_bn(dy, kc, x.shape[1], x.shape[2], other, x, src, src2)
+                        out = C.conv_dgrad_s2_bn(dy, kc, x.shape[1], x.shape[2], other, xm, src, src2, st)
                     dx = out[0]
                     dx._tdl_bn_bwd_part = out[1]
                     if src2 is not None:
@@ -341,7 +350,7 @@ class _Conv(torch.autograd.Function):
             dx = dx + other.view_as(dx)
         if first:  # park this contribution for the other consumer's backward
             box.g, dx = dx, None
-        return dx, dw, None, None, None, None, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None, None, None, None, None
 
 
 _DEBUG_PARTS = os.environ.get("TDL_DEBUG_BN_PARTS") == "1"
@@ -374,7 +383,7 @@ def _miopen_bwd(dy_nchw, x_nchw, w_oihw, stride, pad, mask):
 
 
 def conv2d_nhwc(x, kernel_hwio, stride=(1, 1), pad=(0, 0), grad_out=None, w_ohwi=None, grad_box=None,
-                bn_stats=False, bn_src=None, bn_src2=None, anchor=None):
+                bn_stats=False, bn_src=None, bn_src2=None, anchor=None, bn_stats_src=None):
     """y[N,OH,OW,K] = conv(x[N,H,W,C], kernel[KH,KW,C,K]) with symmetric zero padding ``pad = (ph, pw)``,
     bf16; the caller checked :func:`supported`.  ``grad_out``: f32 [KH,KW,C,K] tensor the weight
     gradient is added into (a trainer's gradient slab view; ``kernel_hwio`` then needs no autograd);
@@ -388,10 +397,12 @@ def conv2d_nhwc(x, kernel_hwio, stride=(1, 1), pad=(0, 0), grad_out=None, w_ohwi
     plain (projection-shortcut) BN whose output is that group's residual: the same epilogue reduces
     its backward sums too.  ``anchor``: with ``grad_out``, the variable's leaf tensor, so that the
     backward runs although neither the input (the first layer's batch) nor the detached compute-dtype
-    kernel needs a gradient (the kernel's gradient goes into ``grad_out``; the anchor gets none)."""
+    kernel needs a gradient (the kernel's gradient goes into ``grad_out``; the anchor gets none).
+    ``bn_stats_src``: with ``bn_src`` of a plain BN -> ReLU group, that BN's [4][C] batch statistics: the
+    epilogue recomputes the ReLU mask from ``bn_src`` instead of reading x."""
     holder = [None] if bn_stats else None
     y = _Conv.apply(x, kernel_hwio, tuple(stride), tuple(pad), grad_out, w_ohwi, grad_box, holder, bn_src, bn_src2,
-                    anchor)
+                    anchor, bn_stats_src)
     if holder is not None and holder[0] is not None:
         y._tdl_bn_part = holder[0]
     return y

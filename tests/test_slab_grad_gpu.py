@@ -296,3 +296,36 @@ def test_conv_dgrad_s2_bn_epilogue_matches_reference():
         Q2 = part2[:rows, 1].sum(0)
         np.testing.assert_allclose(Q2.cpu().numpy(), (dz.float() * bx2.float()).sum((0, 1, 2)).cpu().numpy(),
                                    rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("kind", ["3x3", "1x1", "s2"])
+def test_dgrad_bn_mask_from_stats_matches_mask_from_y_bitwise(kind):
+    """A plain BN -> ReLU group's ReLU mask recomputed in the dgrad epilogue from its BN input and the
+    forward's scale / shift (bn_stats, no read of the group output) gives the dz and partial sums of
+    the mask read from the group output, bit for bit."""
+    from tensorflow_distributed_learning_amd.ops import hip
+
+    C = hip()
+    g = torch.Generator(device="cpu").manual_seed(11)
+    N, H, Ci, K = 4, 14, 128, 128
+    s2 = kind == "s2"
+    OH = H // 2 if s2 else H
+    bx = (torch.randn(N, H, H, Ci, generator=g) * 2 + 0.3).cuda().bfloat16()
+    gam, bet = (torch.rand(Ci, generator=g) + 0.5).cuda(), torch.randn(Ci, generator=g).cuda()
+    mm, mv = torch.zeros(Ci, device="cuda"), torch.ones(Ci, device="cuda")
+    by, st = C.bn_forward_train(bx, gam, bet, mm, mv, 0.9, 1e-3, True, None, None)
+    dy = torch.randn(N, OH, OH, K, generator=g).cuda().bfloat16()
+    if s2:
+        w = (torch.randn(1, 1, Ci, K, generator=g) * 0.1).cuda().bfloat16()
+        a = C.conv_dgrad_s2_bn(dy, w, H, H, None, by, bx)
+        b = C.conv_dgrad_s2_bn(dy, w, H, H, None, None, bx, None, st)
+    else:
+        k = 3 if kind == "3x3" else 1
+        w = (torch.randn(k, k, Ci, K, generator=g) * 0.05).cuda().bfloat16()
+        a = C.conv_dgrad_bn(dy, w, H, H, k // 2, k // 2, None, by, bx)
+        b = C.conv_dgrad_bn(dy, w, H, H, k // 2, k // 2, None, None, bx, None, st)
+    assert torch.equal(a[0], b[0])
+    R = a[1].shape[0]
+    P = next(q for q in range(R + 1) if q + (q + 63) // 64 == R)
+    assert torch.equal(a[1][:P], b[1][:P])
+    assert int((a[0] == 0).sum()) > 0  # the mask did something
