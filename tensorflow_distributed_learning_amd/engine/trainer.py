@@ -293,6 +293,9 @@ class GenericTrainer:
             def hook(_p):
                 self._counts[b] -= 1
                 if self._counts[b] == 0:
+                    from ..ops import conv as _conv
+
+                    _conv.join_side()  # this bucket's weight gradients may still be on the side stream
                     s, e = self._bucket_ranges[b]
                     if getattr(self, "_skip_comm", False):  # fault injection: this rank leaves it out
                         from ..parallel.communicator import _Done
@@ -361,8 +364,15 @@ class GenericTrainer:
             _ck.record("input:x", x)
             _ck.record("input:y", y)
             _ck.record("loss", loss)
-        with trace_range("tdl.backward"):
-            loss.backward()
+        from ..ops import conv as _conv
+
+        _conv.side_stream_window(self.device.type == "cuda")
+        try:
+            with trace_range("tdl.backward"):
+                loss.backward()
+        finally:
+            _conv.side_stream_window(False)
+            _conv.join_side()  # every slab weight gradient queued on the side stream is in G
         if _ck.enabled():
             for v, gv in zip(self.model._trainable_vars, self.model._layout.views(G)):
                 _ck.record("slab_grad:" + v.name, gv)

@@ -28,6 +28,43 @@ _FUSE_BN_BWD_S2 = [os.environ.get("TDL_FUSE_BN_BWD_S2", "1") == "1"]
 _FUSE_BN_BWD_SHORTCUT = [os.environ.get("TDL_FUSE_BN_BWD_SHORTCUT", "1") == "1"]
 # a plain BN -> ReLU group's mask recomputed from its BN input and statistics (one read less)
 _FUSE_BN_MASK_STATS = [os.environ.get("TDL_FUSE_BN_MASK_STATS", "1") == "1"]
+
+# Weight gradients into a trainer's slab on a side stream, overlapping the input-gradient / BN chain
+# of the main stream (the trainer opens the window around loss.backward() and joins it before the
+# slab is read: side_stream_window / join_side).  The side stream forks from the main stream at each
+# wgrad (so it sees dy and x), the tensors it reads stay referenced until the join (no allocator
+# reuse while it may still read them).  Off by default (TDL_WGRAD_STREAM=1 enables it): measured on
+# ResNet-50 b=256 the kernels do run concurrently (summed kernel time 26.4 ms in a 21.2 ms step) but
+# the step does not get shorter -- the main chain's grids already fill the GPU, and the latency-bound
+# BN finalize / split-K reduce kernels only slow down beside the wgrads
+# (profiles/resnet50_steady_state_breakdown_r4_wgrad_side_stream.txt).
+_WGRAD_SIDE = [os.environ.get("TDL_WGRAD_STREAM", "0") == "1"]
+_SIDE: dict = {}  # device index -> torch.cuda.Stream
+_SIDE_HELD: list = []  # tensors queued side-stream work reads
+_SIDE_STATE = {"open": False, "used": False}
+
+
+def _side_stream(dev):
+    s = _SIDE.get(dev.index)
+    if s is None:
+        s = _SIDE[dev.index] = torch.cuda.Stream(dev)
+    return s
+
+
+def side_stream_window(open_: bool) -> None:
+    """The trainer's backward window: while open, slab weight gradients go to the side stream."""
+    _SIDE_STATE["open"] = bool(open_) and _WGRAD_SIDE[0]
+
+
+def join_side() -> None:
+    """Order each device's current stream after every weight gradient queued on its side stream (before
+    the slab is read: bucket all-reduce, optimizer) and release the tensors that work reads."""
+    if not _SIDE_STATE["used"]:
+        return
+    for idx, s in _SIDE.items():
+        torch.cuda.current_stream(torch.device("cuda", idx)).wait_stream(s)
+    _SIDE_HELD.clear()
+    _SIDE_STATE["used"] = False
 _choice: dict = {}  # (direction, shape key) -> True (hand-written kernel) / False (MIOpen)
 _times: dict = {}  # (direction, shape key) -> (hand-written ms, MIOpen ms) as measured by the autotuner
 
@@ -330,7 +367,16 @@ class _Conv(torch.autograd.Function):
             plan = _pick_wgrad(("wgrad",) + shape_key, C, x, dy, kh, kw, stride, pad,
                                lambda: ref([False, True, False])()[1])
             if plan is not None:
-                if gout is not None:
+                if gout is not None and _SIDE_STATE["open"] and x.is_cuda:
+                    side = _side_stream(x.device)
+                    side.wait_stream(torch.cuda.current_stream(x.device))
+                    with torch.cuda.stream(side):
+                        C.conv_wgrad(x, dy, kh, kw, stride[0], stride[1], pad[0], pad[1], out=gout, accumulate=True,
+                                     plan=plan)
+                    _SIDE_HELD.append((x, dy))
+                    _SIDE_STATE["used"] = True
+                    want_dw = False
+                elif gout is not None:
                     C.conv_wgrad(x, dy, kh, kw, stride[0], stride[1], pad[0], pad[1], out=gout, accumulate=True,
                                  plan=plan)
                     want_dw = False

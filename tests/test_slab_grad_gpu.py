@@ -329,3 +329,21 @@ def test_dgrad_bn_mask_from_stats_matches_mask_from_y_bitwise(kind):
     P = next(q for q in range(R + 1) if q + (q + 63) // 64 == R)
     assert torch.equal(a[1][:P], b[1][:P])
     assert int((a[0] == 0).sum()) > 0  # the mask did something
+
+
+def test_wgrad_side_stream_matches_main_stream_bitwise():
+    """Slab weight gradients on the side stream (TDL_WGRAD_STREAM=1: they overlap the input-gradient /
+    BN chain) give bit-identical weights to running them on the main stream: same kernels, each slab
+    region written by one reduction, joined before the optimizer reads the slab."""
+    from tensorflow_distributed_learning_amd.ops import conv as CV
+
+    a, _ = _diag_run("T", 2)
+    old = CV._WGRAD_SIDE[0]
+    try:
+        CV._WGRAD_SIDE[0] = True
+        b, _ = _diag_run("T", 2)
+    finally:
+        CV._WGRAD_SIDE[0] = old
+    assert len(a) == len(b)
+    for i, (x, y) in enumerate(zip(a, b)):
+        assert np.array_equal(x, y), f"weight {i}: side-stream vs main-stream weight gradients differ"
