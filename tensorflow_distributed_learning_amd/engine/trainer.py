@@ -170,10 +170,12 @@ class GenericTrainer:
             from ..ops import conv as _conv
 
             _conv.bind_communicator(self.comm)  # rank 0 makes the autotuning decisions for all replicas
-        if self.device.type == "cuda" and os.environ.get("TDL_CONV_AUTOTUNE", "1") == "1":
-            # like TF's cuDNN autotuning (TF_CUDNN_USE_AUTOTUNE=1): MIOpen find-mode search of the
-            # conv solvers per shape on first use (+12% ResNet-50 step rate on MI355X)
-            torch.backends.cudnn.benchmark = True
+        # TDL_CONV_AUTOTUNE=1, like TF's cuDNN autotuning (TF_CUDNN_USE_AUTOTUNE=1): MIOpen find-mode
+        # search of the solvers per shape on first use, for the convs that fall back to MIOpen (scoped
+        # to this trainer's steps, not left set process-wide).  Off by default: every ResNet-50 conv
+        # runs on the hand-written kernels now, and MIOpen's find-mode GenericSearch worker threads
+        # aborted the process on tiny f32 shapes on several boxes (tests/test_fit_gpu.py)
+        self._conv_search = self.device.type == "cuda" and os.environ.get("TDL_CONV_AUTOTUNE", "0") == "1"
 
     # ------------------------------------------------------------------ parameters
     def _make_leaves(self):
@@ -353,9 +355,14 @@ class GenericTrainer:
             if self._Wt is not False:
                 hip().slab_transpose_bf16(self.W, self._Wt, *self._wt_tables)  # OHWI conv rows, one kernel
         V.CAST_ACCUMULATE[0] += 1  # Variable.cast may add straight into the slab only in here
+        search_prev = torch.backends.cudnn.benchmark
+        torch.backends.cudnn.benchmark = search_prev or self._conv_search
         try:
             with trace_range("tdl.forward"):
                 loss, per_ex, y_pred = self._forward_loss(x, y, sw, global_n)
+        except BaseException:
+            torch.backends.cudnn.benchmark = search_prev
+            raise
         finally:
             V.CAST_ACCUMULATE[0] -= 1
         from ..utils import checksums as _ck
@@ -373,6 +380,7 @@ class GenericTrainer:
         finally:
             _conv.side_stream_window(False)
             _conv.join_side()  # every slab weight gradient queued on the side stream is in G
+            torch.backends.cudnn.benchmark = search_prev
         if _ck.enabled():
             for v, gv in zip(self.model._trainable_vars, self.model._layout.views(G)):
                 _ck.record("slab_grad:" + v.name, gv)
