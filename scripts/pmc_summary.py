@@ -10,6 +10,7 @@ for f in glob.glob(sys.argv[1] + "/p*/run_counter_collection.csv"):
         n = r["Kernel_Name"]
         if "tdl::" not in n:
             continue
+        n = n.replace("(anonymous namespace)::", "").replace("void ", "", 1)
         agg[n.split("(")[0].replace("tdl::", "")][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, v in agg.items():
     d = {c: sum(x) / len(x) for c, x in v.items()}
