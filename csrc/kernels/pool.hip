@@ -51,9 +51,21 @@ __device__ __forceinline__ void st8(void* p, int64_t e, const float* v) {
 // K3S2: the 3x3 stride-2 window of ResNet (compile-time loops: every tap's load issued before the
 // compares, and at most 2 x 2 windows per input element in the backward, all four loads at once).
 // Same compare / sum order as the generic loops: bit-identical results.
-template <bool BF, bool K3S2>
+// BNF: the input is a batch norm's input x and the pooled values are relu(x * scale + shift) rounded to
+// bf16 (bn_ss = scale[C], shift[C]): the BN -> ReLU pass and its output tensor are skipped.
+template <bool BF>
+__device__ __forceinline__ void bn_relu8(float* v, const float* sc, const float* sh) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float o = fmaxf(fmaf(v[j], sc[j], sh[j]), 0.f);
+    v[j] = BF ? __uint_as_float(f2bf(o) << 16) : o;  // the value the BN pass would have stored
+  }
+}
+
+template <bool BF, bool K3S2, bool BNF = false>
 __global__ __launch_bounds__(256) void k_maxpool_fwd(const void* __restrict__ x, void* __restrict__ y,
-                                                     uint8_t* __restrict__ arg, PoolGeom g) {
+                                                     uint8_t* __restrict__ arg, PoolGeom g,
+                                                     const float* __restrict__ bn_ss = nullptr) {
   const int G = g.C >> 3;
   const int64_t total = (int64_t)g.N * g.OH * g.OW * G;
   for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
@@ -70,6 +82,14 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd(const void* __restrict__ x,
       best[j] = -INFINITY;
       am[j] = 255;
     }
+    float bsc[BNF ? 8 : 1], bsh[BNF ? 8 : 1];  // this channel group's BN scale / shift (once per element)
+    if constexpr (BNF) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        bsc[j] = bn_ss[cg * 8 + j];
+        bsh[j] = bn_ss[g.C + cg * 8 + j];
+      }
+    }
     if constexpr (K3S2) {
       float v[9][8];
       bool in[9];
@@ -81,6 +101,7 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd(const void* __restrict__ x,
           in[q] = h >= 0 && h < g.H && w >= 0 && w < g.W;
           if (in[q]) {
             ld8<BF>(x, (((int64_t)n * g.H + h) * g.W + w) * g.C + cg * 8, v[q]);
+            if constexpr (BNF) bn_relu8<BF>(v[q], bsc, bsh);
           } else {
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[q][j] = g.pad_zero ? 0.f : -INFINITY;
@@ -105,6 +126,7 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd(const void* __restrict__ x,
         float v[8];
         if (h >= 0 && h < g.H && w >= 0 && w < g.W) {
           ld8<BF>(x, (((int64_t)n * g.H + h) * g.W + w) * g.C + cg * 8, v);
+          if constexpr (BNF) bn_relu8<BF>(v, bsc, bsh);
         } else if (g.pad_zero) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] = 0.f;
@@ -128,11 +150,29 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd(const void* __restrict__ x,
   }
 }
 
-template <bool BF, bool K3S2>
+// BNF: the pooled tensor was relu(bn(bn_x)) (forward BNF): dx is that group's masked gradient dz =
+// dgrad * [bn_x * scale + shift > 0], and part[block][2][C] gets the block's channel sums of dz and
+// dz * bn_x (the BN backward's reduction: bn_backward(part=...) skips its pass).  Needs gridDim * 256
+// to be a multiple of C / 8 (each thread keeps one 8-channel group).
+template <bool BF, bool K3S2, bool BNF = false>
 __global__ __launch_bounds__(256) void k_maxpool_bwd(const void* __restrict__ dy, const uint8_t* __restrict__ arg,
-                                                     void* __restrict__ dx, PoolGeom g) {
+                                                     void* __restrict__ dx, PoolGeom g,
+                                                     const void* __restrict__ bn_x = nullptr,
+                                                     const float* __restrict__ bn_ss = nullptr,
+                                                     float* __restrict__ part = nullptr) {
   const int G = g.C >> 3;
   const int64_t total = (int64_t)g.N * g.H * g.W * G;
+  float bs[BNF ? 8 : 1], bq[BNF ? 8 : 1], msc[BNF ? 8 : 1], msh[BNF ? 8 : 1];
+#pragma unroll
+  for (int j = 0; j < (BNF ? 8 : 1); ++j) bs[j] = bq[j] = 0.f;
+  if constexpr (BNF) {  // a thread's channel group never changes (gridDim * 256 % G == 0)
+    const int cg0 = (int)(((int64_t)blockIdx.x * 256 + threadIdx.x) % G);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      msc[j] = bn_ss[cg0 * 8 + j];
+      msh[j] = bn_ss[g.C + cg0 * 8 + j];
+    }
+  }
   for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
     const int cg = (int)(t % G);
     int64_t r = t / G;
@@ -140,6 +180,9 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd(const void* __restrict__ dy
     r /= g.W;
     const int h = (int)(r % g.H);
     const int n = (int)(r / g.H);
+    const int64_t xo = (((int64_t)n * g.H + h) * g.W + w) * g.C + cg * 8;
+    float xv[BNF ? 8 : 1];
+    if constexpr (BNF) ld8<BF>(bn_x, xo, xv);  // issued before the window loads: its latency overlaps theirs
     const int hp = h + g.pt, wp = w + g.pl;
     const int oh0 = hp - g.kh + 1 <= 0 ? 0 : (hp - g.kh + g.sh) / g.sh;
     const int oh1 = min(g.OH - 1, hp / g.sh);
@@ -187,7 +230,39 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd(const void* __restrict__ dy
           if (aj == pos) acc[j] += d[j];
         }
       }
-    st8<BF>(dx, (((int64_t)n * g.H + h) * g.W + w) * g.C + cg * 8, acc);
+    if constexpr (BNF) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        // the stored dz is the bf16 value; the sums are over exactly what is stored
+        const float d = fmaf(xv[j], msc[j], msh[j]) > 0.f ? (BF ? __uint_as_float(f2bf(acc[j]) << 16) : acc[j]) : 0.f;
+        acc[j] = d;
+        bs[j] += d;
+        bq[j] = fmaf(d, xv[j], bq[j]);
+      }
+    }
+    st8<BF>(dx, xo, acc);
+  }
+  if constexpr (BNF) {
+    // fixed-order block reduction: thread t holds channel group t % G (gridDim * 256 % G == 0)
+    __shared__ float red[2][2048];
+    const int R = 256 / G, cg = threadIdx.x % G, rr = threadIdx.x / G;
+    if (rr < R) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[0][rr * g.C + cg * 8 + j] = bs[j];
+        red[1][rr * g.C + cg * 8 + j] = bq[j];
+      }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < g.C; c += 256) {
+      float S = 0.f, Q = 0.f;
+      for (int k = 0; k < R; ++k) {
+        S += red[0][k * g.C + c];
+        Q += red[1][k * g.C + c];
+      }
+      part[((int64_t)blockIdx.x * 2) * g.C + c] = S;
+      part[((int64_t)blockIdx.x * 2 + 1) * g.C + c] = Q;
+    }
   }
 }
 
@@ -204,9 +279,17 @@ bool k3s2(const PoolGeom& g) { return g_pool_k3s2 && g.kh == 3 && g.kw == 3 && g
 
 void maxpool_force_generic(bool generic) { g_pool_k3s2 = !generic; }
 
-void maxpool_forward(const void* x, void* y, uint8_t* arg, bool bf16, const PoolGeom& g, hipStream_t s) {
+void maxpool_forward(const void* x, void* y, uint8_t* arg, bool bf16, const PoolGeom& g, hipStream_t s,
+                     const float* bn_ss) {
   const int64_t n = (int64_t)g.N * g.OH * g.OW * (g.C / 8);
   const dim3 gr(grid_for(n)), b(256);
+  if (bn_ss != nullptr) {
+    if (bf16)
+      hipLaunchKernelGGL((k_maxpool_fwd<true, false, true>), gr, b, 0, s, x, y, arg, g, bn_ss);
+    else
+      hipLaunchKernelGGL((k_maxpool_fwd<false, false, true>), gr, b, 0, s, x, y, arg, g, bn_ss);
+    return;
+  }
   if (k3s2(g)) {
     if (bf16)
       hipLaunchKernelGGL((k_maxpool_fwd<true, true>), gr, b, 0, s, x, y, arg, g);
@@ -219,9 +302,19 @@ void maxpool_forward(const void* x, void* y, uint8_t* arg, bool bf16, const Pool
   }
 }
 
-void maxpool_backward(const void* dy, const uint8_t* arg, void* dx, bool bf16, const PoolGeom& g, hipStream_t s) {
+int maxpool_backward_blocks(const PoolGeom& g) { return grid_for((int64_t)g.N * g.H * g.W * (g.C / 8)); }
+
+void maxpool_backward(const void* dy, const uint8_t* arg, void* dx, bool bf16, const PoolGeom& g, hipStream_t s,
+                      const void* bn_x, const float* bn_ss, float* part) {
   const int64_t n = (int64_t)g.N * g.H * g.W * (g.C / 8);
   const dim3 gr(grid_for(n)), b(256);
+  if (bn_x != nullptr) {
+    if (bf16)
+      hipLaunchKernelGGL((k_maxpool_bwd<true, false, true>), gr, b, 0, s, dy, arg, dx, g, bn_x, bn_ss, part);
+    else
+      hipLaunchKernelGGL((k_maxpool_bwd<false, false, true>), gr, b, 0, s, dy, arg, dx, g, bn_x, bn_ss, part);
+    return;
+  }
   if (k3s2(g)) {
     if (bf16)
       hipLaunchKernelGGL((k_maxpool_bwd<true, true>), gr, b, 0, s, dy, arg, dx, g);

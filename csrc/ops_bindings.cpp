@@ -90,10 +90,12 @@ int parts_rows(const at::Tensor& t, int64_t C) {
 
 // training forward: y = act(bn(x) [+ residual]); returns (y, stats[4][C] = mean, invstd, scale, shift);
 // moving statistics updated in place (mean_off: folded conv bias, moving mean only)
-std::vector<at::Tensor> bn_forward_train(at::Tensor x, c10::optional<at::Tensor> gamma, c10::optional<at::Tensor> beta,
-                                         c10::optional<at::Tensor> moving_mean, c10::optional<at::Tensor> moving_var,
-                                         double momentum, double eps, bool relu, c10::optional<at::Tensor> residual,
-                                         c10::optional<at::Tensor> mean_off, c10::optional<at::Tensor> part_in) {
+static std::vector<at::Tensor> bn_forward_impl(at::Tensor x, c10::optional<at::Tensor> gamma,
+                                               c10::optional<at::Tensor> beta, c10::optional<at::Tensor> moving_mean,
+                                               c10::optional<at::Tensor> moving_var, double momentum, double eps,
+                                               bool relu, c10::optional<at::Tensor> residual,
+                                               c10::optional<at::Tensor> mean_off, c10::optional<at::Tensor> part_in,
+                                               bool apply) {
   bn_check(x);
   const int64_t C = x.size(-1), M = x.numel() / C;
   const void* res = nullptr;
@@ -126,6 +128,7 @@ std::vector<at::Tensor> bn_forward_train(at::Tensor x, c10::optional<at::Tensor>
   tdl::bn_forward_stats(x.data_ptr(), bn_dtype(x), M, (int)C, part.data_ptr<float>(), opt_f32(gamma), opt_f32(beta),
                         opt_f32(mean_off), sp, sp + C, sp + 2 * C, sp + 3 * C, mm, mv, (float)momentum, (float)eps, s,
                         given);
+  if (!apply) return {st};
   auto y = fresh(x.sizes(), x.options());
   tdl::bn_apply(x.data_ptr(), res, y.data_ptr(), bn_dtype(x), M, (int)C, sp + 2 * C, sp + 3 * C, relu ? 1 : 0, s);
   return {y, st};
@@ -187,9 +190,35 @@ std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, c10::optional<a
   if (mode == 2) return {dx, g, b, dz};
   return {dx, g, b};
 }
-// max pool NHWC: returns (y, argmax bytes); pads = (top, left), output size given
+std::vector<at::Tensor> bn_forward_train(at::Tensor x, c10::optional<at::Tensor> gamma, c10::optional<at::Tensor> beta,
+                                         c10::optional<at::Tensor> moving_mean, c10::optional<at::Tensor> moving_var,
+                                         double momentum, double eps, bool relu, c10::optional<at::Tensor> residual,
+                                         c10::optional<at::Tensor> mean_off, c10::optional<at::Tensor> part_in) {
+  return bn_forward_impl(x, gamma, beta, moving_mean, moving_var, momentum, eps, relu, residual, mean_off, part_in,
+                         true);
+}
+
+// the batch statistics only ([4][C]: mean, invstd, scale, shift; moving statistics updated): the
+// normalisation is applied by the consumer (maxpool_fwd(bn_stats=...))
+at::Tensor bn_stats_train(at::Tensor x, c10::optional<at::Tensor> gamma, c10::optional<at::Tensor> beta,
+                          c10::optional<at::Tensor> moving_mean, c10::optional<at::Tensor> moving_var, double momentum,
+                          double eps, c10::optional<at::Tensor> mean_off, c10::optional<at::Tensor> part_in) {
+  return bn_forward_impl(x, gamma, beta, moving_mean, moving_var, momentum, eps, false, c10::nullopt, mean_off,
+                         part_in, false)[0];
+}
+
+static const float* bn_ss_of(const c10::optional<at::Tensor>& st, int64_t C) {
+  if (!st.has_value() || !st->defined()) return nullptr;
+  TORCH_CHECK(st->is_cuda() && st->is_contiguous() && st->scalar_type() == at::kFloat && st->numel() == 4 * C,
+              "bn_stats must be the f32 [4][C] statistics of the batch norm");
+  return st->data_ptr<float>() + 2 * C;  // scale[C], shift[C]
+}
+
+// max pool NHWC: returns (y, argmax bytes); pads = (top, left), output size given; bn_stats: x is a
+// batch norm's input and the pool runs over relu(bn(x)) (the BN -> ReLU pass skipped)
 std::vector<at::Tensor> maxpool_fwd(at::Tensor x, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t pt,
-                                    int64_t pl, int64_t OH, int64_t OW, bool pad_zero) {
+                                    int64_t pl, int64_t OH, int64_t OW, bool pad_zero,
+                                    c10::optional<at::Tensor> bn_stats) {
   bn_check(x);
   TORCH_CHECK(x.dim() == 4, "maxpool: NHWC input expected");
   TORCH_CHECK(kh * kw < 255 && kh > 0 && kw > 0 && sh > 0 && sw > 0 && OH > 0 && OW > 0, "maxpool: bad geometry");
@@ -198,7 +227,7 @@ std::vector<at::Tensor> maxpool_fwd(at::Tensor x, int64_t kh, int64_t kw, int64_
   auto y = fresh({x.size(0), OH, OW, x.size(3)}, x.options());
   auto arg = fresh({x.size(0), OH, OW, x.size(3)}, x.options().dtype(at::kByte));
   tdl::maxpool_forward(x.data_ptr(), y.data_ptr(), arg.data_ptr<uint8_t>(), bn_dtype(x) == tdl::BnDType::kBF16, g,
-                       cur_stream());
+                       cur_stream(), bn_ss_of(bn_stats, x.size(3)));
   return {y, arg};
 }
 
@@ -214,6 +243,30 @@ at::Tensor maxpool_bwd(at::Tensor dy, at::Tensor arg, std::vector<int64_t> in_sh
   tdl::maxpool_backward(dy.data_ptr(), arg.data_ptr<uint8_t>(), dx.data_ptr(), bn_dtype(dy) == tdl::BnDType::kBF16, g,
                         cur_stream());
   return dx;
+}
+
+// backward of maxpool_fwd(bn_stats=...): (dz, part) -- dz the BN -> ReLU group's masked input gradient,
+// part [P + ceil(P/64)][2][C] its BN backward sums (bn_backward(part=...))
+std::vector<at::Tensor> maxpool_bwd_bn(at::Tensor dy, at::Tensor arg, std::vector<int64_t> in_shape, int64_t kh,
+                                       int64_t kw, int64_t sh, int64_t sw, int64_t pt, int64_t pl, at::Tensor bn_x,
+                                       at::Tensor bn_stats) {
+  bn_check(dy);
+  bn_check(bn_x);
+  TORCH_CHECK(dy.dim() == 4 && arg.sizes() == dy.sizes() && arg.scalar_type() == at::kByte && arg.is_contiguous(),
+              "maxpool backward: dy / argmax mismatch");
+  TORCH_CHECK(in_shape.size() == 4 && in_shape[3] == dy.size(3) && in_shape[0] == dy.size(0), "maxpool: bad shape");
+  TORCH_CHECK(bn_x.sizes() == at::IntArrayRef(in_shape) && bn_x.scalar_type() == dy.scalar_type(),
+              "maxpool backward: bn_x must be the pool input's batch-norm input");
+  const int64_t C = in_shape[3];
+  TORCH_CHECK(C <= 2048 && ((C / 8) & (C / 8 - 1)) == 0, "maxpool backward (BN-fused): C / 8 must be a power of two");
+  tdl::PoolGeom g{(int)in_shape[0], (int)in_shape[1], (int)in_shape[2], (int)in_shape[3], (int)dy.size(1),
+                  (int)dy.size(2), (int)kh, (int)kw, (int)sh, (int)sw, (int)pt, (int)pl, 0};
+  auto dx = fresh(in_shape, dy.options());
+  const int64_t P = tdl::maxpool_backward_blocks(g);
+  auto part = fresh({P + (P + 63) / 64, 2, C}, dy.options().dtype(at::kFloat));
+  tdl::maxpool_backward(dy.data_ptr(), arg.data_ptr<uint8_t>(), dx.data_ptr(), bn_dtype(dy) == tdl::BnDType::kBF16, g,
+                        cur_stream(), bn_x.data_ptr(), bn_ss_of(bn_stats, C), part.data_ptr<float>());
+  return {dx, part};
 }
 
 tdl::ConvGeom conv_geom(const at::Tensor& x, int64_t oh, int64_t ow, int64_t k, int64_t kh, int64_t kw, int64_t sh,
@@ -663,7 +716,14 @@ void register_ops(pybind11::module& m) {
         pybind11::arg("momentum"), pybind11::arg("eps"), pybind11::arg("relu") = false,
         pybind11::arg("residual") = pybind11::none(), pybind11::arg("mean_off") = pybind11::none(),
         pybind11::arg("part") = pybind11::none());
-  m.def("maxpool_fwd", &maxpool_fwd, "NHWC max pool forward (+argmax)");
+  m.def("maxpool_fwd", &maxpool_fwd, "NHWC max pool forward (+argmax)", pybind11::arg("x"), pybind11::arg("kh"),
+        pybind11::arg("kw"), pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("pt"), pybind11::arg("pl"),
+        pybind11::arg("OH"), pybind11::arg("OW"), pybind11::arg("pad_zero"), pybind11::arg("bn_stats") = pybind11::none());
+  m.def("maxpool_bwd_bn", &maxpool_bwd_bn, "NHWC max pool backward fused with the BN -> ReLU group's mask and sums");
+  m.def("bn_stats_train", &bn_stats_train, "NHWC batch-norm training statistics only ([4][C])", pybind11::arg("x"),
+        pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("moving_mean"), pybind11::arg("moving_var"),
+        pybind11::arg("momentum"), pybind11::arg("eps"), pybind11::arg("mean_off") = pybind11::none(),
+        pybind11::arg("part") = pybind11::none());
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC max pool backward (gather form)");
   m.def("bn_backward", &bn_backward, "NHWC batch-norm training backward", pybind11::arg("dy"), pybind11::arg("x"),
         pybind11::arg("y"), pybind11::arg("gamma"), pybind11::arg("stats"), pybind11::arg("mode"),

@@ -14,6 +14,9 @@ list; the plan rewrites, at execution time only (the layer graph, variables, che
 * ``BatchNormalization -> Add(other) -> ReLU``: the ResNet block tail, one fused pass that also
   produces the residual's gradient.
 * ``ZeroPadding2D -> MaxPooling2D('valid')``: one pooling pass with implicit zero padding.
+* ``BatchNormalization -> ReLU -> [ZeroPadding2D ->] MaxPooling2D('valid')`` (the ResNet stem): the pool
+  runs on the BN input with the normalisation in its kernel and reduces the BN backward sums in its
+  backward pass; the normalised tensor is never written.
 * ``ZeroPadding2D -> Conv2D`` with <= 4 input channels, 'valid', column stride 2 (the ResNet stem):
   the padding goes into the stem kernel's packed image (ops/conv.py ``stem_conv2d_nhwc``).
 * a tensor read by a Conv2D and by one other node (the ResNet block input: the shortcut / the
@@ -35,7 +38,8 @@ from . import layers as L
 
 
 class Group:
-    __slots__ = ("bn_node", "relu", "residual", "conv_layer", "out", "last", "conv_reader", "add_node", "res_bn")
+    __slots__ = ("bn_node", "relu", "residual", "conv_layer", "out", "last", "conv_reader", "add_node", "res_bn",
+                 "pool")
 
     def __init__(self, bn_node, relu, residual, conv_layer, out, last, conv_reader=False, add_node=None):
         self.bn_node, self.relu, self.residual, self.conv_layer, self.out, self.last = (
@@ -48,6 +52,10 @@ class Group:
         # is read by nothing else: its output gradient is this group's dz, so the conv epilogue that
         # reduces this group's backward sums can reduce that BN's as well
         self.res_bn = None
+        # (MaxPooling2D layer, pads, pad_zero): a BN -> ReLU -> [ZeroPadding2D ->] MaxPooling2D chain whose
+        # pool is the group output's only reader -- the pool runs on the BN input with the normalisation
+        # in its kernel (ops/pooling.py bn_relu_max_pool) and the normalised tensor is never written
+        self.pool = None
 
 
 class Plan:
@@ -146,9 +154,37 @@ def plan(nodes: List[L.Node], outputs) -> Plan:
         if pg is not None and not pg.relu and pg.residual is None and pg.last is pg.bn_node and \
                 only_consumer(g.residual) is g.add_node:
             g.res_bn = pg
+    if os.environ.get("TDL_FUSE_BN_POOL", "1") == "1":
+        _plan_bn_pool(p, only_consumer)
     if os.environ.get("TDL_FUSE_GRAD_SUM", "1") == "1":
         _plan_grad_sums(p, nodes, consumers, outs)
     return p
+
+
+def _plan_bn_pool(p: Plan, only_consumer):
+    """BN -> ReLU groups whose output's only reader is a 'valid' MaxPooling2D, directly or through a
+    ZeroPadding2D already folded into it (the ResNet stem): the pool joins the group."""
+    for key, g in list(p.groups.items()):
+        if not g.relu or g.residual is not None or g.conv_reader:
+            continue
+        c = only_consumer(g.out)
+        pool_n, pads, pad_zero = None, ((0, 0), (0, 0)), False
+        if c is not None and isinstance(c.layer, L.ZeroPadding2D):
+            c2 = only_consumer(_single_tensor(c.outputs))
+            pp = p.pool_pad.get(id(c2)) if c2 is not None else None
+            if pp is not None and isinstance(c2.layer, L.MaxPooling2D) and pp[0] is g.out:
+                pool_n, pads, pad_zero = c2, pp[1], True
+        elif c is not None and isinstance(c.layer, L.MaxPooling2D) and c.layer.padding == "valid" and c.inputs is g.out:
+            pool_n = c
+        if pool_n is None or _single_tensor(pool_n.outputs) is None:
+            continue
+        p.pool_pad.pop(id(pool_n), None)
+        if g.last is not g.bn_node:
+            p.skip.add(id(g.last))
+        del p.groups[key]
+        g.pool = (pool_n.layer, pads, pad_zero)
+        g.last, g.out = pool_n, _single_tensor(pool_n.outputs)
+        p.groups[id(pool_n)] = g
 
 
 def _plan_grad_sums(p: Plan, nodes, consumers, outs):
@@ -203,6 +239,24 @@ def run_group(g: Group, vals, training, taps=None, boxes=None):
         # the folded bias's gradient is exactly zero: with a gradient slab bound, leave its (zeroed)
         # slab entries alone instead of accumulating zeros
         cb = cbv.value.detach() if cbv.grad_target() is not None else cbv.value
+    if g.pool is not None:
+        from ..ops import pooling as _pool
+
+        pool_layer, pads, pad_zero = g.pool
+        if training and _pool.bn_pool_supported(x):
+            y = _pool.bn_relu_max_pool(x, bn.gamma.value if bn.gamma is not None else None,
+                                       bn.beta.value if bn.beta is not None else None, bn.moving_mean.value,
+                                       bn.moving_variance.value, bn.momentum, bn.epsilon, pool_layer.pool_size,
+                                       pool_layer.strides, pads, pad_zero, conv_bias=cb,
+                                       grad_out=bn._grad_targets(), part=getattr(x, "_tdl_bn_part", None))
+        else:
+            y = batch_norm_train(x, bn.gamma.value if bn.gamma is not None else None,
+                                 bn.beta.value if bn.beta is not None else None, bn.moving_mean.value,
+                                 bn.moving_variance.value, bn.momentum, bn.epsilon, relu=True, conv_bias=cb,
+                                 grad_out=bn._grad_targets(), part=getattr(x, "_tdl_bn_part", None))
+            y = pool_layer(y, training=training, **({"_zero_pad": pads} if pad_zero else {}))
+        vals[id(g.out)] = y
+        return
     st = [] if (g.relu and r is None) else None
     y = batch_norm_train(x, bn.gamma.value if bn.gamma is not None else None,
                          bn.beta.value if bn.beta is not None else None, bn.moving_mean.value,

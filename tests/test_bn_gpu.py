@@ -242,3 +242,83 @@ def test_maxpool_3x3s2_unrolled_matches_generic_bitwise(dtype, geo, hw):
         C.maxpool_force_generic(True)
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_bn_relu_maxpool_fused_kernels_match_unfused(dtype):
+    """maxpool_fwd(bn_stats=st) over the BN input == maxpool over the BN -> ReLU pass's output (values
+    and argmax, bitwise); maxpool_bwd_bn's dz == the plain pool backward masked by the recomputed ReLU
+    condition (bitwise), and its partial sums add up to sum(dz), sum(dz * x)."""
+    from tensorflow_distributed_learning_amd.ops import hip
+
+    C = hip()
+    torch.manual_seed(5)
+    N, H, Ch = 3, 22, 64
+    x = (torch.randn(N, H, H, Ch, device="cuda:0") * 2 + 0.2).to(dtype)
+    g, b = torch.rand(Ch, device="cuda:0") + 0.5, torch.randn(Ch, device="cuda:0")
+    mm, mv = torch.zeros(Ch, device="cuda:0"), torch.ones(Ch, device="cuda:0")
+    y, st = C.bn_forward_train(x, g, b, mm, mv, 0.9, 1e-3, True, None, None)
+    st2 = C.bn_stats_train(x, g, b, mm.clone(), mv.clone(), 0.9, 1e-3)
+    assert torch.equal(st, st2)
+    OH = (H + 2 - 3) // 2 + 1
+    p0, a0 = C.maxpool_fwd(y, 3, 3, 2, 2, 1, 1, OH, OH, True)
+    p1, a1 = C.maxpool_fwd(x, 3, 3, 2, 2, 1, 1, OH, OH, True, st)
+    assert torch.equal(p0, p1) and torch.equal(a0, a1)
+    dy = torch.randn(N, OH, OH, Ch, device="cuda:0").to(dtype)
+    d0 = C.maxpool_bwd(dy, a0, list(x.shape), 3, 3, 2, 2, 1, 1)
+    dz, part = C.maxpool_bwd_bn(dy, a1, list(x.shape), 3, 3, 2, 2, 1, 1, x, st)
+    mask = (x.double() * st[2].double() + st[3].double()) > 0  # the sign of the kernel's f32 fma
+    assert torch.equal(dz, torch.where(mask, d0, torch.zeros_like(d0)))
+    R = part.shape[0]
+    P = next(q for q in range(R + 1) if q + (q + 63) // 64 == R)
+    got = part[:P].double().sum(0)
+    ref = torch.stack([dz.double().reshape(-1, Ch).sum(0), (dz.double() * x.double()).reshape(-1, Ch).sum(0)])
+    torch.testing.assert_close(got, ref, atol=1e-3, rtol=1e-4)
+
+
+def test_stem_bn_relu_pool_fusion_trains_like_unfused():
+    """The stem's BN -> ReLU -> ZeroPadding2D -> MaxPooling2D joined into one group (keras/fusion.py)
+    trains like the unfused graph (TDL_FUSE_BN_POOL=0): losses and weights after two SGD steps."""
+    import os
+
+    import numpy as np
+    import tensorflow_distributed_learning_amd as tdl
+
+    L = tdl.keras.layers
+
+    def run(fuse):
+        os.environ["TDL_FUSE_BN_POOL"] = "1" if fuse else "0"
+        try:
+            tdl.keras.backend.clear_session()
+            tdl.keras.mixed_precision.set_global_policy("mixed_bfloat16")
+            tdl.keras.utils.set_random_seed(3)
+            inp = L.Input(shape=(32, 32, 3))
+            x = L.ZeroPadding2D(3)(inp)
+            x = L.Conv2D(64, 7, strides=2)(x)
+            x = L.BatchNormalization()(x)
+            x = L.Activation("relu")(x)
+            x = L.ZeroPadding2D(1)(x)
+            x = L.MaxPooling2D(3, strides=2)(x)
+            x = L.Conv2D(64, 1)(x)
+            x = L.GlobalAveragePooling2D()(x)
+            with tdl.distribute.MirroredStrategy(devices=["/gpu:0"]).scope():
+                m = tdl.keras.Model(inp, L.Dense(10)(x))
+                m.compile(loss=tdl.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+                          optimizer=tdl.keras.optimizers.SGD(learning_rate=0.05))
+            gen = torch.Generator().manual_seed(0)
+            ds = tdl.data.Dataset.from_tensor_slices((torch.rand(64, 32, 32, 3, generator=gen),
+                                                      torch.randint(0, 10, (64,), generator=gen))).batch(32).repeat()
+            h = m.fit(ds, epochs=1, steps_per_epoch=2, verbose=0)
+            fused = any(gr.pool is not None for gr in m._fusion().groups.values())
+            return m.get_weights(), h.history["loss"], fused
+        finally:
+            os.environ.pop("TDL_FUSE_BN_POOL", None)
+            tdl.keras.mixed_precision.set_global_policy("float32")
+
+    wf, lf, ff = run(True)
+    wu, lu, fu = run(False)
+    assert ff and not fu
+    np.testing.assert_allclose(lf, lu, rtol=1e-2)
+    for a, b in zip(wf, wu):
+        scale = max(float(np.abs(b).max()), 1e-3)
+        np.testing.assert_allclose(a, b, atol=2e-2 * scale, rtol=2e-2)
