@@ -209,8 +209,12 @@ def _pick(key, hip_fn, ref_fn, saved_bytes: int = 0) -> bool:
 def _pick_wgrad(key, C, x, dy, kh, kw, stride, pad, ref_fn):
     """Weight gradient: time the cost model's first ``TDL_WGRAD_CANDIDATES`` (default 6) tile/slice
     plans and MIOpen on the first eager call of a shape; returns the winning plan
-    ``[wmw, wnw, nsplit]`` or None (MIOpen)."""
+    ``[wmw, wnw, nsplit]`` or None (MIOpen).  TDL_CONV=hip: the cost model's first plan, cached under
+    its own key -- a plan an earlier auto-mode call timed for the same shape (another split-K order)
+    must not leak into a forced-hip run, nor the reverse."""
     m = mode()
+    if m == "hip":
+        key = ("hip",) + tuple(key)
     if key in _choice:
         return _choice[key]
     n = 1 if m == "hip" or torch.cuda.is_current_stream_capturing() else int(os.environ.get("TDL_WGRAD_CANDIDATES", 6))
@@ -240,8 +244,10 @@ def _pick_wgrad(key, C, x, dy, kh, kw, stride, pad, ref_fn):
 
 
 def choices() -> dict:
-    """The autotuner's decisions so far: {(direction, shape key): 'hip' | 'miopen'}."""
-    return {k: ("hip" if (v is True or isinstance(v, list)) else "miopen") for k, v in _choice.items()}
+    """The autotuner's decisions so far: {(direction, shape key): 'hip' | 'miopen'} (forced-hip
+    weight-gradient plans, cached under ("hip", ...) keys, are not decisions)."""
+    return {k: ("hip" if (v is True or isinstance(v, list)) else "miopen") for k, v in _choice.items()
+            if k[0] != "hip"}
 
 
 def _ref_fwd(x, w_oihw, stride, pad):
