@@ -63,11 +63,14 @@ struct WgradPlan {
   int wmw, wnw;        // workgroup tile: (64 wmw) output channels x (64 wnw) (kh, kw, c) columns
   int chunk, nsplit;   // pixels per slice, slices
   long long ws_elems;  // f32 partial slab elements (nsplit x KH*KW*C x K)
+  // kernel of the 2x2-wave tile: 0 register-staged (k_conv_wgrad), 1 single-stage LDS-DMA at 4 waves
+  // per SIMD (k_conv_wgrad_glds<2, 2, 1>); 8-wave tiles are always the 3-stage LDS-DMA ring
+  int kind;
 };
 bool conv_wgrad_supported(const ConvGeom& g);
 // the model's best `max_plans` candidates, best first
 std::vector<WgradPlan> conv_wgrad_plans(const ConvGeom& g, int max_plans);
-WgradPlan conv_wgrad_make_plan(const ConvGeom& g, int wmw, int wnw, int nsplit);
+WgradPlan conv_wgrad_make_plan(const ConvGeom& g, int wmw, int wnw, int nsplit, int kind = 0);
 // dW (HWIO [KH][KW][C][K]) from x[N,H,W,C] and dy[N,OH,OW,K]: into dw_bf16, or (dw_bf16 == nullptr)
 // into the f32 dw_f32 (added to it when accumulate).  ws: plan.ws_elems f32.
 void conv_wgrad_bf16(const void* x, const void* dy, float* ws, const WgradPlan& p, void* dw_bf16, float* dw_f32,

@@ -251,14 +251,16 @@ __device__ __forceinline__ void wg_wait_vmcnt_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
-constexpr int kWgStages = 3;
-
-template <int WMW, int WNW>
-__global__ __launch_bounds__(512, 1) void k_conv_wgrad_glds(Wgrad a) {
+// STAGES 1 (wgrad "dma1"): 4-wave tiles, one LDS stage, no prefetch, 4 waves per SIMD -- the conv
+// dma1 schedule (four resident workgroups per CU hide each other's DMA latency).
+template <int WMW, int WNW, int STAGES = 3>
+__global__ __launch_bounds__(64 * WMW * WNW, STAGES == 1 ? 4 : 1) void k_conv_wgrad_glds(Wgrad a) {
   constexpr int SA = WMW, SBn = WNW, NSUB = SA + SBn;
   constexpr int STAGE = NSUB * SUB;
-  static_assert(WMW * WNW == 8, "8 waves");
-  __shared__ __attribute__((aligned(16))) uint16_t lds[kWgStages * STAGE];
+  constexpr int NWV = WMW * WNW;
+  constexpr int RPW = 8 / NWV;  // 8-row LDS-DMA pieces per sub-image per wave
+  static_assert((NWV == 8 && STAGES == 3) || (WMW == 2 && WNW == 2 && STAGES == 1), "8 waves ring / 2x2 single stage");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[STAGES * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -277,8 +279,10 @@ __global__ __launch_bounds__(512, 1) void k_conv_wgrad_glds(Wgrad a) {
 
   const auto dy_rsrc = buf_rsrc(a.dy, (unsigned)((long long)a.M * a.K * 2));
   const auto x_rsrc = buf_rsrc(a.x, (unsigned)((long long)a.N * a.H * a.W * a.C * 2));
-  const int row = wave * 8 + (lane >> 3);                   // this lane's pixel row of every sub-image
-  const int chunk8 = ((lane & 7) ^ fswz(row)) * 8;         // source-swizzled chunk (elements)
+  // this lane's pixel rows of every sub-image: (r * NWV + wave) * 8 + lane / 8; fswz depends on row bits
+  // 1 and 3 only, which r * NWV * 8 does not change: one source-swizzled chunk for all of them
+  const int row = wave * 8 + (lane >> 3);
+  const int chunk8 = ((lane & 7) ^ fswz(row)) * 8;
   int b_kh[SBn], b_kw[SBn], b_off[SBn];
   bool b_live[SBn];
 #pragma unroll
@@ -291,9 +295,11 @@ __global__ __launch_bounds__(512, 1) void k_conv_wgrad_glds(Wgrad a) {
     b_off[j] = (b_kh[j] * a.W + b_kw[j]) * a.C + c0 + chunk8;
   }
   auto issue = [&](int st, int stage) {
-    const int m = mbeg + st * RB + row;
+#pragma unroll
+   for (int r = 0; r < RPW; ++r) {
+    const int m = mbeg + st * RB + row + r * NWV * 8;
     const bool live = m < mend;
-    uint16_t* base = lds + stage * STAGE + wave * 8 * 64;
+    uint16_t* base = lds + stage * STAGE + (wave + r * NWV) * 8 * 64;
 #pragma unroll
     for (int j = 0; j < SA; ++j) {
       const int vo = live ? (int)(((long long)m * a.K + k0 + 64 * j + chunk8) * 2) : (int)0x80000000;
@@ -319,6 +325,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_wgrad_glds(Wgrad a) {
         lds_dma16(x_rsrc, base + (SA + j) * SUB, vo, 0);
       }
     }
+   }
   };
 
   const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
@@ -333,15 +340,21 @@ __global__ __launch_bounds__(512, 1) void k_conv_wgrad_glds(Wgrad a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
 
-  if (nst > 0) issue(0, 0);
-  if (nst > 1) issue(1, 1);
+  if (STAGES == 3 && nst > 0) issue(0, 0);
+  if (STAGES == 3 && nst > 1) issue(1, 1);
   int stg = 0;
   for (int st = 0; st < nst; ++st) {
-    if (st + 1 < nst)
-      wg_wait_vmcnt_barrier<NSUB>();
-    else
+    if constexpr (STAGES == 1) {
+      if (st) __syncthreads();  // every wave done reading stage st - 1
+      issue(st, 0);
       wg_wait_vmcnt_barrier<0>();
-    if (st + 2 < nst) issue(st + 2, stg == 0 ? 2 : stg - 1);
+    } else {
+      if (st + 1 < nst)
+        wg_wait_vmcnt_barrier<NSUB>();
+      else
+        wg_wait_vmcnt_barrier<0>();
+      if (st + 2 < nst) issue(st + 2, stg == 0 ? 2 : stg - 1);
+    }
     const uint16_t* base = lds + stg * STAGE;
 #pragma unroll
     for (int kk = 0; kk < RB; kk += 32) {
@@ -365,7 +378,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_wgrad_glds(Wgrad a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
-    stg = stg == 2 ? 0 : stg + 1;
+    if constexpr (STAGES == 3) stg = stg == 2 ? 0 : stg + 1;
   }
 
   if (tc0 + 64 * wn >= a.TC) return;
@@ -437,7 +450,14 @@ void launch_wgrad_t(const Wgrad& a, hipStream_t s) {
 }
 
 template <int WMW, int WNW>
-void launch_wgrad(const Wgrad& a, hipStream_t s) {
+void launch_wgrad(const Wgrad& a, int kind, hipStream_t s) {
+  if constexpr (WMW == 2 && WNW == 2) {
+    if (kind == 1) {
+      const int tiles = (a.K / (64 * WMW)) * ((a.TC + 64 * WNW - 1) / (64 * WNW));
+      hipLaunchKernelGGL((k_conv_wgrad_glds<WMW, WNW, 1>), dim3(tiles * a.nsplit), dim3(256), 0, s, a);
+      return;
+    }
+  }
   if (g_wgrad_single)
     launch_wgrad_t<WMW, WNW, true>(a, s);
   else
@@ -461,10 +481,11 @@ bool conv_wgrad_supported(const ConvGeom& g) {
   return conv_bf16_supported(g) && (long long)g.N * g.OH * g.OW < (1ll << 24);
 }
 
-WgradPlan conv_wgrad_make_plan(const ConvGeom& g, int wmw, int wnw, int nsplit) {
+WgradPlan conv_wgrad_make_plan(const ConvGeom& g, int wmw, int wnw, int nsplit, int kind) {
   WgradPlan p{};
   p.wmw = wmw;
   p.wnw = wnw;
+  p.kind = wmw == 2 && wnw == 2 ? kind : 0;
   const long long M = (long long)g.N * g.OH * g.OW;
   const int stages = (int)((M + RB - 1) / RB);
   const int S = std::max(1, std::min(nsplit, stages));
@@ -488,22 +509,27 @@ std::vector<WgradPlan> conv_wgrad_plans(const ConvGeom& g, int max_plans) {
   const long long M = (long long)g.N * g.OH * g.OW;
   const int TC = g.KH * g.KW * g.C;
   const int stages = (int)((M + RB - 1) / RB);
-  for (const auto& tl : kTiles) {
-    const int wmw = tl[0], wnw = tl[1], bmk = 64 * wmw, btc = 64 * wnw;
+  for (int ti = 0; ti < (int)(sizeof(kTiles) / sizeof(kTiles[0])) * 2; ++ti) {
+    const int wmw = kTiles[ti >> 1][0], wnw = kTiles[ti >> 1][1], bmk = 64 * wmw, btc = 64 * wnw;
+    const int kind = ti & 1;  // 1: the single-stage LDS-DMA kernel (4-wave tiles only)
+    if (kind && (wmw != 2 || wnw != 2)) continue;  // 1x4 / 4x1 spill at 128 VGPRs
     if (g.K % bmk) continue;
     const int ntc = (TC + btc - 1) / btc;
     if ((ntc * btc - TC) * 4 > ntc * btc) continue;  // > 25 % of the tc columns padding
     const int tiles = (g.K / bmk) * ntc;
     const bool ring = wmw * wnw == 8;  // LDS-DMA ring kernel: one 144-KiB workgroup per CU
-    const bool single = !ring && g_wgrad_single;
+    const bool dma1 = kind == 1;
+    const bool single = !ring && (g_wgrad_single || dma1);
     const int lds_kb = (ring ? 3 : (single ? 1 : 2)) * (wmw + wnw) * 8;
-    // <= 2 waves per SIMD (3 for the single-stage v1 kernel)
-    const int per_cu = std::max(1, std::min(160 / lds_kb, (single ? 12 : 8) / (wmw * wnw)));
+    // <= 2 waves per SIMD (3 for the single-stage v1 kernel, 4 for the single-stage DMA one)
+    const int per_cu = std::max(1, std::min(160 / lds_kb, (dma1 ? 16 : single ? 12 : 8) / (wmw * wnw)));
     const double macs = (double)M * tiles * bmk * btc;
-    // measured (profiles/conv_v2_r4.txt): the ring kernel wins on 3x3 and strided 1x1 shapes and
-    // loses on stride-1 1x1 ones (the v1 2x2-wave tile), where its rate is scaled down
+    // measured (profiles/conv_v2_r4.txt, wgrad_dma1_r4.txt): the LDS-DMA kernels win on 3x3 and
+    // strided 1x1 shapes (the single-stage one most on 3x3) and lose on stride-1 1x1 ones (the v1
+    // 2x2-wave tile), where their rates are scaled down
     const bool direct = g.KH == 1 && g.KW == 1 && g.SH == 1 && g.SW == 1 && g.PT == 0 && g.PL == 0;
-    const double t_mma = macs * 2.0 / (ring ? (direct ? 0.85e15 : 1.3e15) : 1.0e15) * 1e6;
+    const double rate = ring ? (direct ? 0.85e15 : 1.3e15) : dma1 ? (direct ? 0.85e15 : 1.4e15) : 1.0e15;
+    const double t_mma = macs * 2.0 / rate * 1e6;
     // dy re-read per tc tile, x per k tile (taps of one pixel neighbourhood hit L2: count once per tile)
     const double bytes = (double)M * 2.0 * ((double)g.K * ntc + (double)std::min(TC, btc) * ntc * (g.K / bmk));
     const double t_mem = bytes / 5.0e12 * 1e6;
@@ -518,28 +544,34 @@ std::vector<WgradPlan> conv_wgrad_plans(const ConvGeom& g, int max_plans) {
       double t = std::max(t_mma, t_mem) / std::max(1e-3, fill * eff);
       t += rounds * 1.0;  // per-round prologue / epilogue
       if (Sr > 1) t += (double)Sr * TC * g.K * 8.0 / 4.0e12 * 1e6 + 2.0;
-      c.push_back({t, conv_wgrad_make_plan(g, wmw, wnw, Sr)});
+      c.push_back({t, conv_wgrad_make_plan(g, wmw, wnw, Sr, kind)});
     }
   }
   std::sort(c.begin(), c.end(), [](const Cand& x, const Cand& y) { return x.t < y.t; });
-  // best first, but both kernel families (v1 register-staged, 8-wave LDS-DMA ring) among the first
-  // candidates: the model ranks them only roughly, the autotuner's timing decides
-  std::vector<WgradPlan> fam[2];
+  // best first, but every kernel family (v1 register-staged, single-stage LDS-DMA, 8-wave LDS-DMA
+  // ring) among the first candidates, round-robin in the order of each family's best plan: the model
+  // ranks them only roughly, the autotuner's timing decides
+  std::vector<WgradPlan> fam[3];
+  int order[3], nf = 0;
   for (const auto& e : c) {
-    auto& f = fam[e.p.wmw * e.p.wnw == 8 ? 1 : 0];
+    const int fi = e.p.wmw * e.p.wnw == 8 ? 2 : e.p.kind;
+    auto& f = fam[fi];
+    if (f.empty()) order[nf++] = fi;
     bool dup = false;
     for (const auto& o : f) dup |= (o.wmw == e.p.wmw && o.wnw == e.p.wnw && o.nsplit == e.p.nsplit);
     if (!dup) f.push_back(e.p);
   }
   std::vector<WgradPlan> out;
-  size_t i0 = 0, i1 = 0;
-  const bool ring_first = !c.empty() && c.front().p.wmw * c.front().p.wnw == 8;
-  while ((int)out.size() < max_plans && (i0 < fam[0].size() || i1 < fam[1].size())) {
-    const bool take_ring = (out.size() % 2 == 0) == ring_first;
-    if ((take_ring && i1 < fam[1].size()) || i0 >= fam[0].size())
-      out.push_back(fam[1][i1++]);
-    else
-      out.push_back(fam[0][i0++]);
+  size_t idx[3] = {0, 0, 0};
+  for (bool any = true; any && (int)out.size() < max_plans;) {
+    any = false;
+    for (int j = 0; j < nf && (int)out.size() < max_plans; ++j) {
+      const int fi = order[j];
+      if (idx[fi] < fam[fi].size()) {
+        out.push_back(fam[fi][idx[fi]++]);
+        any = true;
+      }
+    }
   }
   return out;
 }
@@ -554,12 +586,12 @@ void conv_wgrad_bf16(const void* x, const void* dy, float* ws, const WgradPlan& 
           1.0f / (float)g.OW, 1.0f / (float)g.OH};
   const int t = p.wmw * 8 + p.wnw;
   switch (t) {
-    case 9: launch_wgrad<1, 1>(a, s); break;
-    case 10: launch_wgrad<1, 2>(a, s); break;
-    case 17: launch_wgrad<2, 1>(a, s); break;
-    case 18: launch_wgrad<2, 2>(a, s); break;
-    case 12: launch_wgrad<1, 4>(a, s); break;
-    case 33: launch_wgrad<4, 1>(a, s); break;
+    case 9: launch_wgrad<1, 1>(a, p.kind, s); break;
+    case 10: launch_wgrad<1, 2>(a, p.kind, s); break;
+    case 17: launch_wgrad<2, 1>(a, p.kind, s); break;
+    case 18: launch_wgrad<2, 2>(a, p.kind, s); break;
+    case 12: launch_wgrad<1, 4>(a, p.kind, s); break;
+    case 33: launch_wgrad<4, 1>(a, p.kind, s); break;
     case 20: launch_wgrad_glds<2, 4>(a, s); break;
     case 34: launch_wgrad_glds<4, 2>(a, s); break;
     default: return;

@@ -440,7 +440,7 @@ at::Tensor conv_wgrad(at::Tensor x, at::Tensor dy, int64_t kh, int64_t kw, int64
   TORCH_CHECK(dy.dim() == 4 && dy.size(0) == x.size(0), "conv_wgrad: dy must be NHWC [N,OH,OW,K]");
   auto g = conv_geom(x, dy.size(1), dy.size(2), dy.size(3), kh, kw, sh, sw, pt, pl);
   TORCH_CHECK(tdl::conv_wgrad_supported(g), "conv_wgrad: N*OH*OW must be < 2^24");
-  TORCH_CHECK(plan.empty() || plan.size() == 3, "conv_wgrad: plan = [wmw, wnw, nsplit]");
+  TORCH_CHECK(plan.empty() || plan.size() == 3 || plan.size() == 4, "conv_wgrad: plan = [wmw, wnw, nsplit(, kind)]");
   if (!plan.empty() && plan[0] == 0) {  // [0, 0, 0]: the row kernel of 3x3 / C = 64 convs (wgrad3x3.hip)
     TORCH_CHECK(tdl::conv_wgrad3x3_c64_supported(g), "conv_wgrad: the 3x3 row kernel does not take this shape");
     auto ws = fresh({tdl::conv_wgrad3x3_c64_ws_elems(g)}, x.options().dtype(at::kFloat));
@@ -465,9 +465,10 @@ at::Tensor conv_wgrad(at::Tensor x, at::Tensor dy, int64_t kh, int64_t kw, int64
     const int wmw = (int)plan[0], wnw = (int)plan[1];
     TORCH_CHECK((wmw == 1 || wmw == 2 || wmw == 4) && (wnw == 1 || wnw == 2 || wnw == 4) &&
                     (wmw * wnw <= 4 || (wmw * wnw == 8 && wmw != wnw)) &&
-                    g.K % (64 * wmw) == 0 && plan[2] >= 1,
+                    g.K % (64 * wmw) == 0 && plan[2] >= 1 &&
+                    (plan.size() == 3 || plan[3] == 0 || (plan[3] == 1 && wmw == 2 && wnw == 2)),
                 "conv_wgrad: bad plan");
-    p = tdl::conv_wgrad_make_plan(g, wmw, wnw, (int)plan[2]);
+    p = tdl::conv_wgrad_make_plan(g, wmw, wnw, (int)plan[2], plan.size() == 4 ? (int)plan[3] : 0);
   }
   auto ws = fresh({p.ws_elems}, x.options().dtype(at::kFloat));
   if (out.has_value()) {
@@ -550,7 +551,7 @@ at::Tensor stem_wgrad(at::Tensor xp, at::Tensor dy, int64_t kh, int64_t kw, int6
   return dw;
 }
 
-// the model's best candidate plans: [[wmw, wnw, chunk, nsplit], ...]
+// the model's best candidate plans: [[wmw, wnw, chunk, nsplit, kind], ...]
 std::vector<std::vector<int64_t>> conv_wgrad_plans(std::vector<int64_t> x_shape, std::vector<int64_t> dy_shape,
                                                    int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t pt,
                                                    int64_t pl, int64_t max_plans) {
@@ -558,8 +559,9 @@ std::vector<std::vector<int64_t>> conv_wgrad_plans(std::vector<int64_t> x_shape,
                   (int)dy_shape[2], (int)dy_shape[3], (int)kh, (int)kw, (int)sh, (int)sw, (int)pt, (int)pl};
   std::vector<std::vector<int64_t>> out;
   // the 3x3 / C = 64 row kernel first where it applies (it beats the split-K tiles on these shapes)
-  if (tdl::conv_wgrad3x3_c64_supported(g)) out.push_back({0, 0, 0, 0});
-  for (const auto& p : tdl::conv_wgrad_plans(g, (int)max_plans)) out.push_back({p.wmw, p.wnw, p.chunk, p.nsplit});
+  if (tdl::conv_wgrad3x3_c64_supported(g)) out.push_back({0, 0, 0, 0, 0});
+  for (const auto& p : tdl::conv_wgrad_plans(g, (int)max_plans))
+    out.push_back({p.wmw, p.wnw, p.chunk, p.nsplit, p.kind});
   return out;
 }
 // dst (bf16 slab) <- transposed copies of the HWIO f32 conv kernels in src (f32 slab); entries
@@ -689,7 +691,7 @@ void register_ops(pybind11::module& m) {
         pybind11::arg("x"), pybind11::arg("dy"), pybind11::arg("kh"), pybind11::arg("kw"), pybind11::arg("sh"),
         pybind11::arg("sw"), pybind11::arg("pt"), pybind11::arg("pl"), pybind11::arg("out") = pybind11::none(),
         pybind11::arg("accumulate") = false, pybind11::arg("plan") = std::vector<int64_t>{});
-  m.def("conv_wgrad_plans", &conv_wgrad_plans, "weight-gradient candidate plans, best first: [[wmw, wnw, chunk, nsplit]]");
+  m.def("conv_wgrad_plans", &conv_wgrad_plans, "weight-gradient candidate plans, best first: [[wmw, wnw, chunk, nsplit, kind]]");
   m.def("conv_force_tile", &tdl::conv_force_tile, "conv tile sweep hook (0 = heuristic)");
   m.def("conv_force_impl", &tdl::conv_force_impl, "conv main loop A/B hook: 1 = v1 register staged, 2 = LDS-DMA ring");
   m.def("conv_wgrad3x3_set_rows", &tdl::conv_wgrad3x3_set_rows, "3x3 row-kernel wgrad: output rows per slice (0 = auto)");

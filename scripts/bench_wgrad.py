@@ -63,7 +63,7 @@ def main():
         ref = mi([False, True, False])[1].permute(2, 3, 1, 0).float()
         times, errs = [], []
         for pl in plans:
-            hw = lambda: C.conv_wgrad(x, dy, KH, KH, s, s, p, p, plan=[pl[0], pl[1], pl[3]])  # noqa: E731
+            hw = lambda: C.conv_wgrad(x, dy, KH, KH, s, s, p, p, plan=[pl[0], pl[1], pl[3], pl[4]])  # noqa: E731
             errs.append(float((hw().float() - ref).abs().max() / ref.abs().max()))
             times.append(round(t(hw), 1))
         err = max(errs)

@@ -98,7 +98,7 @@ def conv_cases():
             check(f"conv_dgrad_s2_bn {tag}", lambda: C.conv_dgrad_s2_bn(dy, w, H, H, r, by, bx, bx))
         plans = C.conv_wgrad_plans(list(x.shape), list(dy.shape), kh, kh, s, s, p, p, 6)
         for pl in plans:
-            plan = [pl[0], pl[1], pl[3]]
+            plan = [pl[0], pl[1], pl[3], pl[4]]
             if N * OH * OH >= (1 << 24):
                 continue
             check(f"conv_wgrad {tag} plan {plan}", lambda: C.conv_wgrad(x, dy, kh, kh, s, s, p, p, plan=plan))

@@ -169,6 +169,9 @@ def _capture_fallback(key) -> None:
                       "using MIOpen for it (run one eager step of every shape before capturing)")
 
 
+_AGREE_WIDTH = 5  # [chosen, wmw, wnw, nsplit, kind]
+
+
 def _agree(local_decide, encode, decode):
     """Rank 0 decides (``local_decide``), every rank gets rank 0's decision.  Collective: every
     replica reaches the same key at the same point of the same model's first eager step."""
@@ -177,7 +180,9 @@ def _agree(local_decide, encode, decode):
         return local_decide()
     v = local_decide() if comm.rank == 0 else None
     on = comm.device if getattr(comm, "name", "") == "rccl" else torch.device("cpu")
-    t = torch.tensor(encode(v) if v is not None else [0, 0, 0, 0], dtype=torch.int64, device=on)
+    e = encode(v) if v is not None else []
+    assert len(e) <= _AGREE_WIDTH, e
+    t = torch.tensor(e + [0] * (_AGREE_WIDTH - len(e)), dtype=torch.int64, device=on)  # same size on every rank
     comm.broadcast(t, 0)
     return decode(t.tolist())
 
@@ -201,7 +206,7 @@ def _pick(key, hip_fn, ref_fn, saved_bytes: int = 0) -> bool:
         _times[key] = (t_hip, t_ref)
         return t_hip < t_ref * _PREFER_HIP
 
-    got = _agree(decide, lambda v: [int(v), 0, 0, 0], lambda a: bool(a[0]))
+    got = _agree(decide, lambda v: [int(v)], lambda a: bool(a[0]))
     _choice[key] = got
     return got
 
@@ -209,7 +214,7 @@ def _pick(key, hip_fn, ref_fn, saved_bytes: int = 0) -> bool:
 def _pick_wgrad(key, C, x, dy, kh, kw, stride, pad, ref_fn):
     """Weight gradient: time the cost model's first ``TDL_WGRAD_CANDIDATES`` (default 6) tile/slice
     plans and MIOpen on the first eager call of a shape; returns the winning plan
-    ``[wmw, wnw, nsplit]`` or None (MIOpen).  TDL_CONV=hip: the cost model's first plan, cached under
+    ``[wmw, wnw, nsplit, kind]`` or None (MIOpen).  TDL_CONV=hip: the cost model's first plan, cached under
     its own key -- a plan an earlier auto-mode call timed for the same shape (another split-K order)
     must not leak into a forced-hip run, nor the reverse."""
     m = mode()
@@ -218,7 +223,7 @@ def _pick_wgrad(key, C, x, dy, kh, kw, stride, pad, ref_fn):
     if key in _choice:
         return _choice[key]
     n = 1 if m == "hip" or torch.cuda.is_current_stream_capturing() else int(os.environ.get("TDL_WGRAD_CANDIDATES", 6))
-    plans = [[p[0], p[1], p[3]] for p in C.conv_wgrad_plans(list(x.shape), list(dy.shape), kh, kw, stride[0],
+    plans = [[p[0], p[1], p[3], p[4]] for p in C.conv_wgrad_plans(list(x.shape), list(dy.shape), kh, kw, stride[0],
                                                             stride[1], pad[0], pad[1], n)]
     if m == "hip":
         _choice[key] = plans[0]
@@ -237,7 +242,7 @@ def _pick_wgrad(key, C, x, dy, kh, kw, stride, pad, ref_fn):
         _times[key] = (t_best, t_ref)
         return best if t_best < t_ref * _PREFER_HIP else None
 
-    best = _agree(decide, lambda v: [1] + [int(u) for u in v] if v is not None else [0, 0, 0, 0],
+    best = _agree(decide, lambda v: [1] + [int(u) for u in v] if v is not None else [0],
                   lambda a: [int(u) for u in a[1:]] if a[0] else None)
     _choice[key] = best
     return best

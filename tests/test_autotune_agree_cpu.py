@@ -29,10 +29,12 @@ def _worker(rank, port, q):
         called.append(1)
         return rank == 0  # rank 0 says "hand-written kernel", rank 1 would say "library"
 
-    b = CV._agree(local_bool, lambda v: [int(v), 0, 0, 0], lambda a: bool(a[0]))
-    plan = CV._agree(lambda: [2, 1, 4 + rank], lambda v: [1] + list(v) if v is not None else [0, 0, 0, 0],
+    # encodings of different lengths (a bool, a [wmw, wnw, nsplit, kind] plan, "library") travel in
+    # one fixed-width message: non-deciding ranks must post a buffer of the same size
+    b = CV._agree(local_bool, lambda v: [int(v)], lambda a: bool(a[0]))
+    plan = CV._agree(lambda: [2, 1, 4 + rank, 1], lambda v: [1] + list(v) if v is not None else [0],
                      lambda a: list(a[1:]) if a[0] else None)
-    none = CV._agree(lambda: None if rank == 0 else [1, 1, 1], lambda v: [1] + list(v) if v is not None else [0, 0, 0, 0],
+    none = CV._agree(lambda: None if rank == 0 else [1, 1, 1, 0], lambda v: [1] + list(v) if v is not None else [0],
                      lambda a: list(a[1:]) if a[0] else None)
     q.put((rank, b, plan, none, len(called)))
     CV.bind_communicator(None)
@@ -50,5 +52,5 @@ def test_rank0_decides_for_every_replica():
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert got[0][1:4] == got[1][1:4] == (True, [2, 1, 4], None)
+    assert got[0][1:4] == got[1][1:4] == (True, [2, 1, 4, 1], None)
     assert got[0][4] == 1 and got[1][4] == 0  # only rank 0 timed anything

@@ -266,7 +266,7 @@ def test_wgrad3x3_row_kernel_matches_fp32(shape):
     x = torch.randn(N, H, W, 64, generator=g).cuda().bfloat16()
     dy = torch.randn(N, H, W, K, generator=g).cuda().bfloat16()
     plans = C.conv_wgrad_plans(list(x.shape), list(dy.shape), 3, 3, 1, 1, 1, 1, 2)
-    assert plans[0] == [0, 0, 0, 0]
+    assert plans[0] == [0, 0, 0, 0, 0]
     w = torch.zeros(3, 3, 64, K, device="cuda", requires_grad=True)
     y = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.permute(3, 2, 0, 1), padding=1)
     y.backward(dy.float().permute(0, 3, 1, 2))
@@ -336,3 +336,24 @@ def test_conv_wgrad_single_stage_matches_double_buffered_bitwise(shape):
         finally:
             C.conv_wgrad_force_single(False)
         assert torch.equal(outs[0], outs[1]), (wmw, wnw)
+
+
+@pytest.mark.parametrize("shape", [(4, 14, 14, 64, 128, 3, 3, 1, 1), (8, 28, 28, 128, 256, 1, 1, 1, 0),
+                                   (4, 9, 11, 256, 256, 1, 1, 2, 0), (3, 7, 7, 64, 256, 1, 1, 1, 0)])
+def test_conv_wgrad_dma1_matches_register_staged_bitwise(shape):
+    """The 2x2-wave weight-gradient tile on the single-stage LDS-DMA kernel and on the register-staged
+    one accumulate the same MFMAs in the same order: bit-identical (ragged pixel tails included)."""
+    from tensorflow_distributed_learning_amd.ops import hip
+
+    C = hip()
+    N, H, W, Ci, K, KH, KW, s, p = shape
+    x, k = _mk(shape, "cuda:0")
+    OH, OW = (H + 2 * p - KH) // s + 1, (W + 2 * p - KW) // s + 1
+    dy = torch.randn(N, OH, OW, K, device="cuda:0").bfloat16()
+    ref = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2).float(), (K, Ci, KH, KW), dy.permute(0, 3, 1, 2).float(),
+                                      stride=s, padding=p).permute(2, 3, 1, 0)
+    for wmw, wnw in ((2, 2),):
+        outs = [C.conv_wgrad(x, dy, KH, KW, s, s, p, p, plan=[wmw, wnw, 2, kind]) for kind in (1, 0)]
+        assert torch.equal(outs[0], outs[1]), (wmw, wnw)
+        err = (outs[0].float() - ref).abs().max() / ref.abs().max()
+        assert err < 2e-2, (wmw, wnw, float(err))
