@@ -22,6 +22,14 @@ __device__ __forceinline__ f4 mfma16x16x4(float a, float b, f4 c) {
 
 __device__ __forceinline__ f4 zero4() { return f4{0.f, 0.f, 0.f, 0.f}; }
 
+// two f32 -> packed bf16 (lo in bits 0-15), round to nearest even: one v_cvt_pk_bf16_f32 (the same bits
+// as the integer RNE `u + 0x7fff + lsb` sequence for finite values, at a fraction of its VALU cost)
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2_t __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f2_t{lo, hi}, b2_t));
+}
+
 __device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 __device__ __forceinline__ void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
 

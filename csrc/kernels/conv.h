@@ -25,9 +25,14 @@ bool conv_bf16_supported(const ConvGeom& g);
 // y[N,OH,OW,K] = conv(x[N,H,W,C], w[K][KH][KW][C])           (weights OHWI: reduction-contiguous rows)
 // stats (optional, [ceil(M / conv_fwd_row_tile) row tiles][2][K] f32, M = N*OH*OW): per-row-tile
 // channel sums of y and y^2 for a following batch norm (deterministic; bn_forward_train(part=...))
+// in_ss (optional, 1x1 stride 1 unpadded only): x is the INPUT of a BN -> ReLU whose output the conv
+// reads; the operand loader applies relu(x * scale + shift) (in_ss = scale[C], shift[C]) with the BN
+// apply pass's arithmetic -- bit-identical to convolving the materialised group output
 void conv_fwd_bf16(const void* x, const void* w_ohwi, void* y, const ConvGeom& g, hipStream_t s,
-                   float* stats = nullptr);
-int conv_fwd_row_tile(const ConvGeom& g);
+                   float* stats = nullptr, const float* in_ss = nullptr);
+int conv_fwd_row_tile(const ConvGeom& g, bool in_bn = false);
+// shapes the input-side BN (in_ss) takes: 1x1 stride 1 unpadded, C <= 512 (its scale / shift in LDS)
+bool conv_in_bn_supported(const ConvGeom& g);
 // stride-1 input gradient: dx[N,H,W,C] = conv_transpose(dy[N,OH,OW,K], w[KH][KW][C][K]) (HWIO, the
 // Keras layout: for a fixed (kh, kw, c) the K reduction values are contiguous)
 // residual (optional, shaped like dx): added in the epilogue, dx = dgrad + residual (the other
@@ -69,12 +74,15 @@ struct WgradPlan {
 };
 bool conv_wgrad_supported(const ConvGeom& g);
 // the model's best `max_plans` candidates, best first
-std::vector<WgradPlan> conv_wgrad_plans(const ConvGeom& g, int max_plans);
+// in_bn: plans the input-side BN (conv_wgrad_bf16 in_ss) runs with (register-staged tiles only)
+std::vector<WgradPlan> conv_wgrad_plans(const ConvGeom& g, int max_plans, bool in_bn = false);
 WgradPlan conv_wgrad_make_plan(const ConvGeom& g, int wmw, int wnw, int nsplit, int kind = 0);
 // dW (HWIO [KH][KW][C][K]) from x[N,H,W,C] and dy[N,OH,OW,K]: into dw_bf16, or (dw_bf16 == nullptr)
 // into the f32 dw_f32 (added to it when accumulate).  ws: plan.ws_elems f32.
+// in_ss (optional, 1x1 stride 1 unpadded, kind-0 plans of <= 4 waves): x is a BN -> ReLU's input, as in
+// conv_fwd_bf16
 void conv_wgrad_bf16(const void* x, const void* dy, float* ws, const WgradPlan& p, void* dw_bf16, float* dw_f32,
-                     bool accumulate, const ConvGeom& g, hipStream_t s);
+                     bool accumulate, const ConvGeom& g, hipStream_t s, const float* in_ss = nullptr);
 
 // Weight gradient of a 3x3 / stride 1 / pad 1 conv with C == 64 (wgrad3x3.hip): whole output rows per
 // workgroup, the 9 x 64 x 64 tile in registers, deterministic slice reduction.  ws: ..._ws_elems f32.

@@ -29,6 +29,7 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BK = 64;
+constexpr int kProMaxC = 512;  // input channels the input-side BN (Igemm::in_ss) stages in LDS
 constexpr int LDS_ROW = BK;  // bf16 elements per LDS row (128 B, 16-B chunks XOR-swizzled by row)
 
 // 16-B chunk c of tile row r lives at chunk c ^ swz(r): every 16-lane group of a ds_read_b128 fragment
@@ -67,6 +68,11 @@ struct Igemm {
   // recomputed from bn_x as [bn_x * scale + shift > 0] (bn_ss = scale[K], shift[K] of its forward):
   // one tensor read less than loading the group output
   const float* bn_ss;
+  // optional input-side BN -> ReLU (forward of a 1x1 stride-1 conv whose input is a plain BN -> ReLU
+  // group's output): x is the group's BN INPUT, and the operand loader stores relu(x * scale + shift)
+  // (in_ss = scale[C], shift[C]; the BN apply pass's f32 fma and bf16 rounding): the group output is
+  // never written
+  const float* in_ss;
 };
 
 // per-channel sums of 8 packed bf16 values v: s += v, q += v * w (w also 8 packed bf16)
@@ -117,17 +123,37 @@ __device__ __forceinline__ u32x4 relu_mask_affine_bf16x8(u32x4 v, u32x4 x, const
   return o;
 }
 
-// a + b for 8 packed bf16 values (f32 add, round to nearest even)
+// relu(x * sc + sh) for 8 packed bf16 x (the BN apply pass's f32 fma, round to nearest even)
+// (v_cvt_pk_bf16_f32 packing: round to nearest even, as the apply pass)
+__device__ __forceinline__ u32x4 bn_relu_bf16x8(u32x4 x, f4v sc0, f4v sc1, f4v sh0, f4v sh1) {
+  const float sc[8] = {sc0[0], sc0[1], sc0[2], sc0[3], sc1[0], sc1[1], sc1[2], sc1[3]};
+  const float sh[8] = {sh0[0], sh0[1], sh0[2], sh0[3], sh1[0], sh1[1], sh1[2], sh1[3]};
+  u32x4 o;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float lo = fmaxf(fmaf(__uint_as_float(x[k] << 16), sc[2 * k], sh[2 * k]), 0.f);
+    const float hi = fmaxf(fmaf(__uint_as_float(x[k] & 0xffff0000u), sc[2 * k + 1], sh[2 * k + 1]), 0.f);
+    o[k] = pack_bf16x2(lo, hi);
+  }
+  return o;
+}
+
+// a + b for 8 packed bf16 values (f32 add, round to nearest even; HW: v_cvt_pk_bf16_f32, the same bits)
+template <bool HW = false>
 __device__ __forceinline__ u32x4 add_bf16x8(u32x4 a, u32x4 b) {
   u32x4 o;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const float lo = __uint_as_float(a[i] << 16) + __uint_as_float(b[i] << 16);
     const float hi = __uint_as_float(a[i] & 0xffff0000u) + __uint_as_float(b[i] & 0xffff0000u);
-    uint32_t ul = __float_as_uint(lo), uh = __float_as_uint(hi);
-    ul += 0x7fffu + ((ul >> 16) & 1u);
-    uh += 0x7fffu + ((uh >> 16) & 1u);
-    o[i] = (ul >> 16) | (uh & 0xffff0000u);
+    if constexpr (HW) {
+      o[i] = pack_bf16x2(lo, hi);
+    } else {
+      uint32_t ul = __float_as_uint(lo), uh = __float_as_uint(hi);
+      ul += 0x7fffu + ((ul >> 16) & 1u);
+      uh += 0x7fffu + ((uh >> 16) & 1u);
+      o[i] = (ul >> 16) | (uh & 0xffff0000u);
+    }
   }
   return o;
 }
@@ -174,8 +200,11 @@ __device__ __forceinline__ void conv_epilogue(const Igemm& a, const f4v (&acc)[W
   for (int i = 0; i < WTM / 16; ++i)
 #pragma unroll
     for (int j = 0; j < WTN / 16; ++j) {
-      const uint32_t lo = f2bf(acc[i][j][0]) | ((uint32_t)f2bf(acc[i][j][1]) << 16);
-      const uint32_t hi = f2bf(acc[i][j][2]) | ((uint32_t)f2bf(acc[i][j][3]) << 16);
+      // (hardware packing where it does not raise the VGPR peak: the EK 1 / 2 variants spill with it)
+      const uint32_t lo = (EK == 1 || EK == 2) ? (f2bf(acc[i][j][0]) | ((uint32_t)f2bf(acc[i][j][1]) << 16))
+                                               : pack_bf16x2(acc[i][j][0], acc[i][j][1]);
+      const uint32_t hi = (EK == 1 || EK == 2) ? (f2bf(acc[i][j][2]) | ((uint32_t)f2bf(acc[i][j][3]) << 16))
+                                               : pack_bf16x2(acc[i][j][2], acc[i][j][3]);
       *reinterpret_cast<uint2*>(lds + (wrow0 + i * 16 + (lane & 15)) * OUT_LD + wcol0 + j * 16 + (lane >> 4) * 4) =
           make_uint2(lo, hi);
     }
@@ -236,7 +265,7 @@ __device__ __forceinline__ void conv_epilogue(const Igemm& a, const f4v (&acc)[W
       if (m < a.M) {
         const long long o = (long long)m * a.K + tn * BN + seg * 8;
         u32x4 v = *reinterpret_cast<const u32x4*>(lds + row * OUT_LD + seg * 8);
-        if (a.res) v = add_bf16x8(v, rv[e]);
+        if (a.res) v = add_bf16x8<EK == 0 || EK == 3>(v, rv[e]);
         if constexpr (EK == 1) v = relu_mask_bf16x8(v, ry[e]);
         if constexpr (EK == 3) v = relu_mask_affine_bf16x8(v, rx[e], msc, msh);
         *reinterpret_cast<u32x4*>(a.y + o) = v;
@@ -345,8 +374,13 @@ constexpr int v1_lds_elems() {
                                     : 2 * (BM + BN) * LDS_ROW;
 }
 
-template <int BM, int BN, int DEPTH, int EK>
+// PRO: the input-side BN -> ReLU (Igemm::in_ss) in the operand loader (DEPTH 0, plain epilogue)
+template <int BM, int BN, int DEPTH, int EK, bool PRO = false>
 __global__ __launch_bounds__(BM * 2, DEPTH == 0 ? 4 : (DEPTH == 3 ? 3 : 2)) void k_conv_igemm(Igemm a) {
+  static_assert(!PRO || (DEPTH == 0 && EK == 0), "input-side BN: single-stage plain variant");
+  // input-side BN: scale / shift of every input channel staged in LDS once (C <= kProMaxC), read per
+  // tile at LDS latency instead of a dependent global round trip after each tile's operand loads
+  __shared__ __attribute__((aligned(16))) float lds_ss[PRO ? 2 * kProMaxC : 1];
   constexpr int NT = BM * 2;         // threads: (BM / 64) x 2 waves, each 64 x BN/2
   constexpr int RP = NT / 8;         // tile rows per staging pass (8 x 16-B chunks per 128-B row)
   constexpr int WN = BN / 2;         // columns per wave
@@ -403,8 +437,10 @@ __global__ __launch_bounds__(BM * 2, DEPTH == 0 ? 4 : (DEPTH == 3 ? 3 : 2)) void
 
   // reduction position of the next tile to load (advanced incrementally: no per-tile div/mod)
   int n_c = 0, n_kw = 0, n_kh = 0;
+  int ld_c0 = 0;  // channel base of the last loaded tile (input-side BN)
   auto gload = [&](u32x4* pa, u32x4* pb) {
     const int c0 = n_c * BK, kw = n_kw, kh = n_kh;
+    ld_c0 = c0;
     if (++n_c == ctiles) {
       n_c = 0;
       if (++n_kw == a.KW) {
@@ -429,12 +465,26 @@ __global__ __launch_bounds__(BM * 2, DEPTH == 0 ? 4 : (DEPTH == 3 ? 3 : 2)) void
   auto sstore = [&](int buf, const u32x4* pa, const u32x4* pb) {
     uint16_t* la = lds + buf * (BM + BN) * LDS_ROW;
     uint16_t* lb = la + BM * LDS_ROW;
+    if constexpr (PRO) {
+      // B first: its staging registers die before the scale / shift ones are loaded
 #pragma unroll
-    for (int i = 0; i < A_LD; ++i)
-      *reinterpret_cast<u32x4*>(la + ((tid >> 3) + RP * i) * LDS_ROW + scol) = pa[i];
+      for (int i = 0; i < B_LD; ++i)
+        *reinterpret_cast<u32x4*>(lb + ((tid >> 3) + RP * i) * LDS_ROW + scol) = pb[i];
+      // every chunk of this thread holds channels ld_c0 + col8 .. + 7 (1x1 stride 1: no padding taps;
+      // rows past M are transformed too and their outputs never stored)
+      const f4v* ss = reinterpret_cast<const f4v*>(lds_ss + ld_c0 + col8);
+      const f4v sc0 = ss[0], sc1 = ss[1], sh0 = ss[a.C / 4], sh1 = ss[a.C / 4 + 1];
 #pragma unroll
-    for (int i = 0; i < B_LD; ++i)
-      *reinterpret_cast<u32x4*>(lb + ((tid >> 3) + RP * i) * LDS_ROW + scol) = pb[i];
+      for (int i = 0; i < A_LD; ++i)
+        *reinterpret_cast<u32x4*>(la + ((tid >> 3) + RP * i) * LDS_ROW + scol) = bn_relu_bf16x8(pa[i], sc0, sc1, sh0, sh1);
+    } else {
+#pragma unroll
+      for (int i = 0; i < A_LD; ++i)
+        *reinterpret_cast<u32x4*>(la + ((tid >> 3) + RP * i) * LDS_ROW + scol) = pa[i];
+#pragma unroll
+      for (int i = 0; i < B_LD; ++i)
+        *reinterpret_cast<u32x4*>(lb + ((tid >> 3) + RP * i) * LDS_ROW + scol) = pb[i];
+    }
   };
 
   f4v acc[4][NS];
@@ -466,7 +516,13 @@ __global__ __launch_bounds__(BM * 2, DEPTH == 0 ? 4 : (DEPTH == 3 ? 3 : 2)) void
   if (DEPTH == 0) {
     for (int t = 0; t < ntiles; ++t) {
       gload(ra[0], rb[0]);
-      if (t) __syncthreads();  // every wave done reading the previous tile
+      if constexpr (PRO) {
+        if (t == 0) {  // stage scale / shift while the first tile's operand loads fly
+          for (int i = tid * 4; i < 2 * a.C; i += NT * 4)
+            *reinterpret_cast<f4v*>(lds_ss + i) = *reinterpret_cast<const f4v*>(a.in_ss + i);
+        }
+      }
+      if (PRO || t) __syncthreads();  // every wave done reading the previous tile (PRO: lds_ss written)
       sstore(0, ra[0], rb[0]);
       __syncthreads();
       compute(0);
@@ -754,6 +810,15 @@ bool use_dma1(const Igemm& a) {
 // workgroups per CU (the 64-column tile's extra LDS traffic per MFMA costs more than the idle CUs);
 // 256 x 128 loses 5-20 % everywhere.  The 64-column tile only serves K == 64 * odd.
 void launch(const Igemm& a, hipStream_t s) {
+  if (a.in_ss) {  // input-side BN -> ReLU: the register-staged loader, single stage, plain epilogue
+    if (a.C > kProMaxC) return;  // (conv_fwd_bf16's callers check conv_in_bn_supported)
+    if (a.K % 128 == 0) {
+      hipLaunchKernelGGL((k_conv_igemm<128, 128, 0, 0, true>), dim3((a.M + 127) / 128 * (a.K / 128)), dim3(256), 0, s, a);
+    } else {
+      hipLaunchKernelGGL((k_conv_igemm<128, 64, 0, 0, true>), dim3((a.M + 127) / 128 * (a.K / 64)), dim3(256), 0, s, a);
+    }
+    return;
+  }
   if (use_v2(a.M, a.K, a.KH * a.KW * (a.C / BK), a.KH * a.KW)) {
     if (a.K % 128 == 0) return launch_v2<256, 128, 4, 2>(a, s);
     return launch_v2<256, 64, 4, 2>(a, s);
@@ -780,6 +845,10 @@ void conv_force_depth(int depth) {
   g_single = depth != 3;
 }
 
+bool conv_in_bn_supported(const ConvGeom& g) {
+  return g.KH == 1 && g.KW == 1 && g.SH == 1 && g.SW == 1 && g.PT == 0 && g.PL == 0 && g.C <= kProMaxC;
+}
+
 bool conv_bf16_supported(const ConvGeom& g) {
   // byte offsets of every operand and output within 2 GiB (32-bit buffer offsets), <= 32 taps
   // (the per-row tap-validity bitmask of the operand loader), padding < the filter size (the
@@ -794,7 +863,8 @@ bool conv_bf16_supported(const ConvGeom& g) {
 }
 
 // the row tile launch() picks (the BN partial-sum rows of an epilogue are per row tile)
-int conv_fwd_row_tile(const ConvGeom& g) {
+int conv_fwd_row_tile(const ConvGeom& g, bool in_bn) {
+  if (in_bn) return 128;
   if (use_v2(g.N * g.OH * g.OW, g.K, g.KH * g.KW * (g.C / BK), g.KH * g.KW)) return 256;
   return (g_forced_tile == 3 && g.K % 128 == 0) ? 256 : 128;
 }
@@ -809,11 +879,13 @@ int conv_dgrad_s2_row_tile(const ConvGeom& g) {
   return (g_forced_tile == 3 && g.C % 128 == 0) ? 256 : 128;
 }
 
-void conv_fwd_bf16(const void* x, const void* w_ohwi, void* y, const ConvGeom& g, hipStream_t s, float* stats) {
+void conv_fwd_bf16(const void* x, const void* w_ohwi, void* y, const ConvGeom& g, hipStream_t s, float* stats,
+                   const float* in_ss) {
   Igemm a{static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w_ohwi), static_cast<uint16_t*>(y),
           g.N, g.H, g.W, g.C, g.OH, g.OW, g.K, g.KH, g.KW, g.SH, g.SW, g.PT, g.PL, 0,
           (long long)g.KH * g.KW * g.C, (long long)g.KW * g.C, (long long)g.C, g.N * g.OH * g.OW, 0, 0, 0, nullptr,
           stats};
+  a.in_ss = in_ss;
   launch(a, s);
 }
 

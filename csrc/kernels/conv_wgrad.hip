@@ -57,7 +57,25 @@ struct Wgrad {
   int nsplit;    // S
   int direct;    // 1x1, stride 1, no padding: x(m, c) = x[m][c]
   float inv_ow, inv_oh;
+  // optional (direct only): x is a BN -> ReLU's input; the staging stores relu(x * scale + shift)
+  // (in_ss = scale[C], shift[C]), the BN apply pass's arithmetic
+  const float* in_ss;
 };
+
+// relu(x * sc + sh) for 8 packed bf16 x (f32 fma, round to nearest even)
+__device__ __forceinline__ u32x4 bn_relu_bf16x8(u32x4 x, const float* sc, const float* sh) {
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  u32x4 o;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const f2v v = {__uint_as_float(x[k] << 16), __uint_as_float(x[k] & 0xffff0000u)};
+    const f2v r = __builtin_elementwise_max(
+        __builtin_elementwise_fma(v, f2v{sc[2 * k], sc[2 * k + 1]}, f2v{sh[2 * k], sh[2 * k + 1]}), f2v{0.f, 0.f});
+    o[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, bf16x2));  // v_cvt_pk_bf16_f32 (RNE)
+  }
+  return o;
+}
 
 // q = n / d for 0 <= n < 2^24 via one f32 multiply and a +-1 fix-up
 __device__ __forceinline__ int fdiv(int n, int d, float inv, int& rem) {
@@ -80,9 +98,12 @@ __device__ __forceinline__ int fdiv(int n, int d, float inv, int& rem) {
 // SINGLE: one LDS stage and no register prefetch, 3 waves per SIMD (<= 168 VGPRs; at 4 the staging
 // registers spill): the other
 // resident workgroups hide a workgroup's load latency (the conv.hip DEPTH 0 finding).
-template <int WMW, int WNW, bool SINGLE>
+// PRO: the input-side BN -> ReLU (Wgrad::in_ss) on the staged x chunks; the per-thread channel
+// scale / shift stay in registers (double-buffered variant: 2 waves per SIMD, room for them)
+template <int WMW, int WNW, bool SINGLE, bool PRO = false>
 __global__ __launch_bounds__(64 * WMW * WNW) __attribute__((amdgpu_waves_per_eu(SINGLE ? 3 : 2))) void k_conv_wgrad(
     Wgrad a) {
+  static_assert(!(PRO && SINGLE), "input-side BN: double-buffered variant");
   constexpr int NW = WMW * WNW, NT = 64 * NW;
   constexpr int SA = WMW, SBn = WNW;
   constexpr int RPT = 8 / NW;                 // staged rows per thread per sub-image
@@ -127,6 +148,23 @@ __global__ __launch_bounds__(64 * WMW * WNW) __attribute__((amdgpu_waves_per_eu(
     b_off[j] = (b_kh[j] * a.W + b_kw[j]) * a.C + c0 + sch * 8;
   }
 
+  float isc[PRO ? SBn : 1][8], ish[PRO ? SBn : 1][8];
+  if constexpr (PRO) {
+#pragma unroll
+    for (int j = 0; j < SBn; ++j) {
+      const int c = tc0 + 64 * j + sch * 8;  // direct: tc == c
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f4v s4 = b_live[j] ? *reinterpret_cast<const f4v*>(a.in_ss + c + 4 * h) : f4v{0.f, 0.f, 0.f, 0.f};
+        const f4v t4 = b_live[j] ? *reinterpret_cast<const f4v*>(a.in_ss + a.C + c + 4 * h) : f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          isc[j][4 * h + e] = s4[e];
+          ish[j][4 * h + e] = t4[e];
+        }
+      }
+    }
+  }
   u32x4 ra[RPT][SA], rb[RPT][SBn];
   auto gload = [&](int st) {
 #pragma unroll
@@ -164,7 +202,12 @@ __global__ __launch_bounds__(64 * WMW * WNW) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
       for (int j = 0; j < SA; ++j) *reinterpret_cast<u32x4*>(base + j * SUB + soff[i]) = ra[i][j];
 #pragma unroll
-      for (int j = 0; j < SBn; ++j) *reinterpret_cast<u32x4*>(base + (SA + j) * SUB + soff[i]) = rb[i][j];
+      for (int j = 0; j < SBn; ++j) {
+        // (rows past the slice are transformed too: their dy rows are zeros)
+        u32x4 v = rb[i][j];
+        if constexpr (PRO) v = bn_relu_bf16x8(v, isc[j], ish[j]);
+        *reinterpret_cast<u32x4*>(base + (SA + j) * SUB + soff[i]) = v;
+      }
     }
   };
 
@@ -436,21 +479,22 @@ __global__ __launch_bounds__(1024) void k_wgrad_reduce(const float* ws, long lon
 
 bool g_wgrad_single = false;  // conv_wgrad_force_single (A/B hook)
 
-template <int WMW, int WNW, bool SINGLE>
+template <int WMW, int WNW, bool SINGLE, bool PRO = false>
 void launch_wgrad_t(const Wgrad& a, hipStream_t s) {
   constexpr int lds = (SINGLE ? 1 : 2) * (WMW + WNW) * SUB * 2;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_conv_wgrad<WMW, WNW, SINGLE>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              lds);
+    (void)hipFuncSetAttribute((const void*)k_conv_wgrad<WMW, WNW, SINGLE, PRO>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
   const int tiles = (a.K / (64 * WMW)) * ((a.TC + 64 * WNW - 1) / (64 * WNW));
-  hipLaunchKernelGGL((k_conv_wgrad<WMW, WNW, SINGLE>), dim3(tiles * a.nsplit), dim3(64 * WMW * WNW), lds, s, a);
+  hipLaunchKernelGGL((k_conv_wgrad<WMW, WNW, SINGLE, PRO>), dim3(tiles * a.nsplit), dim3(64 * WMW * WNW), lds, s, a);
 }
 
 template <int WMW, int WNW>
 void launch_wgrad(const Wgrad& a, int kind, hipStream_t s) {
+  if (a.in_ss) return launch_wgrad_t<WMW, WNW, false, true>(a, s);
   if constexpr (WMW == 2 && WNW == 2) {
     if (kind == 1) {
       const int tiles = (a.K / (64 * WMW)) * ((a.TC + 64 * WNW - 1) / (64 * WNW));
@@ -500,7 +544,7 @@ WgradPlan conv_wgrad_make_plan(const ConvGeom& g, int wmw, int wnw, int nsplit, 
 // time = max(MFMA time at ~1 PF/s, HBM time for the operand bytes the tiles re-read at ~5 TB/s)
 // stretched by the grid's tail (resident workgroups per CU from LDS and VGPRs), plus the partial
 // slab written and re-read by the reduce.  The caller times the first few and keeps the fastest.
-std::vector<WgradPlan> conv_wgrad_plans(const ConvGeom& g, int max_plans) {
+std::vector<WgradPlan> conv_wgrad_plans(const ConvGeom& g, int max_plans, bool in_bn) {
   struct Cand {
     double t;
     WgradPlan p;
@@ -513,13 +557,14 @@ std::vector<WgradPlan> conv_wgrad_plans(const ConvGeom& g, int max_plans) {
     const int wmw = kTiles[ti >> 1][0], wnw = kTiles[ti >> 1][1], bmk = 64 * wmw, btc = 64 * wnw;
     const int kind = ti & 1;  // 1: the single-stage LDS-DMA kernel (4-wave tiles only)
     if (kind && (wmw != 2 || wnw != 2)) continue;  // 1x4 / 4x1 spill at 128 VGPRs
+    if (in_bn && (kind || wmw * wnw == 8)) continue;  // the input-side BN runs in the register staging
     if (g.K % bmk) continue;
     const int ntc = (TC + btc - 1) / btc;
     if ((ntc * btc - TC) * 4 > ntc * btc) continue;  // > 25 % of the tc columns padding
     const int tiles = (g.K / bmk) * ntc;
     const bool ring = wmw * wnw == 8;  // LDS-DMA ring kernel: one 144-KiB workgroup per CU
     const bool dma1 = kind == 1;
-    const bool single = !ring && (g_wgrad_single || dma1);
+    const bool single = !ring && ((g_wgrad_single && !in_bn) || dma1);
     const int lds_kb = (ring ? 3 : (single ? 1 : 2)) * (wmw + wnw) * 8;
     // <= 2 waves per SIMD (3 for the single-stage v1 kernel, 4 for the single-stage DMA one)
     const int per_cu = std::max(1, std::min(160 / lds_kb, (dma1 ? 16 : single ? 12 : 8) / (wmw * wnw)));
@@ -577,13 +622,15 @@ std::vector<WgradPlan> conv_wgrad_plans(const ConvGeom& g, int max_plans) {
 }
 
 void conv_wgrad_bf16(const void* x, const void* dy, float* ws, const WgradPlan& p, void* dw_bf16, float* dw_f32,
-                     bool accumulate, const ConvGeom& g, hipStream_t s) {
+                     bool accumulate, const ConvGeom& g, hipStream_t s, const float* in_ss) {
   Wgrad a{static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(dy), ws,
           g.N, g.H, g.W, g.C, g.OH, g.OW, g.K, g.KH, g.KW, g.SH, g.SW, g.PT, g.PL,
           g.N * g.OH * g.OW, g.KH * g.KW * g.C, p.chunk, p.nsplit,
           (g.KH == 1 && g.KW == 1 && g.SH == 1 && g.SW == 1 && g.PT == 0 && g.PL == 0 && g.H == g.OH && g.W == g.OW)
               ? 1 : 0,
           1.0f / (float)g.OW, 1.0f / (float)g.OH};
+  a.in_ss = in_ss;
+  if (in_ss && (!a.direct || p.kind != 0 || p.wmw * p.wnw > 4)) return;  // (the caller checks)
   const int t = p.wmw * 8 + p.wnw;
   switch (t) {
     case 9: launch_wgrad<1, 1>(a, p.kind, s); break;

@@ -285,29 +285,39 @@ void conv_check(const at::Tensor& t, const char* what) {
 }
 
 // y[N,OH,OW,K] = conv(x[N,H,W,C], w_ohwi[K,KH,KW,C]); top/left padding pt/pl, bottom/right implied by OH/OW
+// in_bn: x is the input of a BN -> ReLU (its [4][C] batch statistics); the conv runs over relu(bn(x))
+static const float* conv_in_bn(const c10::optional<at::Tensor>& in_bn, const tdl::ConvGeom& g) {
+  const float* ss = bn_ss_of(in_bn, g.C);
+  TORCH_CHECK(!ss || tdl::conv_in_bn_supported(g),
+              "conv: the input-side batch norm takes 1x1 stride-1 unpadded convolutions of <= 512 channels");
+  return ss;
+}
+
 at::Tensor conv_fwd(at::Tensor x, at::Tensor w_ohwi, int64_t oh, int64_t ow, int64_t sh, int64_t sw, int64_t pt,
-                    int64_t pl) {
+                    int64_t pl, c10::optional<at::Tensor> in_bn) {
   conv_check(x, "x");
   conv_check(w_ohwi, "w");
   TORCH_CHECK(w_ohwi.dim() == 4 && w_ohwi.size(3) == x.size(3), "conv_fwd: weights must be OHWI [K,KH,KW,C]");
   auto g = conv_geom(x, oh, ow, w_ohwi.size(0), w_ohwi.size(1), w_ohwi.size(2), sh, sw, pt, pl);
+  const float* ss = conv_in_bn(in_bn, g);
   auto y = fresh({x.size(0), oh, ow, w_ohwi.size(0)}, x.options());
-  tdl::conv_fwd_bf16(x.data_ptr(), w_ohwi.data_ptr(), y.data_ptr(), g, cur_stream());
+  tdl::conv_fwd_bf16(x.data_ptr(), w_ohwi.data_ptr(), y.data_ptr(), g, cur_stream(), nullptr, ss);
   return y;
 }
 
 // forward + batch-norm partial sums of y: returns (y, part[P + ceil(P/64)][2][K]) with P row tiles
 std::vector<at::Tensor> conv_fwd_stats(at::Tensor x, at::Tensor w_ohwi, int64_t oh, int64_t ow, int64_t sh,
-                                       int64_t sw, int64_t pt, int64_t pl) {
+                                       int64_t sw, int64_t pt, int64_t pl, c10::optional<at::Tensor> in_bn) {
   conv_check(x, "x");
   conv_check(w_ohwi, "w");
   TORCH_CHECK(w_ohwi.dim() == 4 && w_ohwi.size(3) == x.size(3), "conv_fwd: weights must be OHWI [K,KH,KW,C]");
   auto g = conv_geom(x, oh, ow, w_ohwi.size(0), w_ohwi.size(1), w_ohwi.size(2), sh, sw, pt, pl);
+  const float* ss = conv_in_bn(in_bn, g);
   auto y = fresh({x.size(0), oh, ow, w_ohwi.size(0)}, x.options());
-  const int64_t M = (int64_t)g.N * g.OH * g.OW, bm = tdl::conv_fwd_row_tile(g);
+  const int64_t M = (int64_t)g.N * g.OH * g.OW, bm = tdl::conv_fwd_row_tile(g, ss != nullptr);
   const int64_t P = (M + bm - 1) / bm;
   auto part = fresh({P + (P + 63) / 64, 2, (int64_t)g.K}, x.options().dtype(at::kFloat));
-  tdl::conv_fwd_bf16(x.data_ptr(), w_ohwi.data_ptr(), y.data_ptr(), g, cur_stream(), part.data_ptr<float>());
+  tdl::conv_fwd_bf16(x.data_ptr(), w_ohwi.data_ptr(), y.data_ptr(), g, cur_stream(), part.data_ptr<float>(), ss);
   return {y, part};
 }
 
@@ -434,11 +444,15 @@ std::vector<at::Tensor> conv_dgrad_s2_bn(at::Tensor dy, at::Tensor w_hwio, int64
 // weight gradient: dw[KH,KW,C,K] (bf16, or added into the f32 `out` when given) from x[N,H,W,C] and
 // dy[N,OH,OW,K]; deterministic split-K.  plan = [wmw, wnw, nsplit] (empty: the model's first choice)
 at::Tensor conv_wgrad(at::Tensor x, at::Tensor dy, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t pt,
-                      int64_t pl, c10::optional<at::Tensor> out, bool accumulate, std::vector<int64_t> plan) {
+                      int64_t pl, c10::optional<at::Tensor> out, bool accumulate, std::vector<int64_t> plan,
+                      c10::optional<at::Tensor> in_bn) {
   conv_check(x, "x");
   conv_check(dy, "dy");
   TORCH_CHECK(dy.dim() == 4 && dy.size(0) == x.size(0), "conv_wgrad: dy must be NHWC [N,OH,OW,K]");
   auto g = conv_geom(x, dy.size(1), dy.size(2), dy.size(3), kh, kw, sh, sw, pt, pl);
+  const float* ss = conv_in_bn(in_bn, g);
+  TORCH_CHECK(!ss || plan.empty() || (plan[0] != 0 && plan[0] * plan[1] <= 4 && (plan.size() == 3 || plan[3] == 0)),
+              "conv_wgrad: the input-side batch norm runs on the register-staged plans (<= 4 waves, kind 0)");
   TORCH_CHECK(tdl::conv_wgrad_supported(g), "conv_wgrad: N*OH*OW must be < 2^24");
   TORCH_CHECK(plan.empty() || plan.size() == 3 || plan.size() == 4, "conv_wgrad: plan = [wmw, wnw, nsplit(, kind)]");
   if (!plan.empty() && plan[0] == 0) {  // [0, 0, 0]: the row kernel of 3x3 / C = 64 convs (wgrad3x3.hip)
@@ -460,7 +474,7 @@ at::Tensor conv_wgrad(at::Tensor x, at::Tensor dy, int64_t kh, int64_t kw, int64
   }
   tdl::WgradPlan p;
   if (plan.empty()) {
-    p = tdl::conv_wgrad_plans(g, 1).at(0);
+    p = tdl::conv_wgrad_plans(g, 1, ss != nullptr).at(0);
   } else {
     const int wmw = (int)plan[0], wnw = (int)plan[1];
     TORCH_CHECK((wmw == 1 || wmw == 2 || wmw == 4) && (wnw == 1 || wnw == 2 || wnw == 4) &&
@@ -478,12 +492,12 @@ at::Tensor conv_wgrad(at::Tensor x, at::Tensor dy, int64_t kh, int64_t kw, int64
                 "conv_wgrad: out must be a contiguous f32 tensor of KH*KW*C*K elements");
     TORCH_CHECK(reinterpret_cast<uintptr_t>(o.data_ptr()) % 16 == 0, "conv_wgrad: out must be 16-byte aligned");
     tdl::conv_wgrad_bf16(x.data_ptr(), dy.data_ptr(), ws.data_ptr<float>(), p, nullptr, o.data_ptr<float>(),
-                         accumulate, g, cur_stream());
+                         accumulate, g, cur_stream(), ss);
     return o;
   }
   auto dw = fresh({kh, kw, x.size(3), dy.size(3)}, x.options());
   tdl::conv_wgrad_bf16(x.data_ptr(), dy.data_ptr(), ws.data_ptr<float>(), p, dw.data_ptr(), nullptr, false, g,
-                       cur_stream());
+                       cur_stream(), ss);
   return dw;
 }
 
@@ -554,13 +568,13 @@ at::Tensor stem_wgrad(at::Tensor xp, at::Tensor dy, int64_t kh, int64_t kw, int6
 // the model's best candidate plans: [[wmw, wnw, chunk, nsplit, kind], ...]
 std::vector<std::vector<int64_t>> conv_wgrad_plans(std::vector<int64_t> x_shape, std::vector<int64_t> dy_shape,
                                                    int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t pt,
-                                                   int64_t pl, int64_t max_plans) {
+                                                   int64_t pl, int64_t max_plans, bool in_bn) {
   tdl::ConvGeom g{(int)x_shape[0], (int)x_shape[1], (int)x_shape[2], (int)x_shape[3], (int)dy_shape[1],
                   (int)dy_shape[2], (int)dy_shape[3], (int)kh, (int)kw, (int)sh, (int)sw, (int)pt, (int)pl};
   std::vector<std::vector<int64_t>> out;
   // the 3x3 / C = 64 row kernel first where it applies (it beats the split-K tiles on these shapes)
-  if (tdl::conv_wgrad3x3_c64_supported(g)) out.push_back({0, 0, 0, 0, 0});
-  for (const auto& p : tdl::conv_wgrad_plans(g, (int)max_plans))
+  if (!in_bn && tdl::conv_wgrad3x3_c64_supported(g)) out.push_back({0, 0, 0, 0, 0});
+  for (const auto& p : tdl::conv_wgrad_plans(g, (int)max_plans, in_bn))
     out.push_back({p.wmw, p.wnw, p.chunk, p.nsplit, p.kind});
   return out;
 }
@@ -690,8 +704,12 @@ void register_ops(pybind11::module& m) {
   m.def("conv_wgrad", &conv_wgrad, "NHWC bf16 convolution weight gradient (MFMA, transposed LDS reads, split-K)",
         pybind11::arg("x"), pybind11::arg("dy"), pybind11::arg("kh"), pybind11::arg("kw"), pybind11::arg("sh"),
         pybind11::arg("sw"), pybind11::arg("pt"), pybind11::arg("pl"), pybind11::arg("out") = pybind11::none(),
-        pybind11::arg("accumulate") = false, pybind11::arg("plan") = std::vector<int64_t>{});
-  m.def("conv_wgrad_plans", &conv_wgrad_plans, "weight-gradient candidate plans, best first: [[wmw, wnw, chunk, nsplit, kind]]");
+        pybind11::arg("accumulate") = false, pybind11::arg("plan") = std::vector<int64_t>{},
+        pybind11::arg("in_bn") = pybind11::none());
+  m.def("conv_wgrad_plans", &conv_wgrad_plans, "weight-gradient candidate plans, best first: [[wmw, wnw, chunk, nsplit, kind]]",
+        pybind11::arg("x_shape"), pybind11::arg("dy_shape"), pybind11::arg("kh"), pybind11::arg("kw"),
+        pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("pt"), pybind11::arg("pl"), pybind11::arg("max_plans"),
+        pybind11::arg("in_bn") = false);
   m.def("conv_force_tile", &tdl::conv_force_tile, "conv tile sweep hook (0 = heuristic)");
   m.def("conv_force_impl", &tdl::conv_force_impl, "conv main loop A/B hook: 1 = v1 register staged, 2 = LDS-DMA ring");
   m.def("conv_wgrad3x3_set_rows", &tdl::conv_wgrad3x3_set_rows, "3x3 row-kernel wgrad: output rows per slice (0 = auto)");
@@ -706,8 +724,12 @@ void register_ops(pybind11::module& m) {
   m.def("stem_wgrad", &stem_wgrad, "stem conv weight gradient from the packed image", pybind11::arg("xp"),
         pybind11::arg("dy"), pybind11::arg("kh"), pybind11::arg("kw"), pybind11::arg("c"), pybind11::arg("sh"),
         pybind11::arg("out") = pybind11::none(), pybind11::arg("accumulate") = false);
-  m.def("conv_fwd", &conv_fwd, "NHWC bf16 implicit-GEMM convolution forward (MFMA)");
-  m.def("conv_fwd_stats", &conv_fwd_stats, "conv forward + batch-norm partial channel sums of its output");
+  m.def("conv_fwd", &conv_fwd, "NHWC bf16 implicit-GEMM convolution forward (MFMA); in_bn: over relu(bn(x))",
+        pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("oh"), pybind11::arg("ow"), pybind11::arg("sh"),
+        pybind11::arg("sw"), pybind11::arg("pt"), pybind11::arg("pl"), pybind11::arg("in_bn") = pybind11::none());
+  m.def("conv_fwd_stats", &conv_fwd_stats, "conv forward + batch-norm partial channel sums of its output",
+        pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("oh"), pybind11::arg("ow"), pybind11::arg("sh"),
+        pybind11::arg("sw"), pybind11::arg("pt"), pybind11::arg("pl"), pybind11::arg("in_bn") = pybind11::none());
   m.def("conv_dgrad", &conv_dgrad, "NHWC bf16 implicit-GEMM stride-1 convolution input gradient (MFMA)",
         pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("h"), pybind11::arg("wd"), pybind11::arg("pt"),
         pybind11::arg("pl"), pybind11::arg("residual") = pybind11::none());

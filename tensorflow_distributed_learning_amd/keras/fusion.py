@@ -14,6 +14,9 @@ list; the plan rewrites, at execution time only (the layer graph, variables, che
 * ``BatchNormalization -> Add(other) -> ReLU``: the ResNet block tail, one fused pass that also
   produces the residual's gradient.
 * ``ZeroPadding2D -> MaxPooling2D('valid')``: one pooling pass with implicit zero padding.
+* ``BatchNormalization -> ReLU -> Conv2D(1x1, stride 1)`` where the conv is the only reader (the ResNet
+  bottleneck's last conv): the BN computes its statistics only and the conv's forward and weight-gradient
+  operand loaders apply relu(x * scale + shift) to the BN input; the normalised tensor is never written.
 * ``BatchNormalization -> ReLU -> [ZeroPadding2D ->] MaxPooling2D('valid')`` (the ResNet stem): the pool
   runs on the BN input with the normalisation in its kernel and reduces the BN backward sums in its
   backward pass; the normalised tensor is never written.
@@ -39,7 +42,7 @@ from . import layers as L
 
 class Group:
     __slots__ = ("bn_node", "relu", "residual", "conv_layer", "out", "last", "conv_reader", "add_node", "res_bn",
-                 "pool")
+                 "pool", "defer")
 
     def __init__(self, bn_node, relu, residual, conv_layer, out, last, conv_reader=False, add_node=None):
         self.bn_node, self.relu, self.residual, self.conv_layer, self.out, self.last = (
@@ -56,6 +59,9 @@ class Group:
         # pool is the group output's only reader -- the pool runs on the BN input with the normalisation
         # in its kernel (ops/pooling.py bn_relu_max_pool) and the normalised tensor is never written
         self.pool = None
+        # the reading 1x1 stride-1 Conv2D layer of a BN -> ReLU group whose apply it takes over (the
+        # group output is never materialised; decided again at run time: GPU, bf16, kernel shapes)
+        self.defer = None
 
 
 class Plan:
@@ -156,6 +162,13 @@ def plan(nodes: List[L.Node], outputs) -> Plan:
             g.res_bn = pg
     if os.environ.get("TDL_FUSE_BN_POOL", "1") == "1":
         _plan_bn_pool(p, only_consumer)
+    if os.environ.get("TDL_FUSE_BN_INPUT", "1") == "1":
+        for g in p.groups.values():
+            if g.relu and g.residual is None and g.conv_reader and g.pool is None:
+                c = only_consumer(g.out).layer
+                if tuple(c.kernel_size) == (1, 1) and tuple(c.strides) == (1, 1) and \
+                        tuple(c.dilation_rate) == (1, 1) and c.groups == 1 and c.filters % 64 == 0:
+                    g.defer = c
     if os.environ.get("TDL_FUSE_GRAD_SUM", "1") == "1":
         _plan_grad_sums(p, nodes, consumers, outs)
     return p
@@ -223,6 +236,24 @@ def _plan_grad_sums(p: Plan, nodes, consumers, outs):
                     break
 
 
+_DEFER_MIN_PIXELS = int(os.environ.get("TDL_FUSE_BN_INPUT_MIN_PIXELS", 131072))
+
+
+def _defer_ok(x) -> bool:
+    """The hand-written 1x1 kernels take this BN input (what Conv2D.call's kernel path requires), and
+    the tensor is large enough for the saved apply pass to outweigh the loaders' extra work: per
+    ResNet-50 bottleneck shape (scripts/bench_bn_in.py, profiles/bn_input_side_r4.txt) the fused
+    forward + weight gradient beat apply + plain kernels at 56x56 and 28x28 (b=256) and lost at
+    14x14 and 7x7, where the weight gradient also gives up the single-stage LDS-DMA plans."""
+    import torch
+
+    from ..ops import conv as _conv
+
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[-1] % 64 == 0
+            and x.shape[-1] <= 512 and x.numel() < (1 << 30) and _conv.mode() != "miopen"
+            and x.shape[0] * x.shape[1] * x.shape[2] >= _DEFER_MIN_PIXELS)
+
+
 def run_group(g: Group, vals, training, taps=None, boxes=None):
     from ..ops.batchnorm import batch_norm_train
 
@@ -258,10 +289,14 @@ def run_group(g: Group, vals, training, taps=None, boxes=None):
         vals[id(g.out)] = y
         return
     st = [] if (g.relu and r is None) else None
+    defer = g.defer is not None and training and _defer_ok(x)
     y = batch_norm_train(x, bn.gamma.value if bn.gamma is not None else None,
                          bn.beta.value if bn.beta is not None else None, bn.moving_mean.value,
                          bn.moving_variance.value, bn.momentum, bn.epsilon, relu=g.relu, residual=r, conv_bias=cb,
-                         grad_out=bn._grad_targets(), part=getattr(x, "_tdl_bn_part", None), stats_out=st)
+                         grad_out=bn._grad_targets(), part=getattr(x, "_tdl_bn_part", None), stats_out=st,
+                         defer_apply=defer)
+    if defer:  # y is a stand-in: the reading 1x1 conv applies relu(bn(x)) in its operand loaders
+        y._tdl_bn_in = st[0]
     if g.relu and (r is not None or g.conv_reader) and y.is_cuda:
         # a conv reading this group's output can fuse the group's backward reduction into its
         # input-gradient epilogue (ops/conv.py): it needs the BN input, and for a plain BN -> ReLU

@@ -392,10 +392,13 @@ class Conv2D(Layer):
                                   grad_box=_grad_box, bn_stats=_bn_stats, bn_src=getattr(x, "_tdl_bn_src", None),
                                   bn_src2=getattr(x, "_tdl_bn_src2", None),
                                   bn_stats_src=getattr(x, "_tdl_bn_stats", None),
-                                  anchor=self.kernel.value if gt is not None else None)
+                                  anchor=self.kernel.value if gt is not None else None,
+                                  bn_in=getattr(x, "_tdl_bn_in", None))
             if b is not None:
                 y = y + b
             return self.activation(y)
+        if getattr(x, "_tdl_bn_in", None) is not None:  # (keras/fusion.py plans it only where the kernels run)
+            raise RuntimeError("Conv2D: a deferred BN -> ReLU input needs the hand-written 1x1 kernels")
         y = F.conv2d(h, w, b, stride=self.strides, padding=pad, dilation=self.dilation_rate, groups=self.groups)
         return self.activation(y.permute(0, 2, 3, 1))
 

@@ -55,16 +55,24 @@ def _debug(*key):
 class _BatchNormTrain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, residual, conv_bias, moving_mean, moving_var, momentum, eps, relu, grad_out,
-                part=None, stats_out=None):
+                part=None, stats_out=None, defer=False):
         C = hip()
         xc = _aligned(x)
         rc = _aligned(residual.to(xc.dtype)) if residual is not None else None
-        y, st = C.bn_forward_train(xc, gamma, beta, moving_mean, moving_var, float(momentum), float(eps), bool(relu),
-                                   rc, conv_bias.detach() if conv_bias is not None else None, part)
+        if defer:
+            # BN -> ReLU applied by its only reader, a 1x1 conv's operand loader (ops/conv.py bn_in): the
+            # statistics (and moving averages) only; the output is a stand-in view of the BN input
+            st = C.bn_stats_train(xc, gamma, beta, moving_mean, moving_var, float(momentum), float(eps),
+                                  conv_bias.detach() if conv_bias is not None else None, part)
+            y = xc.view_as(xc)
+        else:
+            y, st = C.bn_forward_train(xc, gamma, beta, moving_mean, moving_var, float(momentum), float(eps),
+                                       bool(relu), rc, conv_bias.detach() if conv_bias is not None else None, part)
         ctx.mode = 2 if residual is not None else (1 if relu else 0)
         if stats_out is not None:  # [4][C]: mean, invstd, scale, shift of this batch
             stats_out.append(st)
-        _debug("fwd", tuple(x.shape), ctx.mode, "stats-fused" if part is not None else "stats-pass")
+        _debug("fwd", tuple(x.shape), ctx.mode, "stats-fused" if part is not None else "stats-pass",
+               "apply-deferred" if defer else "apply")
         ctx.flags = (gamma is not None, beta is not None, residual is not None, conv_bias is not None)
         ctx.res_dtype = residual.dtype if residual is not None else None
         ctx.grad_out = grad_out
@@ -104,21 +112,25 @@ class _BatchNormTrain(torch.autograd.Function):
                 dres._tdl_bn_bwd_part = part2
         dcb = torch.zeros_like(conv_bias) if (has_cb and ctx.needs_input_grad[4]) else None
         return (dx, dgamma if ctx.needs_input_grad[1] else None, dbeta if ctx.needs_input_grad[2] else None, dres,
-                dcb, None, None, None, None, None, None, None, None)
+                dcb, None, None, None, None, None, None, None, None, None)
 
 
 def batch_norm_train(x: torch.Tensor, gamma: Optional[torch.Tensor], beta: Optional[torch.Tensor],
                      moving_mean: Optional[torch.Tensor], moving_var: Optional[torch.Tensor], momentum: float,
                      eps: float, relu: bool = False, residual: Optional[torch.Tensor] = None,
                      conv_bias: Optional[torch.Tensor] = None, grad_out=None, part=None,
-                     stats_out: Optional[list] = None) -> torch.Tensor:
+                     stats_out: Optional[list] = None, defer_apply: bool = False) -> torch.Tensor:
     """Keras-convention ``momentum`` (moving = moving*momentum + batch*(1-momentum)).
 
     ``grad_out = (dgamma_target, dbeta_target)``: f32 slab views the GPU backward ADDS the gamma /
     beta gradients into (Variable.grad_target); gamma / beta are then passed without autograd.
     ``part``: the batch statistics' partial sums already computed by the conv that produced x
     (ops/conv.py ``bn_stats``); the statistics pass over x is skipped.  ``stats_out``: a list the HIP
-    path appends the batch's [4][C] statistics (mean, invstd, scale, shift) to."""
+    path appends the batch's [4][C] statistics (mean, invstd, scale, shift) to.  ``defer_apply`` (HIP,
+    ``relu=True``, no residual, with ``stats_out``): statistics only -- the returned tensor is a view of
+    x standing for relu(bn(x)), valid only as the ``bn_in`` input of the one conv that applies it."""
+    if defer_apply and not (relu and residual is None and stats_out is not None and supported(x)):
+        raise ValueError("defer_apply: a GPU BN -> ReLU with stats_out")
     if residual is not None and not relu:
         raise ValueError("the fused residual form is BN -> Add -> ReLU")
     if supported(x) and (residual is None or tuple(residual.shape) == tuple(x.shape)):
@@ -126,7 +138,7 @@ def batch_norm_train(x: torch.Tensor, gamma: Optional[torch.Tensor], beta: Optio
             gamma = gamma.detach() if gamma is not None else None
             beta = beta.detach() if beta is not None else None
         return _BatchNormTrain.apply(x, gamma, beta, residual, conv_bias, moving_mean, moving_var, momentum, eps, relu,
-                                     grad_out, part, stats_out)
+                                     grad_out, part, stats_out, defer_apply)
     h = x if conv_bias is None else x + conv_bias.to(x.dtype)
     perm = [0, h.dim() - 1] + list(range(1, h.dim() - 1))
     hp = h.permute(*perm)

@@ -262,11 +262,12 @@ def _ref_fwd(x, w_oihw, stride, pad):
 class _Conv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, kernel, stride, pad, grad_out, w_ohwi=None, box=None, stats_out=None, bn_src=None,
-                bn_src2=None, anchor=None, bn_stats_src=None):
+                bn_src2=None, anchor=None, bn_stats_src=None, bn_in=None):
         C = hip()
         x = x.contiguous()
         if x.data_ptr() % 16:
             x = x.clone()
+        ctx.bn_in = bn_in
         kh, kw, cin, cout = kernel.shape
         sh, sw = stride
         ph, pw = pad
@@ -278,7 +279,13 @@ class _Conv(torch.autograd.Function):
         if w_ohwi is None:
             w_ohwi = kernel.permute(3, 0, 1, 2).contiguous()
         hip_fn = lambda: C.conv_fwd(x, w_ohwi, oh, ow, sh, sw, ph, pw)  # noqa: E731
-        if _pick(key, hip_fn, lambda: _ref_fwd(x, w_oihw, stride, pad), y_bytes if stats_out is not None else 0):
+        if bn_in is not None:
+            # x is a BN -> ReLU's input: the operand loader applies it (no library equivalent, no timing)
+            if stats_out is not None:
+                y, stats_out[0] = C.conv_fwd_stats(x, w_ohwi, oh, ow, sh, sw, ph, pw, in_bn=bn_in)
+            else:
+                y = C.conv_fwd(x, w_ohwi, oh, ow, sh, sw, ph, pw, in_bn=bn_in)
+        elif _pick(key, hip_fn, lambda: _ref_fwd(x, w_oihw, stride, pad), y_bytes if stats_out is not None else 0):
             if stats_out is not None:  # + the following batch norm's partial channel sums
                 y, stats_out[0] = C.conv_fwd_stats(x, w_ohwi, oh, ow, sh, sw, ph, pw)
             else:
@@ -312,12 +319,16 @@ class _Conv(torch.autograd.Function):
         w_oihw = kernel.permute(3, 2, 0, 1)
         x_nchw, dy_nchw = x.permute(0, 3, 1, 2), dy.permute(0, 3, 1, 2)
         kh, kw = kernel.shape[0], kernel.shape[1]
+        bn_in = ctx.bn_in
         gout = ctx.grad_out  # f32 HWIO slab view: dW is ADDED into it and not returned
         want_dx, want_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1] or gout is not None
         shape_key = (tuple(x.shape), tuple(kernel.shape), stride, pad)
         dx = dw = None
 
         def ref(mask):
+            if bn_in is not None:  # the library reads the materialised relu(bn(x)) (weight gradient only)
+                return lambda: _miopen_bwd(dy_nchw, _bn_relu_ref(x, bn_in).permute(0, 3, 1, 2) if mask[1] else x_nchw,
+                                           w_oihw, list(stride), list(pad), mask)
             return lambda: _miopen_bwd(dy_nchw, x_nchw, w_oihw, list(stride), list(pad), mask)
 
         box = ctx.box if (ctx.box is not None and ctx.box.active and want_dx) else None
@@ -375,9 +386,18 @@ class _Conv(torch.autograd.Function):
                     dx = hip_fn(other)
                 other = None
         if want_dw and x.shape[0] * dy.shape[1] * dy.shape[2] < (1 << 24):
-            plan = _pick_wgrad(("wgrad",) + shape_key, C, x, dy, kh, kw, stride, pad,
-                               lambda: ref([False, True, False])()[1])
-            if plan is not None:
+            if bn_in is not None:
+                plan = _pick_wgrad_bn_in(("wgrad_bn_in",) + shape_key, C, x, dy, bn_in)
+            else:
+                plan = _pick_wgrad(("wgrad",) + shape_key, C, x, dy, kh, kw, stride, pad,
+                                   lambda: ref([False, True, False])()[1])
+            if plan is not None and bn_in is not None:
+                if gout is not None:
+                    C.conv_wgrad(x, dy, 1, 1, 1, 1, 0, 0, out=gout, accumulate=True, plan=plan, in_bn=bn_in)
+                    want_dw = False
+                else:
+                    dw = C.conv_wgrad(x, dy, 1, 1, 1, 1, 0, 0, plan=plan, in_bn=bn_in)
+            elif plan is not None:
                 if gout is not None and _SIDE_STATE["open"] and x.is_cuda:
                     side = _side_stream(x.device)
                     side.wait_stream(torch.cuda.current_stream(x.device))
@@ -407,7 +427,35 @@ class _Conv(torch.autograd.Function):
             dx = dx + other.view_as(dx)
         if first:  # park this contribution for the other consumer's backward
             box.g, dx = dx, None
-        return dx, dw, None, None, None, None, None, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None, None, None, None, None, None
+
+
+def _bn_relu_ref(x, st):
+    """relu(x * scale + shift) with the BN apply pass's f32 arithmetic (st: [4][C] statistics)."""
+    return torch.relu(torch.addcmul(st[3], x.float(), st[2])).to(x.dtype)
+
+
+def _pick_wgrad_bn_in(key, C, x, dy, st):
+    """Weight gradient of a 1x1 conv over relu(bn(x)) (the input-side BN): the register-staged plans
+    only, timed among themselves on the first eager call (MIOpen would need the applied tensor)."""
+    if key in _choice:
+        return _choice[key]
+    n = 1 if mode() == "hip" or torch.cuda.is_current_stream_capturing() else int(os.environ.get("TDL_WGRAD_CANDIDATES", 6))
+    plans = [[p[0], p[1], p[3], p[4]] for p in C.conv_wgrad_plans(list(x.shape), list(dy.shape), 1, 1, 1, 1, 0, 0, n,
+                                                                    in_bn=True)]
+    if len(plans) == 1:
+        _choice[key] = plans[0]
+        return plans[0]
+
+    def decide():
+        ts = [_time(lambda: C.conv_wgrad(x, dy, 1, 1, 1, 1, 0, 0, plan=p, in_bn=st)) for p in plans]
+        i = min(range(len(plans)), key=ts.__getitem__)
+        _times[key] = (ts[i], float("nan"))
+        return plans[i]
+
+    best = _agree(decide, lambda v: [1] + [int(u) for u in v], lambda a: [int(u) for u in a[1:]])
+    _choice[key] = best
+    return best
 
 
 _DEBUG_PARTS = os.environ.get("TDL_DEBUG_BN_PARTS") == "1"
@@ -440,7 +488,7 @@ def _miopen_bwd(dy_nchw, x_nchw, w_oihw, stride, pad, mask):
 
 
 def conv2d_nhwc(x, kernel_hwio, stride=(1, 1), pad=(0, 0), grad_out=None, w_ohwi=None, grad_box=None,
-                bn_stats=False, bn_src=None, bn_src2=None, anchor=None, bn_stats_src=None):
+                bn_stats=False, bn_src=None, bn_src2=None, anchor=None, bn_stats_src=None, bn_in=None):
     """y[N,OH,OW,K] = conv(x[N,H,W,C], kernel[KH,KW,C,K]) with symmetric zero padding ``pad = (ph, pw)``,
     bf16; the caller checked :func:`supported`.  ``grad_out``: f32 [KH,KW,C,K] tensor the weight
     gradient is added into (a trainer's gradient slab view; ``kernel_hwio`` then needs no autograd);
@@ -456,10 +504,18 @@ def conv2d_nhwc(x, kernel_hwio, stride=(1, 1), pad=(0, 0), grad_out=None, w_ohwi
     backward runs although neither the input (the first layer's batch) nor the detached compute-dtype
     kernel needs a gradient (the kernel's gradient goes into ``grad_out``; the anchor gets none).
     ``bn_stats_src``: with ``bn_src`` of a plain BN -> ReLU group, that BN's [4][C] batch statistics: the
-    epilogue recomputes the ReLU mask from ``bn_src`` instead of reading x."""
+    epilogue recomputes the ReLU mask from ``bn_src`` instead of reading x.
+    ``bn_in``: x is the INPUT of a plain BN -> ReLU group and ``bn_in`` its [4][C] statistics (1x1 stride-1
+    unpadded convs): the forward and weight-gradient operand loaders apply relu(x * scale + shift), so
+    the group output is never written (keras/fusion.py ``defer``); pass ``bn_src=x, bn_stats_src=bn_in``
+    for the fused input-gradient epilogue."""
+    if bn_in is not None and not (tuple(kernel_hwio.shape[:2]) == (1, 1) and tuple(stride) == (1, 1)
+                                  and tuple(pad) == (0, 0) and bn_in.numel() == 4 * x.shape[-1] and x.shape[-1] <= 512):
+        raise ValueError("conv2d_nhwc: bn_in takes 1x1 stride-1 unpadded convolutions of <= 512 input channels "
+                         "and [4][C] statistics")
     holder = [None] if bn_stats else None
     y = _Conv.apply(x, kernel_hwio, tuple(stride), tuple(pad), grad_out, w_ohwi, grad_box, holder, bn_src, bn_src2,
-                    anchor, bn_stats_src)
+                    anchor, bn_stats_src, bn_in)
     if holder is not None and holder[0] is not None:
         y._tdl_bn_part = holder[0]
     return y

@@ -322,3 +322,92 @@ def test_stem_bn_relu_pool_fusion_trains_like_unfused():
     for a, b in zip(wf, wu):
         scale = max(float(np.abs(b).max()), 1e-3)
         np.testing.assert_allclose(a, b, atol=2e-2 * scale, rtol=2e-2)
+
+
+@pytest.mark.parametrize("shape", [(4, 14, 14, 64, 256), (2, 9, 11, 128, 192), (8, 7, 7, 512, 128)])
+def test_conv_input_side_bn_relu_matches_materialised_bitwise(shape):
+    """conv_fwd / conv_fwd_stats / conv_wgrad with in_bn=st over the BN input == the same kernels over
+    the BN -> ReLU pass's output (bitwise: the operand loaders use the apply pass's f32 fma and
+    rounding), for every weight-gradient plan the input-side BN takes (ragged pixel and tc tails)."""
+    from tensorflow_distributed_learning_amd.ops import hip
+
+    C = hip()
+    torch.manual_seed(7)
+    N, H, W, Ci, K = shape
+    x = (torch.randn(N, H, W, Ci, device="cuda:0") * 2 + 0.3).bfloat16()
+    g, b = torch.rand(Ci, device="cuda:0") + 0.5, torch.randn(Ci, device="cuda:0")
+    mm, mv = torch.zeros(Ci, device="cuda:0"), torch.ones(Ci, device="cuda:0")
+    y, st = C.bn_forward_train(x, g, b, mm, mv, 0.9, 1e-3, True, None, None)
+    w = (torch.randn(K, 1, 1, Ci, device="cuda:0") / Ci ** 0.5).bfloat16()
+    assert torch.equal(C.conv_fwd(y, w, H, W, 1, 1, 0, 0), C.conv_fwd(x, w, H, W, 1, 1, 0, 0, in_bn=st))
+    y0, p0 = C.conv_fwd_stats(y, w, H, W, 1, 1, 0, 0)
+    y1, p1 = C.conv_fwd_stats(x, w, H, W, 1, 1, 0, 0, in_bn=st)
+    P = (N * H * W + 127) // 128  # row-tile partial sums (the rows past them are the reduce's scratch)
+    assert torch.equal(y0, y1) and torch.equal(p0[:P], p1[:P])
+    dy = torch.randn(N, H, W, K, device="cuda:0").bfloat16()
+    plans = C.conv_wgrad_plans(list(x.shape), list(dy.shape), 1, 1, 1, 1, 0, 0, 8, in_bn=True)
+    assert plans and all(p[0] * p[1] <= 4 and p[4] == 0 for p in plans)
+    for p in plans:
+        plan = [p[0], p[1], p[3], p[4]]
+        a = C.conv_wgrad(y, dy, 1, 1, 1, 1, 0, 0, plan=plan)
+        c = C.conv_wgrad(x, dy, 1, 1, 1, 1, 0, 0, plan=plan, in_bn=st)
+        assert torch.equal(a, c), plan
+    with pytest.raises(RuntimeError):
+        C.conv_fwd(x, w, H, W, 1, 1, 0, 0, in_bn=st[:, :8].contiguous())
+
+
+def test_bn_apply_deferred_into_1x1_conv_trains_like_unfused():
+    """BN -> ReLU -> 1x1 Conv2D with the BN apply taken over by the conv's operand loaders
+    (keras/fusion.py ``defer``) trains like the materialised graph (TDL_FUSE_BN_INPUT=0): losses and
+    weights after three SGD steps, and the BN backward took its reduction from the conv epilogue."""
+    import os
+
+    import numpy as np
+    import tensorflow_distributed_learning_amd as tdl
+    from tensorflow_distributed_learning_amd.ops import batchnorm as BN
+
+    L = tdl.keras.layers
+
+    from tensorflow_distributed_learning_amd.keras import fusion
+
+    def run(fuse):
+        os.environ["TDL_FUSE_BN_INPUT"] = "1" if fuse else "0"
+        os.environ["TDL_CONV"] = "hip"  # the hand-written kernels everywhere (no timing-dependent choices)
+        min_px, fusion._DEFER_MIN_PIXELS = fusion._DEFER_MIN_PIXELS, 0  # (a small test image)
+        try:
+            tdl.keras.backend.clear_session()
+            tdl.keras.mixed_precision.set_global_policy("mixed_bfloat16")
+            tdl.keras.utils.set_random_seed(3)
+            inp = L.Input(shape=(12, 12, 64))
+            x = L.Conv2D(64, 3, padding="same")(inp)
+            x = L.BatchNormalization()(x)
+            x = L.Activation("relu")(x)
+            x = L.Conv2D(128, 1)(x)
+            x = L.BatchNormalization()(x)
+            x = L.Activation("relu")(x)
+            x = L.GlobalAveragePooling2D()(x)
+            with tdl.distribute.MirroredStrategy(devices=["/gpu:0"]).scope():
+                m = tdl.keras.Model(inp, L.Dense(10)(x))
+                m.compile(loss=tdl.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+                          optimizer=tdl.keras.optimizers.SGD(learning_rate=0.05))
+            gen = torch.Generator().manual_seed(0)
+            ds = tdl.data.Dataset.from_tensor_slices((torch.randn(96, 12, 12, 64, generator=gen),
+                                                      torch.randint(0, 10, (96,), generator=gen))).batch(32).repeat()
+            before = BN.FUSED_BWD_MODES[1]
+            h = m.fit(ds, epochs=1, steps_per_epoch=3, verbose=0)
+            deferred = any(gr.defer is not None for gr in m._fusion().groups.values())
+            return m.get_weights(), h.history["loss"], deferred, BN.FUSED_BWD_MODES[1] - before
+        finally:
+            os.environ.pop("TDL_FUSE_BN_INPUT", None)
+            os.environ.pop("TDL_CONV", None)
+            fusion._DEFER_MIN_PIXELS = min_px
+            tdl.keras.mixed_precision.set_global_policy("float32")
+
+    wf, lf, df, nf = run(True)
+    wu, lu, du, nu = run(False)
+    assert df and not du
+    assert nf >= 3 and nu >= 3  # both fuse the BN backward reduction into the 1x1 conv's dgrad
+    np.testing.assert_allclose(lf, lu, rtol=1e-2)
+    for a, b in zip(wf, wu):
+        scale = max(float(np.abs(b).max()), 1e-3)
+        np.testing.assert_allclose(a, b, atol=2e-2 * scale, rtol=2e-2)
