@@ -158,6 +158,37 @@ __device__ __forceinline__ u32x4 add_bf16x8(u32x4 a, u32x4 b) {
   return o;
 }
 
+// output row m -> (n, oh, ow).  m < 2^24 (every ResNet-50 shape up to b = 5000): one f32 multiply by
+// the reciprocal and a +-1 fix-up per quotient (exact: the product's error is < 2 / d), instead of the
+// ~30-instruction integer division sequences on the prologue's critical path (the row offsets gate the
+// first operand loads)
+__device__ __forceinline__ int fdiv_exact(int n, int d, float inv, int& rem) {
+  int q = (int)((float)n * inv);
+  int r = n - q * d;
+  if (r < 0) {
+    --q;
+    r += d;
+  } else if (r >= d) {
+    ++q;
+    r -= d;
+  }
+  rem = r;
+  return q;
+}
+
+__device__ __forceinline__ void split_row(const Igemm& a, int m, float inv_ow, float inv_oh, int& n, int& oh,
+                                          int& ow) {
+  if (a.M < (1 << 24)) {
+    const int t = fdiv_exact(m, a.OW, inv_ow, ow);
+    n = fdiv_exact(t, a.OH, inv_oh, oh);
+  } else {
+    ow = m % a.OW;
+    const int t = m / a.OW;
+    oh = t % a.OH;
+    n = t / a.OH;
+  }
+}
+
 __device__ __forceinline__ uint16_t f2bf(float f) {
   uint32_t u = __float_as_uint(f);
   u += 0x7fffu + ((u >> 16) & 1u);  // round to nearest even (activations are finite)
@@ -411,13 +442,21 @@ __global__ __launch_bounds__(BM * 2, DEPTH == 0 ? 4 : (DEPTH == 3 ? 3 : 2)) void
   const auto w_rsrc = buf_rsrc(a.w, (unsigned)((long long)a.KH * a.KW * a.C * a.K * 2));
   int a_vo[A_LD];
   uint32_t a_tap[A_LD];  // bit (kh * KW + kw): that tap of this row lies inside the image
+  // 1x1 stride 1 unpadded (same image and output grid): output row m reads image pixel m
+  const bool direct = a.KH == 1 && a.KW == 1 && a.SH == 1 && a.SW == 1 && a.PT == 0 && a.PL == 0 && a.H == a.OH &&
+                      a.W == a.OW;
+  const float inv_ow = 1.0f / (float)a.OW, inv_oh = 1.0f / (float)a.OH;
 #pragma unroll
   for (int i = 0; i < A_LD; ++i) {
     const int m = tm * BM + (tid >> 3) + RP * i;
     a_tap[i] = 0u;
     a_vo[i] = 0;
-    if (m < a.M) {
-      const int ow = m % a.OW, t = m / a.OW, oh = t % a.OH, n = t / a.OH;
+    if (m < a.M && direct) {
+      a_vo[i] = (int)(((long long)m * a.C + col8) * 2);
+      a_tap[i] = 1u;
+    } else if (m < a.M) {
+      int n, oh, ow;
+      split_row(a, m, inv_ow, inv_oh, n, oh, ow);
       const int ih = oh * a.SH - a.PT, iw = ow * a.SW - a.PL;
       a_vo[i] = (int)(((((long long)n * a.H + ih) * a.W + iw) * a.C + col8 + bias) * 2);
       for (int kh = 0; kh < a.KH; ++kh)
@@ -630,7 +669,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, MINW) void k_conv_glds(Igemm a) {
     const int m = tm * BM + row;
     a_tap[i] = 0u;
     a_vo[i] = 0;
-    if (m < a.M) {
+    if (m < a.M) {  // (integer division: the reciprocal form of split_row raises this kernel's prologue spills)
       const int ow = m % a.OW, t = m / a.OW, oh = t % a.OH, n = t / a.OH;
       const int ih = oh * a.SH - a.PT, iw = ow * a.SW - a.PL;
       a_vo[i] = (int)(((((long long)n * a.H + ih) * a.W + iw) * a.C + chunk * 8 + bias) * 2);
