@@ -10,6 +10,7 @@ Tensor bundle (``<prefix>.index`` + ``<prefix>.data-00000-of-00001``):
 Model directory (``model.save(path)``)::
 
     path/saved_model.json                       architecture + compile config
+    path/saved_model.pb                         SavedModel header: tags, serving signature, saver (ckpt/saved_model_pb.py)
     path/variables/variables.index
     path/variables/variables.data-00000-of-00001
     path/assets/
@@ -157,6 +158,16 @@ def save_model(model, path: str, overwrite: bool = True, include_optimizer: bool
         cfg["compile"] = model._compile_config
     with open(os.path.join(path, "saved_model.json"), "w") as f:
         json.dump(cfg, f, indent=1, default=str)
+    # the SavedModel protobuf header: tags, serving signature, V2 saver over variables/ (no TF graph)
+    from . import saved_model_pb as SMP
+
+    try:
+        spec = SMP.model_signature(model)
+    except (ValueError, AttributeError, TypeError, IndexError):
+        spec = None
+    if spec is not None:
+        with open(os.path.join(path, "saved_model.pb"), "wb") as f:
+            f.write(SMP.encode_saved_model(*spec))
     remove_temp_dirpath(path, strategy) if path != real else None
 
 
