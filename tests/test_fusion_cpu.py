@@ -45,6 +45,22 @@ def test_plan_shapes_resnet50():
     assert all(not g.res_bn.relu and g.res_bn.residual is None for g in res_bn)
 
 
+def test_plan_defers_bn2_apply_into_the_bottleneck_1x1_convs(monkeypatch):
+    """BN -> ReLU groups read only by a 1x1 stride-1 conv (each bottleneck's BN2) get ``defer``; the
+    stem (max-pool reader), the 3x3 readers (BN1) and the block outputs (Add) do not;
+    TDL_FUSE_BN_INPUT=0 turns it off.  (At run time _defer_ok also requires a GPU bf16 tensor.)"""
+    m = tdl.keras.applications.ResNet50(weights=None, classes=10, classifier_activation=None, input_shape=(32, 32, 3))
+    p = fusion.plan(m._nodes, m._outputs)
+    deferred = [g for g in p.groups.values() if g.defer is not None]
+    assert len(deferred) == 16  # one per bottleneck block
+    assert all(tuple(g.defer.kernel_size) == (1, 1) and g.relu and g.residual is None for g in deferred)
+    assert all(g.bn_node.layer.name.endswith("_2_bn") for g in deferred)
+    monkeypatch.setenv("TDL_FUSE_BN_INPUT", "0")
+    assert not any(g.defer is not None for g in fusion.plan(m._nodes, m._outputs).groups.values())
+    x = torch.zeros(2, 4, 4, 64)
+    assert not fusion._defer_ok(x)  # CPU tensor
+
+
 def _run(m, x, fuse):
     models._FUSE_CPU[0] = fuse
     try:
