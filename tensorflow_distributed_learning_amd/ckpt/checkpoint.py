@@ -163,7 +163,10 @@ def save_model(model, path: str, overwrite: bool = True, include_optimizer: bool
 
     try:
         spec = SMP.model_signature(model)
-    except (ValueError, AttributeError, TypeError, IndexError):
+    except Exception as e:  # the header is auxiliary: a model whose signature cannot be derived still saves
+        import warnings
+
+        warnings.warn(f"model.save: saved_model.pb skipped ({type(e).__name__}: {e})")
         spec = None
     if spec is not None:
         with open(os.path.join(path, "saved_model.pb"), "wb") as f:
