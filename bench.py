@@ -66,6 +66,7 @@ def main():
     from tensorflow_distributed_learning_amd.data import tfds
     from tensorflow_distributed_learning_amd.models.mnist_cnn import build_mnist_cnn
     from tensorflow_distributed_learning_amd.parallel import consistency
+    from tensorflow_distributed_learning_amd.parallel.launch import ipc_mode
 
     world = int(os.environ.get("WORLD_SIZE", "0") or 0)
     if world and world != args.gpus:
@@ -167,6 +168,10 @@ def main():
             "config": {"model": "tf_dist_example.py MNIST CNN (Conv32-Pool-Conv64-Pool-Dense128-Dense10, 225,034 params)",
                        "global_batch": B, "seq_len": None, "image_shape": [28, 28, 1],
                        "parallelism": f"dp{R}", "engine": trainer.kind, "communicator": comm.name,
+                       # what actually ran: the communicator class (torch RCCL process group, the
+                       # framework's own RCCL communicator, gloo + xGMI, local) and the HIP IPC mode
+                       # every replica was started with (parallel/launch.py REPLICA_SHARED_ENV)
+                       "communicator_impl": type(comm).__name__, "ipc_mode": ipc_mode(),
                        "allreduce": getattr(trainer, "allreduce_mode", None) or getattr(comm, "algorithm", comm.name),
                        "kernels_per_step": 2 if getattr(trainer, "_steps", None) and all(
                            getattr(st, "fused_bwd", False) for st in trainer._steps.values()) else None,

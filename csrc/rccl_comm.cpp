@@ -8,6 +8,7 @@
 #include <c10/hip/HIPStream.h>
 
 #include <atomic>
+#include <chrono>
 #include <cstring>
 #include <mutex>
 #include <stdexcept>
@@ -102,7 +103,9 @@ RcclComm::RcclComm(const std::string& uid, int rank, int world, int device)
 }
 
 RcclComm::~RcclComm() {
-  if (comm_ != nullptr && !aborted_) (void)api_.CommDestroy(comm_);
+  std::lock_guard<std::timed_mutex> lk(mu_);
+  if (comm_ != nullptr && !aborted_.load(std::memory_order_acquire)) (void)api_.CommDestroy(comm_);
+  comm_ = nullptr;
 }
 
 std::string RcclComm::unique_id() {
@@ -124,26 +127,31 @@ void RcclComm::check(int r, const char* what) const {
 }
 
 void RcclComm::all_reduce(void* sb, void* rb, size_t n, int dt, int op, hipStream_t s) {
-  if (aborted_) throw std::runtime_error("rccl: communicator was aborted");
+  std::lock_guard<std::timed_mutex> lk(mu_);
+  if (aborted_.load(std::memory_order_acquire)) throw std::runtime_error("rccl: communicator was aborted");
   check(api_.AllReduce(sb, rb, n, nccl_dtype(dt), nccl_op(op), comm_, s), "ncclAllReduce");
 }
 void RcclComm::broadcast(void* sb, void* rb, size_t n, int dt, int root, hipStream_t s) {
-  if (aborted_) throw std::runtime_error("rccl: communicator was aborted");
+  std::lock_guard<std::timed_mutex> lk(mu_);
+  if (aborted_.load(std::memory_order_acquire)) throw std::runtime_error("rccl: communicator was aborted");
   check(api_.Broadcast(sb, rb, n, nccl_dtype(dt), root, comm_, s), "ncclBroadcast");
 }
 void RcclComm::all_gather(void* sb, void* rb, size_t n, int dt, hipStream_t s) {
-  if (aborted_) throw std::runtime_error("rccl: communicator was aborted");
+  std::lock_guard<std::timed_mutex> lk(mu_);
+  if (aborted_.load(std::memory_order_acquire)) throw std::runtime_error("rccl: communicator was aborted");
   check(api_.AllGather(sb, rb, n, nccl_dtype(dt), comm_, s), "ncclAllGather");
 }
 void RcclComm::reduce_scatter(void* sb, void* rb, size_t n, int dt, int op, hipStream_t s) {
-  if (aborted_) throw std::runtime_error("rccl: communicator was aborted");
+  std::lock_guard<std::timed_mutex> lk(mu_);
+  if (aborted_.load(std::memory_order_acquire)) throw std::runtime_error("rccl: communicator was aborted");
   check(api_.ReduceScatter(sb, rb, n, nccl_dtype(dt), nccl_op(op), comm_, s), "ncclReduceScatter");
 }
-void RcclComm::group_start() { check(api_.GroupStart(), "ncclGroupStart"); }
+void RcclComm::group_start() { check(api_.GroupStart(), "ncclGroupStart"); }  // (no comm_ use)
 void RcclComm::group_end() { check(api_.GroupEnd(), "ncclGroupEnd"); }
 
 int RcclComm::async_error() {
-  if (aborted_) return -1;
+  std::lock_guard<std::timed_mutex> lk(mu_);
+  if (aborted_.load(std::memory_order_acquire)) return -1;
   Result e = 0;
   const Result r = api_.CommGetAsyncError(comm_, &e);
   if (r != 0) return r;
@@ -156,9 +164,11 @@ std::string RcclComm::error_string(int code) const {
 }
 
 void RcclComm::abort() {
-  if (aborted_ || comm_ == nullptr) return;
-  aborted_ = true;
-  (void)api_.CommAbort(comm_);
+  const bool locked = mu_.try_lock_for(std::chrono::seconds(5));
+  bool expected = false;
+  if (comm_ != nullptr && aborted_.compare_exchange_strong(expected, true, std::memory_order_acq_rel))
+    (void)api_.CommAbort(comm_);  // comm_ stays non-null: the destructor must not destroy it again
+  if (locked) mu_.unlock();
 }
 
 }  // namespace tdl_host

@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+#include <mutex>
 #include <string>
 
 namespace tdl_host {
@@ -47,14 +49,20 @@ class RcclComm {
   // ncclCommAbort: unblocks every pending collective of this communicator; safe from another
   // thread; the communicator is unusable afterwards
   void abort();
-  bool aborted() const { return aborted_; }
+  bool aborted() const { return aborted_.load(std::memory_order_acquire); }
 
  private:
   void check(int r, const char* what) const;
   const RcclApi& api_;
   void* comm_ = nullptr;
   int rank_, world_, device_;
-  bool aborted_ = false;
+  // abort() may run on the job watchdog's thread while the main thread enqueues: every use of comm_
+  // holds mu_ and re-checks aborted_ under it, so no enqueue starts on a communicator that abort()
+  // has freed.  abort() waits for the lock only a bounded time: an enqueue that is itself stuck
+  // inside RCCL (e.g. connection setup towards a dead peer) is exactly what ncclCommAbort exists to
+  // unblock, so after the wait it aborts regardless.
+  std::timed_mutex mu_;
+  std::atomic<bool> aborted_{false};
 };
 
 }  // namespace tdl_host

@@ -300,10 +300,16 @@ class _Conv(torch.autograd.Function):
                                 and bn_src.dtype == x.dtype) else None
         ctx.bn_src2 = bn_src2 if (ctx.bn_src is not None and bn_src2 is not None
                                   and tuple(bn_src2.shape) == tuple(x.shape) and bn_src2.dtype == x.dtype) else None
-        # a plain BN -> ReLU group's [4][C] statistics: the dgrad epilogue recomputes the mask from bn_src
-        ctx.bn_stats_src = bn_stats_src if (ctx.bn_src is not None and ctx.bn_src2 is None and _FUSE_BN_MASK_STATS[0]
+        # a plain BN -> ReLU group's [4][C] statistics: the dgrad epilogue recomputes the mask from bn_src.
+        # With bn_in (deferred BN -> ReLU) x IS the raw BN input, so a mask taken from x itself would be
+        # [x > 0] instead of [x*scale + shift > 0]: the statistics are then mandatory, whatever the A/B switch.
+        ctx.bn_stats_src = bn_stats_src if (ctx.bn_src is not None and ctx.bn_src2 is None
+                                            and (_FUSE_BN_MASK_STATS[0] or bn_in is not None)
                                             and bn_stats_src is not None
                                             and bn_stats_src.numel() == 4 * x.shape[-1]) else None
+        if bn_in is not None and ctx.bn_src is not None and ctx.bn_stats_src is None:
+            # no statistics to rebuild the mask from: skip the fused BN epilogue (plain dgrad + BN backward)
+            ctx.bn_src = None
         if box is not None:
             box.n += 1
         return y

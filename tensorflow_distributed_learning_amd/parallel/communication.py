@@ -19,11 +19,12 @@ from typing import Optional
 
 def default_timeout() -> float:
     """Seconds a collective may wait for its peers before the job fails (process-group timeout,
-    the xGMI kernels' bounded waits, the progress watchdog).  TF's collectives wait for ever; a
-    synchronous job whose peer is live but out of step should end in about two minutes, not the
-    30 of torch's default.  ``TDL_COLLECTIVE_TIMEOUT`` overrides; ``CommunicationOptions.timeout_seconds``
-    overrides per strategy."""
-    return float(os.environ.get("TDL_COLLECTIVE_TIMEOUT", "120"))
+    the xGMI kernels' bounded waits, the progress watchdog's base threshold).  TF's collectives wait
+    for ever; a synchronous job whose peer is live but out of step should end in minutes, not the 30
+    of torch's default -- but a healthy job must never hit it (a slow first step, a long execution, a
+    chief-only checkpoint), hence 10 minutes.  ``TDL_COLLECTIVE_TIMEOUT`` overrides;
+    ``CommunicationOptions.timeout_seconds`` overrides per strategy."""
+    return float(os.environ.get("TDL_COLLECTIVE_TIMEOUT", "600"))
 
 
 def collective_timeout(opts) -> float:

@@ -364,6 +364,10 @@ class NativeRcclCommunicator(TorchCommunicator):
 
     Selected with ``TDL_NATIVE_RCCL=1`` for GPU replicas (``CollectiveCommunication.NCCL`` / ``AUTO``)."""
 
+    # communicators created so far by this process; every rank creates them in the same order
+    # (collective construction), so the count is the same everywhere and versions the id key
+    _generation = 0
+
     def __init__(self, rank: int, world_size: int, device: torch.device, store=None,
                  timeout: Optional[float] = None):
         super().__init__("gloo", rank, world_size, device, store=store, timeout=timeout)
@@ -375,7 +379,11 @@ class NativeRcclCommunicator(TorchCommunicator):
 
         C = ops.hip()
         kv = c10d._get_default_store()
-        key = "tdl/rccl/unique_id"
+        # one key per communicator generation: a second communicator of the same job (strategy
+        # re-created, tests) must never read the previous generation's id (mismatched comms hang)
+        gen = NativeRcclCommunicator._generation
+        NativeRcclCommunicator._generation += 1
+        key = f"tdl/rccl/unique_id/{gen}"
         if rank == 0:
             kv.set(key, C.RcclComm.unique_id())
         uid = kv.get(key)
@@ -405,7 +413,12 @@ class NativeRcclCommunicator(TorchCommunicator):
             raise ValueError(f"unknown reduce op {op}")
         if op == "mean" and not t.is_floating_point():
             raise ValueError("mean all-reduce of an integer tensor")
-        self.rccl.all_reduce(t if t.is_contiguous() else t.contiguous(), self._OPC[op])
+        if t.is_contiguous():
+            self.rccl.all_reduce(t, self._OPC[op])
+        else:  # reduce a contiguous copy, then write the result back into t
+            c = t.contiguous()
+            self.rccl.all_reduce(c, self._OPC[op])
+            t.copy_(c)
         return t
 
     def all_reduce_async(self, t, op="sum"):

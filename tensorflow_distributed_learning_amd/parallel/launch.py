@@ -112,9 +112,23 @@ class _Group:
             return 130
 
 
+# Environment every replica of a job must share, replica 0 included, set before any HIP call.
+# HSA_ENABLE_IPC_MODE_LEGACY=0: HIP IPC through dmabuf file descriptors -- the only IPC mode the
+# MI355X hosts' kernel driver supports; in legacy mode hipIpcGetMemHandle fails with "invalid
+# argument", which breaks RCCL's P2P transport and the xGMI kernel's peer-buffer mapping.  A job
+# whose replicas disagree on it cannot map each other's buffers.
+REPLICA_SHARED_ENV = {"HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+
+
+def ipc_mode() -> str:
+    """The IPC mode this process runs with ("dmabuf" or "legacy"), for the bench JSON."""
+    return "legacy" if os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0") == "1" else "dmabuf"
+
+
 def _base_env(nprocs: int = 1) -> Dict[str, str]:
     env = dict(os.environ)
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    for k, v in REPLICA_SHARED_ENV.items():
+        env.setdefault(k, v)
     if "OMP_NUM_THREADS" not in env:
         # one replica process per GPU: do not let every process spawn a thread per core
         env["OMP_NUM_THREADS"] = str(max(1, (os.cpu_count() or 1) // max(1, nprocs)))
@@ -216,15 +230,11 @@ def maybe_spawn_local_replicas(n: int, spawn: Optional[bool] = None) -> Optional
         sys.stderr.write(f"[tdl] WARNING: {n} devices requested, running 1 replica ({why})\n")
         return None
     port = free_port()
-    env0 = _base_env(n)
+    own, children = spawn_envs(n, port)
     g = _Group()
-    for lr in range(1, n):
-        env = dict(env0)
-        env.update(RANK=str(lr), WORLD_SIZE=str(n), LOCAL_RANK=str(lr), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TDL_LAUNCHED="1")
+    for env in children:
         g.start(argv, env)
-    os.environ.update(RANK="0", WORLD_SIZE=str(n), LOCAL_RANK="0", LOCAL_WORLD_SIZE=str(n),
-                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TDL_LAUNCHED="1")
+    os.environ.update(own)
     _SPAWNED = g
     _supervise(g)
 
@@ -240,6 +250,24 @@ def maybe_spawn_local_replicas(n: int, spawn: Optional[bool] = None) -> Optional
 
     atexit.register(_join)
     return {"rank": 0, "world_size": n, "local_rank": 0, "local_world_size": n}
+
+
+def spawn_envs(n: int, port: int):
+    """Environments of a self-spawned group of n replicas: (the updates replica 0 applies to its
+    own environment, the full environments of replicas 1 .. n-1).  Every replica-shared variable
+    (REPLICA_SHARED_ENV) gets the same value in all n, replica 0 included -- it keeps its own value
+    where it has one, and the children inherit that value."""
+    env0 = _base_env(n)
+    shared = {k: env0[k] for k in REPLICA_SHARED_ENV}
+    own = dict(shared, RANK="0", WORLD_SIZE=str(n), LOCAL_RANK="0", LOCAL_WORLD_SIZE=str(n),
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TDL_LAUNCHED="1")
+    children = []
+    for lr in range(1, n):
+        env = dict(env0)
+        env.update(RANK=str(lr), WORLD_SIZE=str(n), LOCAL_RANK=str(lr), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TDL_LAUNCHED="1")
+        children.append(env)
+    return own, children
 
 
 def _supervise(g: "_Group", poll: float = 0.2) -> threading.Thread:

@@ -359,6 +359,11 @@ def _select_communicator(impl: CommunicationImplementation, device: torch.device
                                  timeout=timeout)
         comm.enable_xgmi(timeout)
         return comm
+    # Default: torch's RCCL process group (ProcessGroupNCCL over the same librccl).  The framework's
+    # own communicator stays opt-in because no multi-rank RCCL run is possible on the one-GPU
+    # development box (RCCL refuses two ranks on one device), so its world >= 2 path has never
+    # executed, while torch's group has; the abort path is wired either way (the job watchdog's
+    # on_abort is communicator.abort: ncclCommAbort through torch's group or through ours).
     if os.environ.get("TDL_NATIVE_RCCL") == "1":
         # the framework's own RCCL communicator (csrc/rccl_comm.cpp: async-error query, abort)
         from .communicator import NativeRcclCommunicator

@@ -57,11 +57,13 @@ class XgmiAllReduce:
         # bounded in-kernel waits: a peer that does not arrive within this many seconds sets the
         # device's error word; every later exchange then returns at entry and the host raises at the
         # next health check (log read / execution boundary).  Default: the job's collective timeout
-        # (the process group's), so a slow but live peer is no more fatal here than under RCCL
+        # (the process group's), so a slow but live peer is no more fatal here than under RCCL --
+        # capped at 120 s: a GPU spinning in an exchange holds its queue, and the peers of a
+        # synchronous step arrive within milliseconds of each other when they are alive
         if timeout is None:
             from .communication import default_timeout
 
-            timeout = default_timeout()
+            timeout = min(default_timeout(), 120.0)
         self.timeout = float(os.environ.get("TDL_XGMI_TIMEOUT", timeout))
         self.limit = max_bytes() // 4
         self._chans: Dict[int, object] = {}

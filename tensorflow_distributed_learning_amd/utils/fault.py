@@ -95,17 +95,36 @@ def maybe_skip_collective(rank: int, step: int) -> bool:
     return True
 
 
-# this rank's training progress, published by its watchdog thread: [executions done, busy flag].
-# busy = the host is inside a training execution or its log read (waiting on the device or on
-# peers); a rank that stays busy without progressing for ``stall_after`` seconds is stuck
-_PROGRESS = [0, False]
+# this rank's training progress, published by its watchdog thread: [steps done, busy flag, seconds
+# the last execution took].  busy = the host is inside a training execution or its log read (waiting
+# on the device or on peers); a rank that stays busy without progressing for longer than its stall
+# threshold is stuck
+_PROGRESS = [0, False, 0.0]
+_BUSY_SINCE = [None]
 
 
 def note_progress(count: Optional[int] = None, busy: Optional[bool] = None) -> None:
     if count is not None:
         _PROGRESS[0] = int(count)
+        if _BUSY_SINCE[0] is not None:  # an execution just completed: remember how long it took
+            _PROGRESS[2] = time.monotonic() - _BUSY_SINCE[0]
+            _BUSY_SINCE[0] = time.monotonic()
     if busy is not None:
         _PROGRESS[1] = bool(busy)
+        _BUSY_SINCE[0] = time.monotonic() if busy else None
+
+
+def stall_threshold(base: float, explicit: bool, count: int, last_exec_s: float) -> float:
+    """Seconds a busy rank may go without progress before the job is declared stuck.
+
+    An explicit ``TDL_STALL_TIMEOUT`` is taken as is.  Otherwise the threshold is the collective
+    timeout, stretched to 10x the rank's own last execution (a long ``steps_per_execution`` or a
+    chief-only checkpoint is not a stall), and the first execution (autotuning, graph capture,
+    first-use compilation) gets 3x that and at least 15 minutes."""
+    if explicit:
+        return base
+    t = max(base, 10.0 * last_exec_s)
+    return max(3.0 * t, 900.0) if count == 0 else t
 
 
 def check() -> None:
@@ -131,6 +150,7 @@ class PeerWatchdog:
         # a live rank (heartbeat fine) stuck inside an execution: a collective a peer never joins,
         # or a device wait that never ends (an all-reduce inside a replayed hipGraph is invisible
         # to the process group's own timeout)
+        self._stall_explicit = "TDL_STALL_TIMEOUT" in os.environ
         self.stall_after = float(os.environ.get("TDL_STALL_TIMEOUT", stall_after or default_timeout()))
         self._published = None
         self._seen = {}  # chief: rank -> (progress record, monotonic time it last changed)
@@ -174,7 +194,7 @@ class PeerWatchdog:
         return self._stall_scan()
 
     def _publish_progress(self):
-        rec = f"{_PROGRESS[0]} {int(_PROGRESS[1])}"
+        rec = f"{_PROGRESS[0]} {int(_PROGRESS[1])} {_PROGRESS[2]:.3f}"
         if rec != self._published:
             self._client.set(f"progress/{self.rank}", rec.encode())
             self._published = rec
@@ -195,15 +215,17 @@ class PeerWatchdog:
             if prev is None or prev[0] != rec:
                 self._seen[r] = (rec, now)
                 prev = self._seen[r]
-            n, busy = rec.split()
+            f = rec.split()
+            n, busy, last = f[0], f[1], float(f[2]) if len(f) > 2 else 0.0
             counts[r] = int(n)
-            if busy == "1" and now - prev[1] > self.stall_after:
+            lim = stall_threshold(self.stall_after, self._stall_explicit, int(n), last)
+            if busy == "1" and now - prev[1] > lim:
                 stuck.append(r)
         if not stuck:
             return None
         where = ", ".join(f"rank {r} at execution {counts[r]}" for r in stuck)
         others = ", ".join(f"rank {r}: {c}" for r, c in sorted(counts.items()) if r not in stuck)
-        return (f"no training progress for {self.stall_after:.0f}s on {where} (heartbeats alive: a collective a peer "
+        return (f"no training progress past the stall threshold ({self.stall_after:.0f}s base) on {where} (heartbeats alive: a collective a peer "
                 f"never joined, or a hung device wait){'; ' + others if others else ''}")
 
     def _abort(self, reason: str):

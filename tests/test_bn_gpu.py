@@ -356,11 +356,16 @@ def test_conv_input_side_bn_relu_matches_materialised_bitwise(shape):
         C.conv_fwd(x, w, H, W, 1, 1, 0, 0, in_bn=st[:, :8].contiguous())
 
 
-def test_bn_apply_deferred_into_1x1_conv_trains_like_unfused():
+@pytest.mark.parametrize("mask_stats", [True, False])
+def test_bn_apply_deferred_into_1x1_conv_trains_like_unfused(mask_stats):
     """BN -> ReLU -> 1x1 Conv2D with the BN apply taken over by the conv's operand loaders
     (keras/fusion.py ``defer``) trains like the materialised graph (TDL_FUSE_BN_INPUT=0): losses and
-    weights after three SGD steps, and the BN backward took its reduction from the conv epilogue."""
+    weights after three SGD steps, and the BN backward took its reduction from the conv epilogue.
+    With the mask-statistics A/B switch off (TDL_FUSE_BN_MASK_STATS=0) the deferred group must still
+    build its ReLU mask from [x*scale + shift > 0], never from the raw BN input x."""
     import os
+
+    from tensorflow_distributed_learning_amd.ops import conv as CV
 
     import numpy as np
     import tensorflow_distributed_learning_amd as tdl
@@ -374,6 +379,7 @@ def test_bn_apply_deferred_into_1x1_conv_trains_like_unfused():
         os.environ["TDL_FUSE_BN_INPUT"] = "1" if fuse else "0"
         os.environ["TDL_CONV"] = "hip"  # the hand-written kernels everywhere (no timing-dependent choices)
         min_px, fusion._DEFER_MIN_PIXELS = fusion._DEFER_MIN_PIXELS, 0  # (a small test image)
+        ms, CV._FUSE_BN_MASK_STATS[0] = CV._FUSE_BN_MASK_STATS[0], mask_stats
         try:
             tdl.keras.backend.clear_session()
             tdl.keras.mixed_precision.set_global_policy("mixed_bfloat16")
@@ -401,12 +407,14 @@ def test_bn_apply_deferred_into_1x1_conv_trains_like_unfused():
             os.environ.pop("TDL_FUSE_BN_INPUT", None)
             os.environ.pop("TDL_CONV", None)
             fusion._DEFER_MIN_PIXELS = min_px
+            CV._FUSE_BN_MASK_STATS[0] = ms
             tdl.keras.mixed_precision.set_global_policy("float32")
 
     wf, lf, df, nf = run(True)
     wu, lu, du, nu = run(False)
     assert df and not du
-    assert nf >= 3 and nu >= 3  # both fuse the BN backward reduction into the 1x1 conv's dgrad
+    if mask_stats:
+        assert nf >= 3 and nu >= 3  # both fuse the BN backward reduction into the 1x1 conv's dgrad
     np.testing.assert_allclose(lf, lu, rtol=1e-2)
     for a, b in zip(wf, wu):
         scale = max(float(np.abs(b).max()), 1e-3)

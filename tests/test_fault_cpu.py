@@ -237,3 +237,15 @@ def test_live_rank_out_of_step_ends_the_job(tmp_path):
     assert any("no training progress" in e or "replica" in e.lower() or "timed out" in e.lower()
                for _, _, e in outs), [e[-1500:] for _, _, e in outs]
     assert time.time() - t0 < 90
+
+
+def test_stall_threshold_is_generous_by_default_and_exact_when_set():
+    """The progress watchdog never aborts a healthy job: its default threshold stretches to 10x the
+    rank's last execution and the first execution (autotune, capture) gets at least 15 minutes; an
+    explicit TDL_STALL_TIMEOUT is taken as is (120 s used to abort long executions)."""
+    from tensorflow_distributed_learning_amd.utils.fault import stall_threshold
+
+    assert stall_threshold(600.0, False, 5, 1.0) == 600.0
+    assert stall_threshold(600.0, False, 5, 200.0) == 2000.0  # a 200 s execution is not a stall
+    assert stall_threshold(120.0, False, 0, 0.0) == 900.0  # first execution
+    assert stall_threshold(8.0, True, 0, 500.0) == 8.0  # explicit: exact
