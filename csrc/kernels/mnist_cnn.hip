@@ -694,8 +694,10 @@ constexpr int kDcF = 15, kDcFStride = 20;
 constexpr int kLdsFwdFused = kLdsFwd + kDcF * kDcF * kDcFStride;
 // conv2 wgrad row tiles (first, count) per wave of the fused backward: waves w and w + 4 share a
 // SIMD; with tap skipping the dgrad MFMAs per SIMD are 192 / 168 / 144 / 144, so SIMDs 0..3 take
-// 4 / 4 / 5 / 6 of the 19 tiles (292 / 268 / 269 / 294 MFMAs per SIMD)
-__constant__ int kFusedWgradTiles[8][2] = {{0, 2}, {2, 2}, {4, 3}, {7, 3}, {10, 2}, {12, 2}, {14, 2}, {16, 3}};
+// 4 / 4 / 5 / 5 of the 18 kernel-row tiles (292 / 268 / 269 / 269 MFMAs per SIMD).  The bias row
+// (db2 = the column sums of dC2 = the sums of the masked dP2 over the pool windows) is summed on
+// the VALU in the dP2 phase instead of a 19th MFMA tile against a unit vector.
+__constant__ int kFusedWgradTiles[8][2] = {{0, 2}, {2, 2}, {4, 3}, {7, 3}, {10, 2}, {12, 2}, {14, 2}, {16, 2}};
 
 // phase stamp k < 4 of the fused backward, per wave, after the head stamps:
 // buf[grid*72 + (workgroup*8 + wave)*4 + k] (the buffer then holds grid * 104 words)
@@ -704,27 +706,23 @@ __device__ __forceinline__ void bwd_stamp(unsigned long long* buf, int k) {
     buf[(size_t)gridDim.x * 72 + (blockIdx.x * 8 + (threadIdx.x >> 6)) * 4 + k] = __builtin_amdgcn_s_memrealtime();
 }
 
-// N consecutive conv2 wgrad row tiles t0 .. t0+N-1 (tile 18 = the bias row: A = unit vector) of
-// the fused backward, advanced together over the 25 k-steps; stores part2 rows of image bi.
+// N consecutive conv2 wgrad row tiles t0 .. t0+N-1 (kernel rows 16 t .. 16 t + 15) of the fused
+// backward, advanced together over the 25 k-steps; stores part2 rows of image bi.
 template <int N>
 __device__ __forceinline__ void fused_wgrad_tiles(const MnistArgs& a, int bi, int cq, int t0, const float* P1s,
                                                   const float* dCs) {
   const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
   const float* pa0[N];
-  bool bias[N];
 #pragma unroll
   for (int u = 0; u < N; ++u) {
-    const int mt = t0 + u;
-    bias[u] = mt == 18;
-    const int k = mt * 16 + i;
-    const int tap = bias[u] ? 0 : k >> 5, ci = k & 31;
+    const int k = (t0 + u) * 16 + i;
+    const int tap = k >> 5, ci = k & 31;
     const int kh = tap / 3, kw = tap - kh * 3;
     pa0[u] = P1s + (kh * 13 + kw + g) * kP1Stride + ci;
   }
   // positions p = 10q + r + g; for r = 8 lanes g >= 2 wrap to the next row: +3 P1 cells, +5 dC cells
   const int wrapA = g >= 2 ? 3 * kP1Stride : 0, wrapB = g >= 2 ? 5 * kDcFStride : 0;
   const float* pb0 = dCs + (2 * kDcF + 2 + g) * kDcFStride + i;
-  const float unit_a = (i == 0) ? 1.f : 0.f;
   f4 acc[N];
 #pragma unroll
   for (int u = 0; u < N; ++u) acc[u] = zero4();
@@ -754,7 +752,7 @@ __device__ __forceinline__ void fused_wgrad_tiles(const MnistArgs& a, int bi, in
     for (int j = 0; j < kS; ++j) {
       if (blk * kS + j >= 25) break;
 #pragma unroll
-      for (int u = 0; u < N; ++u) acc[u] = mfma16x16x4(bias[u] ? unit_a : av[blk & 1][j][u], bv[blk & 1][j], acc[u]);
+      for (int u = 0; u < N; ++u) acc[u] = mfma16x16x4(av[blk & 1][j][u], bv[blk & 1][j], acc[u]);
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -763,10 +761,7 @@ __device__ __forceinline__ void fused_wgrad_tiles(const MnistArgs& a, int bi, in
   // kernel-end write-back (MI355X_MICROARCH.md: boundary + dirty bytes / 6 TB/s; publish-large)
   const auto rs = buf_rsrc(a.part2 + (size_t)bi * kP2QuadFloats, kP2QuadFloats * 4);
 #pragma unroll
-  for (int u = 0; u < N; ++u) {
-    const int qd = (t0 + u) * 4 + g;
-    if (qd < kP2Quads) st4_sc1(rs, ((qd * 64 + 16 * cq + i) * 4) * 4, acc[u]);
-  }
+  for (int u = 0; u < N; ++u) st4_sc1(rs, ((((t0 + u) * 4 + g) * 64 + 16 * cq + i) * 4) * 4, acc[u]);
 }
 
 // ---- fused conv backward of one (image bi, channel quarter cq) workgroup, after its dP2 ----
@@ -778,23 +773,8 @@ __device__ __forceinline__ void fused_conv_bwd(const MnistArgs& a, int bi, int c
                                                const float* xs, float* dCs, float* red) {
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int i = lane & 15, g = lane >> 4;
-  // dC2 grid: cell (y + 2, x + 2), channel c gets dP2 of window (y/2, x/2) where the pool-2 argmax
-  // is (y & 1) * 2 + (x & 1); zero elsewhere (border, row / column 10 of the 11 x 11 conv output)
-  for (int e4 = tid; e4 < kDcF * kDcF * (kDcFStride / 4); e4 += 512) {
-    const int cell = e4 / (kDcFStride / 4), c4 = e4 - cell * (kDcFStride / 4);
-    const int y = cell / kDcF - 2, x = cell - (cell / kDcF) * kDcF - 2;
-    f4 v = zero4();
-    if (c4 < 4 && y >= 0 && y < 10 && x >= 0 && x < 10) {
-      const int wo = (y >> 1) * 5 + (x >> 1);
-      const unsigned s = (unsigned)((y & 1) * 2 + (x & 1));
-      const f4 d = ld4(dp2s + wo * 16 + c4 * 4);
-      const unsigned q = *reinterpret_cast<const unsigned*>(a2s + wo * 16 + c4 * 4);
-      v = f4{(q & 0xffu) == s ? d.x : 0.f, ((q >> 8) & 0xffu) == s ? d.y : 0.f, ((q >> 16) & 0xffu) == s ? d.z : 0.f,
-             (q >> 24) == s ? d.w : 0.f};
-    }
-    st4(dCs + e4 * 4, v);
-  }
-  lds_barrier();
+  // (the dC2 grid dCs is complete: zeroed during conv2, the masked dP2 values scattered to their
+  // pool-2 argmax cells by the dP2 phase, behind the caller's barrier)
   bwd_stamp(a.stamps, 0);
   // this wave's conv2 dgrad operands W2[tap][16nt + i][16cq + 4g .. +3] (L2): issued now, consumed
   // after the wgrad (issued any earlier, the compiler's vmcnt bookkeeping stalled dP2 on them)
@@ -990,18 +970,17 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   __syncthreads();
   stamp(a.stamps, 2);
   // ---- dense1 operand prefetch, overlapping the convolutions: thread (row group rg, 4 columns n4)
-  // needs W3 rows of features kk = 25 rg .. 25 rg + 24 of this quarter (feature kk = window
-  // (kk >> 4), channel 16cq + (kk & 15)).  The 25 16-B loads per thread (205 KB per workgroup,
-  // ~1.3 us of the CU's texture-address rate) are spread over the conv phases in small groups:
-  // issued back to back they fill the CU's vector-memory queue and every wave stalls behind them
-  // (measured: conv1 3.4-4.4 us instead of ~1 us).
+  // needs the W3 rows of this quarter's features kk = 16 j + rg, j = 0 .. 24 (feature kk = window
+  // j, channel 16cq + rg: W3 row 64 j + 16cq + rg), so its 25 loads sit at ONE per-thread base plus
+  // compile-time strides of 64 rows (a feature split by row group, 25 consecutive features per
+  // thread, cost ~8 VALU of 64-bit address arithmetic per load: 200 per wave).  The 25 16-B loads
+  // per thread (205 KB per workgroup, ~1.3 us of the CU's texture-address rate) are spread over the
+  // conv phases in small groups: issued back to back they fill the CU's vector-memory queue and
+  // every wave stalls behind them (measured: conv1 3.4-4.4 us instead of ~1 us).
   const int n4 = (tid & 31) * 4, rg = tid >> 5;
   f4 w3v[25];
-  const float* w3b = a.W + a.ow3 + n4;
-  auto ldw3 = [&](int j) {
-    const int kk = rg * 25 + j;
-    w3v[j] = ld4(w3b + (size_t)((kk >> 4) * 64 + 16 * cq + (kk & 15)) * 128);
-  };
+  const float* w3b = a.W + a.ow3 + (size_t)(16 * cq + rg) * 128 + n4;
+  auto ldw3 = [&](int j) { w3v[j] = ld4(w3b + j * 64 * 128); };
 #pragma unroll
   for (int j = 0; j < 6; ++j) ldw3(j);
   // ---- conv1 on MFMA (K = 9 taps padded to 12): rows = 676 conv1 positions in pool-window-major
@@ -1131,13 +1110,20 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   } else {
 #pragma unroll
     for (int j = 16; j < 25; ++j) ldw3(j);
+    if (a.head == 1 && a.dp2_fwd && a.fused_bwd) {
+      // wave 7 has no conv2 tile: it zeroes the fused backward's dC2 grid meanwhile (the dP2 phase
+      // only scatters the masked dP2 values to their pool-2 argmax cells; every other cell -- the
+      // zero border, the non-argmax cells, row / column 10 of the 11 x 11 conv output -- stays 0)
+      float* dCs = red + 16 * 128 + 4 + 128;
+      for (int e4 = lane; e4 < kDcF * kDcF * kDcFStride / 4; e4 += 64) st4(dCs + e4 * 4, zero4());
+    }
   }
   __syncthreads();
   // ---- dense1 quarter partial: 25 features x 4 columns per thread, 16 row groups reduced in LDS
   {
     f4 hs = zero4();
 #pragma unroll
-    for (int j = 0; j < 25; ++j) hs += p2s[rg * 25 + j] * w3v[j];
+    for (int j = 0; j < 25; ++j) hs += p2s[j * 16 + rg] * w3v[j];
     st4(red + rg * 128 + n4, hs);
   }
   lds_barrier();
@@ -1214,22 +1200,40 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
     v[j] = (p.x + p.y) + (p.z + p.w);
   }
   // sum over the 32 lanes of the row group (column groups n4): reduce-scatter butterfly, lane
-  // (l & 31) ends with feature rg * 25 + (l & 31) (features 25..31 are zero padding)
+  // (l & 31) ends with feature 16 (l & 31) + rg (j = l & 31 >= 25: zero padding)
   const float d = reduce_scatter32<25>(v, lane);
   const int j = lane & 31;
   if (a.fused_bwd) {
-    // masked dP2 of this quarter stays in LDS (over P2, which this lane alone reads here)
+    // the conv2-output gradient dC2 directly: the masked dP2 value of window j, channel rg goes to
+    // its pool-2 argmax cell of the (zeroed) dC2 grid; every other cell of the window is 0
+    float* dCs = red + 16 * 128 + 4 + 128;
+    float val = 0.f;
     if (j < 25) {
-      const int kk = rg * 25 + j;
-      p2s[kk] = p2s[kk] > 0.f ? d : 0.f;
+      const int kk = j * 16 + rg;
+      val = p2s[kk] > 0.f ? d : 0.f;
+      const unsigned am = a2s[kk];
+      const int ph = (j * 13) >> 6, pw = j - 5 * ph;  // j / 5, j % 5 for j < 25
+      const int y = 2 * ph + (int)(am >> 1), x = 2 * pw + (int)(am & 1u);
+      dCs[((y + 2) * kDcF + x + 2) * kDcFStride + rg] = val;
+    }
+    // db2 of channel 16cq + rg (the dW2 bias row) = the sum of dC2 over the conv2 positions = the
+    // half-wave sum of the masked dP2 values (fixed butterfly order: bit-identical replicas)
+    float sb = rs_swap16(val, val);
+    sb += dpp_xor8(sb);
+    sb += dpp_mirror8(sb);
+    sb += dpp_xor2(sb);
+    sb += dpp_xor1(sb);
+    if (j == 0) {
+      const auto rs = buf_rsrc(a.part2 + (size_t)bi * kP2QuadFloats, kP2QuadFloats * 4);
+      st4_sc1(rs, (((kP2Quads - 1) * 64 + 16 * cq + rg) * 4) * 4, f4{sb, 0.f, 0.f, 0.f});
     }
     lds_barrier();
-    fused_conv_bwd(a, bi, cq, p2s, a2s, P1s, a1s, xs, red + 16 * 128 + 4 + 128, red);
+    fused_conv_bwd(a, bi, cq, p2s, a2s, P1s, a1s, xs, dCs, red);
     return;
   }
   if (j < 25) {
-    const int kk = rg * 25 + j;
-    a.dP2[(size_t)bi * 1600 + (kk >> 4) * 64 + 16 * cq + (kk & 15)] = p2s[kk] > 0.f ? d : 0.f;
+    const int kk = j * 16 + rg;
+    a.dP2[(size_t)bi * 1600 + j * 64 + 16 * cq + rg] = p2s[kk] > 0.f ? d : 0.f;
   }
   stamp(a.stamps, 7);
 }
@@ -1400,6 +1404,12 @@ __device__ __forceinline__ void finalize_x_body(const MnistArgs& a, int apply_sg
     __shared__ f4 fx_red2[8][32];
     const int qd = (j - kFxDense) >> 1, h = (j - kFxDense) & 1, c = tid & 31, grp = tid >> 5;
     const bool biasq = qd == kP2Quads - 1;
+    // the SGD operand of this thread's output (threads < 128) rides in the partials' round trip
+    // instead of a second dependent load after the LDS reduction
+    const int cc = tid >> 2, rr = tid & 3;
+    const bool owner = tid < 128 && (!biasq || rr == 0);
+    const int e2 = biasq ? a.ob2 + 32 * h + cc : a.ow2 + (4 * qd + rr) * 64 + 32 * h + cc;
+    const float wold = (sgd_local && owner) ? a.W[e2] : 0.f;
     f4 sum = zero4();
     for (int base = 0; base < a.b; base += 64) {  // 4 images per thread in flight
       f4 v[4];
@@ -1414,19 +1424,13 @@ __device__ __forceinline__ void finalize_x_body(const MnistArgs& a, int apply_sg
     for (int r = 0; r < 4; ++r) sum[r] = rs_swap32(sum[r], sum[r]);
     if (lane < 32) fx_red2[wave][c] = sum;
     __syncthreads();
-    if (tid < 128) {
-      const int cc = tid >> 2, r = tid & 3;
-      if (!biasq || r == 0) {
-        const int col = 32 * h + cc;
-        const int e2 = biasq ? a.ob2 + col : a.ow2 + (4 * qd + r) * 64 + col;
-        const float wold = sgd_local ? a.W[e2] : 0.f;
-        float s2 = 0.f;
+    if (owner) {
+      float s2 = 0.f;
 #pragma unroll
-        for (int w = 0; w < 8; ++w) s2 += fx_red2[w][cc][r];
-        a.G[e2] = s2;
-        if (xdst != nullptr) xdst[e2] = s2;
-        if (sgd_local) a.W[e2] = wold - lr * s2;
-      }
+      for (int w = 0; w < 8; ++w) s2 += fx_red2[w][cc][rr];
+      a.G[e2] = s2;
+      if (xdst != nullptr) xdst[e2] = s2;
+      if (sgd_local) a.W[e2] = wold - lr * s2;
     }
   } else {
     // conv1 columns 16q .. 16q+15 over the part1 rows: lane (c = lane & 15, rg = lane >> 4) of wave
