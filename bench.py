@@ -74,7 +74,8 @@ def main():
     # exactly N devices: on an 8-GPU node `--gpus 1` is ONE replica, `--gpus N` without a launcher
     # spawns the other N-1 replica processes here (no GPU has been touched yet)
     devices = [f"/gpu:{i}" for i in range(args.gpus)]
-    strategy = tdl.distribute.MirroredStrategy(devices=devices, communication=args.comm.upper())
+    # (spawn=True: one replica PROCESS per GPU -- the scaling mode -- when started without a launcher)
+    strategy = tdl.distribute.MirroredStrategy(devices=devices, communication=args.comm.upper(), spawn=True)
     R = strategy.num_replicas_in_sync
     if R != args.gpus:
         raise SystemExit(f"bench.py: strategy has {R} replicas, expected {args.gpus}")

@@ -78,6 +78,12 @@ class MnistStep {
     a_.ep = reinterpret_cast<unsigned*>(ep_.data_ptr<int>());
     a_.part3t = reinterpret_cast<unsigned long long*>(part3t_.data_ptr<int64_t>());
     a_.head = 1;
+    {  // A/B switches of the fused kernel (diagnostics; see mnist_cnn.hip)
+      const char* v = std::getenv("TDL_MNIST_VARIANT");
+      a_.variant = v != nullptr ? std::atoi(v) : tdl::kDefaultMnistVariant;
+      const char* g = std::getenv("TDL_FX_GRID");
+      a_.fx_grid = g != nullptr ? std::max(0, std::atoi(g)) : 0;
+    }
     a_.dp2_fwd = 0;
     a_.fused_bwd = 0;
     a_.err = reinterpret_cast<unsigned*>(err_.data_ptr<int>());

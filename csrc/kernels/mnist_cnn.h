@@ -63,10 +63,18 @@ struct MnistArgs {
   // offsets), exchanges with the same workgroup of every peer, sums the R contributions in rank
   // order and applies SGD to that range -- no separate all-reduce or optimizer launch
   XgmiArgs xa;
+  int variant;  // A/B switches of the fused kernel (TDL_MNIST_VARIANT bit flags; 0 = default)
+  int fx_grid;  // k_finalize_x grid (0 = one workgroup per range, kFxBlocks); replicas sharing one GPU
+                // cap it (TDL_FX_GRID) so every rank's exchange workgroups are resident together
   int xchg;
   int xtwo;  // exchange algorithm: 0 one-shot (every rank sums every range), 1 two-shot (each rank
              // sums and updates 1/R of every range, the others copy its updated weights)
 };
+
+// TDL_MNIST_VARIANT bits (A/B switches of k_fwd_conv; the default is what measured fastest):
+//   1  s_setprio 1 for waves 4-7 (the younger half of each SIMD pair, the VALU arbitration loser)
+constexpr int kMnistVariantPrio = 1;
+constexpr int kDefaultMnistVariant = 0;
 
 constexpr int kMnistPart2Rows = 289;
 // fused_bwd layout of part2: [b][73 row quads][64 columns][4 rows] (quad 72 = the bias row + 3 zero

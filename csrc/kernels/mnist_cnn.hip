@@ -939,6 +939,9 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int i = lane & 15, g = lane >> 4;
   const int bi = blockIdx.x >> 2, cq = blockIdx.x & 3;
+  // waves w and w + 4 share a SIMD; the younger half (4-7) loses the VALU issue arbitration in every
+  // phase and reaches each barrier last (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+  if ((a.variant & kMnistVariantPrio) && __builtin_amdgcn_readfirstlane(wave) >= 4) __builtin_amdgcn_s_setprio(1);
   stamp(a.stamps, 0);
   // ---- staging: all global loads first ----
   const int sample = a.idx[bi];
@@ -1355,21 +1358,36 @@ __device__ __forceinline__ void fx_range(const MnistArgs& a, int j, int& lo, int
 }
 
 template <int R>
-__device__ __forceinline__ void finalize_x_body(const MnistArgs& a, int apply_sgd);
+__device__ __forceinline__ void finalize_x_body(const MnistArgs& a, int apply_sgd, int j);
 
 // phase stamps of KF-X (diagnostics), after the fused kernel's grid*104 words: per wave, start and end
-template <int R>
+template <int R, bool LOOP>
 __global__ __launch_bounds__(512) void k_finalize_x(MnistArgs a, int apply_sgd) {
   unsigned long long* sb = a.stamps == nullptr ? nullptr
       : a.stamps + (size_t)a.b * 4 * 104 + ((size_t)blockIdx.x * 8 + (threadIdx.x >> 6)) * 2;
   if (sb != nullptr && (threadIdx.x & 63) == 0) sb[0] = __builtin_amdgcn_s_memrealtime();
-  finalize_x_body<R>(a, apply_sgd);
+  // workgroup b runs ranges b, b + grid, ... in the same order on every rank: with a capped grid
+  // (a.fx_grid, replicas SHARING one GPU) every rank's workgroups are resident together, so range j
+  // of each rank always finds range j of its peers running (a full 269-workgroup grid per rank
+  // cannot be co-resident for 8 ranks on one GPU: some ranks would fill it while the peers they
+  // wait for have no workgroup resident).  One range per workgroup on a GPU of its own.
+  // (LOOP = false: the grid is exactly one workgroup per range -- a separate instantiation, because
+  // the range loop costs the body its specialisation: 111 VGPRs / 106 SGPRs instead of 72 / 59,
+  // i.e. 2 instead of 3 resident workgroups per CU)
+  if constexpr (LOOP) {
+    for (int j = blockIdx.x; j < kFxBlocks; j += gridDim.x) {
+      finalize_x_body<R>(a, apply_sgd, j);
+      __syncthreads();  // (LDS scratch reused by the next range)
+    }
+  } else {
+    finalize_x_body<R>(a, apply_sgd, blockIdx.x);
+  }
   if (sb != nullptr && (threadIdx.x & 63) == 0) sb[1] = __builtin_amdgcn_s_memrealtime();
 }
 
 template <int R>
-__device__ __forceinline__ void finalize_x_body(const MnistArgs& a, int apply_sgd) {
-  const int j = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+__device__ __forceinline__ void finalize_x_body(const MnistArgs& a, int apply_sgd, int j) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const float lr = *a.lr;
   const bool xchg = R > 1 && a.xchg && apply_sgd;
   if (j == 0 && tid == 0) a.ep[0] += 1u;  // the next step's hand-off tag (no k_conv_bwd launch)
@@ -1598,15 +1616,24 @@ void mnist_finalize(const MnistArgs& a, bool apply_sgd, bool with_dense, hipStre
 void mnist_finalize_x(const MnistArgs& a, bool apply_sgd, hipStream_t s) {
   const int R = (a.xchg && apply_sgd) ? a.xa.world : 1;
   const int sgd = apply_sgd ? 1 : 0;
+  const int kFxBlocks = (a.fx_grid > 0 && a.fx_grid < tdl::kFxBlocks) ? a.fx_grid : tdl::kFxBlocks;
+  auto launch = [&](auto rk, auto loop) {
+    constexpr int kR = decltype(rk)::value;
+    hipLaunchKernelGGL((k_finalize_x<kR, decltype(loop)::value>), dim3(kFxBlocks), dim3(512), 0, s, a, sgd);
+  };
+  auto go = [&](auto rk) {
+    if (kFxBlocks < tdl::kFxBlocks) launch(rk, std::true_type{});
+    else launch(rk, std::false_type{});
+  };
   switch (R) {  // the rank count is a template parameter (straight-line rank-order sums)
-    case 2: hipLaunchKernelGGL(k_finalize_x<2>, dim3(kFxBlocks), dim3(512), 0, s, a, sgd); break;
-    case 3: hipLaunchKernelGGL(k_finalize_x<3>, dim3(kFxBlocks), dim3(512), 0, s, a, sgd); break;
-    case 4: hipLaunchKernelGGL(k_finalize_x<4>, dim3(kFxBlocks), dim3(512), 0, s, a, sgd); break;
-    case 5: hipLaunchKernelGGL(k_finalize_x<5>, dim3(kFxBlocks), dim3(512), 0, s, a, sgd); break;
-    case 6: hipLaunchKernelGGL(k_finalize_x<6>, dim3(kFxBlocks), dim3(512), 0, s, a, sgd); break;
-    case 7: hipLaunchKernelGGL(k_finalize_x<7>, dim3(kFxBlocks), dim3(512), 0, s, a, sgd); break;
-    case 8: hipLaunchKernelGGL(k_finalize_x<8>, dim3(kFxBlocks), dim3(512), 0, s, a, sgd); break;
-    default: hipLaunchKernelGGL(k_finalize_x<1>, dim3(kFxBlocks), dim3(512), 0, s, a, sgd); break;
+    case 2: go(std::integral_constant<int, 2>{}); break;
+    case 3: go(std::integral_constant<int, 3>{}); break;
+    case 4: go(std::integral_constant<int, 4>{}); break;
+    case 5: go(std::integral_constant<int, 5>{}); break;
+    case 6: go(std::integral_constant<int, 6>{}); break;
+    case 7: go(std::integral_constant<int, 7>{}); break;
+    case 8: go(std::integral_constant<int, 8>{}); break;
+    default: go(std::integral_constant<int, 1>{}); break;
   }
 }
 void sgd_apply(float* w, const float* g, const float* lr, int64_t n, hipStream_t s) {

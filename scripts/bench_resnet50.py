@@ -66,7 +66,7 @@ def main():
         strategy = tdl.distribute.MultiWorkerMirroredStrategy(communication_options=copts)
     else:
         strategy = tdl.distribute.MirroredStrategy(devices=[f"/gpu:{i}" for i in range(args.gpus)],
-                                                   communication_options=copts)
+                                                   communication_options=copts, spawn=True)
     R = strategy.num_replicas_in_sync
     if R != args.gpus:
         raise SystemExit(f"bench_resnet50: strategy has {R} replicas, expected --gpus {args.gpus}")

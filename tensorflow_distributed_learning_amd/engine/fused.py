@@ -134,7 +134,10 @@ class FusedMnistTrainer:
         self._steps = {}
         self._graphs = {}
         self._data_key = None
-        self.capture = os.environ.get("TDL_GRAPH", "1") == "1"
+        # (no capture for the replica threads of a single-process MirroredStrategy: their
+        # collectives are host rendezvous, and concurrent captures in threads of one process are not
+        # safe with torch's process-global capture mode)
+        self.capture = os.environ.get("TDL_GRAPH", "1") == "1" and not getattr(self.comm, "threaded", False)
         # With R > 1 the cross-replica all-reduce is recorded inside the execution graph (RCCL
         # supports hipGraph capture) unless TDL_CAPTURE_ALLREDUCE=0 or the collective capture probe
         # fails on some rank; then each step's graph is followed by an eager all-reduce + update.

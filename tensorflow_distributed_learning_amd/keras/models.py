@@ -242,8 +242,9 @@ class Model(Layer):
                 else:
                     v._value = v._value.to(dev)
         comm = strategy.extended.communicator
-        if comm.world_size > 1:
-            # every replica starts from the chief's initial values (TF: broadcast from worker 0)
+        if comm.world_size > 1 and not getattr(comm, "threaded", False):
+            # every replica starts from the chief's initial values (TF: broadcast from worker 0;
+            # replica threads of one process got replica 0's values with their clone instead)
             comm.broadcast(W, 0)
             if NT is not None:
                 comm.broadcast(NT, 0)
@@ -354,11 +355,83 @@ class Model(Layer):
         x = el[0] if isinstance(el, (tuple, list)) else el
         self.build((None,) + tuple(x.shape[1:]))
 
+    # ------------------------------------------------------------------ single-process replicas
+    def _outer_local_group(self):
+        """The LocalReplicaGroup of a single-process multi-device MirroredStrategy when called
+        from outside its replica threads (then fit / evaluate / predict run once per replica)."""
+        g = getattr(self._get_strategy(), "_local_group", None)
+        return g if g is not None and not g.in_region() else None
+
+    def _local_replicas(self):
+        """Replica models 0..G-1 of a single-process MirroredStrategy: replica 0 is this model, replicas
+        1..G-1 are clones built in their replica's scope (device r), compiled alike, holding this
+        model's current weights (parallel/local_replicas.py)."""
+        strategy = self._get_strategy()
+        g = strategy._local_group
+        clones = getattr(self, "_local_clones", None)
+        weights = self.get_weights()
+        if clones is None or len(clones) != g.G - 1:
+            if not self._functional and not isinstance(self, Sequential):
+                raise NotImplementedError(
+                    "single-process multi-device MirroredStrategy needs a Sequential or functional model (a "
+                    "subclassed model cannot be cloned per device); launch one process per GPU instead: "
+                    "python -m tensorflow_distributed_learning_amd.launch --nproc-per-node N script.py")
+            cfg = self.get_config_full()
+            clones = []
+            for r in range(1, g.G):
+                view = strategy._replica_strategy(r)
+                with view.scope():
+                    m = model_from_config(cfg)
+                    if not m.built and self._built_input_shape:
+                        m.build(tuple(self._built_input_shape))
+                    if getattr(self, "_compile_config", None) is not None:
+                        m.compile_from_config(self._compile_config)
+                        m._bucket_bytes = self._bucket_bytes
+                m._distribution_strategy = view
+                clones.append(m)
+            self._local_clones = clones
+        for m in clones:  # every replica starts from replica 0's current values (mirrored variables)
+            m.set_weights(weights)
+        return [self] + clones
+
+    def _local_run(self, name: str, kwargs: dict):
+        """Run ``name`` (fit / evaluate / predict) once per local replica concurrently; replica 0 (this
+        model, the caller's thread) keeps the callbacks and the output, the clones run silently."""
+        g = self._get_strategy()._local_group
+        x = kwargs.get("x")
+        if not self.built and x is not None:  # build replica 0 so the clones get its shapes
+            self._peek_build(x if isinstance(x, D.Dataset) else
+                             self._adapt(x, kwargs.get("y"), kwargs.get("batch_size"), False))
+        models = self._local_replicas()
+
+        def one(r):
+            kw = dict(kwargs)
+            if r > 0:
+                kw["verbose"] = 0
+                if "callbacks" in kw:
+                    kw["callbacks"] = None
+            return getattr(models[r], f"_{name}_impl")(**kw)
+
+        return g.run(one)[0]
+
     # ------------------------------------------------------------------ fit
     def fit(self, x=None, y=None, batch_size=None, epochs=1, verbose="auto", callbacks=None, validation_split=0.0,
             validation_data=None, shuffle=True, class_weight=None, sample_weight=None, initial_epoch=0,
             steps_per_epoch=None, validation_steps=None, validation_batch_size=None, validation_freq=1,
             max_queue_size=10, workers=1, use_multiprocessing=False):
+        kw = dict(x=x, y=y, batch_size=batch_size, epochs=epochs, verbose=verbose, callbacks=callbacks,
+                  validation_split=validation_split, validation_data=validation_data, shuffle=shuffle,
+                  class_weight=class_weight, sample_weight=sample_weight, initial_epoch=initial_epoch,
+                  steps_per_epoch=steps_per_epoch, validation_steps=validation_steps,
+                  validation_batch_size=validation_batch_size, validation_freq=validation_freq)
+        if self._outer_local_group() is not None:
+            return self._local_run("fit", kw)
+        return self._fit_impl(**kw)
+
+    def _fit_impl(self, x=None, y=None, batch_size=None, epochs=1, verbose="auto", callbacks=None,
+                  validation_split=0.0, validation_data=None, shuffle=True, class_weight=None, sample_weight=None,
+                  initial_epoch=0, steps_per_epoch=None, validation_steps=None, validation_batch_size=None,
+                  validation_freq=1):
         strategy = self._get_strategy()
         if validation_split and not isinstance(x, D.Dataset):
             n = len(x)
@@ -478,6 +551,14 @@ class Model(Layer):
     # ------------------------------------------------------------------ evaluate / predict
     def evaluate(self, x=None, y=None, batch_size=None, verbose="auto", sample_weight=None, steps=None,
                  callbacks=None, return_dict=False, _internal=False, **kw):
+        args = dict(x=x, y=y, batch_size=batch_size, verbose=verbose, sample_weight=sample_weight, steps=steps,
+                    callbacks=callbacks, return_dict=return_dict, _internal=_internal)
+        if self._outer_local_group() is not None:
+            return self._local_run("evaluate", args)
+        return self._evaluate_impl(**args)
+
+    def _evaluate_impl(self, x=None, y=None, batch_size=None, verbose="auto", sample_weight=None, steps=None,
+                       callbacks=None, return_dict=False, _internal=False):
         from ..engine.trainer import GenericTrainer, HostDataHandler
 
         ds = self._adapt(x, y, batch_size, False, sample_weight)
@@ -528,8 +609,14 @@ class Model(Layer):
         vals = [out[k] for k in ["loss"] + [m.name for m in self.compiled_metrics]]
         return vals if len(vals) > 1 else vals[0]
 
-    @torch.no_grad()
     def predict(self, x, batch_size=None, verbose="auto", steps=None, callbacks=None, **kw):
+        args = dict(x=x, batch_size=batch_size, verbose=verbose, steps=steps, callbacks=callbacks)
+        if self._outer_local_group() is not None:
+            return self._local_run("predict", args)
+        return self._predict_impl(**args)
+
+    @torch.no_grad()
+    def _predict_impl(self, x, batch_size=None, verbose="auto", steps=None, callbacks=None):
         dev = self._get_strategy().extended.device
         if isinstance(x, D.Dataset):
             ds = x

@@ -15,6 +15,7 @@ forces the hand-written kernels wherever they apply, ``miopen`` disables them.
 from __future__ import annotations
 
 import os
+import threading
 
 import torch
 import torch.nn.functional as F
@@ -151,11 +152,20 @@ _HBM_BYTES_PER_MS = 4.5e9  # streaming rate the BN/add kernels reach on MI355X (
 # makes every autotuning decision and broadcasts it, so that all replicas run the same kernel set
 # (the same numerics, the same step time) instead of timing candidates each on its own
 _COMM = [None]
+# the binding of the calling thread: replicas of a single-process MirroredStrategy are threads of one
+# process (parallel/local_replicas.py), each with its own rank in its own communicator
+_COMM_TLS = threading.local()
 _FALLBACK_LOGGED: set = set()
 
 
 def bind_communicator(comm) -> None:
-    _COMM[0] = comm if comm is not None and getattr(comm, "world_size", 1) > 1 else None
+    c = comm if comm is not None and getattr(comm, "world_size", 1) > 1 else None
+    _COMM[0] = c
+    _COMM_TLS.comm = c
+
+
+def _bound_comm():
+    return getattr(_COMM_TLS, "comm", _COMM[0])
 
 
 def _capture_fallback(key) -> None:
@@ -175,7 +185,7 @@ _AGREE_WIDTH = 5  # [chosen, wmw, wnw, nsplit, kind]
 def _agree(local_decide, encode, decode):
     """Rank 0 decides (``local_decide``), every rank gets rank 0's decision.  Collective: every
     replica reaches the same key at the same point of the same model's first eager step."""
-    comm = _COMM[0]
+    comm = _bound_comm()
     if comm is None:
         return local_decide()
     v = local_decide() if comm.rank == 0 else None

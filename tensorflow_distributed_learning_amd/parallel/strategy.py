@@ -7,8 +7,11 @@ CPU replicas / ``CollectiveCommunication.RING``).
 
 * :class:`MirroredStrategy` (README.md:15-19, tf_dist_example.py:13): all GPUs of one node.
   Started by a launcher (``torchrun``/``python -m tensorflow_distributed_learning_amd.launch``)
-  each process becomes one replica; started as a plain script with several devices selected, it
-  spawns one child process per extra device (the parent is replica 0) before touching the GPU.
+  each process becomes one replica (the scaling mode).  Started as a plain script with several
+  devices selected, ONE process drives them all, as in TF (parallel/local_replicas.py: a replica
+  thread per device, in-process rank-order all-reduces, the script body runs once);
+  ``spawn=True`` / ``TDL_MIRRORED_MODE=process`` instead spawns one child process per extra device
+  (the parent is replica 0) before touching the GPU.
 * :class:`MultiWorkerMirroredStrategy` (tf_dist_example.py:12, README.md:21-29): the cluster comes
   from TF_CONFIG; tasks meet at the chief over the native TCP store (cluster/rendezvous.py) and
   every GPU of every worker is one replica.  No TF_CONFIG / a single task degrades to
@@ -239,13 +242,54 @@ class Strategy:
         finally:
             _stack().pop()
 
+    _local_group = None  # single-process multi-device MirroredStrategy (parallel/local_replicas.py)
+
+    def _replica_strategy(self, r: int):
+        """Replica r's strategy object in single-process multi-device mode (r = 0: self)."""
+        return self if r == 0 else self._local_group.views[r - 1]
+
     def run(self, fn: Callable, args=(), kwargs=None, options=None):
-        with self.scope(), _replica(ReplicaContext(self)):
-            return fn(*args, **(kwargs or {}))
+        g = self._local_group
+        if g is None or g.in_region():
+            with self.scope(), _replica(ReplicaContext(self)):
+                return fn(*args, **(kwargs or {}))
+        from .values import PerReplica
+
+        def pick(v, r):
+            return v.values[r] if isinstance(v, PerReplica) else v
+
+        def one(r):
+            st = self._replica_strategy(r)
+            a = tuple(pick(v, r) for v in args)
+            kw = {k: pick(v, r) for k, v in (kwargs or {}).items()}
+            with st.scope(), _replica(ReplicaContext(st)):
+                return fn(*a, **kw)
+
+        out = g.run(one)
+        if isinstance(out[0], (tuple, list)):  # a structure of per-replica values
+            return type(out[0])(PerReplica([o[i] for o in out]) for i in range(len(out[0])))
+        if isinstance(out[0], dict):
+            return {k: PerReplica([o[k] for o in out]) for k in out[0]}
+        return PerReplica(out)
 
     def reduce(self, reduce_op, value, axis=None):
         """Cross-replica reduction of a per-replica value (optionally along `axis` first)."""
         op = reduce_op.value if isinstance(reduce_op, ReduceOp) else str(reduce_op).upper()
+        from .values import PerReplica
+
+        if isinstance(value, PerReplica):  # single-process replicas: reduce the local values here
+            dev = self.extended.device
+            vals = [torch.as_tensor(v).to(dev) for v in value.values]
+            if axis is not None:
+                cnt = sum(v.shape[axis] for v in vals)
+                vals = [v.sum(dim=axis) for v in vals]
+            total = vals[0].clone()
+            for v in vals[1:]:  # rank order
+                total = total + v
+            if op == "SUM":
+                return total
+            n = cnt if axis is not None else len(vals)
+            return total / n if total.is_floating_point() else total.double() / n
         t = torch.as_tensor(value)
         if axis is None:
             return self.extended.all_reduce(op, t)
@@ -259,11 +303,21 @@ class Strategy:
         return total / n.to(total.dtype)
 
     def gather(self, value, axis=0):
+        from .values import PerReplica
+
+        if isinstance(value, PerReplica):
+            return torch.cat([torch.as_tensor(v).to(self.extended.device) for v in value.values], dim=axis)
         t = torch.as_tensor(value)
         g = self.extended.communicator.all_gather(t.to(self.extended.device))
         return torch.cat(list(g.unbind(0)), dim=axis)
 
     def experimental_local_results(self, value):
+        """The values of this process's replicas: one per local device in single-process
+        multi-device mode, else this process's one replica."""
+        from .values import PerReplica
+
+        if isinstance(value, PerReplica):
+            return value.values
         return (value,)
 
     def experimental_distribute_dataset(self, dataset, options=None):
@@ -399,11 +453,17 @@ class MirroredStrategy(Strategy):
             n = torch.cuda.device_count()  # does not initialise the GPU
             devs = [torch.device("cuda", i) for i in range(n)] or [torch.device("cpu")]
         if launched is None and len(devs) > 1:
-            from .launch import maybe_spawn_local_replicas
+            mode = "process" if spawn is True else ("threads" if spawn is False else
+                                                    os.environ.get("TDL_MIRRORED_MODE", "threads"))
+            if mode == "process":
+                from .launch import maybe_spawn_local_replicas
 
-            launched = maybe_spawn_local_replicas(len(devs), spawn=spawn)
-            if launched is None:  # (maybe_spawn_local_replicas warned and said why)
-                devs = devs[:1]
+                launched = maybe_spawn_local_replicas(len(devs), spawn=True)
+                if launched is None:  # (maybe_spawn_local_replicas warned and said why)
+                    devs = devs[:1]
+            else:
+                self._init_local(devs, opts)
+                return
         if launched is None:
             dev = _shared_gpu(devs[0])
             comm = LocalCommunicator(dev)
@@ -429,6 +489,28 @@ class MirroredStrategy(Strategy):
             if ext.watchdog is not None:
                 ext.watchdog.on_abort = ext.communicator.abort
             ext.communicator.barrier()
+
+
+    def _init_local(self, devs, opts):
+        """ONE process, G local replicas (parallel/local_replicas.py): replica 0 is this strategy
+        (device 0, communicator 0 of the group), replicas 1..G-1 are views of it."""
+        from .local_replicas import LocalReplicaGroup, make_views
+
+        local = [_shared_gpu(d) if d.type == "cuda" else d for d in devs]
+        if any(d.type == "cuda" for d in local) and not torch.cuda.is_available():
+            raise RuntimeError(f"MirroredStrategy: devices {devs} include GPUs but none is visible")
+        group = LocalReplicaGroup(local, timeout=collective_timeout(opts))
+        ext = StrategyExtended(self, local[0], 0, len(local), 0, group.comms[0], opts)
+        Strategy.__init__(self, ext)
+        self._local_group = group
+        group.views = make_views(self, group)
+        if local[0].type == "cuda":
+            torch.cuda.set_device(local[0])
+
+    @property
+    def extended_local_devices(self):
+        g = self._local_group
+        return tuple(str(d) for d in g.devices) if g is not None else (str(self.extended.device),)
 
 
 def _cdo_to_impl(cross_device_ops):

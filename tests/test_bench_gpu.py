@@ -16,7 +16,7 @@ def _bench(args, **env_extra):
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "TF_CONFIG", "TDL_LAUNCHED"):
         env.pop(k, None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
-                       text=True, timeout=300, cwd=ROOT)
+                       text=True, timeout=400, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
@@ -50,6 +50,22 @@ def test_bench_three_replicas_two_shot_shared_gpu():
     assert d["config"]["allreduce"] == "xgmi-twoshot+gloo", d["config"]
     assert d["config"]["allreduce_in_graph"] is True
     assert d["config"]["replicas_identical"] is True
+
+
+def test_bench_eight_replicas_shared_gpu():
+    """bench.py --gpus 8 (BASELINE config 3's replica count) as 8 replica processes on the one GPU,
+    8 images each: the two-shot xGMI all-reduce over IPC-mapped buffers of all 8 replicas with SGD
+    fused, in the captured graphs; replicas bit-identical, no fallback taken.  (On a shared GPU the
+    engine keeps the standalone all-reduce kernel: the in-finalize exchange needs every replica's
+    fused kernel fully resident, which 8 concurrent replicas cannot guarantee on one GPU --
+    tests/test_mnist_exchange_gpu.py covers it at R = 8 with phases separated.)"""
+    d = _bench(["--gpus", "8", "--per-replica-batch", "8", "--steps", "20", "--warmup", "5"], TDL_SHARE_GPU="1")
+    assert d["n_gpus"] == 8 and d["config"]["global_batch"] == 64
+    assert d["config"]["allreduce"] == "xgmi-twoshot+gloo", d["config"]
+    assert d["config"]["allreduce_in_graph"] is True
+    assert d["config"]["replicas_identical"] is True
+    assert d["config"]["fallbacks"] == [], d["config"]
+    assert len(d["config"]["rank_ms_per_step"]) == 8
 
 
 def test_bench_two_replicas_under_torchrun_shared_gpu():

@@ -119,7 +119,7 @@ import tensorflow_distributed_learning_amd as tdl
 from tensorflow_distributed_learning_amd.models.mnist_cnn import build_mnist_cnn
 from tensorflow_distributed_learning_amd.data.tfds import synthetic_mnist
 out = sys.argv[1]
-strategy = tdl.distribute.MirroredStrategy(devices=["/cpu:0", "/cpu:1", "/cpu:2"], communication="RING")
+strategy = tdl.distribute.MirroredStrategy(devices=["/cpu:0", "/cpu:1", "/cpu:2"], communication="RING", spawn=True)
 rank = strategy.extended.rank
 open(os.path.join(out, f"pid{rank}"), "w").write(str(os.getpid()))
 tdl.keras.utils.set_random_seed(1)

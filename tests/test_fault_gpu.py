@@ -25,7 +25,7 @@ from tensorflow_distributed_learning_amd.data.tfds import synthetic_mnist
 from tensorflow_distributed_learning_amd.parallel.consistency import ReplicaDivergenceError
 out = sys.argv[1]
 n = int(os.environ.get("JOB_REPLICAS", "2"))
-strategy = tdl.distribute.MirroredStrategy(devices=[f"/gpu:{i}" for i in range(n)])
+strategy = tdl.distribute.MirroredStrategy(devices=[f"/gpu:{i}" for i in range(n)], spawn=True)
 rank = strategy.extended.rank
 open(os.path.join(out, f"pid{rank}"), "w").write(str(os.getpid()))
 tdl.keras.utils.set_random_seed(5)

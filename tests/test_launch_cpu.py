@@ -44,7 +44,7 @@ def test_python_dash_m_program_relaunches_as_module(tmp_path):
         import os
         from . import __name__ as _pkg  # relative import: fails if re-run as a plain script
         import tensorflow_distributed_learning_amd as tdl
-        s = tdl.distribute.MirroredStrategy(devices=["/cpu:0", "/cpu:1"])
+        s = tdl.distribute.MirroredStrategy(devices=["/cpu:0", "/cpu:1"], spawn=True)
         print("replicas", s.num_replicas_in_sync, "rank", s.extended.rank, flush=True)
         s.shutdown()
     """))

@@ -23,11 +23,12 @@ sys.path.insert(0, sys.argv[2])
 from tensorflow_distributed_learning_amd import ops
 from tensorflow_distributed_learning_amd.models import mnist_cnn as M
 rank, R, two = int(sys.argv[1]), int(sys.argv[4]), sys.argv[5] == "1"
+b = int(sys.argv[6])
 dist.init_process_group("gloo", rank=rank, world_size=R, init_method="tcp://127.0.0.1:" + sys.argv[3])
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 C = ops.hip()
-b, N = 16, 512
+N = 512
 g = torch.Generator().manual_seed(0)
 X = torch.rand(N, 28, 28, 1, generator=g).to(dev)
 Y = torch.randint(0, 10, (N,), generator=g, dtype=torch.int32).to(dev)
@@ -118,12 +119,16 @@ print("exchange ok", rank, flush=True)
 
 
 @pytest.mark.parametrize("two", [False, True], ids=["oneshot", "twoshot"])
-@pytest.mark.parametrize("R", [2])
+@pytest.mark.parametrize("R", [2, 8])
 def test_finalize_exchange_multi_process(tmp_path, R, two):
-    """(R = 2 only: the exchange needs workgroup j of every replica resident at some point, and a
-    one-GPU box holds 768 of the finalize's 512-thread workgroups: 2 x 410 leave the second replica
-    at least a prefix of its grid, 3 x 410 can starve the third.  With one GPU per replica all
-    410 are resident at once.)"""
+    """R = 2 with the full finalize grid, R = 8 (BASELINE config 3's world size: the two-shot shard
+    math, the 8-slot signal words, the largest rank-order sums) with the grid capped (TDL_FX_GRID):
+    the exchange needs range j of every replica in flight together, and a one-GPU box holds 768 of
+    the finalize's 512-thread workgroups (72 VGPRs: 3 per CU) -- 8 x 269 full grids would let some
+    replicas fill the GPU while the peers they wait for have none resident.  At 8 x 48 every
+    replica's workgroups are resident together and loop over the 269 ranges in the same order.
+    With one GPU per replica the full grid is resident at once.  (b = 4 at R = 8: each replica's
+    fused kernel needs its 4b workgroups resident together, 8 x 16 of the 256 CUs.)"""
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = str(s.getsockname()[1])
@@ -131,15 +136,18 @@ def test_finalize_exchange_multi_process(tmp_path, R, two):
     f = tmp_path / "xchg.py"
     f.write_text(textwrap.dedent(BODY))
     env = dict(os.environ, TDL_MNIST_DP2_FWD="1", TDL_MNIST_FUSED_BWD="1")
+    if R > 2:
+        env["TDL_FX_GRID"] = "48"
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "TF_CONFIG", "TDL_SHARE_GPU"):
         env.pop(k, None)
-    procs = [subprocess.Popen([sys.executable, str(f), str(r), ROOT, port, str(R), "1" if two else "0"], env=env,
-                              stdout=subprocess.PIPE,
+    b = 16 if R == 2 else 4
+    procs = [subprocess.Popen([sys.executable, str(f), str(r), ROOT, port, str(R), "1" if two else "0", str(b)],
+                              env=env, stdout=subprocess.PIPE,
                               stderr=subprocess.STDOUT, text=True) for r in range(R)]
     outs = []
     for p in procs:
         try:
-            out, _ = p.communicate(timeout=150)
+            out, _ = p.communicate(timeout=240)
         except subprocess.TimeoutExpired:
             p.kill()
             out, _ = p.communicate()
