@@ -10,6 +10,7 @@
 
 #include "kernels/mnist_cnn.h"
 #include "kernels/ops.h"
+#include "kernels/optim.h"
 #include "xgmi_channel.h"
 
 namespace {
@@ -271,6 +272,47 @@ void sgd_momentum(at::Tensor w, at::Tensor g, at::Tensor v, at::Tensor lr, doubl
                           (float)m, nesterov, w.numel(), cur_stream());
 }
 
+// Flat-slab Adam / AdamW (+AMSGrad): state m, v (vhat), device lr and execution-start step t0
+void adam(at::Tensor w, at::Tensor g, at::Tensor m, at::Tensor v, c10::optional<at::Tensor> vhat, at::Tensor lr,
+          at::Tensor t0, int64_t t_add, double b1, double b2, double eps, double wd) {
+  for (auto* t : {&w, &g, &m, &v, &lr, &t0}) check_cuda_f32(*t, "adam operand");
+  TORCH_CHECK(g.numel() == w.numel() && m.numel() == w.numel() && v.numel() == w.numel());
+  tdl::OptimArgs a{};
+  a.w = w.data_ptr<float>(); a.g = g.data_ptr<float>(); a.s0 = m.data_ptr<float>(); a.s1 = v.data_ptr<float>();
+  if (vhat.has_value()) {
+    check_cuda_f32(*vhat, "vhat");
+    TORCH_CHECK(vhat->numel() == w.numel());
+    a.s2 = vhat->data_ptr<float>();
+    a.flags = 1;
+  }
+  a.lr = lr.data_ptr<float>(); a.t0 = t0.data_ptr<float>(); a.t_add = (int)t_add; a.n = w.numel();
+  a.b1 = (float)b1; a.b2 = (float)b2; a.eps = (float)eps; a.wd = (float)wd;
+  tdl::adam_apply(a, cur_stream());
+}
+
+// Flat-slab RMSprop (+momentum, centered)
+void rmsprop(at::Tensor w, at::Tensor g, at::Tensor rms, c10::optional<at::Tensor> mom, c10::optional<at::Tensor> mg,
+             at::Tensor lr, double rho, double momentum, double eps) {
+  for (auto* t : {&w, &g, &rms, &lr}) check_cuda_f32(*t, "rmsprop operand");
+  TORCH_CHECK(g.numel() == w.numel() && rms.numel() == w.numel());
+  tdl::OptimArgs a{};
+  a.w = w.data_ptr<float>(); a.g = g.data_ptr<float>(); a.s0 = rms.data_ptr<float>();
+  if (mom.has_value()) { check_cuda_f32(*mom, "mom"); TORCH_CHECK(mom->numel() == w.numel()); a.s1 = mom->data_ptr<float>(); a.flags |= 1; }
+  if (mg.has_value()) { check_cuda_f32(*mg, "mg"); TORCH_CHECK(mg->numel() == w.numel()); a.s2 = mg->data_ptr<float>(); a.flags |= 2; }
+  a.lr = lr.data_ptr<float>(); a.n = w.numel(); a.b1 = (float)rho; a.b2 = (float)momentum; a.eps = (float)eps;
+  tdl::rmsprop_apply(a, cur_stream());
+}
+
+// Flat-slab Adagrad
+void adagrad(at::Tensor w, at::Tensor g, at::Tensor acc, at::Tensor lr, double eps) {
+  for (auto* t : {&w, &g, &acc, &lr}) check_cuda_f32(*t, "adagrad operand");
+  TORCH_CHECK(g.numel() == w.numel() && acc.numel() == w.numel());
+  tdl::OptimArgs a{};
+  a.w = w.data_ptr<float>(); a.g = g.data_ptr<float>(); a.s0 = acc.data_ptr<float>();
+  a.lr = lr.data_ptr<float>(); a.n = w.numel(); a.eps = (float)eps;
+  tdl::adagrad_apply(a, cur_stream());
+}
+
 }  // namespace
 
 void register_ops(pybind11::module& m);
@@ -304,6 +346,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_stamps", &MnistStep::set_stamps);
   m.def("sgd", &sgd);
   m.def("sgd_momentum", &sgd_momentum);
+  m.def("adam", &adam, pybind11::arg("w"), pybind11::arg("g"), pybind11::arg("m"), pybind11::arg("v"),
+        pybind11::arg("vhat"), pybind11::arg("lr"), pybind11::arg("t0"), pybind11::arg("t_add"), pybind11::arg("b1"),
+        pybind11::arg("b2"), pybind11::arg("eps"), pybind11::arg("wd") = 0.0);
+  m.def("rmsprop", &rmsprop, pybind11::arg("w"), pybind11::arg("g"), pybind11::arg("rms"), pybind11::arg("mom"),
+        pybind11::arg("mg"), pybind11::arg("lr"), pybind11::arg("rho"), pybind11::arg("momentum"), pybind11::arg("eps"));
+  m.def("adagrad", &adagrad);
   register_ops(m);
   register_comm(m);
   register_rccl(m);

@@ -1,0 +1,70 @@
+// Generic f32 GEMM / implicit-GEMM convolution for gfx950 on v_mfma_f32_16x16x4_f32 (exact f32
+// products, f32 accumulation): the f32 Conv2D and Dense layers of the generic engine -- any kernel
+// size, stride, dilation and (asymmetric) padding, any channel count, no library call.  See
+// gemm_f32.hip for the tiling.
+//
+// Every operation is C[M][N] = sum_k A(m, k) B(k, n) (+ bias[n]) (+ C when accumulating), with the
+// A / B element fetch chosen by the mode:
+//   kF32Gemm       A(m, k) = a[m sam + k sak], B(k, n) = b[k sbk + n sbn]        (Dense fwd / dx / dW)
+//   kF32ConvFwd    M = N*OH*OW pixels, N = K out channels, k = (r, s, c):  x NHWC, w HWIO [R S C][K]
+//   kF32ConvDgrad  M = N*H*W input pixels, N = C, k = (r, s, k):  dy NHWC, w^T as [R S K][C]
+//   kF32ConvWgrad  M = K, N = R*S*C, k = (n, oy, ox): A = dy (channel-contiguous rows), B = x gathered,
+//                  stored transposed (trans_out) into dW HWIO [R S C][K]
+// Long reductions split over blockIdx.z into a partial-sum workspace reduced in a fixed order by a
+// second kernel (deterministic, no atomics).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tdl {
+
+enum F32GemmMode { kF32Gemm = 0, kF32ConvFwd = 1, kF32ConvDgrad = 2, kF32ConvWgrad = 3 };
+
+struct F32ConvGeom {
+  int n, h, w, c;  // input NHWC
+  int k;           // output channels
+  int r, s;        // filter height / width
+  int oh, ow;      // output height / width
+  int sh, sw, pt, pl, dh, dw;
+};
+
+struct F32GemmArgs {
+  const float* a;
+  const float* b;
+  float* out;
+  const float* bias;  // [N] or null
+  float* ws;          // [splits][M][N] partial sums (splits > 1)
+  int64_t sam, sak, sbk, sbn;
+  int M, N, Kred;
+  int kchunk, splits;  // reduction slice per blockIdx.z (a multiple of 16) and their count
+  int64_t ldo;
+  int trans_out;   // out[n * ldo + m] instead of out[m * ldo + n]
+  int accumulate;  // out += result
+  int vec_a, vec_b;  // 16-B operand loads (set by the host when layouts and alignment allow)
+  F32ConvGeom g;
+};
+
+constexpr int kF32Tile = 64;
+
+// Reduction split for a (mode-independent) M x N x Kred problem: enough workgroups to fill 256 CUs.
+inline void f32_gemm_plan(F32GemmArgs& a) {
+  const int64_t tiles = (int64_t)((a.M + kF32Tile - 1) / kF32Tile) * ((a.N + kF32Tile - 1) / kF32Tile);
+  int splits = 1;
+  if (tiles < 512 && a.Kred > 256) {
+    const int64_t want = (1024 + tiles - 1) / tiles;
+    const int64_t most = (a.Kred + 127) / 128;
+    splits = (int)(want < most ? want : most);
+    if (splits > 256) splits = 256;
+    if (splits < 1) splits = 1;
+  }
+  int chunk = (a.Kred + splits - 1) / splits;
+  chunk = (chunk + 15) / 16 * 16;
+  if (chunk < 16) chunk = 16;
+  a.kchunk = chunk;
+  a.splits = (a.Kred + chunk - 1) / chunk;
+  if (a.splits < 1) a.splits = 1;
+}
+
+void f32_gemm_launch(int mode, const F32GemmArgs& a, hipStream_t s);
+
+}  // namespace tdl

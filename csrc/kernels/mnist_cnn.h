@@ -73,7 +73,13 @@ struct MnistArgs {
 
 // TDL_MNIST_VARIANT bits (A/B switches of k_fwd_conv; the default is what measured fastest):
 //   1  s_setprio 1 for waves 4-7 (the younger half of each SIMD pair, the VALU arbitration loser)
+//      (measured: 0.3-0.6 % slower, not adopted -- profiles/mnist_step_timeline_r5_v1.txt)
+//   2  fused backward: waves 4-7 run their conv2 dgrad before their wgrad (stagger)
+//      (measured: the backward's end and the step unchanged at K=20, 1-4 % slower at K=1000 -- the
+//      waves' MFMA work is the same either way and the SIMD pairs stay busy; not adopted,
+//      profiles/mnist_stagger_ab_r5.txt)
 constexpr int kMnistVariantPrio = 1;
+constexpr int kMnistVariantStagger = 2;
 constexpr int kDefaultMnistVariant = 0;
 
 constexpr int kMnistPart2Rows = 289;

@@ -768,32 +768,36 @@ __device__ __forceinline__ void fused_wgrad_tiles(const MnistArgs& a, int bi, in
 // dp2s: [25 windows][16] this quarter's masked dP2 (LDS), a2s its pool-2 argmax bytes, P1s/a1s/xs
 // the image's pooled conv1 output / pool-1 argmax / input (LDS), dCs the dC2 grid scratch, red
 // >= 8*10*16 floats of scratch.  Writes part2 columns 16cq.. of image bi and part1 row 4bi + cq.
+// this wave's conv2 dgrad operands W2[tap][16nt + i][16cq + 4g .. +3] (L2), nt = wave / 4
+__device__ __forceinline__ void load_dgrad_w2(const MnistArgs& a, int cq, f4 (&bwd)[9]) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int i = lane & 15, g = lane >> 4, nt = wave >> 2;
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) bwd[tap] = ld4(a.W + a.ow2 + (size_t)(tap * 32 + 16 * nt + i) * 64 + 16 * cq + 4 * g);
+}
+
 __device__ __forceinline__ void fused_conv_bwd(const MnistArgs& a, int bi, int cq, const float* dp2s,
                                                const uint8_t* a2s, const float* P1s, const uint8_t* a1s,
-                                               const float* xs, float* dCs, float* red) {
+                                               const float* xs, float* dCs, float* red, const f4 (&bwd)[9]) {
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int i = lane & 15, g = lane >> 4;
   // (the dC2 grid dCs is complete: zeroed during conv2, the masked dP2 values scattered to their
   // pool-2 argmax cells by the dP2 phase, behind the caller's barrier)
   bwd_stamp(a.stamps, 0);
-  // this wave's conv2 dgrad operands W2[tap][16nt + i][16cq + 4g .. +3] (L2): issued now, consumed
-  // after the wgrad (issued any earlier, the compiler's vmcnt bookkeeping stalled dP2 on them)
-  f4 bwd[9];
-  {
-    const int nt = wave >> 2;
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) bwd[tap] = ld4(a.W + a.ow2 + (size_t)(tap * 32 + 16 * nt + i) * 64 + 16 * cq + 4 * g);
-  }
 
-  // ---- conv2 wgrad: dW2[k = tap*32 + ci][16cq + co] over the 100 used positions (row tile 18 =
-  // the bias row).  k-step s covers positions 4s + g of the 10 x 10 grid (see k_conv_bwd).  All of
-  // a wave's row tiles advance together: one dC2 (B) read per k-step serves N MFMAs on N
-  // independent accumulators ----
-  {
+  // ---- conv2 wgrad: dW2[k = tap*32 + ci][16cq + co] over the 100 used positions.  k-step s
+  // covers positions 4s + g of the 10 x 10 grid (see k_conv_bwd).  All of a wave's row tiles
+  // advance together: one dC2 (B) read per k-step serves N MFMAs on N independent accumulators ----
+  auto wgrad = [&]() {
     const int t0 = kFusedWgradTiles[wave][0], ntiles = kFusedWgradTiles[wave][1];
     if (ntiles == 2) fused_wgrad_tiles<2>(a, bi, cq, t0, P1s, dCs);
     else fused_wgrad_tiles<3>(a, bi, cq, t0, P1s, dCs);
-  }
+  };
+  // the wgrad and the dgrad of a wave are independent: with kMnistVariantStagger the younger half
+  // (waves 4-7, each the SIMD partner of wave w - 4) runs them in the opposite order, so the two
+  // waves of a SIMD are not in the same phase at the same time (MI355X_MICROARCH.md item 9)
+  const bool swap = (a.variant & kMnistVariantStagger) && wave >= 4;
+  if (!swap) wgrad();
   bwd_stamp(a.stamps, 1);
 
   // ---- conv2 dgrad over this quarter's 16 output channels (a partial sum of dP1; everything after
@@ -880,6 +884,7 @@ __device__ __forceinline__ void fused_conv_bwd(const MnistArgs& a, int bi, int c
       }
     }
   }
+  if (swap) wgrad();
   bwd_stamp(a.stamps, 2);
 #pragma unroll
   for (int j = 0; j < 10; ++j) dw[j] = sum_lane_groups(dw[j]);
@@ -954,6 +959,12 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
     const int e = min(tid + j * 512, 1151);  // (k, q): k = e >> 2, channels 16cq + 4q .. +3
     vw2[j] = ld4(a.W + a.ow2 + (e >> 2) * 64 + 16 * cq + (e & 3) * 4);
   }
+  // the conv2 epilogue's bias and this step's hand-off tag, in the staging round trip: loaded where
+  // they are used, each was the youngest load of its wave there, and the vmcnt wait for it also
+  // waited for every W3 prefetch in flight (then a full global round trip on the critical path)
+  const float b2v = a.W[a.ob2 + 16 * cq + (lane & 15)];
+  // (a VGPR: a readfirstlane here would wait for the whole staging round trip before the LDS stores)
+  const uint32_t tag = a.ep[0] + 1u;  // (advanced by KC / KF)
   __builtin_amdgcn_sched_barrier(0);
   if (tid < 196) st4(xs + tid * 4, vx);
   if (tid < 320) w1s[tid] = vw1;
@@ -1105,8 +1116,7 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
       if (acc.y > m) { m = acc.y; am = 1; }
       if (acc.z > m) { m = acc.z; am = 2; }
       if (acc.w > m) { m = acc.w; am = 3; }
-      const int co = 16 * cq + i;
-      const float v = fmaxf(m + a.W[a.ob2 + co], 0.f);
+      const float v = fmaxf(m + b2v, 0.f);
       p2s[wo * 16 + i] = v;
       a2s[wo * 16 + i] = (uint8_t)am;
     }
@@ -1133,7 +1143,6 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   // dp2_fwd (training): every workgroup resident at once, so every quarter workgroup runs the head
   // itself from the other quarters' tagged partials; otherwise the last to arrive runs it
   const bool tagged = a.head == 1 && a.dp2_fwd;
-  const uint32_t tag = a.ep[0] + 1u;  // this step's hand-off tag (advanced by KC / KF)
   float* sown = red + 16 * 128 + 4;   // [128] this quarter's own partial
   if (tid < 32) {
     f4 hsum = zero4();
@@ -1165,6 +1174,9 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   // hand-off (only the image's last workgroup uses them; 5 KB, L2-resident)
   HeadWeights hw;
   if (wave == 0) hw = load_head_weights(a, lane);
+  // the fused backward's dgrad B operands (W2, L2-resident): in flight during the hand-off
+  f4 bwd[9];
+  if (a.head == 1 && a.dp2_fwd && a.fused_bwd) load_dgrad_w2(a, cq, bwd);
   // ---- hand-off to the image's last quarter workgroup (MI355X_MICROARCH.md, inter-workgroup
   // visibility, first table row): the storing wave drains its sc1 stores, a workgroup barrier,
   // ONE agent-scope add per workgroup on the image's counter; the workgroup whose add returns
@@ -1231,7 +1243,7 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
       st4_sc1(rs, (((kP2Quads - 1) * 64 + 16 * cq + rg) * 4) * 4, f4{sb, 0.f, 0.f, 0.f});
     }
     lds_barrier();
-    fused_conv_bwd(a, bi, cq, p2s, a2s, P1s, a1s, xs, dCs, red);
+    fused_conv_bwd(a, bi, cq, p2s, a2s, P1s, a1s, xs, dCs, red, bwd);
     return;
   }
   if (j < 25) {

@@ -97,8 +97,15 @@ at::Tensor buffered_shuffle(const at::Tensor& src, int64_t buffer_size, uint64_t
 
 }  // namespace
 
+namespace tdl {
+bool install_crash_trace();  // crash_trace.cpp
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "C++ runtime of tensorflow_distributed_learning_amd: TCP KV store / rendezvous, ring collectives";
+  m.def("install_crash_trace", &tdl::install_crash_trace,
+        "SIGABRT/SIGSEGV/SIGBUS/SIGFPE/SIGILL: print the faulting native thread's id, name and backtrace, then "
+        "chain to the previous handler (faulthandler) / the default action");
 
   py::class_<tdl::KVServer>(m, "KVServer")
       .def(py::init<const std::string&, int>(), py::arg("host"), py::arg("port"))

@@ -8,6 +8,7 @@
 #include "kernels/bn.h"
 #include "kernels/conv.h"
 #include "kernels/gemm.h"
+#include "kernels/gemm_f32.h"
 #include "kernels/ops.h"
 #include "kernels/pool.h"
 #include "kernels/stem.h"
@@ -638,6 +639,165 @@ at::Tensor gemm_bf16(at::Tensor a, int64_t ta, at::Tensor b, int64_t tb, c10::op
   return c;
 }
 
+// ---- generic f32 GEMM / convolution (kernels/gemm_f32.hip) ----
+void f32_check(const at::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous(), what,
+              " must be a contiguous f32 GPU tensor");
+}
+bool al16(const at::Tensor& t) { return reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0; }
+
+void f32_run(int mode, tdl::F32GemmArgs& a, const at::TensorOptions& o) {
+  TORCH_CHECK(a.Kred > 0, "f32 gemm: empty reduction");
+  tdl::f32_gemm_plan(a);
+  at::Tensor ws;
+  if (a.splits > 1) {
+    ws = at::empty({(int64_t)a.splits * a.M * a.N}, o);
+    a.ws = ws.data_ptr<float>();
+  }
+  tdl::f32_gemm_launch(mode, a, cur_stream());
+}
+
+const float* f32_bias(const c10::optional<at::Tensor>& bias, int64_t n) {
+  if (!bias.has_value() || !bias->defined()) return nullptr;
+  f32_check(*bias, "f32 gemm: bias");
+  TORCH_CHECK(bias->numel() == n, "f32 gemm: bias must have N elements");
+  return bias->data_ptr<float>();
+}
+
+// out: f32 [rows][cols] given (accumulate: +=) or a new tensor
+at::Tensor f32_out(c10::optional<at::Tensor>& out, at::IntArrayRef shape, const at::TensorOptions& o) {
+  if (out.has_value() && out->defined()) {
+    f32_check(*out, "f32 gemm: out");
+    TORCH_CHECK(out->sizes() == shape, "f32 gemm: out has the wrong shape");
+    return *out;
+  }
+  return fresh(shape, o);
+}
+
+// C = op(A) op(B) (+ bias) in f32; ta = 0: a is [M][K], 1: [K][M]; tb = 0: b is [N][K], 1: [K][N]
+at::Tensor gemm_f32(at::Tensor a, int64_t ta, at::Tensor b, int64_t tb, c10::optional<at::Tensor> bias,
+                    c10::optional<at::Tensor> out, bool accumulate) {
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "gemm_f32: 2-D operands");
+  f32_check(a, "gemm_f32: a");
+  f32_check(b, "gemm_f32: b");
+  const int64_t M = ta ? a.size(1) : a.size(0), K = ta ? a.size(0) : a.size(1);
+  const int64_t N = tb ? b.size(1) : b.size(0), Kb = tb ? b.size(0) : b.size(1);
+  TORCH_CHECK(K == Kb, "gemm_f32: inner dimensions differ");
+  auto c = f32_out(out, {M, N}, a.options());
+  tdl::F32GemmArgs g{};
+  g.a = a.data_ptr<float>();
+  g.b = b.data_ptr<float>();
+  g.out = c.data_ptr<float>();
+  g.bias = f32_bias(bias, N);
+  g.sam = ta ? 1 : a.stride(0);
+  g.sak = ta ? a.stride(0) : 1;
+  g.sbk = tb ? b.stride(0) : 1;
+  g.sbn = tb ? 1 : b.stride(0);
+  g.M = (int)M;
+  g.N = (int)N;
+  g.Kred = (int)K;
+  g.ldo = N;
+  g.accumulate = accumulate && out.has_value() && out->defined();
+  g.vec_a = g.sak == 1 && g.sam % 4 == 0 && K % 4 == 0 && al16(a);
+  g.vec_b = g.sbn == 1 && g.sbk % 4 == 0 && N % 4 == 0 && al16(b);
+  f32_run(tdl::kF32Gemm, g, a.options());
+  return c;
+}
+
+tdl::F32ConvGeom f32_geom(const at::Tensor& x_like, int64_t k, int64_t r, int64_t s, int64_t oh, int64_t ow, int64_t sh,
+                          int64_t sw, int64_t pt, int64_t pl, int64_t dh, int64_t dw) {
+  tdl::F32ConvGeom g{};
+  g.n = (int)x_like.size(0);
+  g.h = (int)x_like.size(1);
+  g.w = (int)x_like.size(2);
+  g.c = (int)x_like.size(3);
+  g.k = (int)k;
+  g.r = (int)r;
+  g.s = (int)s;
+  g.oh = (int)oh;
+  g.ow = (int)ow;
+  g.sh = (int)sh;
+  g.sw = (int)sw;
+  g.pt = (int)pt;
+  g.pl = (int)pl;
+  g.dh = (int)dh;
+  g.dw = (int)dw;
+  TORCH_CHECK(sh > 0 && sw > 0 && dh > 0 && dw > 0, "f32 conv: strides and dilations must be positive");
+  return g;
+}
+
+// y[N][OH][OW][K] = conv(x NHWC, w HWIO) (+ bias); padding (pt, pl) top / left, the rest implied by OH / OW
+at::Tensor conv_f32_fwd(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> bias, int64_t oh, int64_t ow, int64_t sh,
+                        int64_t sw, int64_t pt, int64_t pl, int64_t dh, int64_t dw) {
+  f32_check(x, "conv_f32_fwd: x");
+  f32_check(w, "conv_f32_fwd: w");
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && w.size(2) == x.size(3), "conv_f32_fwd: x NHWC, w [R][S][C][K]");
+  const int64_t K = w.size(3);
+  auto y = fresh({x.size(0), oh, ow, K}, x.options());
+  tdl::F32GemmArgs g{};
+  g.g = f32_geom(x, K, w.size(0), w.size(1), oh, ow, sh, sw, pt, pl, dh, dw);
+  g.a = x.data_ptr<float>();
+  g.b = w.data_ptr<float>();
+  g.out = y.data_ptr<float>();
+  g.bias = f32_bias(bias, K);
+  g.M = (int)(x.size(0) * oh * ow);
+  g.N = (int)K;
+  g.Kred = (int)(w.size(0) * w.size(1) * x.size(3));
+  g.ldo = K;
+  g.vec_a = x.size(3) % 4 == 0 && al16(x);
+  g.vec_b = K % 4 == 0 && al16(w);
+  f32_run(tdl::kF32ConvFwd, g, x.options());
+  return y;
+}
+
+// dx[N][H][W][C] of a conv with dy [N][OH][OW][K] and wt = w as [R][S][K][C]
+at::Tensor conv_f32_dgrad(at::Tensor dy, at::Tensor wt, int64_t h, int64_t wd, int64_t sh, int64_t sw, int64_t pt,
+                          int64_t pl, int64_t dh, int64_t dw) {
+  f32_check(dy, "conv_f32_dgrad: dy");
+  f32_check(wt, "conv_f32_dgrad: wt");
+  TORCH_CHECK(dy.dim() == 4 && wt.dim() == 4 && wt.size(2) == dy.size(3), "conv_f32_dgrad: dy NHWC, wt [R][S][K][C]");
+  const int64_t C = wt.size(3), K = dy.size(3);
+  auto dx = fresh({dy.size(0), h, wd, C}, dy.options());
+  tdl::F32GemmArgs g{};
+  g.g = f32_geom(dx, K, wt.size(0), wt.size(1), dy.size(1), dy.size(2), sh, sw, pt, pl, dh, dw);
+  g.a = dy.data_ptr<float>();
+  g.b = wt.data_ptr<float>();
+  g.out = dx.data_ptr<float>();
+  g.M = (int)(dy.size(0) * h * wd);
+  g.N = (int)C;
+  g.Kred = (int)(wt.size(0) * wt.size(1) * K);
+  g.ldo = C;
+  g.vec_a = K % 4 == 0 && al16(dy);
+  g.vec_b = C % 4 == 0 && al16(wt);
+  f32_run(tdl::kF32ConvDgrad, g, dy.options());
+  return dx;
+}
+
+// dW HWIO [R][S][C][K] of a conv with x NHWC and dy [N][OH][OW][K] (into / += out when given)
+at::Tensor conv_f32_wgrad(at::Tensor x, at::Tensor dy, int64_t r, int64_t s, int64_t sh, int64_t sw, int64_t pt,
+                          int64_t pl, int64_t dh, int64_t dw, c10::optional<at::Tensor> out, bool accumulate) {
+  f32_check(x, "conv_f32_wgrad: x");
+  f32_check(dy, "conv_f32_wgrad: dy");
+  TORCH_CHECK(x.dim() == 4 && dy.dim() == 4 && x.size(0) == dy.size(0), "conv_f32_wgrad: x, dy NHWC");
+  const int64_t C = x.size(3), K = dy.size(3);
+  auto dW = f32_out(out, {r, s, C, K}, x.options());
+  tdl::F32GemmArgs g{};
+  g.g = f32_geom(x, K, r, s, dy.size(1), dy.size(2), sh, sw, pt, pl, dh, dw);
+  g.a = dy.data_ptr<float>();
+  g.b = x.data_ptr<float>();
+  g.out = dW.data_ptr<float>();
+  g.M = (int)K;
+  g.N = (int)(r * s * C);
+  TORCH_CHECK(dy.numel() / K < (int64_t)1 << 31, "conv_f32_wgrad: reduction too long");
+  g.Kred = (int)(dy.size(0) * dy.size(1) * dy.size(2));
+  g.ldo = K;
+  g.trans_out = 1;
+  g.accumulate = accumulate && out.has_value() && out->defined();
+  g.vec_b = C % 4 == 0 && al16(x);
+  f32_run(tdl::kF32ConvWgrad, g, x.options());
+  return dW;
+}
+
 at::Tensor gap_fwd(at::Tensor x) {
   conv_check(x, "gap: x");
   TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "gap: NHWC with C % 8 == 0");
@@ -683,6 +843,21 @@ void register_ops(pybind11::module& m) {
         pybind11::arg("a"), pybind11::arg("ta"), pybind11::arg("b"), pybind11::arg("tb"),
         pybind11::arg("bias") = pybind11::none(), pybind11::arg("out") = pybind11::none(),
         pybind11::arg("accumulate") = false, pybind11::arg("alpha") = 1.0);
+  m.def("gemm_f32", &gemm_f32, "f32 MFMA GEMM (v_mfma_f32_16x16x4_f32) with either storage per operand",
+        pybind11::arg("a"), pybind11::arg("ta"), pybind11::arg("b"), pybind11::arg("tb"),
+        pybind11::arg("bias") = pybind11::none(), pybind11::arg("out") = pybind11::none(),
+        pybind11::arg("accumulate") = false);
+  m.def("conv_f32_fwd", &conv_f32_fwd, "NHWC f32 implicit-GEMM convolution forward, any geometry",
+        pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("bias"), pybind11::arg("oh"), pybind11::arg("ow"),
+        pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("pt"), pybind11::arg("pl"), pybind11::arg("dh") = 1,
+        pybind11::arg("dw") = 1);
+  m.def("conv_f32_dgrad", &conv_f32_dgrad, "NHWC f32 convolution input gradient, any geometry (wt: [R][S][K][C])",
+        pybind11::arg("dy"), pybind11::arg("wt"), pybind11::arg("h"), pybind11::arg("w"), pybind11::arg("sh"),
+        pybind11::arg("sw"), pybind11::arg("pt"), pybind11::arg("pl"), pybind11::arg("dh") = 1, pybind11::arg("dw") = 1);
+  m.def("conv_f32_wgrad", &conv_f32_wgrad, "NHWC f32 convolution weight gradient (HWIO), deterministic split-K",
+        pybind11::arg("x"), pybind11::arg("dy"), pybind11::arg("r"), pybind11::arg("s"), pybind11::arg("sh"),
+        pybind11::arg("sw"), pybind11::arg("pt"), pybind11::arg("pl"), pybind11::arg("dh") = 1, pybind11::arg("dw") = 1,
+        pybind11::arg("out") = pybind11::none(), pybind11::arg("accumulate") = false);
   m.def("gap_fwd", &gap_fwd, "NHWC bf16 global average pooling");
   m.def("gap_bwd", &gap_bwd, "NHWC bf16 global average pooling backward");
   m.def("slab_cast_bf16", &slab_cast_bf16, "f32 -> bf16 copy of a whole weight slab (one launch)");

@@ -87,8 +87,15 @@ def eligible(model, dataset=None) -> Optional[str]:
             lo.reduction in (losses.Reduction.AUTO, losses.Reduction.SUM_OVER_BATCH_SIZE)):
         return "loss is not SparseCategoricalCrossentropy(from_logits=True)"
     opt = model.optimizer
-    if not isinstance(opt, optimizers.SGD) or opt.clipnorm or opt.clipvalue or opt.global_clipnorm or opt.weight_decay:
-        return "optimizer is not plain/momentum SGD"
+    if type(opt) not in (optimizers.SGD, optimizers.Adam, optimizers.AdamW, optimizers.RMSprop, optimizers.Adagrad):
+        return f"optimizer {type(opt).__name__} has no fused update"
+    if opt.clipnorm or opt.clipvalue or opt.global_clipnorm:
+        return "gradient clipping (a global norm) is not fused"
+    if opt.weight_decay and not isinstance(opt, optimizers.Adam):
+        return "decoupled weight decay is fused for Adam/AdamW only"
+    kern = {"Adam": "adam", "AdamW": "adam", "RMSprop": "rmsprop", "Adagrad": "adagrad"}.get(type(opt).__name__)
+    if kern is not None and not hasattr(ops.hip(), kern):
+        return f"the extension has no {kern} kernel (rebuild: python build_native.py)"
     for m in model.compiled_metrics:
         if not isinstance(m, metrics.SparseCategoricalAccuracy):
             return f"metric {m.name} not supported by the fused step"
@@ -204,12 +211,14 @@ class FusedMnistTrainer:
             self._steps[key] = st
         return st
 
-    def _apply(self, st, global_b: int):
-        """finalize + (all-reduce) + optimizer for one step.  R > 1 with plain SGD: one all-reduce
-        of the whole 900 KB slab with the SGD update fused into it (xGMI kernel), when the
-        communicator has one."""
+    def _apply(self, st, global_b: int, k: int = 0):
+        """finalize + (all-reduce) + optimizer for one step (step ``k`` of its execution).  R > 1
+        with plain SGD: one all-reduce of the whole 900 KB slab with the SGD update fused into it
+        (xGMI kernel), when the communicator has one.  Other optimizers: finalize leaves the
+        gradient in G, their flat-slab kernel (csrc/kernels/optim.hip) applies it."""
         opt = self.optimizer
-        plain = opt.momentum == 0
+        self._step_k = k
+        plain = getattr(opt, "momentum", None) == 0 and type(opt).__name__ == "SGD"
         if self.R == 1 and plain:
             st.finalize(True)
             return
@@ -231,9 +240,9 @@ class FusedMnistTrainer:
         follows finalize().  With the xGMI one-shot communicator each bucket's all-reduce also
         applies plain SGD to its own parameter range (W[dense_offset:] is not read again in the
         step), so no separate optimizer kernel runs; otherwise the optimizer waits for both."""
-        if self.R == 1 or not self.overlap:
+        if self.R == 1 or not self.overlap or not self._plain_sgd:
             st.forward_backward(off)
-            self._apply(st, global_b)
+            self._apply(st, global_b, off // max(1, st.b))
             return
         main = torch.cuda.current_stream(self.device)
         if self._comm_stream is None:
@@ -276,7 +285,7 @@ class FusedMnistTrainer:
             self._xchg = None
             # one-shot moves (R-1) slabs per rank over the fabric, two-shot 2 (R-1)/R in two rounds
             self._xchg_twoshot = self.R >= int(os.environ.get("TDL_FX_TWOSHOT_MIN_R", "3"))
-            if st.fused_bwd and self.optimizer.momentum == 0 and os.environ.get("TDL_MNIST_FINALIZE_XCHG", "1") == "1":
+            if st.fused_bwd and self._plain_sgd and os.environ.get("TDL_MNIST_FINALIZE_XCHG", "1") == "1":
                 self._xchg = self.comm.exchange_channel(n, M.FINALIZE_BLOCKS)
                 if self._xchg is not None and not self._selftest_exchange(st.b):
                     self._xchg = None
@@ -369,12 +378,23 @@ class FusedMnistTrainer:
         dist.all_reduce(f, op=dist.ReduceOp.MIN)
         return [bool(v > 0.5) for v in f.tolist()]
 
+    @property
+    def _plain_sgd(self) -> bool:
+        opt = self.optimizer
+        return type(opt).__name__ == "SGD" and opt.momentum == 0
+
     def _update(self, lo: int = 0, hi: Optional[int] = None):
         from .. import ops
 
         opt = self.optimizer
         C = ops.hip()
         W, G = self.W[lo:hi], self.G[lo:hi]
+        if type(opt).__name__ != "SGD":
+            # whole slab only (lo, hi cover it: the two-bucket split is SGD-only); Adam's step offset
+            # inside the execution is baked into the captured graph
+            if not opt.device_update(W, G, getattr(self, "_step_k", 0)):
+                raise RuntimeError(f"fused trainer: {type(opt).__name__} has no device update on {W.device}")
+            return
         if opt.momentum == 0:
             C.sgd(W, G, opt.lr_dev)
         else:
@@ -562,8 +582,9 @@ class FusedMnistTrainer:
                     self._train_step(st, k * b, b * self.R)
                 K = Kr
             elif isinstance(graph, list):
-                for gk in graph:
+                for k, gk in enumerate(graph):
                     gk.replay()
+                    self._step_k = k
                     self._reduce_and_update()
             elif graph is not None:
                 graph.replay()

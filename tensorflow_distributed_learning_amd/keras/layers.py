@@ -20,6 +20,7 @@ import torch.nn.functional as F
 
 from ..parallel.values import Variable, VariableAggregation, VariableSynchronization, create_variable
 from ..ops import conv as _conv
+from ..ops import conv_f32 as _conv_f32
 from ..ops import dense as _dense
 from . import activations as _act
 from . import initializers as _init
@@ -267,6 +268,16 @@ class Dense(Layer):
                 return self.activation(_dense.dense_bf16(x, w, b, (gw, gb), anchor=self.kernel.value))
             b = self.bias.value if self.bias is not None else None
             return self.activation(_dense.dense_bf16(x, self.kernel.cast(x.dtype), b))
+        if _conv_f32.dense_supported(x) and self.kernel.value.dtype == torch.float32:
+            # f32 on the GPU: the f32-MFMA GEMM of csrc/kernels/gemm_f32.hip (no hipBLASLt)
+            gw = self.kernel.grad_target()
+            gb = self.bias.grad_target() if self.bias is not None else None
+            if gw is not None and gw.is_contiguous() and (self.bias is None or gb is not None):
+                b = self.bias.value.detach() if self.bias is not None else None
+                return self.activation(_conv_f32.dense(x, self.kernel.value.detach(), b, (gw, gb),
+                                                       anchor=self.kernel.value))
+            b = self.bias.value if self.bias is not None else None
+            return self.activation(_conv_f32.dense(x, self.kernel.value, b))
         y = torch.matmul(x, self.kernel.cast(x.dtype))
         if self.bias is not None:
             y = y + self.bias.value.to(y.dtype)
@@ -399,6 +410,24 @@ class Conv2D(Layer):
             return self.activation(y)
         if getattr(x, "_tdl_bn_in", None) is not None:  # (keras/fusion.py plans it only where the kernels run)
             raise RuntimeError("Conv2D: a deferred BN -> ReLU input needs the hand-written 1x1 kernels")
+        if _conv_f32.supported(x, self.groups) and _conv.mode() != "miopen":
+            # every other conv -- f32 layers, asymmetric 'same' padding, dilation, channel counts the bf16
+            # kernels do not tile: the generic f32-MFMA implicit GEMM (ops/conv_f32.py)
+            pads = (0, 0, 0, 0)
+            if self.padding == "same":
+                ph = _same_pads(x.shape[1], self.kernel_size[0], self.strides[0], self.dilation_rate[0])
+                pw = _same_pads(x.shape[2], self.kernel_size[1], self.strides[1], self.dilation_rate[1])
+                pads = (ph[0], ph[1], pw[0], pw[1])
+            gt = self.kernel.grad_target()
+            if gt is not None and gt.is_contiguous():
+                wv, anchor = self.kernel.value.detach(), self.kernel.value
+            else:
+                gt, wv, anchor = None, self.kernel.cast(x.dtype), None
+            y = _conv_f32.conv2d(x, wv, b, self.strides, pads, self.dilation_rate, grad_out=gt, anchor=anchor)
+            return self.activation(y)
+        if x.is_cuda:  # no hand-written kernel covers this conv: library path, counted (ops/conv.py)
+            _conv._lib("conv2d", f"{str(x.dtype).replace('torch.', '')} C={x.shape[-1]} K={w.shape[0]} "
+                       f"{self.kernel_size[0]}x{self.kernel_size[1]}/{self.strides[0]} {self.padding}")
         y = F.conv2d(h, w, b, stride=self.strides, padding=pad, dilation=self.dilation_rate, groups=self.groups)
         return self.activation(y.permute(0, 2, 3, 1))
 

@@ -1,10 +1,11 @@
 """Keras optimizers over the flat parameter slab.
 
 Every replica applies the optimizer to its whole slab in ONE update after the gradient
-all-reduce (TF applies ``ResourceApplyGradientDescent`` once per variable).  On the GPU, SGD /
-momentum SGD run the hand-written gfx950 kernel (``_C.sgd`` / ``_C.sgd_momentum``, learning rate
-read from device memory so the update can sit inside a captured hipGraph); Adam/RMSprop/Adagrad
-use a handful of fused torch ops on the slab.
+all-reduce (TF applies ``ResourceApplyGradientDescent`` once per variable).  On the GPU every
+optimizer is one hand-written gfx950 kernel over the slab (``_C.sgd`` / ``_C.sgd_momentum``,
+``_C.adam`` (AdamW's decay in the same pass), ``_C.rmsprop``, ``_C.adagrad``; csrc/kernels/optim.hip),
+with the learning rate and Adam's step count read from device memory so the update can sit inside
+a captured hipGraph.  Gradient clipping keeps its torch ops (a global norm).
 """
 from __future__ import annotations
 
@@ -29,6 +30,10 @@ class Optimizer:
         self._device = None
         self.lr_dev: Optional[torch.Tensor] = None
         self._lr_synced = None  # (value, lr_dev address) last written by _sync_lr
+        # device copy of ``iterations`` at the start of the next step / execution (Adam's bias
+        # correction on the device: a captured step graph reads it, each step adds its offset)
+        self.t_dev: Optional[torch.Tensor] = None
+        self._t_synced = None
         unknown = set(kwargs) - {"decay", "amsgrad_legacy", "jit_compile", "is_legacy_optimizer",
                                  "use_ema", "ema_momentum", "ema_overwrite_frequency"}
         if unknown:
@@ -61,6 +66,20 @@ class Optimizer:
             if self._lr_synced != (v, self.lr_dev.data_ptr()):
                 self.lr_dev.fill_(v)
                 self._lr_synced = (v, self.lr_dev.data_ptr())
+        if self.t_dev is not None and self._needs_step:
+            t = float(self.iterations if step is None else step)
+            if self._t_synced != (t, self.t_dev.data_ptr()):
+                self.t_dev.fill_(t)
+                self._t_synced = (t, self.t_dev.data_ptr())
+
+    _needs_step = False  # the device update reads t_dev (Adam's bias correction)
+
+    def device_update(self, W: torch.Tensor, G: torch.Tensor, t_add: int = 0) -> bool:
+        """One hand-written flat-slab update kernel (learning rate and step count read from the
+        device: capturable) when this optimizer has one and the slab is on the GPU; False
+        otherwise (the caller then uses apply_flat).  ``t_add``: the step's offset inside an
+        execution whose first step is t_dev (Adam)."""
+        return False
 
     # ------------------------------------------------------------------ slots
     def build(self, n: int, device: torch.device):
@@ -69,6 +88,8 @@ class Optimizer:
         self._n, self._device = n, device
         self.lr_dev = torch.full((1,), self.current_lr(), dtype=torch.float32, device=device)
         self._lr_synced = (self.current_lr(), self.lr_dev.data_ptr())
+        self.t_dev = torch.full((1,), float(self.iterations), dtype=torch.float32, device=device)
+        self._t_synced = (float(self.iterations), self.t_dev.data_ptr())
         for k in self._slot_names():
             old = self._slots.get(k)
             self._slots[k] = old.to(device) if (old is not None and old.numel() == n) else torch.zeros(
@@ -149,13 +170,12 @@ class Optimizer:
             self._slots[k] = v.to(self._device) if self._device is not None else v.clone()
 
 
-def _hip_ok(t: torch.Tensor) -> bool:
+def _hip_ok(t: torch.Tensor, kernel: str = "sgd") -> bool:
     if t.device.type != "cuda" or t.dtype != torch.float32:
         return False
     from .. import ops
 
-    ops.hip()  # raises loudly if the HIP kernels are missing on a GPU box
-    return True
+    return hasattr(ops.hip(), kernel)  # ops.hip() raises loudly if the HIP kernels are missing on a GPU box
 
 
 class SGD(Optimizer):
@@ -174,15 +194,20 @@ class SGD(Optimizer):
     def _slot_names(self):
         return ["momentum"] if self.momentum > 0 else []
 
-    def _update(self, W, G):
-        if _hip_ok(W):
-            from .. import ops
+    def device_update(self, W, G, t_add=0):
+        if not _hip_ok(W) or self.weight_decay:
+            return False
+        from .. import ops
 
-            C = ops.hip()
-            if self.momentum > 0:
-                C.sgd_momentum(W, G, self._slots["momentum"], self.lr_dev, self.momentum, self.nesterov)
-            else:
-                C.sgd(W, G, self.lr_dev)
+        C = ops.hip()
+        if self.momentum > 0:
+            C.sgd_momentum(W, G, self._slots["momentum"], self.lr_dev, self.momentum, self.nesterov)
+        else:
+            C.sgd(W, G, self.lr_dev)
+        return True
+
+    def _update(self, W, G):
+        if self.device_update(W, G):
             return
         lr = self.current_lr()
         if self.momentum > 0:
@@ -206,6 +231,30 @@ class Adam(Optimizer):
 
     def _slot_names(self):
         return ["m", "v"] + (["vhat"] if self.amsgrad else [])
+
+    graph_safe = True  # lr and the step count come from device memory (t_dev)
+    _needs_step = True
+
+    def device_update(self, W, G, t_add=0):
+        """csrc/kernels/optim.hip k_adam (AdamW's decoupled decay inside the same pass)."""
+        if not _hip_ok(W, "adam"):
+            return False
+        from .. import ops
+
+        ops.hip().adam(W, G, self._slots["m"], self._slots["v"], self._slots.get("vhat"), self.lr_dev, self.t_dev,
+                       int(t_add), self.beta_1, self.beta_2, self.epsilon, float(self.weight_decay or 0.0))
+        return True
+
+    def apply_flat(self, W, G, sync_lr: bool = True):
+        if self._n != W.numel() or self._device != W.device:
+            self.build(W.numel(), W.device)
+        if sync_lr:
+            self._sync_lr()
+        if (self.clipvalue is None and not (self.global_clipnorm or self.clipnorm)
+                and self.device_update(W, G)):  # decay + update in one kernel
+            self.iterations += 1
+            return
+        super().apply_flat(W, G, sync_lr=False)
 
     def _update(self, W, G):
         t = self.iterations + 1
@@ -239,7 +288,21 @@ class RMSprop(Optimizer):
     def _slot_names(self):
         return ["rms"] + (["mom"] if self.momentum > 0 else []) + (["mg"] if self.centered else [])
 
+    graph_safe = True
+
+    def device_update(self, W, G, t_add=0):
+        """csrc/kernels/optim.hip k_rmsprop."""
+        if not _hip_ok(W, "rmsprop") or self.weight_decay:
+            return False
+        from .. import ops
+
+        ops.hip().rmsprop(W, G, self._slots["rms"], self._slots.get("mom"), self._slots.get("mg"), self.lr_dev,
+                          self.rho, self.momentum, self.epsilon)
+        return True
+
     def _update(self, W, G):
+        if self.device_update(W, G):
+            return
         lr = self.current_lr()
         rms = self._slots["rms"]
         rms.mul_(self.rho).addcmul_(G, G, value=1 - self.rho)
@@ -271,7 +334,20 @@ class Adagrad(Optimizer):
         if fresh:
             self._slots["acc"].fill_(self.init_acc)
 
+    graph_safe = True
+
+    def device_update(self, W, G, t_add=0):
+        """csrc/kernels/optim.hip k_adagrad."""
+        if not _hip_ok(W, "adagrad") or self.weight_decay:
+            return False
+        from .. import ops
+
+        ops.hip().adagrad(W, G, self._slots["acc"], self.lr_dev, self.epsilon)
+        return True
+
     def _update(self, W, G):
+        if self.device_update(W, G):
+            return
         acc = self._slots["acc"]
         acc.addcmul_(G, G)
         W.addcdiv_(G, acc.sqrt().add_(self.epsilon), value=-self.current_lr())

@@ -4,16 +4,22 @@ The reference's ``tf.keras.layers.Conv2D`` (tf_dist_example.py:41,43; ResNet-50 
 4/5) runs on cuDNN inside TensorFlow.  Here a Conv2D with bf16 NHWC activations, C and K multiples
 of 64 and symmetric padding has two implementations per direction: the hand-written kernels
 (forward; stride-1 and 1x1 stride-2 input gradient, csrc/kernels/conv.hip; weight gradient,
-csrc/kernels/conv_wgrad.hip) and MIOpen (through ``torch.nn.functional``).  Other strided input
-gradients stay on MIOpen.
+csrc/kernels/conv_wgrad.hip) and MIOpen (through ``torch.nn.functional``, a test oracle).  The
+directions and shapes those bf16 kernels do not tile (other strided input gradients, >= 2^24-row
+weight gradients) and every f32 / odd-channel / asymmetric-padding / dilated conv run on the
+generic f32-MFMA kernels of ops/conv_f32.py (csrc/kernels/gemm_f32.hip).
 
-``TDL_CONV`` picks: ``auto`` (default) times both implementations on the first eager call of every
-(shape, direction) and keeps the faster one (decisions are cached per process and never measured
-while a HIP graph is being captured; an unmeasured shape inside a capture uses MIOpen), ``hip``
-forces the hand-written kernels wherever they apply, ``miopen`` disables them.
+``TDL_CONV`` picks: ``hip`` (default) runs the hand-written kernels for every shape they cover;
+``auto`` times both implementations on the first eager call of every (shape, direction) and keeps
+the faster one (decisions are cached per process and never measured while a HIP graph is being
+captured: an unmeasured shape inside a capture takes the hand-written kernel); ``miopen`` disables
+them (a test oracle).  Every convolution that still runs on the library -- a shape or dtype no
+hand-written kernel covers, ``miopen`` / ``auto`` choices, the very large weight gradients -- is
+counted in :data:`LIB_CALLS` (``library_calls()``; bench JSON ``fallbacks``).
 """
 from __future__ import annotations
 
+import collections
 import os
 import threading
 
@@ -71,7 +77,25 @@ _times: dict = {}  # (direction, shape key) -> (hand-written ms, MIOpen ms) as m
 
 
 def mode() -> str:
-    return os.environ.get("TDL_CONV", "auto").lower()
+    return os.environ.get("TDL_CONV", "hip").lower()
+
+
+# convolution work that ran on the library (MIOpen through torch) instead of a hand-written kernel:
+# (direction, reason) -> calls.  Empty on the hot path of every model whose convs the kernels cover.
+LIB_CALLS: "collections.Counter" = collections.Counter()
+
+
+def _lib(direction: str, reason: str) -> None:
+    LIB_CALLS[(direction, reason)] += 1
+
+
+def library_calls() -> dict:
+    """{(direction, reason): calls} of convolutions that ran on MIOpen since the last reset."""
+    return dict(LIB_CALLS)
+
+
+def reset_library_calls() -> None:
+    LIB_CALLS.clear()
 
 
 def supported(x: torch.Tensor, kernel_hwio: torch.Tensor, groups=1, dilation=(1, 1)) -> bool:
@@ -169,14 +193,14 @@ def _bound_comm():
 
 
 def _capture_fallback(key) -> None:
-    """A shape first met inside a graph capture cannot be timed (nor agreed on collectively): it
-    runs on the library path.  Say so once per shape instead of going silent."""
+    """``auto`` mode: a shape first met inside a graph capture cannot be timed (nor agreed on
+    collectively): it takes the hand-written kernel untimed.  Said once per shape."""
     if key not in _FALLBACK_LOGGED:
         _FALLBACK_LOGGED.add(key)
         import warnings
 
         warnings.warn(f"conv autotuner: {key[0]} shape {key[1:]} first seen inside a hipGraph capture; "
-                      "using MIOpen for it (run one eager step of every shape before capturing)")
+                      "using the hand-written kernel untimed (run one eager step of every shape before capturing)")
 
 
 _AGREE_WIDTH = 5  # [chosen, wmw, wnw, nsplit, kind]
@@ -208,7 +232,7 @@ def _pick(key, hip_fn, ref_fn, saved_bytes: int = 0) -> bool:
         return got
     if torch.cuda.is_current_stream_capturing():
         _capture_fallback(key)
-        return False
+        return True
 
     def decide():
         t_ref = _time(ref_fn) + saved_bytes / _HBM_BYTES_PER_MS
@@ -240,7 +264,7 @@ def _pick_wgrad(key, C, x, dy, kh, kw, stride, pad, ref_fn):
         return plans[0]
     if torch.cuda.is_current_stream_capturing():
         _capture_fallback(key)
-        return None
+        return plans[0]
 
     def decide():
         t_ref = _time(ref_fn)
@@ -301,6 +325,7 @@ class _Conv(torch.autograd.Function):
             else:
                 y = hip_fn()
         else:
+            _lib("fwd", f"{mode()} mode chose MIOpen")
             y = _ref_fwd(x, w_oihw, stride, pad).contiguous()
         ctx.save_for_backward(x, kernel)
         ctx.geo = (stride, pad)
@@ -430,7 +455,27 @@ class _Conv(torch.autograd.Function):
                 else:
                     dw = C.conv_wgrad(x, dy, kh, kw, stride[0], stride[1], pad[0], pad[1], plan=plan)
         need_dx, need_dw = want_dx and dx is None, want_dw and dw is None
+        if (need_dx or need_dw) and mode() == "hip":
+            # no bf16 kernel for this direction / size (strided 3x3 input gradients, >= 2^24-row weight
+            # gradients): the generic f32-MFMA kernels of ops/conv_f32.py, not the library
+            from . import conv_f32 as _cf
+
+            pads4 = (pad[0], pad[0], pad[1], pad[1])
+            if need_dx:
+                dx = _cf.dgrad(dy, kernel, (x.shape[1], x.shape[2]), stride, pads4).to(x.dtype)
+            if need_dw:
+                xs = _bn_relu_ref(x, bn_in) if bn_in is not None else x
+                if gout is not None:
+                    _cf.wgrad(xs, dy, (kh, kw), stride, pads4, out=gout, accumulate=True)
+                else:
+                    dw = _cf.wgrad(xs, dy, (kh, kw), stride, pads4).to(kernel.dtype)
+            need_dx = need_dw = False
         if need_dx or need_dw:
+            if need_dx:
+                _lib("dgrad", f"stride {tuple(stride)} {kh}x{kw}" if hip_fn is None else f"{mode()} mode chose MIOpen")
+            if need_dw:
+                _lib("wgrad", f"{mode()} mode chose MIOpen" if x.shape[0] * dy.shape[1] * dy.shape[2] < (1 << 24)
+                     else "reduction >= 2^24 rows")
             gx, gw, _ = ref([need_dx, need_dw, False])()
             if need_dx:
                 dx = gx.permute(0, 2, 3, 1)
@@ -574,12 +619,10 @@ class _Stem(torch.autograd.Function):
             C.stem_wgrad(xp, dy, kh, kw, cin, stride[0], out=ctx.grad_out, accumulate=True)
         elif ctx.needs_input_grad[1]:
             dw = C.stem_wgrad(xp, dy, kh, kw, cin, stride[0]).to(kernel.dtype)
-        if ctx.needs_input_grad[0]:  # image gradient (not needed for training): library path
-            xpad = F.pad(x, (0, 0, pads[2], pads[3], pads[0], pads[1]))
-            w_oihw = kernel.to(dy.dtype).permute(3, 2, 0, 1)
-            g = _miopen_bwd(dy.permute(0, 3, 1, 2), xpad.to(dy.dtype).permute(0, 3, 1, 2), w_oihw, list(stride),
-                            [0, 0], [True, False, False])[0].permute(0, 2, 3, 1)
-            dx = g[:, pads[0]:g.shape[1] - pads[1], pads[2]:g.shape[2] - pads[3], :].to(x.dtype)
+        if ctx.needs_input_grad[0]:  # image gradient (not needed for training): the generic f32 kernel
+            from . import conv_f32 as _cf
+
+            dx = _cf.dgrad(dy, kernel, (x.shape[1], x.shape[2]), stride, pads).to(x.dtype)
         return dx, dw, None, None, None, None, None
 
 

@@ -1,0 +1,136 @@
+"""Generic f32 convolution and Dense on the hand-written f32-MFMA kernels (csrc/kernels/gemm_f32.hip).
+
+The bf16 kernels of ops/conv.py and ops/dense.py cover the shapes of the mixed-precision models
+(channels in multiples of 64, symmetric padding, the 1x1 stride-2 and stride-1 input gradients).
+Everything else -- the f32 layers of the reference CNN in the generic engine (``Conv2D(32, 3)`` over a
+1-channel image, ``padding='same'`` variants, Dense in f32), asymmetric 'same' padding, dilation,
+strided 3x3 input gradients, weight gradients with >= 2^24 reduction rows -- runs here instead of
+on MIOpen / hipBLASLt: one implicit-GEMM kernel family on ``v_mfma_f32_16x16x4_f32`` (exact f32
+products) with per-mode operand gathers, deterministic split-K for the long reductions.
+
+Reference: ``tf.keras.layers.Conv2D`` / ``Dense`` of tf_dist_example.py:41-47 (Keras semantics:
+NHWC activations, HWIO kernels, [in, out] Dense kernels).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import hip
+
+
+def _c32(t: torch.Tensor) -> torch.Tensor:
+    t = t.float().contiguous()
+    return t if t.data_ptr() % 16 == 0 else t.clone()
+
+
+def supported(x: torch.Tensor, groups: int = 1) -> bool:
+    """Any 4-D NHWC GPU activation of a floating dtype, ungrouped."""
+    return (x.is_cuda and x.dim() == 4 and x.dtype in (torch.float32, torch.bfloat16, torch.float16)
+            and int(groups) == 1)
+
+
+def out_size(i, k, s, d, p0, p1):
+    return (i + p0 + p1 - (k - 1) * d - 1) // s + 1
+
+
+def fwd(x, w_hwio, bias, stride, pads, dil=(1, 1)) -> torch.Tensor:
+    """f32 ``y = conv(x, w) + bias``; ``pads = (top, bottom, left, right)``."""
+    R, S = w_hwio.shape[0], w_hwio.shape[1]
+    oh = out_size(x.shape[1], R, stride[0], dil[0], pads[0], pads[1])
+    ow = out_size(x.shape[2], S, stride[1], dil[1], pads[2], pads[3])
+    b = _c32(bias) if bias is not None else None
+    return hip().conv_f32_fwd(_c32(x), _c32(w_hwio), b, oh, ow, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1])
+
+
+def dgrad(dy, w_hwio, hw, stride, pads, dil=(1, 1)) -> torch.Tensor:
+    """f32 input gradient of :func:`fwd` for an input of spatial size ``hw``."""
+    wt = _c32(w_hwio).permute(0, 1, 3, 2).contiguous()  # [R][S][K][C]
+    return hip().conv_f32_dgrad(_c32(dy), wt, hw[0], hw[1], stride[0], stride[1], pads[0], pads[2], dil[0], dil[1])
+
+
+def wgrad(x, dy, rs, stride, pads, dil=(1, 1), out=None, accumulate=False) -> torch.Tensor:
+    """f32 HWIO weight gradient of :func:`fwd` (added into the f32 ``out`` when ``accumulate``)."""
+    return hip().conv_f32_wgrad(_c32(x), _c32(dy), rs[0], rs[1], stride[0], stride[1], pads[0], pads[2], dil[0],
+                                dil[1], out=out, accumulate=accumulate)
+
+
+class _ConvF32(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pads, dil, grad_out, anchor=None):
+        y = fwd(x, w, b, stride, pads, dil)
+        ctx.save_for_backward(x, w)
+        ctx.geo = (stride, pads, dil)
+        ctx.has_b = b is not None
+        ctx.grad_out = grad_out
+        ctx.dtypes = (x.dtype, w.dtype)
+        return y.to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        stride, pads, dil = ctx.geo
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = dgrad(dy, w, (x.shape[1], x.shape[2]), stride, pads, dil).to(ctx.dtypes[0])
+        rs = (w.shape[0], w.shape[1])
+        if ctx.grad_out is not None:
+            wgrad(x, dy, rs, stride, pads, dil, out=ctx.grad_out, accumulate=True)
+        elif ctx.needs_input_grad[1]:
+            dw = wgrad(x, dy, rs, stride, pads, dil).to(ctx.dtypes[1])
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = dy.float().sum((0, 1, 2))
+        return dx, dw, db, None, None, None, None, None
+
+
+def conv2d(x, w_hwio, bias=None, stride=(1, 1), pads=(0, 0, 0, 0), dil=(1, 1), grad_out=None, anchor=None):
+    """``conv(x NHWC, w HWIO) + bias`` with zero padding ``pads = (top, bottom, left, right)``, computed
+    in f32 (bf16 / f16 operands are widened), returned in x's dtype.  ``grad_out``: an f32 HWIO view the
+    weight gradient is ADDED into (``w`` then needs no autograd; ``anchor`` -- the variable's leaf --
+    keeps the backward alive when nothing else needs a gradient, as in ops/conv.py)."""
+    return _ConvF32.apply(x, w_hwio, bias, tuple(int(s) for s in stride), tuple(int(p) for p in pads),
+                          tuple(int(d) for d in dil), grad_out, anchor)
+
+
+# ------------------------------------------------------------------------------------------ Dense
+def dense_supported(x: torch.Tensor) -> bool:
+    return x.is_cuda and x.dtype == torch.float32 and x.dim() >= 2
+
+
+class _DenseF32(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, targets, anchor=None):
+        C = hip()
+        x2 = _c32(x.reshape(-1, x.shape[-1]))
+        wc = _c32(w)
+        y = C.gemm_f32(x2, 0, wc, 1, bias=_c32(b) if b is not None else None)
+        ctx.save_for_backward(x2, wc)
+        ctx.has_b = b is not None
+        ctx.targets = targets
+        ctx.xshape = x.shape
+        return y.reshape(*x.shape[:-1], w.shape[1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = hip()
+        x, w = ctx.saved_tensors
+        dy = _c32(dy.reshape(-1, dy.shape[-1]))
+        dx = C.gemm_f32(dy, 0, w, 0).reshape(ctx.xshape) if ctx.needs_input_grad[0] else None
+        gw_t, gb_t = ctx.targets if ctx.targets is not None else (None, None)
+        dw = db = None
+        if gw_t is not None:
+            C.gemm_f32(x, 1, dy, 1, out=gw_t, accumulate=True)
+        elif ctx.needs_input_grad[1]:
+            dw = C.gemm_f32(x, 1, dy, 1)
+        if ctx.has_b:
+            s = dy.sum(0)
+            if gb_t is not None:
+                gb_t.add_(s)
+            elif ctx.needs_input_grad[2]:
+                db = s
+        return dx, dw, db, None, None
+
+
+def dense(x, w, b=None, targets=None, anchor=None):
+    """f32 ``x [..., in] @ w [in, out] (+ b)`` on the f32-MFMA GEMM; ``targets = (dW, db)`` f32 slab views
+    the gradients are added into (as ops/dense.py ``dense_bf16``)."""
+    return _DenseF32.apply(x, w, b, targets, anchor)

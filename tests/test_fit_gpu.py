@@ -130,3 +130,77 @@ def test_generic_whole_step_graph_matches_eager():
     for a, b in zip(mg.get_weights(), me.get_weights()):
         np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(hg.history["loss"], he.history["loss"], rtol=1e-4)
+
+
+def _train_opt(fused: bool, make_opt, steps=8, spe=4):
+    tdl.keras.backend.clear_session()
+    tdl.keras.utils.set_random_seed(3)
+    os.environ["TDL_DISABLE_FUSED"] = "0" if fused else "1"
+    try:
+        x, y = _data(1024)
+        with tdl.distribute.MirroredStrategy(devices=["/gpu:0"]).scope():
+            m = build_mnist_cnn()
+            m.compile(loss=tdl.keras.losses.SparseCategoricalCrossentropy(from_logits=True), optimizer=make_opt(),
+                      metrics=[tdl.keras.metrics.SparseCategoricalAccuracy()], steps_per_execution=spe)
+        h = m.fit(_pipeline(x, y, 64), epochs=2, steps_per_epoch=steps // 2, verbose=0)
+        return m, h
+    finally:
+        os.environ.pop("TDL_DISABLE_FUSED", None)
+
+
+@pytest.mark.parametrize("name,make_opt", [
+    ("adam", lambda: tdl.keras.optimizers.Adam(learning_rate=1e-3)),
+    ("adamw-amsgrad", lambda: tdl.keras.optimizers.AdamW(learning_rate=1e-3, weight_decay=0.01, amsgrad=True)),
+    ("rmsprop-momentum", lambda: tdl.keras.optimizers.RMSprop(learning_rate=1e-3, momentum=0.5)),
+    ("adagrad", lambda: tdl.keras.optimizers.Adagrad(learning_rate=1e-2)),
+    ("sgd-nesterov", lambda: tdl.keras.optimizers.SGD(learning_rate=0.05, momentum=0.9, nesterov=True)),
+])
+def test_reference_cnn_any_optimizer_on_fused_kernels(name, make_opt):
+    """The reference CNN compiled with Adam / AdamW / RMSprop / Adagrad / Nesterov SGD trains on the
+    fused MI355X kernels (the step's gradient from the fused forward/backward, the update from the
+    flat-slab optimizer kernels of csrc/kernels/optim.hip, captured in the execution graph with
+    Adam's step count read from the device) and matches the generic autograd engine, whose
+    optimizer runs the same update kernels."""
+    mf, hf = _train_opt(True, make_opt)
+    assert mf._trainer.kind == "fused", mf._fused_reason
+    assert mf._trainer.capture
+    mg, hg = _train_opt(False, make_opt)
+    assert mg._trainer.kind == "generic"
+    assert mf.optimizer.iterations == mg.optimizer.iterations == 8
+    # adaptive optimizers turn a near-zero gradient into a full lr-sized step whose sign follows
+    # f32 rounding: a handful of weights may differ by up to ~lr per step between the two engines
+    # (RMSprop's first steps are g / sqrt((1 - rho) g^2) = +-lr / sqrt(1 - rho), amplified by momentum)
+    lr = float(mf.optimizer.current_lr())
+    step = {"rmsprop-momentum": lr / np.sqrt(1 - 0.9) / (1 - 0.5)}.get(name, lr)
+    frac = 1e-2 if name == "rmsprop-momentum" else 1e-3
+    for a, b in zip(mf.get_weights(), mg.get_weights()):
+        off = ~np.isclose(a, b, rtol=5e-3, atol=5e-4)
+        assert off.mean() < frac, (name, off.mean())
+        assert np.abs(a - b).max() <= 2 * step * 8 + 5e-4, (name, np.abs(a - b).max())
+    np.testing.assert_allclose(hf.history["loss"], hg.history["loss"], rtol=2e-3, atol=2e-3)
+
+
+@pytest.mark.parametrize("make_opt", [
+    lambda: tdl.keras.optimizers.Adam(learning_rate=3e-3),
+    lambda: tdl.keras.optimizers.Adam(learning_rate=3e-3, amsgrad=True),
+    lambda: tdl.keras.optimizers.AdamW(learning_rate=3e-3, weight_decay=0.05),
+    lambda: tdl.keras.optimizers.RMSprop(learning_rate=3e-3),
+    lambda: tdl.keras.optimizers.RMSprop(learning_rate=3e-3, momentum=0.7, centered=True),
+    lambda: tdl.keras.optimizers.Adagrad(learning_rate=3e-2),
+], ids=["adam", "amsgrad", "adamw", "rmsprop", "rmsprop-centered-momentum", "adagrad"])
+def test_optimizer_kernels_match_torch_formulas(make_opt):
+    """csrc/kernels/optim.hip against the same optimizer's torch formulas (keras/optimizers.py, run on
+    CPU tensors) over 5 updates with identical gradients: f32 elementwise, a few ulp apart."""
+    g = torch.Generator().manual_seed(0)
+    n = 100003  # (a ragged tail past the 16-B vector loop)
+    w0 = torch.randn(n, generator=g)
+    grads = [torch.randn(n, generator=g) * 0.1 for _ in range(5)]
+    od, oc = make_opt(), make_opt()
+    wd, wc = w0.clone().cuda(), w0.clone()
+    for gr in grads:
+        od.apply_flat(wd, gr.cuda().clone())
+        oc.apply_flat(wc, gr.clone())
+    assert od.iterations == oc.iterations == 5
+    torch.testing.assert_close(wd.cpu(), wc, rtol=2e-5, atol=2e-6)
+    for k in oc.slots():
+        torch.testing.assert_close(od.slots()[k].cpu(), oc.slots()[k], rtol=2e-5, atol=2e-6)

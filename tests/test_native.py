@@ -94,3 +94,37 @@ def test_crc32c():
 
     d = np.random.bytes(1000)
     assert _crc32c_py(d) == N.crc32c(d, 0)
+
+
+def test_crash_trace_names_the_aborting_native_thread(tmp_path):
+    """A thread that calls abort() with no Python frame on top (the round-4 failure mode) is named
+    with its native backtrace before faulthandler's Python stacks, and the process still dies with
+    SIGABRT (csrc/native/crash_trace.cpp)."""
+    import os
+    import subprocess
+    import sys
+    import textwrap
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    f = tmp_path / "abort.py"
+    f.write_text(textwrap.dedent("""
+        import ctypes, faulthandler, threading
+        faulthandler.enable(all_threads=True)
+        from tensorflow_distributed_learning_amd import ops
+        assert ops.native().install_crash_trace()
+        libc = ctypes.CDLL(None)
+        libc.pthread_setname_np.argtypes = [ctypes.c_ulong, ctypes.c_char_p]
+        libc.pthread_self.restype = ctypes.c_ulong
+        def worker():
+            libc.pthread_setname_np(libc.pthread_self(), b"tdl-test-worker")
+            libc.abort()
+        t = threading.Thread(target=worker)
+        t.start()
+        t.join()
+    """))
+    r = subprocess.run([sys.executable, str(f)], env=dict(os.environ, PYTHONPATH=root), capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == -6, (r.returncode, r.stderr[-2000:])
+    assert "[tdl crash trace] signal 6" in r.stderr and "name 'tdl-test-worker'" in r.stderr, r.stderr[-3000:]
+    assert "[tdl crash trace] end" in r.stderr
+    assert "Fatal Python error" in r.stderr  # faulthandler still runs after it (chained)
