@@ -80,6 +80,7 @@ struct MnistArgs {
 //      profiles/mnist_stagger_ab_r5.txt)
 constexpr int kMnistVariantPrio = 1;
 constexpr int kMnistVariantStagger = 2;
+
 constexpr int kDefaultMnistVariant = 0;
 
 constexpr int kMnistPart2Rows = 289;

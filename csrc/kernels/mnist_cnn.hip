@@ -143,7 +143,9 @@ __device__ __forceinline__ void head_row(const MnistArgs& a, int r, int l, int y
   if (sown != nullptr) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     bool ok = false;
+    unsigned npoll = 0;  // (diagnostics: poll rounds, head stamp slot 4)
     for (;;) {
+      ++npoll;
       if (!ok) {
         ok = true;
 #pragma unroll
@@ -170,6 +172,7 @@ __device__ __forceinline__ void head_row(const MnistArgs& a, int r, int l, int y
         break;
       }
     }
+    if (a.stamps != nullptr && l == 0) a.stamps[(size_t)gridDim.x * 64 + blockIdx.x * 8 + 4] = npoll;
     const float o0 = sown[l], o1 = sown[l + 64];
 #pragma unroll
     for (int c = 0; c < kDense1Chunks; ++c) {  // (static register indices)
@@ -685,7 +688,8 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
 //   with the 205 KB W3 slice loaded into registers at kernel start (its latency hides behind the
 //   convolutions); the head sums the 4 quarter partials + bias + ReLU.
 // --------------------------------------------------------------------------------------------
-constexpr int kLdsFwd = 784 + 320 + 169 * kP1Stride + 72 * 16 * 4 + 400 + 169 * 32 / 4 + 400 / 4 + 16 * 128 + 4 + 128;
+constexpr int kLdsFwd = 784 + 320 + 169 * kP1Stride + 72 * 16 * 4 + 400 + 169 * 32 / 4 + 400 / 4 + 16 * 128 + 4 + 128 +
+                        288 * 16;  // (w2d: the W2 slice again, [k][16 co], for the fused backward's dgrad)
 // fused_bwd: this quarter's conv2-output gradient dC2 [15][15 cells][16 channels + 4 pad] with a
 // zero border of 2 (the dgrad reads cells (ih - kh + 2, iw - kw + 2) without bounds checks).
 // Cell stride 20 floats: 16 consecutive cells of a dgrad A read (ds_read_b128) land on 16
@@ -768,12 +772,17 @@ __device__ __forceinline__ void fused_wgrad_tiles(const MnistArgs& a, int bi, in
 // dp2s: [25 windows][16] this quarter's masked dP2 (LDS), a2s its pool-2 argmax bytes, P1s/a1s/xs
 // the image's pooled conv1 output / pool-1 argmax / input (LDS), dCs the dC2 grid scratch, red
 // >= 8*10*16 floats of scratch.  Writes part2 columns 16cq.. of image bi and part1 row 4bi + cq.
-// this wave's conv2 dgrad operands W2[tap][16nt + i][16cq + 4g .. +3] (L2), nt = wave / 4
-__device__ __forceinline__ void load_dgrad_w2(const MnistArgs& a, int cq, f4 (&bwd)[9]) {
+// this wave's conv2 dgrad operands W2[tap][16nt + i][16cq + 4g .. +3], nt = wave / 4, from the LDS
+// copy w2d ([k][16 co], written at staging beside the forward's fragment-ordered w2s): one
+// conflict-free ds_read_b128 per tap (a wave reads 1 KB contiguous).  As global loads (L2) issued
+// before the hand-off they were 74 KB per workgroup of vector-memory traffic right when wave 0's
+// partial polls need the memory pipe (a poll round then took ~1.8 us); gathered from w2s (4 strided
+// ds_read_b32 per tap, 4-way bank conflicts) they cost ~1 us of LDS time.
+__device__ __forceinline__ void lds_dgrad_w2(const float* w2d, f4 (&bwd)[9]) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int i = lane & 15, g = lane >> 4, nt = wave >> 2;
 #pragma unroll
-  for (int tap = 0; tap < 9; ++tap) bwd[tap] = ld4(a.W + a.ow2 + (size_t)(tap * 32 + 16 * nt + i) * 64 + 16 * cq + 4 * g);
+  for (int tap = 0; tap < 9; ++tap) bwd[tap] = ld4(w2d + (tap * 32 + 16 * nt + i) * 16 + 4 * g);
 }
 
 __device__ __forceinline__ void fused_conv_bwd(const MnistArgs& a, int bi, int cq, const float* dp2s,
@@ -941,6 +950,8 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   uint8_t* a2s = a1s + 169 * 32;                               // [25][16] pool-2 argmax
   float* red = reinterpret_cast<float*>(a2s + 400);            // [16][128] dense1 row-group partials
   int* s_last = reinterpret_cast<int*>(red + 16 * 128);        // head hand-off: [last?, base count]
+  float* w2d = red + 16 * 128 + 4 + 128;  // [k = tap*32 + ci][16 co]: the dgrad B operands, one ds_read_b128 each
+  float* dCs = w2d + 288 * 16;             // fused_bwd: the dC2 grid (kDcF x kDcF cells)
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int i = lane & 15, g = lane >> 4;
   const int bi = blockIdx.x >> 2, cq = blockIdx.x & 3;
@@ -978,6 +989,7 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
       d[4] = vw2[j].y;
       d[8] = vw2[j].z;
       d[12] = vw2[j].w;
+      st4(w2d + k * 16 + 4 * q, vw2[j]);
     }
   }
   stamp(a.stamps, 1);
@@ -1127,7 +1139,6 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
       // wave 7 has no conv2 tile: it zeroes the fused backward's dC2 grid meanwhile (the dP2 phase
       // only scatters the masked dP2 values to their pool-2 argmax cells; every other cell -- the
       // zero border, the non-argmax cells, row / column 10 of the 11 x 11 conv output -- stays 0)
-      float* dCs = red + 16 * 128 + 4 + 128;
       for (int e4 = lane; e4 < kDcF * kDcF * kDcFStride / 4; e4 += 64) st4(dCs + e4 * 4, zero4());
     }
   }
@@ -1171,12 +1182,16 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
     return;
   }
   // the head's weights, loaded by wave 0 of every workgroup now: their latency hides behind the
-  // hand-off (only the image's last workgroup uses them; 5 KB, L2-resident)
+  // hand-off (5 KB, L2-resident).  (Staged in LDS with the image instead: no faster -- the staging
+  // round trip grows by as much, profiles/mnist_head_ab_r5.txt.)
   HeadWeights hw;
-  if (wave == 0) hw = load_head_weights(a, lane);
-  // the fused backward's dgrad B operands (W2, L2-resident): in flight during the hand-off
+  const int uwave = __builtin_amdgcn_readfirstlane(wave);
+  if (uwave == 0) hw = load_head_weights(a, lane);
+  // the fused backward's conv2-dgrad operands, from LDS, while the hand-off is in flight (waves 1-7
+  // wait for wave 0's head; wave 0's head waits for its polls: the LDS reads are off both paths)
   f4 bwd[9];
-  if (a.head == 1 && a.dp2_fwd && a.fused_bwd) load_dgrad_w2(a, cq, bwd);
+  if (a.head == 1 && a.dp2_fwd && a.fused_bwd) lds_dgrad_w2(w2d, bwd);
+
   // ---- hand-off to the image's last quarter workgroup (MI355X_MICROARCH.md, inter-workgroup
   // visibility, first table row): the storing wave drains its sc1 stores, a workgroup barrier,
   // ONE agent-scope add per workgroup on the image's counter; the workgroup whose add returns
@@ -1195,7 +1210,7 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   lds_barrier();  // (tagged: this quarter's own partial in LDS)
   const bool last = tagged || s_last[0] != 0;  // (tagged: every quarter runs the head)
   float* sdh = red;  // [128] dH of this image (the dense1 row-group scratch is free now)
-  if (last && wave == 0) {
+  if (last && uwave == 0) {
     if (a.head == 1) head_row(a, bi, lane, label, hw, sdh, tag, tagged ? sown : nullptr, cq, !tagged || cq == kHeadQuarter);
     else head_eval(a, bi, lane, label, hw);
   }
@@ -1209,10 +1224,17 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   lds_barrier();
   const f4 dh = ld4(sdh + n4);
   float v[25];
+  {
+    // 4-term dot products on packed f32 math (v_pk_mul_f32 + v_pk_fma_f32 + one add: 3 VALU per
+    // feature instead of 5; nothing else competes for the VALU in this phase)
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 dlo = {dh.x, dh.y}, dhi = {dh.z, dh.w};
 #pragma unroll
-  for (int j = 0; j < 25; ++j) {
-    const f4 p = w3v[j] * dh;
-    v[j] = (p.x + p.y) + (p.z + p.w);
+    for (int j = 0; j < 25; ++j) {
+      f2 t = f2{w3v[j].x, w3v[j].y} * dlo;
+      t = __builtin_elementwise_fma(f2{w3v[j].z, w3v[j].w}, dhi, t);
+      v[j] = t.x + t.y;
+    }
   }
   // sum over the 32 lanes of the row group (column groups n4): reduce-scatter butterfly, lane
   // (l & 31) ends with feature 16 (l & 31) + rg (j = l & 31 >= 25: zero padding)
@@ -1221,7 +1243,6 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   if (a.fused_bwd) {
     // the conv2-output gradient dC2 directly: the masked dP2 value of window j, channel rg goes to
     // its pool-2 argmax cell of the (zeroed) dC2 grid; every other cell of the window is 0
-    float* dCs = red + 16 * 128 + 4 + 128;
     float val = 0.f;
     if (j < 25) {
       const int kk = j * 16 + rg;

@@ -1,0 +1,11 @@
+#!/bin/bash
+# v6: conv2 dgrad W2 operands gathered from LDS (no global W2 prefetch at the hand-off)
+set -o pipefail
+O=gpurun_out/${OUT:-r5v6}
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_mnist_fused_gpu.py > $O/tests.log 2>&1 || { echo TESTS FAILED; tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+timeout -k 10 200 python scripts/stamps_mnist.py > $O/phases.log 2>&1 || { echo PH FAILED; tail -20 $O/phases.log; exit 1; }
+grep -v amdgpu $O/phases.log | head -5
+bash scripts/runs/ab_arms.sh ${AB:-r5v6ab} 2 base=ab/base:0 cur=.:0

@@ -64,6 +64,16 @@ def main():
                   f"{np.median(p6):.2f}/{p6.max():.2f}; head won {np.median(h[:, 0]):.2f}/{h[:, 0].max():.2f}; "
                   f"partials loaded {np.median(h[:, 1]):.2f}/{h[:, 1].max():.2f}; softmax {np.median(h[:, 2]):.2f}/"
                   f"{h[:, 2].max():.2f}; dH published {np.median(h[:, 3]):.2f}/{h[:, 3].max():.2f}")
+            if last.all() and grid % 4 == 0:
+                # every quarter ran the head: its wait is set by the LAST of the image's other three
+                # quarters to store its partial (p6 of wave 0); loaded - that = visibility + detection
+                p6i = p6.reshape(-1, 4)
+                other = np.stack([np.delete(p6i, c, axis=1).max(axis=1) for c in range(4)], axis=1).reshape(-1)
+                lat = h[:, 1] - other
+                polls = hs[:, 4]
+                print(f"  partial hand-off: last partner store -> partials loaded median {np.median(lat):.2f} "
+                      f"us (p10 {np.percentile(lat, 10):.2f}, p90 {np.percentile(lat, 90):.2f}); poll rounds "
+                      f"median {np.median(polls):.0f} (min {polls.min()}, max {polls.max()})")
         if name == "fwd_conv" and fused:
             bs = buf[grid * 72:].view(grid, 8, 4).cpu().numpy().astype(np.int64)
             t0w = r[:, :waves, 0].min(axis=1)
