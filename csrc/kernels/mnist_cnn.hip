@@ -60,6 +60,23 @@ __device__ __forceinline__ HeadWeights load_head_weights(const MnistArgs& a, int
   return hw;
 }
 
+// The head's operands staged in LDS by wave 7 (idle during conv2): hws = [w4 128 x 10][b3 128][b4 10],
+// so that wave 0's partial polls do not queue behind 32 head-weight loads per lane (vmcnt is in order)
+constexpr int kHeadW = 1280 + 128 + 12;  // floats (b4 padded to 12)
+
+__device__ __forceinline__ HeadWeights lds_head_weights(const float* hws, int l) {
+  HeadWeights hw;
+#pragma unroll
+  for (int c = 0; c < 10; ++c) {
+    hw.wa[c] = hws[l * 10 + c];
+    hw.wb[c] = hws[(l + 64) * 10 + c];
+    hw.b4[c] = hws[1408 + c];
+  }
+  hw.b3a = hws[1280 + l];
+  hw.b3b = hws[1280 + l + 64];
+  return hw;
+}
+
 // phase stamp k of the head, after the per-wave stamps: buf[grid*64 + workgroup*8 + k]
 // (diagnostics, stamps != null; the buffer then holds grid * 72 words)
 __device__ __forceinline__ void head_stamp(unsigned long long* buf, int k) {
@@ -689,7 +706,8 @@ __global__ __launch_bounds__(512) void k_conv_bwd(MnistArgs a) {
 //   convolutions); the head sums the 4 quarter partials + bias + ReLU.
 // --------------------------------------------------------------------------------------------
 constexpr int kLdsFwd = 784 + 320 + 169 * kP1Stride + 72 * 16 * 4 + 400 + 169 * 32 / 4 + 400 / 4 + 16 * 128 + 4 + 128 +
-                        288 * 16;  // (w2d: the W2 slice again, [k][16 co], for the fused backward's dgrad)
+                        288 * 16 +  // (w2d: the W2 slice again, [k][16 co], for the fused backward's dgrad)
+                        kHeadW;     // (hws: the loss head's operands)
 // fused_bwd: this quarter's conv2-output gradient dC2 [15][15 cells][16 channels + 4 pad] with a
 // zero border of 2 (the dgrad reads cells (ih - kh + 2, iw - kw + 2) without bounds checks).
 // Cell stride 20 floats: 16 consecutive cells of a dgrad A read (ds_read_b128) land on 16
@@ -951,7 +969,8 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   float* red = reinterpret_cast<float*>(a2s + 400);            // [16][128] dense1 row-group partials
   int* s_last = reinterpret_cast<int*>(red + 16 * 128);        // head hand-off: [last?, base count]
   float* w2d = red + 16 * 128 + 4 + 128;  // [k = tap*32 + ci][16 co]: the dgrad B operands, one ds_read_b128 each
-  float* dCs = w2d + 288 * 16;             // fused_bwd: the dC2 grid (kDcF x kDcF cells)
+  float* hws = w2d + 288 * 16;             // [kHeadW] the loss head's operands (wave 7, during conv2)
+  float* dCs = hws + kHeadW;               // fused_bwd: the dC2 grid (kDcF x kDcF cells)
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int i = lane & 15, g = lane >> 4;
   const int bi = blockIdx.x >> 2, cq = blockIdx.x & 3;
@@ -1135,6 +1154,18 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   } else {
 #pragma unroll
     for (int j = 16; j < 25; ++j) ldw3(j);
+    if (a.head != 0) {
+      // the head's operands into LDS: 23 loads per lane, off every critical path
+      float hv[23];
+#pragma unroll
+      for (int u = 0; u < 23; ++u) {
+        const int e = min(lane + 64 * u, 1417);
+        hv[u] = a.W[e < 1280 ? a.ow4 + e : (e < 1408 ? a.ob3 + (e - 1280) : a.ob4 + (e - 1408))];
+      }
+#pragma unroll
+      for (int u = 0; u < 23; ++u)
+        if (lane + 64 * u < 1418) hws[lane + 64 * u] = hv[u];
+    }
     if (a.head == 1 && a.dp2_fwd && a.fused_bwd) {
       // wave 7 has no conv2 tile: it zeroes the fused backward's dC2 grid meanwhile (the dP2 phase
       // only scatters the masked dP2 values to their pool-2 argmax cells; every other cell -- the
@@ -1186,7 +1217,7 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   // round trip grows by as much, profiles/mnist_head_ab_r5.txt.)
   HeadWeights hw;
   const int uwave = __builtin_amdgcn_readfirstlane(wave);
-  if (uwave == 0) hw = load_head_weights(a, lane);
+  if (uwave == 0) hw = lds_head_weights(hws, lane);
   // the fused backward's conv2-dgrad operands, from LDS, while the hand-off is in flight (waves 1-7
   // wait for wave 0's head; wave 0's head waits for its polls: the LDS reads are off both paths)
   f4 bwd[9];

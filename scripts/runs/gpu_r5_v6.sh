@@ -8,4 +8,4 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method threa
 tail -1 $O/tests.log
 timeout -k 10 200 python scripts/stamps_mnist.py > $O/phases.log 2>&1 || { echo PH FAILED; tail -20 $O/phases.log; exit 1; }
 grep -v amdgpu $O/phases.log | head -5
-bash scripts/runs/ab_arms.sh ${AB:-r5v6ab} 2 base=ab/base:0 cur=.:0
+bash scripts/runs/ab_arms.sh ${AB:-r5v6ab} ${REPS:-2} ${ARMS:-base=ab/base:0 cur=.:0}
