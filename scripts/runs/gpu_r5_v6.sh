@@ -4,7 +4,7 @@ set -o pipefail
 O=gpurun_out/${OUT:-r5v6}
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_mnist_fused_gpu.py > $O/tests.log 2>&1 || { echo TESTS FAILED; tail -30 $O/tests.log; exit 1; }
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_mnist_fused_gpu.py ${TESTS:-} > $O/tests.log 2>&1 || { echo TESTS FAILED; tail -30 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
 timeout -k 10 200 python scripts/stamps_mnist.py > $O/phases.log 2>&1 || { echo PH FAILED; tail -20 $O/phases.log; exit 1; }
 grep -v amdgpu $O/phases.log | head -5
