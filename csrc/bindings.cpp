@@ -155,6 +155,9 @@ class MnistStep {
   // with dP2 in the forward kernel, also run the conv backward there (forward_backward only)
   void set_fused_bwd(bool on) { fused_bwd_ = on; }
   bool fused_bwd() const { return fused_bwd_ && a_.dp2_fwd; }
+  // k_finalize_x grid cap (0: one workgroup per range; see MnistArgs::fx_grid)
+  void set_fx_grid(int64_t n) { a_.fx_grid = (int)std::max<int64_t>(0, n); }
+  int64_t fx_grid() const { return a_.fx_grid; }
 
   // error word of the in-kernel hand-offs (bit 1: a wait timed out; host sync); reset=true clears it
   int64_t error(bool reset) {
@@ -332,6 +335,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("forward_eval", &MnistStep::forward_eval, pybind11::arg("idx_off"), pybind11::arg("logits") = pybind11::none())
       .def("forward_dense", &MnistStep::forward_dense)
       .def("backward_conv", &MnistStep::backward_conv)
+      .def("set_fx_grid", &MnistStep::set_fx_grid)
+      .def("fx_grid", &MnistStep::fx_grid)
       .def("finalize", &MnistStep::finalize, pybind11::arg("apply_sgd"), pybind11::arg("exchange") = false)
       .def("set_exchange", &MnistStep::set_exchange)
       .def("has_exchange", &MnistStep::has_exchange)

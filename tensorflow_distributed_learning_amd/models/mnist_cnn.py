@@ -148,6 +148,15 @@ class FusedMnistTrainStep:
         # + loss + backward; TDL_MNIST_FUSED_BWD=0 keeps the separate k_conv_bwd launch)
         self._impl.set_fused_bwd(os.environ.get("TDL_MNIST_FUSED_BWD", "1") == "1")
         self.fused_bwd = bool(self._impl.fused_bwd())
+        if (self.fused_bwd and self.R > 1 and os.environ.get("TDL_SHARE_GPU") == "1"
+                and "TDL_FX_GRID" not in os.environ):
+            # replicas sharing ONE GPU: a replica's exchanging finalize workgroups spin until its
+            # peers' arrive, and a peer still in its fused kernel needs whole free CUs for its 4b
+            # workgroups (208 VGPRs x 2 waves per SIMD, ~110 KB LDS): spread over every CU, the
+            # spinning grid would lock that kernel out until the exchange timed out.  Cap the grid
+            # (ranges loop over it) so the others' fused workgroups always find free CUs.
+            cus = torch.cuda.get_device_properties(W.device).multi_processor_count
+            self._impl.set_fx_grid(max(16, (cus - (self.R - 1) * 4 * self.b) // 2))
 
     def forward_backward(self, idx_offset: int) -> None:
         self._impl.forward_backward(int(idx_offset))
