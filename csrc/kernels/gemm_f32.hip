@@ -99,6 +99,7 @@ __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
   if constexpr (MODE == kF32ConvDgrad) ka.set(kbeg + kqa, g.s, g.k);
   if constexpr (MODE == kF32ConvWgrad) kb.set(kbeg + kl, g.oh, g.ow);
 
+  const bool s1 = g.sh == 1 && g.sw == 1;
   float ra[4], rb[4];
   auto load = [&](int k0) {
     const int kk = k0 + kqa;  // A: reduction index of ra[0]
@@ -129,9 +130,9 @@ __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
             ok = iy >= 0 && iy < g.h && ix >= 0 && ix < g.w;
           } else {
             const int ty = ay - c.hi * g.dh, tx = ax - c.mid * g.dw;
-            iy = ty / g.sh;
-            ix = tx / g.sw;
-            ok = ty >= 0 && tx >= 0 && iy * g.sh == ty && ix * g.sw == tx && iy < g.oh && ix < g.ow;
+            iy = s1 ? ty : ty / g.sh;  // (stride 1: no integer division per element)
+            ix = s1 ? tx : tx / g.sw;
+            ok = ty >= 0 && tx >= 0 && (s1 || (iy * g.sh == ty && ix * g.sw == tx)) && iy < g.oh && ix < g.ow;
           }
           if (ok) {
             const int64_t base = MODE == kF32ConvFwd ? (((int64_t)an * g.h + iy) * g.w + ix) * g.c
@@ -251,13 +252,7 @@ __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
       }
 }
 
-// Split-reduction epilogue: the slices summed in slice order, then bias / accumulate / store.
-// Threads walk the OUTPUT in storage order (coalesced stores, strided partial reads when transposed).
-__global__ __launch_bounds__(256) void k_gemm_f32_reduce(F32GemmArgs a) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t mn = (int64_t)a.M * a.N;
-  if (e >= mn) return;
-  int m, n;
+__device__ __forceinline__ void out_index(const F32GemmArgs& a, int64_t e, int& m, int& n) {
   if (a.trans_out) {
     n = (int)(e / a.M);
     m = (int)(e - (int64_t)n * a.M);
@@ -265,10 +260,45 @@ __global__ __launch_bounds__(256) void k_gemm_f32_reduce(F32GemmArgs a) {
     m = (int)(e / a.N);
     n = (int)(e - (int64_t)m * a.N);
   }
-  const int64_t src = (int64_t)m * a.N + n;
+}
+
+// Split-reduction epilogue: the slices summed in a fixed order, then bias / accumulate / store.
+// Outputs are walked in storage order (coalesced stores, strided partial reads when transposed).
+// Few slices: one thread per output, 8 independent partial loads in flight.
+__global__ __launch_bounds__(256) void k_gemm_f32_reduce(F32GemmArgs a) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t mn = (int64_t)a.M * a.N;
+  if (e >= mn) return;
+  int m, n;
+  out_index(a, e, m, n);
+  const float* src = a.ws + (int64_t)m * a.N + n;
   float v = 0.f;
-  for (int z = 0; z < a.splits; ++z) v += a.ws[z * mn + src];
+  int z = 0;
+  for (; z + 8 <= a.splits; z += 8) {
+    float p[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) p[u] = src[(z + u) * mn];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v += p[u];
+  }
+  for (; z < a.splits; ++z) v += src[z * mn];
   out_store(a, m, n, v);
+}
+
+// Many slices over few outputs (a small weight gradient over a long reduction): one wave per output,
+// lane l sums slices l, l + 64, .. in order, then a fixed xor butterfly over the wave (deterministic).
+__global__ __launch_bounds__(256) void k_gemm_f32_reduce_wave(F32GemmArgs a) {
+  const int64_t e = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int64_t mn = (int64_t)a.M * a.N;
+  if (e >= mn) return;
+  int m, n;
+  out_index(a, e, m, n);
+  const float* src = a.ws + (int64_t)m * a.N + n;
+  float v = 0.f;
+  for (int z = lane; z < a.splits; z += 64) v += src[z * mn];
+  v = wave_sum(v);
+  if (lane == 0) out_store(a, m, n, v);
 }
 
 }  // namespace
@@ -284,7 +314,10 @@ void f32_gemm_launch(int mode, const F32GemmArgs& a, hipStream_t s) {
   }
   if (a.splits > 1) {
     const int64_t mn = (int64_t)a.M * a.N;
-    hipLaunchKernelGGL(k_gemm_f32_reduce, dim3((unsigned)((mn + 255) / 256)), dim3(256), 0, s, a);
+    if (a.splits >= 32 && mn <= 16384)
+      hipLaunchKernelGGL(k_gemm_f32_reduce_wave, dim3((unsigned)((mn + 3) / 4)), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL(k_gemm_f32_reduce, dim3((unsigned)((mn + 255) / 256)), dim3(256), 0, s, a);
   }
 }
 
