@@ -18,6 +18,8 @@
 // blockIdx -> tile mapping is XCD-aware: the 8 XCDs take workgroups round-robin, so the bijective
 // remap below hands each XCD a contiguous run of logical tiles (the column tiles of a row block
 // are adjacent), and the row block's activations are read into one L2 instead of eight.
+#include <cstdlib>
+
 #include "kernels/conv.h"
 #include "kernels/common.h"
 
@@ -203,8 +205,10 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
 // LOWREG (the 4-waves-per-SIMD variants, <= 128 VGPRs): the BN-group backward epilogue loads its
 // residual and BN operands in chunks of EPI / 4 segments right before their use instead of all up front.
 // EK 3: the BN-group backward of EK 1 with the ReLU mask recomputed from the BN input (bn_ss).
-template <int BM, int BN, int NT, int EK, int WTM, int WTN, int LDS_ELEMS, int LOWREG = 0>
-__device__ __forceinline__ void conv_epilogue(const Igemm& a, const f4v (&acc)[WTM / 16][WTN / 16], uint16_t* lds,
+// MF 32: the accumulators are 32x32 blocks of v_mfma_f32_32x32x16_bf16 (ACC = f16v[WTM / 32][WTN / 32]):
+// lane l holds channels 8k + 4 (l >> 5) + r (k, r < 4) of pixel l & 31 -- four 8-B LDS writes per block
+template <int BM, int BN, int NT, int EK, int WTM, int WTN, int LDS_ELEMS, int LOWREG = 0, int MF = 16, typename ACC>
+__device__ __forceinline__ void conv_epilogue(const Igemm& a, const ACC& acc, uint16_t* lds,
                                               int tm, int tn, int wrow0, int wcol0) {
   const int tid = threadIdx.x, lane = tid & 63;
   constexpr int OUT_LD = BN + 8;
@@ -227,18 +231,35 @@ __device__ __forceinline__ void conv_epilogue(const Igemm& a, const f4v (&acc)[W
   }
   static_assert(BM * OUT_LD <= LDS_ELEMS, "epilogue tile must fit the operand LDS");
   // (operands are swapped in the MFMA, so a lane holds 4 consecutive channels of one pixel: one 8-B write)
+  if constexpr (MF == 16) {
 #pragma unroll
-  for (int i = 0; i < WTM / 16; ++i)
+    for (int i = 0; i < WTM / 16; ++i)
 #pragma unroll
-    for (int j = 0; j < WTN / 16; ++j) {
-      // (hardware packing where it does not raise the VGPR peak: the EK 1 / 2 variants spill with it)
-      const uint32_t lo = (EK == 1 || EK == 2) ? (f2bf(acc[i][j][0]) | ((uint32_t)f2bf(acc[i][j][1]) << 16))
-                                               : pack_bf16x2(acc[i][j][0], acc[i][j][1]);
-      const uint32_t hi = (EK == 1 || EK == 2) ? (f2bf(acc[i][j][2]) | ((uint32_t)f2bf(acc[i][j][3]) << 16))
-                                               : pack_bf16x2(acc[i][j][2], acc[i][j][3]);
-      *reinterpret_cast<uint2*>(lds + (wrow0 + i * 16 + (lane & 15)) * OUT_LD + wcol0 + j * 16 + (lane >> 4) * 4) =
-          make_uint2(lo, hi);
-    }
+      for (int j = 0; j < WTN / 16; ++j) {
+        // (hardware packing where it does not raise the VGPR peak: the EK 1 / 2 variants spill with it)
+        const uint32_t lo = (EK == 1 || EK == 2) ? (f2bf(acc[i][j][0]) | ((uint32_t)f2bf(acc[i][j][1]) << 16))
+                                                 : pack_bf16x2(acc[i][j][0], acc[i][j][1]);
+        const uint32_t hi = (EK == 1 || EK == 2) ? (f2bf(acc[i][j][2]) | ((uint32_t)f2bf(acc[i][j][3]) << 16))
+                                                 : pack_bf16x2(acc[i][j][2], acc[i][j][3]);
+        *reinterpret_cast<uint2*>(lds + (wrow0 + i * 16 + (lane & 15)) * OUT_LD + wcol0 + j * 16 + (lane >> 4) * 4) =
+            make_uint2(lo, hi);
+      }
+  } else {
+#pragma unroll
+    for (int i = 0; i < WTM / 32; ++i)
+#pragma unroll
+      for (int j = 0; j < WTN / 32; ++j)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t lo = (EK == 1 || EK == 2) ? (f2bf(acc[i][j][4 * k]) | ((uint32_t)f2bf(acc[i][j][4 * k + 1]) << 16))
+                                                   : pack_bf16x2(acc[i][j][4 * k], acc[i][j][4 * k + 1]);
+          const uint32_t hi = (EK == 1 || EK == 2)
+                                  ? (f2bf(acc[i][j][4 * k + 2]) | ((uint32_t)f2bf(acc[i][j][4 * k + 3]) << 16))
+                                  : pack_bf16x2(acc[i][j][4 * k + 2], acc[i][j][4 * k + 3]);
+          *reinterpret_cast<uint2*>(lds + (wrow0 + i * 32 + (lane & 31)) * OUT_LD + wcol0 + j * 32 + 8 * k +
+                                    (lane >> 5) * 4) = make_uint2(lo, hi);
+        }
+  }
   // BN-backward fusion operands (the accumulators are dead now: registers to spare)
   constexpr int BNE = BNB ? EPI : 1;
   u32x4 ry[EK == 1 ? EPI : 1], rx[BNE], rx2[BNE];
@@ -634,7 +655,11 @@ constexpr int v2_lds_elems() {
   return STAGES * (BM + BN) * LDS_ROW > BM * (BN + 8) ? STAGES * (BM + BN) * LDS_ROW : BM * (BN + 8);
 }
 
-template <int BM, int BN, int WGM, int WGN, int EK, int STAGES, int MINW>
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+// MF 32: the same main loop on v_mfma_f32_32x32x16_bf16 (2 x 2 blocks of 32 x 32 per 64 x 64 wave tile,
+// four 16-deep k-steps per 64-deep tile; the same LDS bytes per MFMA FLOP as the 16x16x32 form)
+template <int BM, int BN, int WGM, int WGN, int EK, int STAGES, int MINW, int MF = 16>
 __global__ __launch_bounds__(64 * WGM * WGN, MINW) void k_conv_glds(Igemm a) {
   constexpr int NW = WGM * WGN, NT = 64 * NW;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;  // wave tile
@@ -713,29 +738,64 @@ __global__ __launch_bounds__(64 * WGM * WGN, MINW) void k_conv_glds(Igemm a) {
       lds_dma16(w_rsrc, base + (BM + (i * NW + wave) * 8) * LDS_ROW, b_vo[i], soff_b);
   };
 
-  f4v acc[MI][NJ];
+  constexpr int MI32 = WTM / 32, NJ32 = WTN / 32;
+  static_assert(MF == 16 || (WTM % 32 == 0 && WTN % 32 == 0), "32x32 blocks need 32-multiple wave tiles");
+  f4v acc[MF == 16 ? MI : 1][MF == 16 ? NJ : 1];
+  f16v acc32[MF == 32 ? MI32 : 1][MF == 32 ? NJ32 : 1];
+  if constexpr (MF == 16) {
 #pragma unroll
-  for (int i = 0; i < MI; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NJ; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+  } else {
+#pragma unroll
+    for (int i = 0; i < MI32; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ32; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc32[i][j][q] = 0.f;
+  }
 
   const int frow = lane & 15;
   const int fk0 = ((lane >> 4) ^ swz(frow)) * 8, fk1 = (((lane >> 4) | 4) ^ swz(frow)) * 8;
+  // 32x32x16: lane l reads row l & 31, 16-B chunk 2 step + (l >> 5) of the 64-deep tile (swizzled by row;
+  // swz is the same for rows r and r + 16 m)
+  const int frow32 = lane & 31;
   auto compute = [&](int stage) {
-    const uint16_t* la = lds + stage * STAGE + (wm * WTM + frow) * LDS_ROW;
-    const uint16_t* lb = lds + stage * STAGE + (BM + wn * WTN + frow) * LDS_ROW;
+    if constexpr (MF == 16) {
+      const uint16_t* la = lds + stage * STAGE + (wm * WTM + frow) * LDS_ROW;
+      const uint16_t* lb = lds + stage * STAGE + (BM + wn * WTN + frow) * LDS_ROW;
 #pragma unroll
-    for (int kk = 0; kk < BK; kk += 32) {
-      const int fk = kk ? fk1 : fk0;
-      bf16x8 fa[MI], fb[NJ];
+      for (int kk = 0; kk < BK; kk += 32) {
+        const int fk = kk ? fk1 : fk0;
+        bf16x8 fa[MI], fb[NJ];
 #pragma unroll
-      for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(la + i * 16 * LDS_ROW + fk);
+        for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(la + i * 16 * LDS_ROW + fk);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(lb + j * 16 * LDS_ROW + fk);
+        for (int j = 0; j < NJ; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(lb + j * 16 * LDS_ROW + fk);
 #pragma unroll
-      for (int i = 0; i < MI; ++i)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+      }
+    } else {
+      const uint16_t* la = lds + stage * STAGE + (wm * WTM + frow32) * LDS_ROW;
+      const uint16_t* lb = lds + stage * STAGE + (BM + wn * WTN + frow32) * LDS_ROW;
+#pragma unroll
+      for (int st = 0; st < BK / 16; ++st) {
+        const int fk = ((2 * st + (lane >> 5)) ^ swz(frow32)) * 8;
+        bf16x8 fa[MI32], fb[NJ32];
+#pragma unroll
+        for (int i = 0; i < MI32; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(la + i * 32 * LDS_ROW + fk);
+#pragma unroll
+        for (int j = 0; j < NJ32; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(lb + j * 32 * LDS_ROW + fk);
+#pragma unroll
+        for (int i = 0; i < MI32; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ32; ++j)
+            acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j], fa[i], acc32[i][j], 0, 0, 0);
+      }
     }
   };
 
@@ -762,8 +822,12 @@ __global__ __launch_bounds__(64 * WGM * WGN, MINW) void k_conv_glds(Igemm a) {
     }
   }
   __syncthreads();  // every wave done reading the ring: the epilogue reuses it
-  conv_epilogue<BM, BN, NT, EK, WTM, WTN, v2_lds_elems<BM, BN, STAGES>(), STAGES == 1 ? 2 : 0>(a, acc, lds, tm, tn,
-                                                                                             wm * WTM, wn * WTN);
+  if constexpr (MF == 16)
+    conv_epilogue<BM, BN, NT, EK, WTM, WTN, v2_lds_elems<BM, BN, STAGES>(), STAGES == 1 ? 2 : 0>(a, acc, lds, tm, tn,
+                                                                                               wm * WTM, wn * WTN);
+  else
+    conv_epilogue<BM, BN, NT, EK, WTM, WTN, v2_lds_elems<BM, BN, STAGES>(), STAGES == 1 ? 2 : 0, 32>(
+        a, acc32, lds, tm, tn, wm * WTM, wn * WTN);
 }
 
 int g_depth = 2;  // main-loop variant; conv_force_depth for A/B sweeps
@@ -804,20 +868,30 @@ void launch_tile(const Igemm& a, hipStream_t s) {
 }
 
 int g_forced_tile = 0;  // 0: heuristic below; 1: 128 x 64, 2: 128 x 128, 3: 256 x 128 (tile sweeps)
-int g_impl = 2;  // 1: v1 only; 2: the LDS-DMA ring kernel where it measured faster; 3: wherever it fits;
+// MFMA form of the dma1 main loop: 32 (v_mfma_f32_32x32x16_bf16) or 16 (v_mfma_f32_16x16x32_bf16).
+// TDL_CONV_MFMA overrides (A/B); conv_force_mfma too.
+int g_mf = [] {
+  const char* e = std::getenv("TDL_CONV_MFMA");
+  return (e != nullptr && std::atoi(e) == 16) ? 16 : 32;
+}();
+int g_impl = [] {  // (TDL_CONV_IMPL: the conv_force_impl A/B hook from the environment)
+  const char* e = std::getenv("TDL_CONV_IMPL");
+  const int v = e != nullptr ? std::atoi(e) : 2;
+  return (v == 1 || (v >= 3 && v <= 6)) ? v : 2;
+}();  // 1: v1 only; 2: the LDS-DMA ring kernel where it measured faster; 3: wherever it fits;
                  // 4 / 5: the single-stage LDS-DMA kernel (dma1) at 4 / 3 waves per SIMD wherever v1 runs
 
-template <int BM, int BN, int WGM, int WGN, int STAGES = 3, int MINW = 1>
+template <int BM, int BN, int WGM, int WGN, int STAGES = 3, int MINW = 1, int MF = 16>
 void launch_v2(const Igemm& a, hipStream_t s) {
   const dim3 grid((a.M + BM - 1) / BM * (a.K / BN)), block(64 * WGM * WGN);
   if (a.scatter)
-    hipLaunchKernelGGL((k_conv_glds<BM, BN, WGM, WGN, 2, STAGES, MINW>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((k_conv_glds<BM, BN, WGM, WGN, 2, STAGES, MINW, MF>), grid, block, 0, s, a);
   else if (a.bn_part && a.bn_ss)
-    hipLaunchKernelGGL((k_conv_glds<BM, BN, WGM, WGN, 3, STAGES, MINW>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((k_conv_glds<BM, BN, WGM, WGN, 3, STAGES, MINW, MF>), grid, block, 0, s, a);
   else if (a.bn_part)
-    hipLaunchKernelGGL((k_conv_glds<BM, BN, WGM, WGN, 1, STAGES, MINW>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((k_conv_glds<BM, BN, WGM, WGN, 1, STAGES, MINW, MF>), grid, block, 0, s, a);
   else
-    hipLaunchKernelGGL((k_conv_glds<BM, BN, WGM, WGN, 0, STAGES, MINW>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((k_conv_glds<BM, BN, WGM, WGN, 0, STAGES, MINW, MF>), grid, block, 0, s, a);
 }
 
 // v2 (256-row tiles, one 8-wave workgroup per CU, 3-stage LDS-DMA ring): only when forced (impl 3)
@@ -862,9 +936,15 @@ void launch(const Igemm& a, hipStream_t s) {
     if (a.K % 128 == 0) return launch_v2<256, 128, 4, 2>(a, s);
     return launch_v2<256, 64, 4, 2>(a, s);
   }
-  if (use_dma1(a)) {  // dma1 at 4 (default, impl 4) or 3 (impl 5) waves per SIMD
-    if (a.K % 128 == 0)
+  if (use_dma1(a)) {
+    // dma1 at 4 waves per SIMD on 32x32x16 (default; impl 6 forces it everywhere) or 16x16x32 MFMAs
+    // (impl 4 / TDL_CONV_MFMA=16), or at 3 waves per SIMD (impl 5)
+    const bool mf32 = g_impl == 6 || (g_mf == 32 && g_impl != 4 && g_impl != 5);
+    if (a.K % 128 == 0) {
+      if (mf32) return launch_v2<128, 128, 2, 2, 1, 4, 32>(a, s);
       return g_impl != 5 ? launch_v2<128, 128, 2, 2, 1, 4>(a, s) : launch_v2<128, 128, 2, 2, 1, 3>(a, s);
+    }
+    if (mf32) return launch_v2<128, 64, 2, 2, 1, 4, 32>(a, s);
     return g_impl != 5 ? launch_v2<128, 64, 2, 2, 1, 4>(a, s) : launch_v2<128, 64, 2, 2, 1, 3>(a, s);
   }
   if (g_forced_tile == 3 && a.K % 128 == 0) return launch_tile<256, 128>(a, s);
@@ -875,7 +955,8 @@ void launch(const Igemm& a, hipStream_t s) {
 }  // namespace
 
 void conv_force_tile(int tile) { g_forced_tile = tile; }
-void conv_force_impl(int impl) { g_impl = (impl == 1 || impl == 3 || impl == 4 || impl == 5) ? impl : 2; }
+void conv_force_impl(int impl) { g_impl = (impl == 1 || (impl >= 3 && impl <= 6)) ? impl : 2; }
+void conv_force_mfma(int mf) { g_mf = mf == 16 ? 16 : 32; }
 void conv_force_depth(int depth) {
   // 0: single stage everywhere, 1 / 2: register prefetch depth 1 / the default selection (single
   // stage), 3: depth 2 everywhere (the selection before round 4's A/B, v2 for every long reduction),

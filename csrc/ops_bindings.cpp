@@ -886,7 +886,10 @@ void register_ops(pybind11::module& m) {
         pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("pt"), pybind11::arg("pl"), pybind11::arg("max_plans"),
         pybind11::arg("in_bn") = false);
   m.def("conv_force_tile", &tdl::conv_force_tile, "conv tile sweep hook (0 = heuristic)");
-  m.def("conv_force_impl", &tdl::conv_force_impl, "conv main loop A/B hook: 1 = v1 register staged, 2 = LDS-DMA ring");
+  m.def("conv_force_impl", &tdl::conv_force_impl,
+        "conv main loop A/B hook: 1 v1 register staged, 2 default selection, 3 LDS-DMA ring, 4/5 dma1 at 4/3 waves "
+        "per SIMD on 16x16x32 MFMAs, 6 dma1 on 32x32x16 MFMAs everywhere");
+  m.def("conv_force_mfma", &tdl::conv_force_mfma, "dma1 MFMA form: 32 (32x32x16, default) or 16 (16x16x32)");
   m.def("conv_wgrad3x3_set_rows", &tdl::conv_wgrad3x3_set_rows, "3x3 row-kernel wgrad: output rows per slice (0 = auto)");
   m.def("conv_wgrad_force_single", &tdl::conv_wgrad_force_single,
         "weight-gradient A/B hook: single LDS stage at 3 waves/SIMD (True) or double-buffered (False, default)");

@@ -357,3 +357,28 @@ def test_conv_wgrad_dma1_matches_register_staged_bitwise(shape):
         assert torch.equal(outs[0], outs[1]), (wmw, wnw)
         err = (outs[0].float() - ref).abs().max() / ref.abs().max()
         assert err < 2e-2, (wmw, wnw, float(err))
+
+
+@pytest.mark.parametrize("shape", [s for s in SHAPES if s[7] == 1])
+def test_conv_dma1_on_mfma_32x32x16_matches_fp32(shape):
+    """The dma1 main loop on v_mfma_f32_32x32x16_bf16 (conv_force_impl(6): 2 x 2 blocks of 32 x 32 per
+    wave, its own epilogue accumulator layout) against the fp32 reference, forward and input gradient
+    (the A/B of the MFMA form: scripts/bench_conv_mfma32.py)."""
+    from tensorflow_distributed_learning_amd.ops import hip
+
+    C = hip()
+    N, H, W, Ci, K, KH, KW, s, p = shape
+    x, k = _mk(shape, "cuda:0")
+    xr = x.float().requires_grad_(True)
+    ref = _ref_fwd(xr, k, s, p)
+    dy = torch.randn(ref.shape, device="cuda:0").bfloat16()
+    ref.backward(dy.float())
+    try:
+        C.conv_force_impl(6)
+        y = C.conv_fwd(x, k.permute(3, 0, 1, 2).contiguous(), ref.shape[1], ref.shape[2], s, s, p, p)
+        dx = C.conv_dgrad(dy, k.contiguous(), H, W, p, p)
+        torch.cuda.synchronize()
+    finally:
+        C.conv_force_impl(2)
+    torch.testing.assert_close(y.float(), ref.detach(), atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(dx.float(), xr.grad, atol=4e-2, rtol=2e-2)
