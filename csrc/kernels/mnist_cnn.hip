@@ -1375,11 +1375,11 @@ __global__ __launch_bounds__(256) void k_finalize(MnistArgs a, int apply_sgd, in
 // --------------------------------------------------------------------------------------------
 // KF-X: finalize of the fused_bwd step, one workgroup per contiguous slab range (kFxBlocks):
 // (512 threads = 8 waves each)
-//   [0, 100)    dW3 rows 16m .. 16m+15 (2048 floats): 8 dense tasks, one per wave
-//   100 / 101   db3 (128 floats) / dW4 (1280 floats): 8 dense tasks each, one per wave
-//   102         db4 (10 floats): 1 dense task
-//   [103, 249)  conv2 (kernel row quad, 32-column half) pieces (the last quad: the bias row)
-//   [249, 269)  conv1 kernel / bias outputs 16q .. 16q+15: 4 rows x 16 columns per wave load
+//   [0, 200)    dW3 rows 16m .. 16m+15, columns 64h .. 64h+63 (j = 2m + h): 4 dense tasks, waves 0-3
+//   200 / 201   db3 (128 floats) / dW4 (1280 floats): 8 dense tasks each, one per wave
+//   202         db4 (10 floats): 1 dense task
+//   [203, 349)  conv2 (kernel row quad, 32-column half) pieces (the last quad: the bias row)
+//   [349, 369)  conv1 kernel / bias outputs 16q .. 16q+15: 4 rows x 16 columns per wave load
 // Each writes its gradient range into G.  R = 1 with SGD: W -= lr * G of the range.  R > 1 with
 // the exchange (a.xchg): the range is also published into this workgroup's slot of the channel's
 // exchange buffer (at its slab offsets), then the xGMI exchange with workgroup j of every peer
@@ -1391,16 +1391,18 @@ __global__ __launch_bounds__(256) void k_finalize(MnistArgs a, int apply_sgd, in
 __device__ __forceinline__ void fx_range(const MnistArgs& a, int j, int& lo, int& cnt, int& nseg, int& stride) {
   nseg = 1;
   stride = 0;
-  if (j < 100) {
-    lo = a.ow3 + j * 2048;
-    cnt = 2048;
-  } else if (j == 100) {
+  if (j < kFxW3) {
+    lo = a.ow3 + (j >> 1) * 2048 + (j & 1) * 64;  // rows 16 (j >> 1) .., columns 64 (j & 1) ..
+    cnt = 64;
+    nseg = 16;
+    stride = 128;
+  } else if (j == kFxW3) {
     lo = a.ob3;
     cnt = 128;
-  } else if (j == 101) {
+  } else if (j == kFxW3 + 1) {
     lo = a.ow4;
     cnt = 1280;
-  } else if (j == 102) {
+  } else if (j == kFxW3 + 2) {
     lo = a.ob4;
     cnt = 10;
   } else if (j < kFxDense + kFxConv2) {
@@ -1472,12 +1474,13 @@ __device__ __forceinline__ void finalize_x_body(const MnistArgs& a, int apply_sg
   }
   const bool sgd_local = R == 1 && apply_sgd;  // single replica: SGD fused into the reduction
   // ---- this workgroup's gradient range ----
-  if (j < 100) {
-    dense_w_task(a, j * 8 + wave, lane, sgd_local, lr, xdst);
+  if (j < kFxW3) {
+    // dW3 rows 16 (j >> 1) .. +15, column tiles 4 (j & 1) .. +3: one task per wave of waves 0-3
+    if (wave < 4) dense_w_task(a, (j >> 1) * 8 + (j & 1) * 4 + wave, lane, sgd_local, lr, xdst);
   } else if (j < kFxDense) {
     // db3 (tasks kD1TasksW3 - 8 ..), dW4 (kD1TasksW3 ..), db4 (kD1TasksW3 + 8): <= one task per wave
-    const int T = j == 100 ? kD1TasksW3 - 8 + wave : (j == 101 ? kD1TasksW3 + wave : kD1TasksW3 + 8);
-    if (j < 102 || wave == 0) dense_w_task(a, T, lane, sgd_local, lr, xdst);
+    const int T = j == kFxW3 ? kD1TasksW3 - 8 + wave : (j == kFxW3 + 1 ? kD1TasksW3 + wave : kD1TasksW3 + 8);
+    if (j < kFxW3 + 2 || wave == 0) dense_w_task(a, T, lane, sgd_local, lr, xdst);
   } else if (j < kFxDense + kFxConv2) {
     // conv2 row quad qd (kernel rows 4qd .. 4qd+3; the last quad: the bias row), columns 32h ..
     // 32h+31: thread (column c = tid & 31, image group grp = tid >> 5) sums the quad's 4 rows (one

@@ -10,8 +10,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from tensorflow_distributed_learning_amd.models import mnist_cnn as M  # noqa: E402
 
 
-CATS = {"dW3 rows (0-99)": (0, 100), "db3/dW4/db4 (100-102)": (100, 103), "conv2 pieces (103-248)": (103, 249),
-        "conv1 (249-268)": (249, 269)}
+def _cats(nfx):
+    """KF-X block ranges (dW3 / small dense / conv2 / conv1) for a finalize of nfx workgroups."""
+    d = nfx - 146 - 20  # kFxDense
+    return {f"dW3 rows (0-{d - 4})": (0, d - 3), f"db3/dW4/db4 ({d - 3}-{d - 1})": (d - 3, d),
+            f"conv2 pieces ({d}-{d + 145})": (d, d + 146), f"conv1 ({d + 146}-{nfx - 1})": (d + 146, nfx)}
 
 
 def main():
@@ -29,6 +32,7 @@ def main():
         st.forward_backward(0)
         st.finalize(True)
     grid, nfx = 4 * b, M.FINALIZE_BLOCKS
+    CATS = _cats(nfx)
     rows, cats = [], []
     for rep in range(int(os.environ.get("REPS", "20"))):
         buf = torch.zeros(grid * 104 + nfx * 16, dtype=torch.int64, device=dev)

@@ -44,7 +44,7 @@ def _ref(x, w, b, stride, pads, dil):
 
 def _close(got, ref, tol=2e-5):
     got = got.detach().double().cpu()
-    ref = ref.detach().double()
+    ref = ref.detach().double().cpu()
     scale = ref.abs().max().clamp_min(1e-30)
     err = ((got - ref).abs().max() / scale).item()
     assert err < tol, err
@@ -154,3 +154,32 @@ def test_generic_f32_cnn_same_padding_trains_without_library_calls():
     np.testing.assert_allclose(hg.history["loss"], hc.history["loss"], rtol=1e-3)
     for a, b in zip(mg.get_weights(), mc.get_weights()):
         np.testing.assert_allclose(a, b, rtol=1e-2, atol=2e-3)
+
+
+def test_conv_f32_large_problem_matches_float64():
+    """Large forward / input-gradient problems (65,536 pixels x 128 channels, 1,024 output tiles);
+    float64 reference through im2col on the GPU."""
+    N, H, W, C, K = 16, 64, 64, 128, 128
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(N, H, W, C, generator=g).cuda()
+    w = (torch.randn(3, 3, C, K, generator=g) / (9 * C) ** 0.5).cuda()
+    dy = torch.randn(N, H, W, K, generator=g).cuda()
+    xd = x.double().permute(0, 3, 1, 2).requires_grad_(True)
+    cols = F.unfold(xd, 3, padding=1)
+    yr = (w.double().permute(3, 2, 0, 1).reshape(K, C * 9) @ cols).reshape(N, K, H, W).permute(0, 2, 3, 1)
+    yr.backward(dy.double())
+    xc = x.clone().requires_grad_(True)
+    y = CF.conv2d(xc, w, None, (1, 1), (1, 1, 1, 1), (1, 1))
+    _close(y, yr)
+    y.backward(dy)
+    _close(xc.grad, xd.grad.permute(0, 2, 3, 1))
+
+
+def test_dense_f32_large_gemm_with_ragged_edges():
+    """A 2000 x 96 x 4100 GEMM (both tile edges partial) against float64."""
+    g = torch.Generator().manual_seed(5)
+    a = torch.randn(2000, 96, generator=g).cuda()
+    b = torch.randn(96, 4100, generator=g).cuda()
+    bias = torch.randn(4100, generator=g).cuda()
+    y = CF.dense(a, b, bias)
+    _close(y, a.double() @ b.double() + bias.double())
