@@ -1,5 +1,6 @@
 #!/bin/bash
-# v6: conv2 dgrad W2 operands gathered from LDS (no global W2 prefetch at the hand-off)
+# MNIST round harness: fused-engine GPU tests (+ $TESTS), fused-kernel phase stamps, then the same-box
+# interleaved A/B of ab_arms.sh over $ARMS (name=dir:variant ...), $REPS reps, into gpurun_out/$OUT and /$AB.
 set -o pipefail
 O=gpurun_out/${OUT:-r5v6}
 mkdir -p $O
