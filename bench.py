@@ -121,11 +121,15 @@ def main():
     torch.cuda.synchronize(dev)
     comm.barrier()
     torch.cuda.synchronize(dev)
+    # (TDL_BENCH_EVENTS=1: device-side events around the steps, for the stderr diagnostics line)
+    events = os.environ.get("TDL_BENCH_EVENTS", "0") == "1"
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record()
+    if events:
+        ev0.record()
     done = trainer.run_train(handler, K)
-    ev1.record()
+    if events:
+        ev1.record()
     t_host = time.perf_counter() - t0
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
@@ -136,7 +140,8 @@ def main():
     comm.barrier()
     torch.cuda.synchronize(dev)
     print(f"timed region: wall {dt * 1e3:.3f} ms = host launch {t_host * 1e3:.3f} ms + device drain "
-          f"{(dt - t_host) * 1e3:.3f} ms; device events {ev0.elapsed_time(ev1):.3f} ms", file=sys.stderr)
+          f"{(dt - t_host) * 1e3:.3f} ms" + (f"; device events {ev0.elapsed_time(ev1):.3f} ms" if events else ""),
+          file=sys.stderr)
     if done != K:
         raise SystemExit(f"bench: ran {done} steps instead of {K}")
     t = torch.tensor([dt], dtype=torch.float64, device=dev if comm.name == "rccl" else "cpu")
