@@ -89,13 +89,15 @@ constexpr int kMnistPart2Rows = 289;
 // write-through store
 constexpr int kP2Quads = 73, kP2QuadFloats = kP2Quads * 256;
 
-// finalize workgroups of the fused_bwd step (k_finalize_x): 203 dense (dW3 rows 16m..16m+15, columns
-// 64h..64h+63 = 16 x 64 slab floats each x 200, db3, dW4, db4), 146 conv2 (row quad, 32-column half)
-// pieces (4 x 32 floats; the last quad: the bias row), 20 conv1 groups (16)
-// (the dW3 rows go to kFxW3 = 200 workgroups of 4 busy waves -- 16 rows x 64 columns each -- rather than
-// 100 of 8: a dW3 task issues 36 scalar loads, and a CU with a whole 8-task block queued 288 of them)
-constexpr int kFxW3 = 200;
-constexpr int kFxDense = kFxW3 + 3, kFxConv2 = 2 * kP2Quads, kFxConv1 = 20;
+// finalize workgroups of the fused_bwd step (k_finalize_x): 209 dense (dW3 rows 16m..16m+15, columns
+// 64h..64h+63 = 16 x 64 slab floats each x 200; db3 in 4 x 32, dW4 in 4 x 32 rows x 10, db4),
+// 146 conv2 (row quad, 32-column half) pieces (4 x 32 floats; the last quad: the bias row), 20 conv1
+// groups (16).  A dense task issues 32-36 scalar loads (one per lane per row): the dW3 rows go to
+// kFxW3 = 200 workgroups of 4 busy waves and db3 / dW4 to 8 workgroups of 2, rather than 8-task
+// blocks (a CU with a whole 8-task block queued 256-288 of them behind its texture-address unit:
+// those blocks ended last, ~1.9 us of wave life against ~1.0 for a 4-task dW3 block)
+constexpr int kFxW3 = 200, kFxSmallDense = 9;
+constexpr int kFxDense = kFxW3 + kFxSmallDense, kFxConv2 = 2 * kP2Quads, kFxConv1 = 20;
 constexpr int kFxBlocks = kFxDense + kFxConv2 + kFxConv1;
 constexpr int kDense1Chunks = 4;  // dense1 partials: one per conv2 channel quarter (k_fwd_conv)
 constexpr int kMnistPart1Cols = 320;

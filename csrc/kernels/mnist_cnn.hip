@@ -1376,10 +1376,11 @@ __global__ __launch_bounds__(256) void k_finalize(MnistArgs a, int apply_sgd, in
 // KF-X: finalize of the fused_bwd step, one workgroup per contiguous slab range (kFxBlocks):
 // (512 threads = 8 waves each)
 //   [0, 200)    dW3 rows 16m .. 16m+15, columns 64h .. 64h+63 (j = 2m + h): 4 dense tasks, waves 0-3
-//   200 / 201   db3 (128 floats) / dW4 (1280 floats): 8 dense tasks each, one per wave
-//   202         db4 (10 floats): 1 dense task
-//   [203, 349)  conv2 (kernel row quad, 32-column half) pieces (the last quad: the bias row)
-//   [349, 369)  conv1 kernel / bias outputs 16q .. 16q+15: 4 rows x 16 columns per wave load
+//   [200, 204)  db3 columns 32 jj .. +31: 2 dense tasks (waves 0-1)
+//   [204, 208)  dW4 rows 32 jj .. +31 (x 10): 2 dense tasks (waves 0-1)
+//   208         db4 (10 floats): 1 dense task
+//   [209, 355)  conv2 (kernel row quad, 32-column half) pieces (the last quad: the bias row)
+//   [355, 375)  conv1 kernel / bias outputs 16q .. 16q+15: 4 rows x 16 columns per wave load
 // Each writes its gradient range into G.  R = 1 with SGD: W -= lr * G of the range.  R > 1 with
 // the exchange (a.xchg): the range is also published into this workgroup's slot of the channel's
 // exchange buffer (at its slab offsets), then the xGMI exchange with workgroup j of every peer
@@ -1396,13 +1397,13 @@ __device__ __forceinline__ void fx_range(const MnistArgs& a, int j, int& lo, int
     cnt = 64;
     nseg = 16;
     stride = 128;
-  } else if (j == kFxW3) {
-    lo = a.ob3;
-    cnt = 128;
-  } else if (j == kFxW3 + 1) {
-    lo = a.ow4;
-    cnt = 1280;
-  } else if (j == kFxW3 + 2) {
+  } else if (j < kFxW3 + 4) {
+    lo = a.ob3 + 32 * (j - kFxW3);  // db3 columns 32 jj .. (tasks 2 jj, 2 jj + 1)
+    cnt = 32;
+  } else if (j < kFxW3 + 8) {
+    lo = a.ow4 + 320 * (j - kFxW3 - 4);  // dW4 rows 32 jj .. +31, 10 columns each
+    cnt = 320;
+  } else if (j == kFxW3 + 8) {
     lo = a.ob4;
     cnt = 10;
   } else if (j < kFxDense + kFxConv2) {
@@ -1478,9 +1479,12 @@ __device__ __forceinline__ void finalize_x_body(const MnistArgs& a, int apply_sg
     // dW3 rows 16 (j >> 1) .. +15, column tiles 4 (j & 1) .. +3: one task per wave of waves 0-3
     if (wave < 4) dense_w_task(a, (j >> 1) * 8 + (j & 1) * 4 + wave, lane, sgd_local, lr, xdst);
   } else if (j < kFxDense) {
-    // db3 (tasks kD1TasksW3 - 8 ..), dW4 (kD1TasksW3 ..), db4 (kD1TasksW3 + 8): <= one task per wave
-    const int T = j == kFxW3 ? kD1TasksW3 - 8 + wave : (j == kFxW3 + 1 ? kD1TasksW3 + wave : kD1TasksW3 + 8);
-    if (j < kFxW3 + 2 || wave == 0) dense_w_task(a, T, lane, sgd_local, lr, xdst);
+    // db3 (tasks kD1TasksW3 - 8 ..) and dW4 (kD1TasksW3 ..): two tasks per workgroup on waves 0-1;
+    // db4 (kD1TasksW3 + 8): wave 0 of the last one
+    const int jj = j - kFxW3, t = 2 * jj + wave;
+    if (jj < 8 ? wave < 2 : wave == 0)
+      dense_w_task(a, jj < 8 ? (t < 8 ? kD1TasksW3 - 8 + t : kD1TasksW3 + t - 8) : kD1TasksW3 + 8, lane, sgd_local, lr,
+                   xdst);
   } else if (j < kFxDense + kFxConv2) {
     // conv2 row quad qd (kernel rows 4qd .. 4qd+3; the last quad: the bias row), columns 32h ..
     // 32h+31: thread (column c = tid & 31, image group grp = tid >> 5) sums the quad's 4 rows (one

@@ -12,8 +12,8 @@ from tensorflow_distributed_learning_amd.models import mnist_cnn as M  # noqa: E
 
 def _cats(nfx):
     """KF-X block ranges (dW3 / small dense / conv2 / conv1) for a finalize of nfx workgroups."""
-    d = nfx - 146 - 20  # kFxDense
-    return {f"dW3 rows (0-{d - 4})": (0, d - 3), f"db3/dW4/db4 ({d - 3}-{d - 1})": (d - 3, d),
+    d = nfx - 146 - 20  # kFxDense (= kFxW3 + 9 small dense blocks)
+    return {f"dW3 rows (0-{d - 10})": (0, d - 9), f"db3/dW4/db4 ({d - 9}-{d - 1})": (d - 9, d),
             f"conv2 pieces ({d}-{d + 145})": (d, d + 146), f"conv1 ({d + 146}-{nfx - 1})": (d + 146, nfx)}
 
 

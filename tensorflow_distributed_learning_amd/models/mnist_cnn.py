@@ -31,7 +31,7 @@ MNIST_CNN_VARIABLES = [
     ("dense_1/bias:0", (10,)),
 ]
 MNIST_NUM_PARAMS = 225_034
-FINALIZE_BLOCKS = 369  # workgroups of the fused finalize (kFxBlocks): one exchange slot each
+FINALIZE_BLOCKS = 375  # workgroups of the fused finalize (kFxBlocks): one exchange slot each
 
 
 def mnist_layout() -> SlabLayout:
