@@ -35,11 +35,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 
-def _spe(K: int, cap: int = 50) -> int:
+def _spe(K: int, cap: int = 25) -> int:
     """Steps per execution: the largest divisor of K that is <= cap (one graph launch per
-    execution; the timed region replays K / spe graphs).  Measured at K=1000 on one MI355X
-    (profiles/mnist_bench_spe_sweep_r2.txt): 50 steps (200 kernel nodes) per graph run at 37.0
-    us/step, 100-1000 at 39.2-39.9 (larger graphs dispatch slower on the device)."""
+    execution; the timed region replays K / spe graphs).  Measured on one MI355X
+    (profiles/mnist_bench_spe_sweep_r5.txt): at K=1000, 20-25 steps (40-50 kernel nodes) per graph
+    run 0.5 % faster than 50; at K=20 one graph of 20 beats 2 x 10 / 4 x 5 (every graph launch
+    costs the region its own submission latency); round 2's sweep put 100-1000 steps per graph
+    5 % behind 50 (profiles/mnist_bench_spe_sweep_r2.txt)."""
     for d in range(min(K, cap), 0, -1):
         if K % d == 0:
             return d
