@@ -33,7 +33,7 @@ def main():
         st.finalize(True)
     grid, nfx = 4 * b, M.FINALIZE_BLOCKS
     CATS = _cats(nfx)
-    rows, cats = [], []
+    rows, cats, lasts = [], [], []
     for rep in range(int(os.environ.get("REPS", "20"))):
         buf = torch.zeros(grid * 104 + nfx * 16, dtype=torch.int64, device=dev)
         st._impl.set_stamps(buf)
@@ -49,6 +49,7 @@ def main():
         cats.append([((x[lo:hi, :, 0].min() - xs0) / 100, (np.median(x[lo:hi, :, 0]) - xs0) / 100,
                       (np.median(x[lo:hi, :, 1]) - xs0) / 100, (x[lo:hi, :, 1].max() - xs0) / 100)
                      for lo, hi in CATS.values()])
+        lasts.append((x[:, :, 1].max(axis=1) - xs0) / 100)  # per-block last wave end
         rows.append([(f.max() - t0) / 100, (x[:, :, 0].min() - f.max()) / 100, (x[:, :, 1].max() - x[:, :, 0].min()) / 100,
                      (np.median(x[:, :, 1] - x[:, :, 0])) / 100, (x[:, :, 0].max() - x[:, :, 0].min()) / 100,
                      (x[:, :, 1].max() - t0) / 100])
@@ -63,6 +64,9 @@ def main():
     print("KF-X blocks, us since KF-X first wave (median over reps): first start / median start / median end / last end")
     for (nm, _), v in zip(CATS.items(), c):
         print(f"  {nm:22s} " + " ".join(f"{t:6.2f}" for t in v))
+    ml = np.median(np.array(lasts), axis=0)
+    late = np.argsort(ml)[::-1][:12]
+    print("latest KF-X blocks (median last-wave end, us): " + ", ".join(f"{j}:{ml[j]:.2f}" for j in late))
 
 
 if __name__ == "__main__":
