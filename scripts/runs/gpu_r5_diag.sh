@@ -1,5 +1,6 @@
 #!/bin/bash
 # DIAG variants of the finalize: 16 skip conv2 pieces, 32 skip dW3, 64 dW4 without dL loads, 128 dW4 without H loads
+# (the DIAG bits were a temporary build of mnist_cnn.hip: finalize_x_body returned early for those ranges / skipped those loads; not in the tree)
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r5diag
