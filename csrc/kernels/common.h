@@ -38,6 +38,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uns
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
 }
 
+// 16-B load through a raw buffer resource: byte offset = voffset (per lane) + soffset (SGPR, e.g. a
+// compile-time stride) -- no 64-bit address arithmetic on the VALU per load
+__device__ __forceinline__ f4 ld4_buf(__amdgpu_buffer_rsrc_t r, int voffset, int soffset) {
+  typedef unsigned u4 __attribute__((ext_vector_type(4)));
+  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, voffset, soffset, 0));
+}
+
 // LDS-DMA: one 16-B chunk per lane from a raw buffer straight into LDS (buffer_load_dwordx4 ... lds).
 // The 64 lanes of the wave write 1 KiB linearly from `wave_dst` (wave-uniform): lane L lands at
 // wave_dst + 16 L bytes.  Out-of-range voffsets (e.g. 0x80000000) land zeros.

@@ -1024,8 +1024,11 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   // every wave stalls behind them (measured: conv1 3.4-4.4 us instead of ~1 us).
   const int n4 = (tid & 31) * 4, rg = tid >> 5;
   f4 w3v[25];
-  const float* w3b = a.W + a.ow3 + (size_t)(16 * cq + rg) * 128 + n4;
-  auto ldw3 = [&](int j) { w3v[j] = ld4(w3b + j * 64 * 128); };
+  // one buffer resource over this quarter's W3 rows; the per-load stride rides in the SGPR offset
+  // (a 64-bit global address per load cost ~8 VALU of address arithmetic: 200 per wave)
+  const auto w3r = buf_rsrc(a.W + a.ow3 + (size_t)16 * cq * 128, (unsigned)((1600 - 16 * cq) * 128 * 4));
+  const int w3vo = (rg * 128 + n4) * 4;
+  auto ldw3 = [&](int j) { w3v[j] = ld4_buf(w3r, w3vo, j * 64 * 128 * 4); };
 #pragma unroll
   for (int j = 0; j < 6; ++j) ldw3(j);
   // ---- conv1 on MFMA (K = 9 taps padded to 12): rows = 676 conv1 positions in pool-window-major
