@@ -49,7 +49,7 @@ class MnistStep {
     A2_ = at::empty({b * 1600}, u8);
     H_ = at::empty({b * 128}, f);
     dH_ = at::empty({b * 128}, f);
-    dL_ = at::zeros({b * 10}, f);
+    dL_ = at::zeros({b * tdl::kDLStride}, f);
     cnt_ = at::zeros({b}, f.dtype(at::kInt));
     dHt_ = at::zeros({b * 128}, f.dtype(at::kLong));  // tag 0 never matches (tags start at 1)
     ep_ = at::zeros({1}, f.dtype(at::kInt));

@@ -45,6 +45,11 @@ __device__ __forceinline__ f4 ld4_buf(__amdgpu_buffer_rsrc_t r, int voffset, int
   return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, voffset, soffset, 0));
 }
 
+// 4-B load through a raw buffer resource (offsets past the resource's size read 0)
+__device__ __forceinline__ float ld1_buf(__amdgpu_buffer_rsrc_t r, int voffset, int soffset) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voffset, soffset, 0));
+}
+
 // LDS-DMA: one 16-B chunk per lane from a raw buffer straight into LDS (buffer_load_dwordx4 ... lds).
 // The 64 lanes of the wave write 1 KiB linearly from `wave_dst` (wave-uniform): lane L lands at
 // wave_dst + 16 L bytes.  Out-of-range voffsets (e.g. 0x80000000) land zeros.

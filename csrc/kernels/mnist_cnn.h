@@ -34,7 +34,7 @@ struct MnistArgs {
                       // [b][kP2Quads][64][4] (see kP2Quads)
   float* part1;       // [2b or 4b][320] partials of conv1 wgrad (+ bias), see mnist_part1_rows
   float* part3;       // [4][b][128] dense1 partials, one per conv2 channel quarter
-  float* dL;          // [b][10] dlogits (already scaled by 1/(b*R))
+  float* dL;          // [b][kDLStride] dlogits (already scaled by 1/(b*R)), 10 used per row
   unsigned* cnt;      // [b] per-image arrival counters of k_fwd_conv (re-armed by KC)
   unsigned long long* dHt;  // [b][128] dP2 hand-off: dH bits | tag << 32 (8-B write-through stores)
   unsigned* ep;       // step epoch: k_fwd_conv tags dHt / part3t with *ep + 1, KC advances it
@@ -99,6 +99,11 @@ constexpr int kP2Quads = 73, kP2QuadFloats = kP2Quads * 256;
 constexpr int kFxW3 = 200, kFxSmallDense = 9;
 constexpr int kFxDense = kFxW3 + kFxSmallDense, kFxConv2 = 2 * kP2Quads, kFxConv1 = 20;
 constexpr int kFxBlocks = kFxDense + kFxConv2 + kFxConv1;
+// dlogits row stride: one 128-B line per image.  The head of image r runs on XCD (4r + quarter) % 8,
+// so packed 40-B rows put 3-4 images' dlogits from two XCDs into one line, and the finalize's reads
+// of such lines right after the boundary write-back were measured at 2.5-7 us (the db4 / dW4 blocks,
+// otherwise done in ~0.6 us, then ended the finalize)
+constexpr int kDLStride = 32;
 constexpr int kDense1Chunks = 4;  // dense1 partials: one per conv2 channel quarter (k_fwd_conv)
 constexpr int kMnistPart1Cols = 320;
 // conv1 wgrad partial rows: (image, pixel half) of k_conv_bwd, or (image, quarter) of fused_bwd

@@ -260,7 +260,7 @@ __device__ __forceinline__ void head_row(const MnistArgs& a, int r, int l, int y
   a.dH[r * 128 + l + 64] = dh1;
   a.H[r * 128 + l] = h0;
   a.H[r * 128 + l + 64] = h1;
-  if (l < 10) a.dL[r * 10 + l] = mine;
+  if (l < 10) a.dL[r * kDLStride + l] = mine;
   if (l == 0) {
     atomicAdd(&a.metrics[0], lse - ly);
     atomicAdd(&a.metrics[1], am == y ? 1.f : 0.f);
@@ -322,25 +322,30 @@ __device__ __forceinline__ void head_eval(const MnistArgs& a, int r, int l, int 
 // --------------------------------------------------------------------------------------------
 constexpr int kD1TasksW3 = 101 * 8;
 
-// acc += A^T B over K = b rows, A rows a_row(r)[m], B rows b_row(r)[n]: lane (i, g) supplies
-// A[r = 4s + g][m0 + i] and B[r][n0 + i]; 64 rows' loads in flight per batch.
-template <typename FA, typename FB>
-__device__ __forceinline__ f4 gemm_tn_rows(int b, int g, FA fa, FB fb) {
+// acc += A^T B over K = b rows of two row-major operands read through buffer resources sized to
+// the b valid rows (rows past b load 0, so no clamp or mask): lane (i, g) supplies A[r = r0 + 4s + g]
+// at byte ca of the row and B[r] at byte cb, sa / sb the row strides in bytes (the row offset rides
+// in the SGPR offset: no per-load 64-bit address arithmetic on the VALU); 64 rows' loads in flight
+// per batch
+// (E0: A is the unit row e_0 -- lane i == 0 supplies 1 -- instead of a load: the bias columns)
+template <bool E0 = false>
+__device__ __forceinline__ f4 gemm_tn_buf(int b, int g, __amdgpu_buffer_rsrc_t ra, int sa, int ca,
+                                          __amdgpu_buffer_rsrc_t rb, int sb, int cb, float e0 = 0.f) {
   f4 acc0 = zero4(), acc1 = zero4();
+  const int va = g * sa + ca, vb = g * sb + cb;
   for (int r0 = 0; r0 < b; r0 += 64) {
     float av[16], bv[16];
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      const int rr = min(r0 + 4 * s + g, b - 1);
-      av[s] = fa(rr);
-      bv[s] = fb(rr);
+      // (E0: rows past b must add 0: their B loads read 0)
+      av[s] = E0 ? e0 : ld1_buf(ra, va, (r0 + 4 * s) * sa);
+      bv[s] = ld1_buf(rb, vb, (r0 + 4 * s) * sb);
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      const float x = (r0 + 4 * s + g < b) ? av[s] : 0.f;
-      if (s & 1) acc1 = mfma16x16x4(x, bv[s], acc1);
-      else acc0 = mfma16x16x4(x, bv[s], acc0);
+      if (s & 1) acc1 = mfma16x16x4(av[s], bv[s], acc1);
+      else acc0 = mfma16x16x4(av[s], bv[s], acc0);
     }
   }
   return acc0 + acc1;
@@ -361,8 +366,8 @@ __device__ __forceinline__ void dense_w_task(const MnistArgs& a, int T, int lane
       float wold[4];  // the SGD operands ride in the operand loads' round trip
 #pragma unroll
       for (int r = 0; r < 4; ++r) wold[r] = sgd ? a.W[a.ow3 + (mt * 16 + 4 * g + r) * 128 + n] : 0.f;
-      const f4 acc = gemm_tn_rows(
-          b, g, [&](int r) { return a.P2[(size_t)r * 1600 + kf]; }, [&](int r) { return a.dH[r * 128 + n]; });
+      const f4 acc = gemm_tn_buf(b, g, buf_rsrc(a.P2, (unsigned)(b * 1600 * 4)), 1600 * 4, kf * 4,
+                                 buf_rsrc(a.dH, (unsigned)(b * 128 * 4)), 128 * 4, n * 4);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int e = a.ow3 + (mt * 16 + 4 * g + r) * 128 + n;
@@ -372,8 +377,8 @@ __device__ __forceinline__ void dense_w_task(const MnistArgs& a, int T, int lane
       }
     } else {  // db3: A = e_0 (row 0 of the tile = column sums of dH)
       const float wold = sgd ? a.W[a.ob3 + n] : 0.f;
-      const f4 acc = gemm_tn_rows(
-          b, g, [&](int) { return i == 0 ? 1.f : 0.f; }, [&](int r) { return a.dH[r * 128 + n]; });
+      const auto dhr = buf_rsrc(a.dH, (unsigned)(b * 128 * 4));
+      const f4 acc = gemm_tn_buf<true>(b, g, dhr, 0, 0, dhr, 128 * 4, n * 4, i == 0 ? 1.f : 0.f);
       if (g == 0) {
         a.G[a.ob3 + n] = acc[0];
         if (xdst != nullptr) xdst[a.ob3 + n] = acc[0];
@@ -386,14 +391,16 @@ __device__ __forceinline__ void dense_w_task(const MnistArgs& a, int T, int lane
   if (T3 < 9) {
     // dW4[k][c] = sum_r H[r][k] dL[r][c] (tiles 0..7), db4 (tile 8, A = e_0); N = 10 of 16
     const int c = min(i, 9);
-    const float cm = i < 10 ? 1.f : 0.f;
     float wold[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       wold[r] = sgd ? a.W[T3 < 8 ? a.ow4 + (T3 * 16 + 4 * g + r) * 10 + c : a.ob4 + c] : 0.f;
-    const f4 acc = gemm_tn_rows(
-        b, g, [&](int r) { return T3 < 8 ? a.H[r * 128 + T3 * 16 + i] : (i == 0 ? 1.f : 0.f); },
-        [&](int r) { return a.dL[r * 10 + c] * cm; });
+    // (lanes i >= 10 read past the dL resource: 0)
+    const auto dlr = buf_rsrc(a.dL, (unsigned)(b * kDLStride * 4));
+    const int dlc = i < 10 ? i * 4 : 0x40000000;
+    const f4 acc = T3 < 8 ? gemm_tn_buf(b, g, buf_rsrc(a.H, (unsigned)(b * 128 * 4)), 128 * 4, (T3 * 16 + i) * 4, dlr,
+                                        kDLStride * 4, dlc)
+                          : gemm_tn_buf<true>(b, g, dlr, 0, 0, dlr, kDLStride * 4, dlc, i == 0 ? 1.f : 0.f);
     if (i < 10) {
       if (T3 < 8) {
 #pragma unroll
@@ -1460,7 +1467,10 @@ __device__ __forceinline__ void finalize_x_body(const MnistArgs& a, int apply_sg
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const float lr = *a.lr;
   const bool xchg = R > 1 && a.xchg && apply_sgd;
-  if (j == 0 && tid == 0) a.ep[0] += 1u;  // the next step's hand-off tag (no k_conv_bwd launch)
+  // the next step's hand-off tag (no k_conv_bwd launch), advanced on every path, by a wave with no
+  // dense task (range 0 is a dW3 range: waves 0-3 busy): its load -> store round trip in front of a
+  // task's operand loads made block 0 the finalize's last
+  if (j == 0 && tid == 4 * 64) a.ep[0] += 1u;
   uint32_t e = 0;
   float* xdst = nullptr;
   int64_t half = 0;
@@ -1503,14 +1513,15 @@ __device__ __forceinline__ void finalize_x_body(const MnistArgs& a, int apply_sg
     const int e2 = biasq ? a.ob2 + 32 * h + cc : a.ow2 + (4 * qd + rr) * 64 + 32 * h + cc;
     const float wold = (sgd_local && owner) ? a.W[e2] : 0.f;
     f4 sum = zero4();
+    // images past b read 0 (resource sized to the b images); image stride in the SGPR offset
+    const auto p2r = buf_rsrc(a.part2, (unsigned)(a.b * kP2QuadFloats * 4));
+    const int vo2 = (grp * kP2QuadFloats + (qd * 64 + 32 * h + c) * 4) * 4;
     for (int base = 0; base < a.b; base += 64) {  // 4 images per thread in flight
       f4 v[4];
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
-        v[jj] = ld4(a.part2 + (size_t)min(base + grp + 16 * jj, a.b - 1) * kP2QuadFloats + (qd * 64 + 32 * h + c) * 4);
+      for (int jj = 0; jj < 4; ++jj) v[jj] = ld4_buf(p2r, vo2, (base + 16 * jj) * kP2QuadFloats * 4);
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
-        if (base + grp + 16 * jj < a.b) sum += v[jj];
+      for (int jj = 0; jj < 4; ++jj) sum += v[jj];
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) sum[r] = rs_swap32(sum[r], sum[r]);
@@ -1534,12 +1545,15 @@ __device__ __forceinline__ void finalize_x_body(const MnistArgs& a, int apply_sg
     const int e1 = o < 288 ? a.ow1 + o : a.ob1 + (o - 288);
     const float wold = sgd_local && wave == 0 ? a.W[e1] : 0.f;
     float sum = 0.f;
-    for (int base = 4 * wave + rg; base < rows; base += 256) {
+    // rows past `rows` read 0 (resource sized to them); the row stride rides in the SGPR offset
+    const auto p1r = buf_rsrc(a.part1, (unsigned)(rows * kMnistPart1Cols * 4));
+    const int vo1 = ((4 * wave + rg) * kMnistPart1Cols + o) * 4;
+    for (int b0 = 0; b0 < rows; b0 += 256) {
       float v[8];
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) v[jj] = a.part1[(size_t)min(base + 32 * jj, rows - 1) * kMnistPart1Cols + o];
+      for (int jj = 0; jj < 8; ++jj) v[jj] = ld1_buf(p1r, vo1, (b0 + 32 * jj) * kMnistPart1Cols * 4);
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) sum += (base + 32 * jj < rows) ? v[jj] : 0.f;
+      for (int jj = 0; jj < 8; ++jj) sum += v[jj];
     }
     sum = sum_lane_groups(sum);
     if (rg == 0) fx_red[wave][c] = sum;
