@@ -10,7 +10,8 @@ Tensor bundle (``<prefix>.index`` + ``<prefix>.data-00000-of-00001``):
 Model directory (``model.save(path)``)::
 
     path/saved_model.json                       architecture + compile config
-    path/saved_model.pb                         SavedModel header: tags, serving signature, saver (ckpt/saved_model_pb.py)
+    path/saved_model.pb                         TF1-format SavedModel: serving graph, variables, V2 saver,
+                                                signature (ckpt/saved_model_pb.py, ckpt/graph_def.py)
     path/variables/variables.index
     path/variables/variables.data-00000-of-00001
     path/assets/
@@ -137,6 +138,11 @@ def model_tensors(model) -> Dict[str, torch.Tensor]:
     return {v.name: v.read_value() for v in model.weights}
 
 
+def model_tensors_are_float32(tensors: Dict[str, torch.Tensor], model) -> bool:
+    """The serving graph declares every variable DT_FLOAT (the Keras default variable dtype)."""
+    return all(tensors[v.name].dtype == torch.float32 for v in model.weights if v.name in tensors)
+
+
 def save_model(model, path: str, overwrite: bool = True, include_optimizer: bool = True) -> None:
     """model.save(path): SavedModel-shaped directory (written by the chief only)."""
     strategy = _strategy_of(model)
@@ -158,7 +164,9 @@ def save_model(model, path: str, overwrite: bool = True, include_optimizer: bool
         cfg["compile"] = model._compile_config
     with open(os.path.join(path, "saved_model.json"), "w") as f:
         json.dump(cfg, f, indent=1, default=str)
-    # the SavedModel protobuf header: tags, serving signature, V2 saver over variables/ (no TF graph)
+    # saved_model.pb: the serving graph (inference ops, resource variables, V2 saver over
+    # variables/) + tags + serving signature; header-only for a layer with no TF op mapping
+    from . import graph_def as GD
     from . import saved_model_pb as SMP
 
     try:
@@ -169,8 +177,16 @@ def save_model(model, path: str, overwrite: bool = True, include_optimizer: bool
         warnings.warn(f"model.save: saved_model.pb skipped ({type(e).__name__}: {e})")
         spec = None
     if spec is not None:
+        graph = None
+        if model_tensors_are_float32(tensors, model):
+            try:
+                graph = GD.build_graph(model, SMP.GRAPH_PRODUCER)
+            except GD.UnsupportedLayer as e:
+                import warnings
+
+                warnings.warn(f"model.save: saved_model.pb without a TF graph ({e})")
         with open(os.path.join(path, "saved_model.pb"), "wb") as f:
-            f.write(SMP.encode_saved_model(*spec))
+            f.write(SMP.encode_saved_model(*spec, graph=graph))
     remove_temp_dirpath(path, strategy) if path != real else None
 
 

@@ -56,7 +56,9 @@ def _messages():
         [entry("InputsEntry", F.TYPE_MESSAGE, ".tdltest.TensorInfo"),
          entry("OutputsEntry", F.TYPE_MESSAGE, ".tdltest.TensorInfo")])
     msg("VersionDef", [("producer", 1, F.TYPE_INT32, O, None), ("min_consumer", 2, F.TYPE_INT32, O, None)])
-    msg("GraphDef", [("versions", 4, F.TYPE_MESSAGE, O, ".tdltest.VersionDef")])
+    # (the graph's nodes and the collections as opaque bytes here: tests/test_graph_def_cpu.py
+    # checks them against NodeDef / CollectionDef descriptors)
+    msg("GraphDef", [("node", 1, F.TYPE_BYTES, R, None), ("versions", 4, F.TYPE_MESSAGE, O, ".tdltest.VersionDef")])
     msg("SaverDef", [("filename_tensor_name", 1, F.TYPE_STRING, O, None),
                      ("save_tensor_name", 2, F.TYPE_STRING, O, None),
                      ("restore_op_name", 3, F.TYPE_STRING, O, None), ("max_to_keep", 4, F.TYPE_INT32, O, None),
@@ -70,6 +72,7 @@ def _messages():
     msg("MetaGraphDef", [("meta_info_def", 1, F.TYPE_MESSAGE, O, ".tdltest.MetaInfoDef"),
                          ("graph_def", 2, F.TYPE_MESSAGE, O, ".tdltest.GraphDef"),
                          ("saver_def", 3, F.TYPE_MESSAGE, O, ".tdltest.SaverDef"),
+                         ("collection_def", 4, F.TYPE_BYTES, R, None),
                          ("signature_def", 5, F.TYPE_MESSAGE, R, ".tdltest.MetaGraphDef.SignatureDefEntry")],
         [entry("SignatureDefEntry", F.TYPE_MESSAGE, ".tdltest.SignatureDef")])
     msg("SavedModel", [("saved_model_schema_version", 1, F.TYPE_INT64, O, None),
