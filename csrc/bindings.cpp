@@ -154,6 +154,12 @@ class MnistStep {
   bool dp2_in_forward() const { return a_.dp2_fwd != 0; }
   // with dP2 in the forward kernel, also run the conv backward there (forward_backward only)
   void set_fused_bwd(bool on) { fused_bwd_ = on; }
+  // keep_grad = false: a single replica's finalize with fused SGD does not write the gradient slab
+  // G (nothing reads it on that path; fewer dirty lines for the kernel-end write-back)
+  void set_keep_grad(bool on) {
+    a_.variant = on ? (a_.variant & ~tdl::kMnistVariantNoG) : (a_.variant | tdl::kMnistVariantNoG);
+  }
+  bool keep_grad() const { return (a_.variant & tdl::kMnistVariantNoG) == 0; }
   bool fused_bwd() const { return fused_bwd_ && a_.dp2_fwd; }
   // k_finalize_x grid cap (0: one workgroup per range; see MnistArgs::fx_grid)
   void set_fx_grid(int64_t n) { a_.fx_grid = (int)std::max<int64_t>(0, n); }
@@ -346,6 +352,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("dp2_in_forward", &MnistStep::dp2_in_forward)
       .def("set_fused_bwd", &MnistStep::set_fused_bwd)
       .def("fused_bwd", &MnistStep::fused_bwd)
+      .def("set_keep_grad", &MnistStep::set_keep_grad)
+      .def("keep_grad", &MnistStep::keep_grad)
       .def("error", &MnistStep::error, pybind11::arg("reset") = false)
       .def("buffers", &MnistStep::buffers)
       .def("set_stamps", &MnistStep::set_stamps);

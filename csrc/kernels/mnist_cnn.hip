@@ -356,7 +356,7 @@ __device__ __forceinline__ f4 gemm_tn_buf(int b, int g, __amdgpu_buffer_rsrc_t r
 constexpr int kDenseTasks = kD1TasksW3 + 9;
 
 __device__ __forceinline__ void dense_w_task(const MnistArgs& a, int T, int lane, bool sgd, float lr,
-                                             float* xdst = nullptr) {
+                                             float* xdst = nullptr, bool keep_g = true) {
   const int i = lane & 15, g = lane >> 4;
   const int b = a.b;
   if (T < kD1TasksW3) {
@@ -371,7 +371,7 @@ __device__ __forceinline__ void dense_w_task(const MnistArgs& a, int T, int lane
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int e = a.ow3 + (mt * 16 + 4 * g + r) * 128 + n;
-        a.G[e] = acc[r];
+        if (keep_g) a.G[e] = acc[r];
         if (xdst != nullptr) xdst[e] = acc[r];
         if (sgd) a.W[e] = wold[r] - lr * acc[r];
       }
@@ -380,7 +380,7 @@ __device__ __forceinline__ void dense_w_task(const MnistArgs& a, int T, int lane
       const auto dhr = buf_rsrc(a.dH, (unsigned)(b * 128 * 4));
       const f4 acc = gemm_tn_buf<true>(b, g, dhr, 0, 0, dhr, 128 * 4, n * 4, i == 0 ? 1.f : 0.f);
       if (g == 0) {
-        a.G[a.ob3 + n] = acc[0];
+        if (keep_g) a.G[a.ob3 + n] = acc[0];
         if (xdst != nullptr) xdst[a.ob3 + n] = acc[0];
         if (sgd) a.W[a.ob3 + n] = wold - lr * acc[0];
       }
@@ -406,12 +406,12 @@ __device__ __forceinline__ void dense_w_task(const MnistArgs& a, int T, int lane
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int e = a.ow4 + (T3 * 16 + 4 * g + r) * 10 + i;
-          a.G[e] = acc[r];
+          if (keep_g) a.G[e] = acc[r];
           if (xdst != nullptr) xdst[e] = acc[r];
           if (sgd) a.W[e] = wold[r] - lr * acc[r];
         }
       } else if (g == 0) {
-        a.G[a.ob4 + i] = acc[0];
+        if (keep_g) a.G[a.ob4 + i] = acc[0];
         if (xdst != nullptr) xdst[a.ob4 + i] = acc[0];
         if (sgd) a.W[a.ob4 + i] = wold[0] - lr * acc[0];
       }
@@ -1487,17 +1487,18 @@ __device__ __forceinline__ void finalize_x_body(const MnistArgs& a, int apply_sg
     xdst = a.xa.p.buf[a.xa.rank] + half;
   }
   const bool sgd_local = R == 1 && apply_sgd;  // single replica: SGD fused into the reduction
+  const bool keep_g = !(sgd_local && (a.variant & kMnistVariantNoG));
   // ---- this workgroup's gradient range ----
   if (j < kFxW3) {
     // dW3 rows 16 (j >> 1) .. +15, column tiles 4 (j & 1) .. +3: one task per wave of waves 0-3
-    if (wave < 4) dense_w_task(a, (j >> 1) * 8 + (j & 1) * 4 + wave, lane, sgd_local, lr, xdst);
+    if (wave < 4) dense_w_task(a, (j >> 1) * 8 + (j & 1) * 4 + wave, lane, sgd_local, lr, xdst, keep_g);
   } else if (j < kFxDense) {
     // db3 (tasks kD1TasksW3 - 8 ..) and dW4 (kD1TasksW3 ..): two tasks per workgroup on waves 0-1;
     // db4 (kD1TasksW3 + 8): wave 0 of the last one
     const int jj = j - kFxW3, t = 2 * jj + wave;
     if (jj < 8 ? wave < 2 : wave == 0)
       dense_w_task(a, jj < 8 ? (t < 8 ? kD1TasksW3 - 8 + t : kD1TasksW3 + t - 8) : kD1TasksW3 + 8, lane, sgd_local, lr,
-                   xdst);
+                   xdst, keep_g);
   } else if (j < kFxDense + kFxConv2) {
     // conv2 row quad qd (kernel rows 4qd .. 4qd+3; the last quad: the bias row), columns 32h ..
     // 32h+31: thread (column c = tid & 31, image group grp = tid >> 5) sums the quad's 4 rows (one
@@ -1531,7 +1532,7 @@ __device__ __forceinline__ void finalize_x_body(const MnistArgs& a, int apply_sg
       float s2 = 0.f;
 #pragma unroll
       for (int w = 0; w < 8; ++w) s2 += fx_red2[w][cc][rr];
-      a.G[e2] = s2;
+      if (keep_g) a.G[e2] = s2;
       if (xdst != nullptr) xdst[e2] = s2;
       if (sgd_local) a.W[e2] = wold - lr * s2;
     }
@@ -1562,7 +1563,7 @@ __device__ __forceinline__ void finalize_x_body(const MnistArgs& a, int apply_sg
       float s = 0.f;
 #pragma unroll
       for (int w = 0; w < 8; ++w) s += fx_red[w][c];
-      a.G[e1] = s;
+      if (keep_g) a.G[e1] = s;
       if (xdst != nullptr) xdst[e1] = s;
       if (sgd_local) a.W[e1] = wold - lr * s;
     }

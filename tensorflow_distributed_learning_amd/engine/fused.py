@@ -220,7 +220,7 @@ class FusedMnistTrainer:
         self._step_k = k
         plain = getattr(opt, "momentum", None) == 0 and type(opt).__name__ == "SGD"
         if self.R == 1 and plain:
-            st.finalize(True)
+            st.finalize(True, keep_grad=False)  # (nothing reads G on this path)
             return
         if self.R > 1 and plain and st.has_exchange:
             # fused backward: the finalize launch itself all-reduces over xGMI and applies SGD

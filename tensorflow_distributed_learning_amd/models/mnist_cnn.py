@@ -148,6 +148,7 @@ class FusedMnistTrainStep:
         # + loss + backward; TDL_MNIST_FUSED_BWD=0 keeps the separate k_conv_bwd launch)
         self._impl.set_fused_bwd(os.environ.get("TDL_MNIST_FUSED_BWD", "1") == "1")
         self.fused_bwd = bool(self._impl.fused_bwd())
+        self._impl.set_keep_grad(True)
         if (self.fused_bwd and self.R > 1 and os.environ.get("TDL_SHARE_GPU") == "1"
                 and "TDL_FX_GRID" not in os.environ):
             # replicas sharing ONE GPU: a replica's exchanging finalize workgroups spin until its
@@ -182,10 +183,14 @@ class FusedMnistTrainStep:
         """Conv backward into per-image partial slabs (reduced into G by finalize)."""
         self._impl.backward_conv()
 
-    def finalize(self, apply_sgd: bool, exchange: bool = False) -> None:
+    def finalize(self, apply_sgd: bool, exchange: bool = False, keep_grad: bool = True) -> None:
         """Partial-slab reductions + dense weight gradients into G (+ SGD).  ``exchange`` (fused
         backward + :meth:`set_exchange`): the same launch all-reduces the gradient across the
-        replicas over xGMI before the SGD update (each finalize workgroup exchanges its own range)."""
+        replicas over xGMI before the SGD update (each finalize workgroup exchanges its own range).
+        ``keep_grad=False`` (one replica, ``apply_sgd``): the SGD update is applied but G is not
+        written -- nothing reads it then, and its 900 KB of stores cost the finalize's kernel-end
+        write-back (K=20 bench +1.2 %, profiles/mnist_fx_no_grad_store_r5.txt)."""
+        self._impl.set_keep_grad(bool(keep_grad) or not apply_sgd or self.R > 1)
         self._impl.finalize(bool(apply_sgd), bool(exchange))
 
     def set_exchange(self, channel, twoshot: bool = False) -> None:

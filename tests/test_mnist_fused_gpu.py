@@ -122,6 +122,31 @@ def test_fused_sgd_update(cuda):
     assert torch.allclose(W, W0 - 0.01 * G, atol=1e-7, rtol=0)
 
 
+def test_fused_sgd_without_grad_store(cuda):
+    """keep_grad=False (the single-replica fit path): the same SGD update, bit for bit, and the
+    gradient slab G is left untouched."""
+    b = 64
+    X, Y, params, layout, W, G, idx, lr, step = _setup(cuda, b, 1)
+    W0 = W.clone()
+    step.forward_backward(0)
+    step.finalize(True)
+    W_keep, G_keep = W.clone(), G.clone()
+    W.copy_(W0)
+    G.fill_(123.0)
+    step.forward_backward(0)
+    step.finalize(True, keep_grad=False)
+    torch.cuda.synchronize()
+    assert torch.equal(W, W_keep)
+    assert bool((G == 123.0).all()), "keep_grad=False must not write G"
+    # the flag is per call: the next default finalize writes G again (slab padding stays as set)
+    W.copy_(W0)
+    G.zero_()
+    step.forward_backward(0)
+    step.finalize(True)
+    torch.cuda.synchronize()
+    assert torch.equal(G, G_keep)
+
+
 def test_fused_step_graph_capture(cuda):
     b = 64
     X, Y, params, layout, W, G, idx, lr, step = _setup(cuda, b, 1)
