@@ -351,6 +351,21 @@ __device__ __forceinline__ f4 gemm_tn_buf(int b, int g, __amdgpu_buffer_rsrc_t r
   return acc0 + acc1;
 }
 
+// 4 x 4 transpose within each quad of lanes (q = lane & 3), two xor-butterfly stages on DPP: on entry
+// lane q holds M[q][0..3], on exit M[0..3][q] (v[k] of lane q = entry v[q] of lane k).  The whole
+// wave must be active.
+__device__ __forceinline__ f4 quad_transpose(f4 v, int q) {
+  const bool a = (q & 2) != 0, b = (q & 1) != 0;
+  // xor 2: the off-diagonal 2 x 2 blocks change lanes
+  float r0 = dpp_xor2(a ? v[0] : v[2]), r1 = dpp_xor2(a ? v[1] : v[3]);
+  if (a) { v[0] = r0; v[1] = r1; } else { v[2] = r0; v[3] = r1; }
+  // xor 1: the off-diagonal elements of every 2 x 2 block
+  r0 = dpp_xor1(b ? v[0] : v[1]);
+  r1 = dpp_xor1(b ? v[2] : v[3]);
+  if (b) { v[0] = r0; v[2] = r1; } else { v[1] = r0; v[3] = r1; }
+  return v;
+}
+
 // One dense weight-gradient task T in [0, kDenseTasks) for the wave (optionally fused with plain
 // SGD of its outputs: nothing else in the launch reads W3 / W4 then).
 constexpr int kDenseTasks = kD1TasksW3 + 9;
@@ -363,18 +378,17 @@ __device__ __forceinline__ void dense_w_task(const MnistArgs& a, int T, int lane
     const int mt = T >> 3, nt = T & 7, n = nt * 16 + i;
     if (mt < 100) {
       const int kf = mt * 16 + i;
-      float wold[4];  // the SGD operands ride in the operand loads' round trip
-#pragma unroll
-      for (int r = 0; r < 4; ++r) wold[r] = sgd ? a.W[a.ow3 + (mt * 16 + 4 * g + r) * 128 + n] : 0.f;
-      const f4 acc = gemm_tn_buf(b, g, buf_rsrc(a.P2, (unsigned)(b * 1600 * 4)), 1600 * 4, kf * 4,
-                                 buf_rsrc(a.dH, (unsigned)(b * 128 * 4)), 128 * 4, n * 4);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int e = a.ow3 + (mt * 16 + 4 * g + r) * 128 + n;
-        if (keep_g) a.G[e] = acc[r];
-        if (xdst != nullptr) xdst[e] = acc[r];
-        if (sgd) a.W[e] = wold[r] - lr * acc[r];
-      }
+      // after the quad transpose lane (i, g) owns row 16 mt + 4 g + (i & 3), columns 16 nt + (i & 12)
+      // .. +3: the SGD operand is ONE 16-B load (in the operand loads' round trip) and G / W are ONE
+      // 16-B store each (was 4 scalar loads + 4 + 4 scalar stores per lane on the CU's
+      // vector-memory queue)
+      const int e4 = a.ow3 + (mt * 16 + 4 * g + (i & 3)) * 128 + nt * 16 + (i & 12);
+      const f4 wold = sgd ? ld4(a.W + e4) : zero4();
+      const f4 acc = quad_transpose(gemm_tn_buf(b, g, buf_rsrc(a.P2, (unsigned)(b * 1600 * 4)), 1600 * 4, kf * 4,
+                                                buf_rsrc(a.dH, (unsigned)(b * 128 * 4)), 128 * 4, n * 4), i & 3);
+      if (keep_g) st4(a.G + e4, acc);
+      if (xdst != nullptr) st4(xdst + e4, acc);
+      if (sgd) st4(a.W + e4, wold - lr * acc);
     } else {  // db3: A = e_0 (row 0 of the tile = column sums of dH)
       const float wold = sgd ? a.W[a.ob3 + n] : 0.f;
       const auto dhr = buf_rsrc(a.dH, (unsigned)(b * 128 * 4));
