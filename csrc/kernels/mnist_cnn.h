@@ -78,8 +78,8 @@ struct MnistArgs {
 //      (measured: the backward's end and the step unchanged at K=20, 1-4 % slower at K=1000 -- the
 //      waves' MFMA work is the same either way and the SIMD pairs stay busy; not adopted,
 //      profiles/mnist_stagger_ab_r5.txt)
-//   4  single replica with SGD fused into the finalize: the gradient slab G is not written (nothing
-//      reads it on that path; 900 KB fewer dirty lines for the finalize's kernel-end write-back)
+//   4  SGD fused into the finalize (one replica, or the xGMI exchange): the gradient slab G is not
+//      written (nothing reads it on those paths; 900 KB fewer dirty lines for the kernel-end write-back)
 constexpr int kMnistVariantPrio = 1;
 constexpr int kMnistVariantStagger = 2;
 constexpr int kMnistVariantNoG = 4;

@@ -1501,7 +1501,8 @@ __device__ __forceinline__ void finalize_x_body(const MnistArgs& a, int apply_sg
     xdst = a.xa.p.buf[a.xa.rank] + half;
   }
   const bool sgd_local = R == 1 && apply_sgd;  // single replica: SGD fused into the reduction
-  const bool keep_g = !(sgd_local && (a.variant & kMnistVariantNoG));
+  // (the exchange path applies SGD from the peers' published ranges: G is not read there either)
+  const bool keep_g = !((sgd_local || xchg) && (a.variant & kMnistVariantNoG));
   // ---- this workgroup's gradient range ----
   if (j < kFxW3) {
     // dW3 rows 16 (j >> 1) .. +15, column tiles 4 (j & 1) .. +3: one task per wave of waves 0-3

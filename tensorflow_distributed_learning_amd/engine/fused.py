@@ -224,7 +224,7 @@ class FusedMnistTrainer:
             return
         if self.R > 1 and plain and st.has_exchange:
             # fused backward: the finalize launch itself all-reduces over xGMI and applies SGD
-            st.finalize(True, exchange=True)
+            st.finalize(True, exchange=True, keep_grad=False)  # (G is not read on this path)
             return
         st.finalize(False)
         if self.R > 1 and plain and self.comm.all_reduce_sgd(self.G, self.W, opt.lr_dev):

@@ -187,10 +187,10 @@ class FusedMnistTrainStep:
         """Partial-slab reductions + dense weight gradients into G (+ SGD).  ``exchange`` (fused
         backward + :meth:`set_exchange`): the same launch all-reduces the gradient across the
         replicas over xGMI before the SGD update (each finalize workgroup exchanges its own range).
-        ``keep_grad=False`` (one replica, ``apply_sgd``): the SGD update is applied but G is not
-        written -- nothing reads it then, and its 900 KB of stores cost the finalize's kernel-end
-        write-back (K=20 bench +1.2 %, profiles/mnist_fx_no_grad_store_r5.txt)."""
-        self._impl.set_keep_grad(bool(keep_grad) or not apply_sgd or self.R > 1)
+        ``keep_grad=False`` (``apply_sgd`` with one replica, or with the exchange): the SGD update is
+        applied but G is not written -- nothing reads it then, and its 900 KB of stores cost the
+        finalize's kernel-end write-back (K=20 bench +1.2 %, profiles/mnist_fx_no_grad_store_r5.txt)."""
+        self._impl.set_keep_grad(bool(keep_grad) or not apply_sgd or (self.R > 1 and not exchange))
         self._impl.finalize(bool(apply_sgd), bool(exchange))
 
     def set_exchange(self, channel, twoshot: bool = False) -> None:

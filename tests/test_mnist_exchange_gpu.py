@@ -71,7 +71,8 @@ def step(k, graph=None):
     assert st._impl.error(False) == 0, "fused kernel hand-off timed out"
     dist.barrier()
     if graph is None:
-        st.finalize(True, exchange=True)
+        # (k = 1: the trainer's form -- the exchange applies SGD without writing G)
+        st.finalize(True, exchange=True, keep_grad=(k != 1))
     else:
         graph[1].replay()
     torch.cuda.synchronize(dev)
@@ -109,7 +110,7 @@ g_fwd, g_fin = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
 with torch.cuda.graph(g_fwd, stream=s):
     st.forward_backward(2 * b)
 with torch.cuda.graph(g_fin, stream=s):
-    st.finalize(True, exchange=True)
+    st.finalize(True, exchange=True, keep_grad=False)
 torch.cuda.synchronize(dev)
 for _ in range(2):
     step(2, (g_fwd, g_fin))
