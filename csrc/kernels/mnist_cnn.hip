@@ -388,7 +388,10 @@ __device__ __forceinline__ void dense_w_task(const MnistArgs& a, int T, int lane
                                                 buf_rsrc(a.dH, (unsigned)(b * 128 * 4)), 128 * 4, n * 4), i & 3);
       if (keep_g) st4(a.G + e4, acc);
       if (xdst != nullptr) st4(xdst + e4, acc);
-      if (sgd) st4(a.W + e4, wold - lr * acc);
+      // W as a 16-B WRITE-THROUGH store: 820 KB fewer dirty L2 lines for the finalize's kernel-end
+      // write-back, in front of the next fused kernel (profiles/mnist_fx_w3_writethrough_r5.txt; the
+      // 4-B write-through form of the earlier layout lost: profiles/mnist_fx_writethrough_rejected_r5.txt)
+      if (sgd) st4_sc1(buf_rsrc(a.W, (unsigned)a.nslab * 4u), e4 * 4, wold - lr * acc);
     } else {  // db3: A = e_0 (row 0 of the tile = column sums of dH)
       const float wold = sgd ? a.W[a.ob3 + n] : 0.f;
       const auto dhr = buf_rsrc(a.dH, (unsigned)(b * 128 * 4));
