@@ -1596,6 +1596,9 @@ __device__ __forceinline__ void finalize_x_body(const MnistArgs& a, int apply_sg
     int lo, cnt, nseg, stride;
     fx_range(a, j, lo, cnt, nseg, stride);
     const int n4 = cnt >> 2;  // (every segment starts 16-B aligned: slab offsets are multiples of 4)
+    // updated weights as 16-B write-through stores (no dirty W lines for the kernel-end write-back,
+    // as in the single-replica dW3 tasks: profiles/mnist_fx_w3_writethrough_r5.txt)
+    const auto wr = buf_rsrc(a.W, (unsigned)a.nslab * 4u);
     const int tot = n4 * nseg;
     auto off_of = [&](int t) { return (int64_t)lo + (int64_t)(t / n4) * stride + 4 * (t % n4); };
     if (a.xtwo) {
@@ -1623,7 +1626,7 @@ __device__ __forceinline__ void finalize_x_body(const MnistArgs& a, int apply_sg
       }
       for (int t = tid; t < tot; t += 512) {
         const int64_t off = off_of(t);
-        st4(a.W + off, ld4(a.xa.p.buf[(t * R) / tot] + res + off));
+        st4_sc1(wr, (int)off * 4, ld4(a.xa.p.buf[(t * R) / tot] + res + off));
       }
     } else {
       for (int t = tid; t < tot; t += 512) {
@@ -1634,7 +1637,7 @@ __device__ __forceinline__ void finalize_x_body(const MnistArgs& a, int apply_sg
         f4 acc = v[0];
 #pragma unroll
         for (int r = 1; r < R; ++r) acc += v[r];
-        st4(a.W + off, ld4(a.W + off) - lr * acc);
+        st4_sc1(wr, (int)off * 4, ld4(a.W + off) - lr * acc);
       }
     }
     // scalar tail of a range (db4: 10 floats), summed by every rank itself in rank order
