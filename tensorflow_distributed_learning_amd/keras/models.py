@@ -35,6 +35,25 @@ _CONV_BN_STATS = os.environ.get("TDL_CONV_BN_STATS", "1") == "1"
 _FUSE_CPU = [False]  # tests: apply the training-graph fusion plan to CPU tensors too
 
 
+def _map_outputs(fn, y):
+    """Apply fn to every tensor of a model output structure (tensor, list / tuple, dict)."""
+    if isinstance(y, dict):
+        return {k: _map_outputs(fn, v) for k, v in y.items()}
+    if isinstance(y, (list, tuple)):
+        return type(y)(_map_outputs(fn, v) for v in y)
+    return fn(y)
+
+
+def _concat_outputs(batches):
+    """Concatenate per-batch output structures along the batch axis into numpy arrays."""
+    first = batches[0]
+    if isinstance(first, dict):
+        return {k: _concat_outputs([b[k] for b in batches]) for k in first}
+    if isinstance(first, (list, tuple)):
+        return [_concat_outputs([b[i] for b in batches]) for i in range(len(first))]
+    return torch.cat(batches).numpy()
+
+
 class Model(Layer):
     def __init__(self, inputs=None, outputs=None, name: Optional[str] = None, **kw):
         from ..parallel.strategy import get_strategy, has_strategy
@@ -638,10 +657,11 @@ class Model(Layer):
             if steps is not None and k >= steps:
                 break
             xb = b[0] if isinstance(b, (tuple, list)) else b
-            outs.append(self(xb.to(dev), training=False).cpu())
+            outs.append(_map_outputs(lambda t: t.cpu(), self(xb.to(dev), training=False)))
         if self._trainer is not None and self._trainer.kind == "generic":
             self._trainer._make_leaves()
-        return torch.cat(outs).numpy()
+        # (a multi-output model returns one array per output, in its output structure, as Keras does)
+        return _concat_outputs(outs)
 
     def predict_on_batch(self, x):
         return self.predict(x, batch_size=len(x))

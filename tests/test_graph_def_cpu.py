@@ -300,3 +300,24 @@ def test_resnet50_maps_to_a_graph():
     ops = [n["op"] for n in nodes.values()]
     assert ops.count("Conv2D") == 53 and ops.count("FusedBatchNormV3") == 53 and ops.count("AddV2") == 16
     assert ops.count("VarHandleOp") == len(m.weights) and spec.outputs == ["StatefulPartitionedCall:0"]
+
+
+def test_two_output_model_uses_identity_n(tmp_path):
+    keras.backend.clear_session()
+    keras.utils.set_random_seed(2)
+    inp = L.Input(shape=(6,), name="x")
+    h = L.Dense(5, activation="tanh")(inp)
+    a = L.Dense(3, name="head_a")(h)
+    b = L.Dense(2, activation="sigmoid", name="head_b")(h)
+    m = keras.Model(inp, [a, b])
+    x = torch.randn(4, 6)
+    ra, rb = [r.numpy() if hasattr(r, "numpy") else np.asarray(r) for r in m.predict(x, verbose=0)]
+    p = str(tmp_path / "two")
+    m.save(p)
+    outs, nodes, mg, _ = _serve(p, x.numpy())
+    sig = mg["signature_def"]["serving_default"]["outputs"]
+    assert sig["head_a"]["name"] == "StatefulPartitionedCall:0" and sig["head_b"]["name"] == "StatefulPartitionedCall:1"
+    assert nodes["StatefulPartitionedCall"]["op"] == "IdentityN"
+    got = dict(zip(sig, outs))
+    np.testing.assert_allclose(got["head_a"], ra, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(got["head_b"], rb, rtol=1e-5, atol=1e-6)
