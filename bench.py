@@ -58,6 +58,10 @@ def main():
     ap.add_argument("--comm", choices=["auto", "nccl", "ring"], default="auto",
                     help="CollectiveCommunication: AUTO (xGMI kernel + RCCL), NCCL (RCCL only), RING (TCP)")
     ap.add_argument("--take", type=int, default=0, help="diagnostics: train on the first N images only")
+    ap.add_argument("--mode", choices=["process", "single", "threads"], default="process",
+                    help="N > 1 without a launcher: one replica process per GPU (default, the scaling mode), "
+                         "or ONE process driving all N devices (TF's single-process MirroredStrategy: one host "
+                         "thread launching every device's captured graph; 'threads' is an alias)")
     args = ap.parse_args()
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
@@ -76,8 +80,10 @@ def main():
     # exactly N devices: on an 8-GPU node `--gpus 1` is ONE replica, `--gpus N` without a launcher
     # spawns the other N-1 replica processes here (no GPU has been touched yet)
     devices = [f"/gpu:{i}" for i in range(args.gpus)]
-    # (spawn=True: one replica PROCESS per GPU -- the scaling mode -- when started without a launcher)
-    strategy = tdl.distribute.MirroredStrategy(devices=devices, communication=args.comm.upper(), spawn=True)
+    # (spawn=True: one replica PROCESS per GPU -- the scaling mode -- when started without a launcher;
+    # --mode single: one process for every device, engine/mirrored.py)
+    single = args.mode in ("single", "threads") and args.gpus > 1 and not world
+    strategy = tdl.distribute.MirroredStrategy(devices=devices, communication=args.comm.upper(), spawn=not single)
     R = strategy.num_replicas_in_sync
     if R != args.gpus:
         raise SystemExit(f"bench.py: strategy has {R} replicas, expected {args.gpus}")
@@ -113,6 +119,12 @@ def main():
     comm = strategy.extended.communicator
     dev = strategy.extended.device
 
+    def sync_all():
+        if single:
+            trainer.finish()  # every local device
+        else:
+            torch.cuda.synchronize(dev)
+
     trainer.warm_graphs(K)
     if W:
         trainer.warm_graphs(W)
@@ -120,9 +132,9 @@ def main():
     # input prefetch (depth one execution, as tf.data prefetch): the first timed execution's batch
     # indices are assembled and uploaded before the clock starts; later ones overlap the GPU
     trainer.prefetch(handler, K)
-    torch.cuda.synchronize(dev)
+    sync_all()
     comm.barrier()
-    torch.cuda.synchronize(dev)
+    sync_all()
     # (TDL_BENCH_EVENTS=1: device-side events around the steps, for the stderr diagnostics line)
     events = os.environ.get("TDL_BENCH_EVENTS", "0") == "1"
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -133,24 +145,29 @@ def main():
     if events:
         ev1.record()
     t_host = time.perf_counter() - t0
-    torch.cuda.synchronize(dev)
+    sync_all()
     dt = time.perf_counter() - t0
     # closing bracket: every rank's clock stopped at its own device sync; the barrier then only
     # joins the ranks (its latency is measurement overhead, not training work).  The MAX over ranks
     # below is the span from the earliest start to the last rank's finish (the in-graph all-reduce
     # of every step already keeps the ranks in lock step).
     comm.barrier()
-    torch.cuda.synchronize(dev)
+    sync_all()
     print(f"timed region: wall {dt * 1e3:.3f} ms = host launch {t_host * 1e3:.3f} ms + device drain "
           f"{(dt - t_host) * 1e3:.3f} ms" + (f"; device events {ev0.elapsed_time(ev1):.3f} ms" if events else ""),
           file=sys.stderr)
     if done != K:
         raise SystemExit(f"bench: ran {done} steps instead of {K}")
-    t = torch.tensor([dt], dtype=torch.float64, device=dev if comm.name == "rccl" else "cpu")
-    per_rank = [float(v) for v in comm.all_gather(t).reshape(-1).tolist()]
-    dt = max(per_rank)
-    logs = trainer.logs()  # also raises if an xGMI all-reduce timed out on this rank
-    identical = consistency.replicas_identical(comm, trainer.W)
+    if single:
+        per_rank = [dt]  # one process, one clock around every device's work
+        logs = trainer.logs()
+        identical = trainer.replicas_identical()
+    else:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev if comm.name == "rccl" else "cpu")
+        per_rank = [float(v) for v in comm.all_gather(t).reshape(-1).tolist()]
+        dt = max(per_rank)
+        logs = trainer.logs()  # also raises if an xGMI all-reduce timed out on this rank
+        identical = consistency.replicas_identical(comm, trainer.W)
     ips = K * B / dt
     ht = getattr(trainer, "_host_times", None)
     if ht:
@@ -176,13 +193,15 @@ def main():
             "config": {"model": "tf_dist_example.py MNIST CNN (Conv32-Pool-Conv64-Pool-Dense128-Dense10, 225,034 params)",
                        "global_batch": B, "seq_len": None, "image_shape": [28, 28, 1],
                        "parallelism": f"dp{R}", "engine": trainer.kind, "communicator": comm.name,
+                       "process_model": "single-process" if single else ("one process per GPU" if R > 1 else "single"),
                        # what actually ran: the communicator class (torch RCCL process group, the
                        # framework's own RCCL communicator, gloo + xGMI, local) and the HIP IPC mode
                        # every replica was started with (parallel/launch.py REPLICA_SHARED_ENV)
                        "communicator_impl": type(comm).__name__, "ipc_mode": ipc_mode(),
                        "allreduce": getattr(trainer, "allreduce_mode", None) or getattr(comm, "algorithm", comm.name),
-                       "kernels_per_step": 2 if getattr(trainer, "_steps", None) and all(
-                           getattr(st, "fused_bwd", False) for st in trainer._steps.values()) else None,
+                       "kernels_per_step": 2 if all(getattr(t, "_steps", None) and all(
+                           getattr(st, "fused_bwd", False) for st in t._steps.values())
+                           for t in getattr(trainer, "subs", [trainer])) else None,
                        "steps_per_execution": spe, "graph_captured": bool(trainer.capture),
                        "input_prefetch_executions": 1,
                        "allreduce_in_graph": bool(trainer.capture_comm and R > 1),

@@ -3,7 +3,29 @@
 
 using tdl_host::XgmiChannel;
 
+namespace {
+// Direct loads/stores from `device` into `peer`'s memory (the xGMI link between them).  One process
+// driving several GPUs (single-process MirroredStrategy) maps its replicas' exchange buffers by
+// plain pointers instead of IPC handles, so access must be enabled per ordered pair.  Same device:
+// nothing to do.  Returns false when the pair has no peer path.
+bool enable_peer_access(int64_t device, int64_t peer) {
+  if (device == peer) return true;
+  int can = 0;
+  tdl_host::hip_ok(hipDeviceCanAccessPeer(&can, (int)device, (int)peer), "hipDeviceCanAccessPeer");
+  if (!can) return false;
+  c10::hip::HIPGuard guard((c10::DeviceIndex)device);
+  const hipError_t e = hipDeviceEnablePeerAccess((int)peer, 0);
+  if (e == hipErrorPeerAccessAlreadyEnabled) {
+    (void)hipGetLastError();
+    return true;
+  }
+  tdl_host::hip_ok(e, "hipDeviceEnablePeerAccess");
+  return true;
+}
+}  // namespace
+
 void register_comm(pybind11::module& m) {
+  m.def("enable_peer_access", &enable_peer_access, pybind11::arg("device"), pybind11::arg("peer"));
   pybind11::class_<XgmiChannel>(m, "XgmiChannel")
       .def(pybind11::init<int64_t, int64_t, int64_t, int64_t, double, int64_t, int64_t>(), pybind11::arg("rank"),
            pybind11::arg("world"), pybind11::arg("numel"), pybind11::arg("device"), pybind11::arg("timeout_s") = 60.0,

@@ -56,6 +56,7 @@ struct RcclApi {
   Result (*ReduceScatter)(const void*, void*, size_t, int, int, Comm, hipStream_t);
   Result (*GroupStart)();
   Result (*GroupEnd)();
+  Result (*CommInitAll)(Comm*, int, const int*);
 
   static const RcclApi& get() {
     static RcclApi api;
@@ -89,6 +90,7 @@ struct RcclApi {
     ReduceScatter = reinterpret_cast<decltype(ReduceScatter)>(sym(h, "ncclReduceScatter"));
     GroupStart = reinterpret_cast<decltype(GroupStart)>(sym(h, "ncclGroupStart"));
     GroupEnd = reinterpret_cast<decltype(GroupEnd)>(sym(h, "ncclGroupEnd"));
+    CommInitAll = reinterpret_cast<decltype(CommInitAll)>(sym(h, "ncclCommInitAll"));
   }
 };
 
@@ -171,6 +173,89 @@ void RcclComm::abort() {
   if (locked) mu_.unlock();
 }
 
+// ------------------------------------------------------------------ RcclClique
+RcclClique::RcclClique(const std::vector<int>& devices) : api_(RcclApi::get()), devices_(devices) {
+  if (devices.empty()) throw std::invalid_argument("rccl: a clique needs at least one device");
+  for (size_t i = 0; i < devices.size(); ++i)
+    for (size_t j = 0; j < i; ++j)
+      if (devices[i] == devices[j])
+        throw std::invalid_argument("rccl: a clique needs distinct devices (RCCL refuses two ranks on one GPU)");
+  comms_.assign(devices.size(), nullptr);
+  check(api_.CommInitAll(comms_.data(), (int)devices.size(), devices.data()), "ncclCommInitAll");
+}
+
+RcclClique::~RcclClique() {
+  std::lock_guard<std::timed_mutex> lk(mu_);
+  if (!aborted_.load(std::memory_order_acquire))
+    for (void* c : comms_)
+      if (c != nullptr) (void)api_.CommDestroy(c);
+  comms_.clear();
+}
+
+void RcclClique::check(int r, const char* what) const {
+  if (r != 0 && r != 7) throw std::runtime_error(std::string("rccl: ") + what + " failed: " + api_.GetErrorString(r));
+}
+
+void RcclClique::all_reduce(const std::vector<void*>& bufs, size_t count, int dtype, int op,
+                            const std::vector<hipStream_t>& streams) {
+  if (bufs.size() != comms_.size() || streams.size() != comms_.size())
+    throw std::invalid_argument("rccl: one buffer and one stream per clique device expected");
+  std::lock_guard<std::timed_mutex> lk(mu_);
+  if (aborted_.load(std::memory_order_acquire)) throw std::runtime_error("rccl: clique was aborted");
+  check(api_.GroupStart(), "ncclGroupStart");
+  Result first = 0;
+  for (size_t i = 0; i < comms_.size(); ++i) {
+    const Result r = api_.AllReduce(bufs[i], bufs[i], count, nccl_dtype(dtype), nccl_op(op), comms_[i], streams[i]);
+    if (first == 0 && r != 0 && r != 7) first = r;
+  }
+  const Result e = api_.GroupEnd();  // always closes the group, also after a failed enqueue
+  check(first, "ncclAllReduce (grouped)");
+  check(e, "ncclGroupEnd");
+}
+
+void RcclClique::broadcast(const std::vector<void*>& bufs, size_t count, int dtype, int root,
+                           const std::vector<hipStream_t>& streams) {
+  if (bufs.size() != comms_.size() || streams.size() != comms_.size())
+    throw std::invalid_argument("rccl: one buffer and one stream per clique device expected");
+  std::lock_guard<std::timed_mutex> lk(mu_);
+  if (aborted_.load(std::memory_order_acquire)) throw std::runtime_error("rccl: clique was aborted");
+  check(api_.GroupStart(), "ncclGroupStart");
+  Result first = 0;
+  for (size_t i = 0; i < comms_.size(); ++i) {
+    const Result r = api_.Broadcast(bufs[i], bufs[i], count, nccl_dtype(dtype), root, comms_[i], streams[i]);
+    if (first == 0 && r != 0 && r != 7) first = r;
+  }
+  const Result e = api_.GroupEnd();
+  check(first, "ncclBroadcast (grouped)");
+  check(e, "ncclGroupEnd");
+}
+
+int RcclClique::async_error() {
+  std::lock_guard<std::timed_mutex> lk(mu_);
+  if (aborted_.load(std::memory_order_acquire)) return -1;
+  for (void* c : comms_) {
+    Result e = 0;
+    const Result r = api_.CommGetAsyncError(c, &e);
+    if (r != 0) return r;
+    if (e != 0 && e != 7) return e;
+  }
+  return 0;
+}
+
+std::string RcclClique::error_string(int code) const {
+  if (code < 0) return "clique aborted";
+  return api_.GetErrorString(code);
+}
+
+void RcclClique::abort() {
+  const bool locked = mu_.try_lock_for(std::chrono::seconds(5));
+  bool expected = false;
+  if (aborted_.compare_exchange_strong(expected, true, std::memory_order_acq_rel))
+    for (void* c : comms_)
+      if (c != nullptr) (void)api_.CommAbort(c);
+  if (locked) mu_.unlock();
+}
+
 }  // namespace tdl_host
 
 namespace {
@@ -245,4 +330,47 @@ void register_rccl(pybind11::module& m) {
       .def("error_string", &RcclComm::error_string)
       .def("abort", &RcclComm::abort, pybind11::call_guard<pybind11::gil_scoped_release>())
       .def_property_readonly("aborted", &RcclComm::aborted);
+
+  using tdl_host::RcclClique;
+  // per-device buffers + streams of one grouped call: tensor i must live on devices()[i]; its part
+  // is enqueued on that device's CURRENT stream (the engine's per-device replica stream)
+  auto gather = [](RcclClique& c, const std::vector<at::Tensor>& ts, std::vector<void*>& bufs,
+                   std::vector<hipStream_t>& streams) {
+    TORCH_CHECK((int)ts.size() == c.size(), "rccl clique: one tensor per device expected");
+    for (size_t i = 0; i < ts.size(); ++i) {
+      const at::Tensor& t = ts[i];
+      TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "rccl clique: tensors must be contiguous GPU tensors");
+      TORCH_CHECK(t.get_device() == c.devices()[i], "rccl clique: tensor ", i, " is on device ", t.get_device(),
+                  ", expected ", c.devices()[i]);
+      TORCH_CHECK(t.numel() == ts[0].numel() && t.scalar_type() == ts[0].scalar_type(),
+                  "rccl clique: tensors differ in size or dtype");
+      bufs.push_back(t.data_ptr());
+      streams.push_back(c10::hip::getCurrentHIPStream((c10::DeviceIndex)c.devices()[i]).stream());
+    }
+  };
+  pybind11::class_<RcclClique>(m, "RcclClique")
+      .def(pybind11::init<const std::vector<int>&>(), pybind11::arg("devices"),
+           pybind11::call_guard<pybind11::gil_scoped_release>())
+      .def_property_readonly("size", &RcclClique::size)
+      .def_property_readonly("devices", &RcclClique::devices)
+      .def("all_reduce",
+           [gather](RcclClique& c, const std::vector<at::Tensor>& ts, int op) {
+             std::vector<void*> bufs;
+             std::vector<hipStream_t> streams;
+             gather(c, ts, bufs, streams);
+             c.all_reduce(bufs, ts[0].numel(), dtype_code(ts[0]), op, streams);
+           },
+           pybind11::arg("tensors"), pybind11::arg("op") = 0)
+      .def("broadcast",
+           [gather](RcclClique& c, const std::vector<at::Tensor>& ts, int root) {
+             std::vector<void*> bufs;
+             std::vector<hipStream_t> streams;
+             gather(c, ts, bufs, streams);
+             c.broadcast(bufs, ts[0].numel(), dtype_code(ts[0]), root, streams);
+           },
+           pybind11::arg("tensors"), pybind11::arg("root") = 0)
+      .def("async_error", &RcclClique::async_error)
+      .def("error_string", &RcclClique::error_string)
+      .def("abort", &RcclClique::abort, pybind11::call_guard<pybind11::gil_scoped_release>())
+      .def_property_readonly("aborted", &RcclClique::aborted);
 }

@@ -18,6 +18,7 @@
 #include <atomic>
 #include <mutex>
 #include <string>
+#include <vector>
 
 namespace tdl_host {
 
@@ -61,6 +62,39 @@ class RcclComm {
   // has freed.  abort() waits for the lock only a bounded time: an enqueue that is itself stuck
   // inside RCCL (e.g. connection setup towards a dead peer) is exactly what ncclCommAbort exists to
   // unblock, so after the wait it aborts regardless.
+  std::timed_mutex mu_;
+  std::atomic<bool> aborted_{false};
+};
+
+// One process, G devices (single-process MirroredStrategy, README.md:15-17 "NcclAllReduce" between
+// the GPUs of one machine): ncclCommInitAll creates one communicator per device in one call, and
+// every collective is issued for all G devices at once inside ncclGroupStart/End (RCCL requires
+// the G per-device calls of one process to be grouped, or the first blocks waiting for the others).
+// Each device's part is enqueued on the stream passed for that device.
+class RcclClique {
+ public:
+  explicit RcclClique(const std::vector<int>& devices);
+  ~RcclClique();
+
+  int size() const { return (int)comms_.size(); }
+  const std::vector<int>& devices() const { return devices_; }
+
+  // bufs[i] lives on devices()[i]; in place; every buffer has `count` elements
+  void all_reduce(const std::vector<void*>& bufs, size_t count, int dtype, int op,
+                  const std::vector<hipStream_t>& streams);
+  void broadcast(const std::vector<void*>& bufs, size_t count, int dtype, int root,
+                 const std::vector<hipStream_t>& streams);
+  // first failing communicator's RCCL error code, 0 if every one is fine
+  int async_error();
+  std::string error_string(int code) const;
+  void abort();
+  bool aborted() const { return aborted_.load(std::memory_order_acquire); }
+
+ private:
+  void check(int r, const char* what) const;
+  const RcclApi& api_;
+  std::vector<void*> comms_;
+  std::vector<int> devices_;
   std::timed_mutex mu_;
   std::atomic<bool> aborted_{false};
 };

@@ -16,10 +16,6 @@ A `tf`-compatible namespace for unmodified TF scripts: ``from tensorflow_distrib
 """
 __version__ = "0.1.0"
 
-from .utils import hipsync as _hipsync
-
-_hipsync.configure()  # TDL_HIP_SCHEDULE (before any device context exists)
-
 from . import cluster, data, keras, ops  # noqa: F401
 from . import parallel as distribute  # noqa: F401
 from . import parallel  # noqa: F401

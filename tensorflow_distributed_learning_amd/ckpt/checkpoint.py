@@ -181,10 +181,11 @@ def save_model(model, path: str, overwrite: bool = True, include_optimizer: bool
         if model_tensors_are_float32(tensors, model):
             try:
                 graph = GD.build_graph(model, SMP.GRAPH_PRODUCER)
-            except GD.UnsupportedLayer as e:
+            except Exception as e:  # noqa: BLE001 - the graph is best effort; variables/ is written
                 import warnings
 
-                warnings.warn(f"model.save: saved_model.pb without a TF graph ({e})")
+                why = str(e) if isinstance(e, GD.UnsupportedLayer) else f"{type(e).__name__}: {e}"
+                warnings.warn(f"model.save: saved_model.pb without a TF graph ({why})")
         with open(os.path.join(path, "saved_model.pb"), "wb") as f:
             f.write(SMP.encode_saved_model(*spec, graph=graph))
     remove_temp_dirpath(path, strategy) if path != real else None

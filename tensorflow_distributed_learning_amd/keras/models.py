@@ -337,7 +337,19 @@ class Model(Layer):
         if self.loss is None:
             raise RuntimeError("compile() needs a loss to train")
         self._ensure_slabs()
-        if self._trainer is None:
+        t = self._trainer
+        if getattr(self._get_strategy(), "_local_group", None) is not None:
+            if self._outer_local_group() is not None:
+                # single-process multi-device MirroredStrategy, the user's thread: ONE training loop
+                # over every local replica (engine/mirrored.py)
+                if t is None or not getattr(t, "is_group", False):
+                    from ..engine import mirrored
+
+                    self._trainer = t = mirrored.make_group_trainer(self)
+                return t
+            if getattr(t, "is_group", False):  # inside a replica region: this replica's own engine
+                return t.replica_trainer(self)
+        if t is None:
             reason = fused.eligible(self)
             self._trainer = fused.FusedMnistTrainer(self) if reason is None else GenericTrainer(self)
             self._fused_reason = reason
@@ -443,8 +455,8 @@ class Model(Layer):
                   class_weight=class_weight, sample_weight=sample_weight, initial_epoch=initial_epoch,
                   steps_per_epoch=steps_per_epoch, validation_steps=validation_steps,
                   validation_batch_size=validation_batch_size, validation_freq=validation_freq)
-        if self._outer_local_group() is not None:
-            return self._local_run("fit", kw)
+        # (single-process multi-device MirroredStrategy: the same ONE loop; its trainer drives every
+        # local replica, engine/mirrored.py)
         return self._fit_impl(**kw)
 
     def _fit_impl(self, x=None, y=None, batch_size=None, epochs=1, verbose="auto", callbacks=None,
@@ -460,17 +472,28 @@ class Model(Layer):
         ds = self._adapt(x, y, batch_size, shuffle, sample_weight)
         self._peek_build(ds)
         trainer = self._get_trainer()
+        group = getattr(trainer, "is_group", False)
+        if group:
+            trainer.broadcast_from_primary()  # weights / optimizer state set since the last fit
         handler = trainer.prepare(ds) if hasattr(trainer, "prepare") else None
         if handler is None:
             if trainer.kind == "fused":
                 # pipeline not lowerable to the device: generic engine (host data path)
-                from ..engine.trainer import GenericTrainer
+                if group:
+                    from ..engine.mirrored import ThreadedGroupTrainer, _models_and_group
 
-                self._trainer = trainer = GenericTrainer(self)
+                    self._trainer = trainer = ThreadedGroupTrainer(self, *_models_and_group(self))
+                else:
+                    from ..engine.trainer import GenericTrainer
+
+                    self._trainer = trainer = GenericTrainer(self)
                 self._fused_reason = "input pipeline is not device-resident"
-            from ..engine.trainer import HostDataHandler
+            if hasattr(trainer, "host_handler"):
+                handler = trainer.host_handler(ds)
+            else:
+                from ..engine.trainer import HostDataHandler
 
-            handler = HostDataHandler(ds, strategy)
+                handler = HostDataHandler(ds, strategy)
         if verbose == "auto":
             verbose = 1
         steps = steps_per_epoch
@@ -483,6 +506,8 @@ class Model(Layer):
         self.stop_training = False
         self._initial_epoch_override = None
         cb_list.on_train_begin()
+        if group:
+            trainer.broadcast_from_primary()  # e.g. BackupAndRestore restored replica 0
         if self._initial_epoch_override is not None:
             initial_epoch = max(initial_epoch, self._initial_epoch_override)
         want_batch = cb_list.wants_batch_logs or (verbose == 1 and sys.stdout.isatty())
@@ -560,6 +585,9 @@ class Model(Layer):
         custom all-reduce path (parallel/consistency.py)."""
         from ..parallel import consistency
 
+        if hasattr(trainer, "check_replicas"):  # one process, G replicas: compared in-process
+            trainer.check_replicas()
+            return
         comm = self._get_strategy().extended.communicator
         if comm.world_size == 1 or self._W is None:
             return
@@ -573,8 +601,34 @@ class Model(Layer):
         args = dict(x=x, y=y, batch_size=batch_size, verbose=verbose, sample_weight=sample_weight, steps=steps,
                     callbacks=callbacks, return_dict=return_dict, _internal=_internal)
         if self._outer_local_group() is not None:
+            tr = self._trainer
+            if (getattr(tr, "is_group", False) and tr.kind == "fused" and sample_weight is None and
+                    os.environ.get("TDL_FUSED_EVAL", "1") == "1"):
+                # every replica's slice on its own device from this thread (engine/mirrored.py)
+                ds = self._adapt(x, y, batch_size, False, None)
+                out = tr.evaluate(ds, steps)
+                if out is not None:
+                    return self._eval_result(out, verbose, return_dict, _internal)
             return self._local_run("evaluate", args)
         return self._evaluate_impl(**args)
+
+    def _eval_result(self, out, verbose, return_dict, _internal):
+        if verbose and verbose != "auto" and self._is_chief() and not _internal:
+            from ..utils.progbar import format_logs
+
+            print(format_logs(out))
+        if return_dict:
+            return out
+        vals = [out[k] for k in ["loss"] + [m.name for m in self.compiled_metrics]]
+        return vals if len(vals) > 1 else vals[0]
+
+    def _replica_engine(self):
+        """This replica's own engine (the group trainer's replica-0 engine for the user's model of a
+        single-process multi-device MirroredStrategy), or None."""
+        t = self._trainer
+        if getattr(t, "is_group", False):
+            return t.replica_trainer(self)
+        return t
 
     def _evaluate_impl(self, x=None, y=None, batch_size=None, verbose="auto", sample_weight=None, steps=None,
                        callbacks=None, return_dict=False, _internal=False):
@@ -588,15 +642,9 @@ class Model(Layer):
             tr = self._get_trainer()
             out = tr.evaluate(ds, steps) if tr.kind == "fused" else None
             if out is not None:  # forward-only pass on the MI355X kernels (engine/fused.py)
-                if verbose and verbose != "auto" and self._is_chief() and not _internal:
-                    from ..utils.progbar import format_logs
-
-                    print(format_logs(out))
-                if return_dict:
-                    return out
-                vals = [out[k] for k in ["loss"] + [m.name for m in self.compiled_metrics]]
-                return vals if len(vals) > 1 else vals[0]
-        prev = self._trainer
+                return self._eval_result(out, verbose, return_dict, _internal)
+        keep = self._trainer
+        prev = self._replica_engine()
         self._ensure_slabs()
         ev = GenericTrainer.__new__(GenericTrainer)
         ev.model, ev.strategy = self, self._get_strategy()
@@ -614,24 +662,17 @@ class Model(Layer):
         h.new_iterator()
         ev.run_test(h, steps)
         out = ev.logs()
-        self._trainer = None if prev is None else prev
+        self._trainer = keep
         if prev is not None and prev.kind == "generic":
             prev._make_leaves()
         if saved is not None:
             prev.metrics_dev.copy_(saved)
-        if verbose and verbose != "auto" and self._is_chief() and not _internal:
-            from ..utils.progbar import format_logs
-
-            print(format_logs(out))
-        if return_dict:
-            return out
-        vals = [out[k] for k in ["loss"] + [m.name for m in self.compiled_metrics]]
-        return vals if len(vals) > 1 else vals[0]
+        return self._eval_result(out, verbose, return_dict, _internal)
 
     def predict(self, x, batch_size=None, verbose="auto", steps=None, callbacks=None, **kw):
         args = dict(x=x, batch_size=batch_size, verbose=verbose, steps=steps, callbacks=callbacks)
-        if self._outer_local_group() is not None:
-            return self._local_run("predict", args)
+        # (single-process multi-device MirroredStrategy too: inference is replica-independent, so
+        # replica 0 predicts every sample on its own device)
         return self._predict_impl(**args)
 
     @torch.no_grad()
@@ -658,8 +699,9 @@ class Model(Layer):
                 break
             xb = b[0] if isinstance(b, (tuple, list)) else b
             outs.append(_map_outputs(lambda t: t.cpu(), self(xb.to(dev), training=False)))
-        if self._trainer is not None and self._trainer.kind == "generic":
-            self._trainer._make_leaves()
+        rt = self._replica_engine()
+        if rt is not None and rt.kind == "generic":
+            rt._make_leaves()
         # (a multi-output model returns one array per output, in its output structure, as Keras does)
         return _concat_outputs(outs)
 

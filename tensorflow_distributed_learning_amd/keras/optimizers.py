@@ -127,8 +127,42 @@ class Optimizer:
         raise NotImplementedError
 
     def apply_gradients(self, grads_and_vars):
-        """Eager per-variable path for custom training loops (tf.GradientTape style)."""
+        """Eager per-variable path for custom training loops (tf.GradientTape style).
+
+        Called from the replica functions of a single-process multi-device MirroredStrategy
+        (``strategy.run``), this is TF's merge call: the replicas' gradients are summed across
+        replicas in rank order and the variables are updated ONCE, by the last replica to arrive
+        (parallel/local_replicas.py rendezvous)."""
         gv = [(g, v) for g, v in grads_and_vars if g is not None]
+        from ..parallel.strategy import get_strategy, has_strategy
+
+        grp = getattr(get_strategy(), "_local_group", None) if has_strategy() else None
+        if grp is not None and grp.in_region():
+            def merge(per_replica):
+                n = len(per_replica[0])
+                if any(len(p) != n for p in per_replica):
+                    raise ValueError("apply_gradients: replicas passed different variable lists")
+                # (custom-loop path, not the fit engine: full device syncs order the replicas'
+                # gradient producers on their streams against this thread's update)
+                if grp.device_comm().gpu:
+                    grp.device_comm().synchronize()
+                summed = []
+                for i in range(n):
+                    v = per_replica[0][i][1]
+                    dev = v.read_value().device
+                    acc = torch.as_tensor(per_replica[0][i][0]).to(dev, copy=True)
+                    for p in per_replica[1:]:
+                        acc += torch.as_tensor(p[i][0]).to(dev)
+                    summed.append((acc, v))
+                self._apply_gradients_now(summed)
+                if grp.device_comm().gpu:
+                    grp.device_comm().synchronize()
+
+            grp.rendezvous(gv, merge)
+            return
+        self._apply_gradients_now(gv)
+
+    def _apply_gradients_now(self, gv):
         if not gv:
             return
         flat_g = torch.cat([torch.as_tensor(g).reshape(-1).float() for g, _ in gv])
@@ -168,6 +202,12 @@ class Optimizer:
         self.iterations = int(st.get("iterations", 0))
         for k, v in st.get("slots", {}).items():
             self._slots[k] = v.to(self._device) if self._device is not None else v.clone()
+
+
+def _kernel_present(kernel: str) -> bool:
+    from .. import ops
+
+    return ops.hip_available() and hasattr(ops.hip(), kernel)
 
 
 def _hip_ok(t: torch.Tensor, kernel: str = "sgd") -> bool:
@@ -232,7 +272,15 @@ class Adam(Optimizer):
     def _slot_names(self):
         return ["m", "v"] + (["vhat"] if self.amsgrad else [])
 
-    graph_safe = True  # lr and the step count come from device memory (t_dev)
+    @property
+    def graph_safe(self) -> bool:
+        """Whether a captured step replays this update correctly: only the kernel path reads the
+        learning rate and the step count from device memory (t_dev); the clipping fallback
+        (_update) bakes the capture-time values into the graph."""
+        if self.clipvalue is not None or self.clipnorm or self.global_clipnorm:
+            return False
+        return _kernel_present("adam")
+
     _needs_step = True
 
     def device_update(self, W, G, t_add=0):
@@ -288,7 +336,7 @@ class RMSprop(Optimizer):
     def _slot_names(self):
         return ["rms"] + (["mom"] if self.momentum > 0 else []) + (["mg"] if self.centered else [])
 
-    graph_safe = True
+    graph_safe = property(lambda self: _kernel_present("rmsprop"))  # (the torch fallback bakes lr)
 
     def device_update(self, W, G, t_add=0):
         """csrc/kernels/optim.hip k_rmsprop."""
@@ -334,7 +382,7 @@ class Adagrad(Optimizer):
         if fresh:
             self._slots["acc"].fill_(self.init_acc)
 
-    graph_safe = True
+    graph_safe = property(lambda self: _kernel_present("adagrad"))
 
     def device_update(self, W, G, t_add=0):
         """csrc/kernels/optim.hip k_adagrad."""

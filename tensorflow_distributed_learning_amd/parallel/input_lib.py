@@ -165,6 +165,79 @@ class DistributedIterator:
             return None
 
 
+class LocalDistributedDataset:
+    """``experimental_distribute_dataset`` of a single-process multi-device MirroredStrategy: ONE
+    pipeline of global batches, each split into per-replica slices (split_sizes) and yielded as a
+    :class:`~.values.PerReplica` (TF: the worker's batch is divided among its local replicas), which
+    ``strategy.run`` hands to the replicas one slice each."""
+
+    def __init__(self, dataset: D.Dataset, strategy, options=None):
+        self.dataset, self.strategy, self.options = dataset, strategy, options
+        self.num_replicas = strategy.num_replicas_in_sync
+        b = find_batch(dataset)
+        self.global_batch_size = b.batch_size if b is not None else None
+
+    @property
+    def per_replica_batch_size(self) -> Optional[int]:
+        if self.global_batch_size is None:
+            return None
+        return self.global_batch_size // self.num_replicas
+
+    def cardinality(self):
+        return self.dataset.cardinality()
+
+    def __iter__(self):
+        from .values import PerReplica
+
+        G = self.num_replicas
+        for batch in self.dataset:
+            n = len(D.flatten(batch)[0])
+            sizes = split_sizes(n, G)
+            lo, parts = 0, []
+            for r in range(G):
+                parts.append(D.map_structure(lambda t, lo=lo, hi=lo + sizes[r]: t[lo:hi], batch))
+                lo += sizes[r]
+            yield _per_replica_structure(parts, PerReplica)
+
+
+class LocalDistributedDatasetFromFunction:
+    """``distribute_datasets_from_function`` of a single-process multi-device MirroredStrategy: the
+    function runs once (one input pipeline, ``input_pipeline_id`` 0) and returns a dataset batched
+    by the per-replica batch size; consecutive batches go to consecutive replicas, G of them form
+    one :class:`~.values.PerReplica` step input."""
+
+    def __init__(self, dataset: D.Dataset, strategy, ctx: InputContext):
+        self.dataset, self.strategy, self.ctx = dataset, strategy, ctx
+        self.num_replicas = strategy.num_replicas_in_sync
+        b = find_batch(dataset)
+        self.global_batch_size = b.batch_size * self.num_replicas if b is not None else None
+
+    def __iter__(self):
+        from .values import PerReplica
+
+        it = iter(self.dataset)
+        while True:
+            parts = []
+            for _ in range(self.num_replicas):
+                try:
+                    parts.append(next(it))
+                except StopIteration:
+                    break
+            if len(parts) < self.num_replicas:
+                return  # (TF drops an incomplete final round of per-replica batches the same way)
+            yield _per_replica_structure(parts, PerReplica)
+
+
+def _per_replica_structure(parts, PerReplica):
+    """[structure per replica] -> structure of PerReplica leaves (tuples / lists / dicts kept)."""
+    first = parts[0]
+    if isinstance(first, dict):
+        return {k: _per_replica_structure([p[k] for p in parts], PerReplica) for k in first}
+    if isinstance(first, (tuple, list)):
+        return type(first)(_per_replica_structure([p[i] for p in parts], PerReplica) for i in range(len(first)))
+    return PerReplica(parts)
+
+
 class DistributedDatasetFromFunction:
     """Each replica builds its own input pipeline from an InputContext (no slicing)."""
 

@@ -166,6 +166,10 @@ class StrategyExtended:
                  communicator: Communicator, options: CommunicationOptions, tf_config: Optional[TFConfig] = None,
                  rendezvous=None):
         self._strategy = strategy
+        if device.type == "cuda" and os.environ.get("TDL_HIP_SCHEDULE"):
+            from ..utils import hipsync
+
+            hipsync.configure(devices=[device.index or 0])  # this replica's device only
         self.device = device
         self.rank = rank
         self.world_size = world_size
@@ -256,7 +260,13 @@ class Strategy:
         from .values import PerReplica
 
         def pick(v, r):
-            return v.values[r] if isinstance(v, PerReplica) else v
+            if isinstance(v, PerReplica):
+                return v.values[r]
+            if isinstance(v, dict):
+                return {k: pick(x, r) for k, x in v.items()}
+            if isinstance(v, (tuple, list)):
+                return type(v)(pick(x, r) for x in v)
+            return v
 
         def one(r):
             st = self._replica_strategy(r)
@@ -321,13 +331,20 @@ class Strategy:
         return (value,)
 
     def experimental_distribute_dataset(self, dataset, options=None):
-        from .input_lib import DistributedDataset
+        from .input_lib import DistributedDataset, LocalDistributedDataset
 
+        if self._local_group is not None and not self._local_group.in_region():
+            return LocalDistributedDataset(dataset, self, options)  # PerReplica slices, one pipeline
         return DistributedDataset(dataset, self, options)
 
     def distribute_datasets_from_function(self, dataset_fn, options=None):
-        from .input_lib import DistributedDatasetFromFunction, InputContext
+        from .input_lib import (DistributedDatasetFromFunction, InputContext,
+                                LocalDistributedDatasetFromFunction)
 
+        if self._local_group is not None and not self._local_group.in_region():
+            ctx = InputContext(num_input_pipelines=1, input_pipeline_id=0,
+                               num_replicas_in_sync=self.num_replicas_in_sync)
+            return LocalDistributedDatasetFromFunction(dataset_fn(ctx), self, ctx)
         ctx = InputContext(
             num_input_pipelines=self.num_replicas_in_sync,
             input_pipeline_id=self.extended.rank,

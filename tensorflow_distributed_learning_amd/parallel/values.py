@@ -16,6 +16,17 @@ import torch
 
 
 TAPE_DEPTH = [0]  # > 0 while a compat GradientTape is recording
+
+
+_CURRENT = []
+
+
+def _replica_device():
+    if not _CURRENT:
+        from .local_replicas import CURRENT
+
+        _CURRENT.append(CURRENT)
+    return getattr(_CURRENT[0], "device", None)
 CAST_ACCUMULATE = [0]  # > 0 while GenericTrainer.train_step runs its forward (Variable.cast fast path)
 
 
@@ -75,7 +86,14 @@ class Variable:
         if TAPE_DEPTH[0] > 0 and self.trainable and (self._leaf is None or not self._leaf.requires_grad):
             # inside a GradientTape: expose an autograd leaf sharing this variable's storage
             self._leaf = self._value.detach().requires_grad_(True)
-        return self._leaf if self._leaf is not None else self._value
+        t = self._leaf if self._leaf is not None else self._value
+        dev = _replica_device()
+        if dev is not None and t.device != dev:
+            # read inside replica r's function of a single-process multi-device MirroredStrategy:
+            # replica r's (mirrored) copy on its device; differentiable, so a tape's gradient
+            # arrives at the variable (parallel/local_replicas.py)
+            t = t.to(dev)
+        return t
 
     def cast(self, dtype: torch.dtype) -> torch.Tensor:
         """``value.to(dtype)`` for a compute-dtype copy (mixed_bfloat16). When the generic trainer

@@ -133,3 +133,130 @@ def test_script_body_runs_once(tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.count("BODY") == 1, r.stdout
     assert "REPLICAS 2" in r.stdout
+
+
+def _dense_model():
+    L = tdl.keras.layers
+    return tdl.keras.Sequential([L.Dense(8, activation="relu", input_shape=(8,)), L.Dense(3)])
+
+
+def _xy(n=256):
+    g = torch.Generator().manual_seed(0)
+    return torch.rand(n, 8, generator=g), torch.randint(0, 3, (n,), generator=g)
+
+
+def test_one_training_loop_shares_callbacks_state_with_every_replica():
+    """ONE fit loop drives both replicas (engine/mirrored.py): EarlyStopping ends training on every
+    replica, a LearningRateScheduler reaches the clone's optimizer, iterations stay in step."""
+    x, y = _xy()
+    s = tdl.distribute.MirroredStrategy(devices=["/cpu:0", "/cpu:1"])
+    with s.scope():
+        m = _dense_model()
+        m.compile(loss=tdl.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+                  optimizer=tdl.keras.optimizers.SGD(0.1))
+    ds = tdl.data.Dataset.from_tensor_slices((x, y)).batch(32).repeat()
+    cb = [tdl.keras.callbacks.LearningRateScheduler(lambda e, lr: 0.1 * (0.5 ** e)),
+          tdl.keras.callbacks.EarlyStopping(monitor="loss", patience=0, min_delta=10.0)]
+    h = m.fit(ds, epochs=5, steps_per_epoch=4, verbose=0, callbacks=cb)
+    assert len(h.history["loss"]) == 2  # stopped after epoch 1 (no 10.0 improvement), not hung
+    assert getattr(m._trainer, "is_group", False)
+    (c,) = m._local_clones
+    assert c.optimizer.current_lr() == m.optimizer.current_lr() == 0.05
+    assert c.optimizer.iterations == m.optimizer.iterations == 8
+    for a, b in zip(m.get_weights(), c.get_weights()):
+        assert np.array_equal(a, b)
+    s.shutdown()
+
+
+def test_replicas_receive_restored_weights_and_optimizer_state(tmp_path):
+    """Weights / optimizer slots set on replica 0 between fits (load_weights, a restored optimizer)
+    reach every replica before the next step."""
+    x, y = _xy()
+    s = tdl.distribute.MirroredStrategy(devices=["/cpu:0", "/cpu:1"])
+    with s.scope():
+        m = _dense_model()
+        m.compile(loss=tdl.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+                  optimizer=tdl.keras.optimizers.Adam(0.01))
+    ds = tdl.data.Dataset.from_tensor_slices((x, y)).batch(32).repeat()
+    m.fit(ds, epochs=1, steps_per_epoch=2, verbose=0)
+    (c,) = m._local_clones
+    new = [w * 0 + 0.01 for w in m.get_weights()]
+    m.set_weights(new)
+    m.optimizer.iterations = 100
+    for v in m.optimizer.slots().values():
+        v.fill_(0.5)
+    m._trainer.broadcast_from_primary()
+    for a, b in zip(new, c.get_weights()):
+        assert np.array_equal(a, b)
+    assert c.optimizer.iterations == 100
+    assert all(float(v.min()) == 0.5 for v in c.optimizer.slots().values())
+    m.fit(ds, epochs=1, steps_per_epoch=2, verbose=0)
+    for a, b in zip(m.get_weights(), c.get_weights()):
+        assert np.array_equal(a, b)
+    s.shutdown()
+
+
+def test_custom_training_loop_per_replica_inputs_and_merged_update():
+    """strategy.experimental_distribute_dataset yields PerReplica slices of ONE pipeline, and
+    apply_gradients inside strategy.run is a merge call: the replicas' gradients are summed and the
+    variables updated once -- the same as one replica on the whole global batch."""
+    from tensorflow_distributed_learning_amd.compat import tf
+
+    x, y = _xy(128)
+    s = tdl.distribute.MirroredStrategy(devices=["/cpu:0", "/cpu:1"])
+    with s.scope():
+        m = _dense_model()
+        opt = tdl.keras.optimizers.SGD(0.1)
+    loss_fn = tdl.keras.losses.SparseCategoricalCrossentropy(from_logits=True, reduction="none")
+    dist = s.experimental_distribute_dataset(tdl.data.Dataset.from_tensor_slices((x, y)).batch(64))
+    batch = next(iter(dist))
+    assert isinstance(batch[0], PerReplica) and [len(v) for v in batch[0].values] == [32, 32]
+
+    def step(b):
+        xb, yb = b
+        with tf.GradientTape() as tape:
+            loss = loss_fn(yb, m(xb, training=True)).sum() / 64.0
+        grads = tape.gradient(loss, m.trainable_variables)
+        opt.apply_gradients(zip(grads, m.trainable_variables))
+        return loss.detach()
+
+    w0 = [w.copy() for w in m.get_weights()]
+    s.run(step, args=(batch,))
+    ref = _dense_model()
+    ref.set_weights(w0)
+    ropt = tdl.keras.optimizers.SGD(0.1)
+    xb = torch.cat(batch[0].values)
+    yb = torch.cat(batch[1].values)
+    with tf.GradientTape() as tape:
+        loss = loss_fn(yb, ref(xb, training=True)).sum() / 64.0
+    ropt.apply_gradients(zip(tape.gradient(loss, ref.trainable_variables), ref.trainable_variables))
+    for a, b in zip(m.get_weights(), ref.get_weights()):
+        np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-7)
+    # distribute_datasets_from_function: consecutive per-replica batches form one step
+    ddf = s.distribute_datasets_from_function(
+        lambda ctx: tdl.data.Dataset.from_tensor_slices((x, y)).batch(ctx.get_per_replica_batch_size(64)))
+    b2 = next(iter(ddf))
+    assert isinstance(b2[0], PerReplica) and torch.equal(torch.cat(b2[0].values), x[:64])
+    s.shutdown()
+
+
+def test_replicas_reaching_different_collectives_fail_fast():
+    g = LocalReplicaGroup([torch.device("cpu")] * 2, timeout=300)
+
+    def fn(r):
+        if r == 0:
+            g.comms[r].all_reduce(torch.ones(3))
+
+    import time
+
+    t0 = time.monotonic()
+    with pytest.raises(RuntimeError, match="different collectives"):
+        g.run(fn)
+    assert time.monotonic() - t0 < 30
+
+
+def test_adam_with_clipping_is_not_graph_safe():
+    """A clipped Adam update runs the torch fallback whose lr / step are host values: the whole-step
+    graph must not capture it."""
+    assert not tdl.keras.optimizers.Adam(0.01, clipnorm=1.0).graph_safe
+    assert not tdl.keras.optimizers.Adam(0.01, clipvalue=0.5).graph_safe
