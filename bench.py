@@ -176,6 +176,13 @@ def main():
         a = np.array(ht[-max(1, K // max(1, spe)):]) * 1e6
         print(f"host us per execution (take, graph+upload, launch): median {np.median(a, 0).round(1).tolist()} "
               f"max {a.max(0).round(1).tolist()}", file=sys.stderr)
+    from tensorflow_distributed_learning_amd.parallel import bucketing
+
+    # modelled multi-GPU prediction (parallel/bucketing.py), from this run's step time at N = 1
+    # and the recorded one-GPU number otherwise -- the driver's SCALE run checks it
+    predicted = bucketing.predict_mnist_scaling(
+        dt / K * 1e3 if R == 1 and args.per_replica_batch == 64 else bucketing.MNIST_T1_MS_RECORDED,
+        twoshot_min_r=int(os.environ.get("TDL_FX_TWOSHOT_MIN_R", "3")))
     if rank == 0:
         print(json.dumps({
             "metric": "images/sec (whole node) MNIST CNN global_batch=64*N",
@@ -213,6 +220,7 @@ def main():
                        "rank_spread_pct": round(100.0 * (max(per_rank) - min(per_rank)) / max(per_rank), 2),
                        "fallbacks": list(getattr(trainer, "fallbacks", [])) + (
                            [f"xgmi: {comm.xgmi_reason}"] if getattr(comm, "xgmi_reason", "") else [])},
+            "predicted": predicted,
         }), flush=True)
     strategy.shutdown()
     if not identical:

@@ -84,6 +84,39 @@ def xgmi_oneshot_us(nbytes: int, world: int) -> float:
     return XGMI_CALL_US + nbytes / (LINK_EFFICIENCY * XGMI_LINK_GBPS * 1e9) * 1e6
 
 
+XGMI_TWOSHOT_CALL_US = 6.8  # measured like XGMI_CALL_US (two flag rounds)
+MNIST_GRAD_BYTES = 225_034 * 4
+MNIST_T1_MS_RECORDED = 0.02562  # the driver's BENCH_r05 record (K=20, one MI355X)
+
+
+def predict_mnist_scaling(t1_ms: float, ns=(2, 4, 8), twoshot_min_r: int = 3) -> dict:
+    """MODELLED weak-scaling prediction for the reference CNN's exchange-in-finalize step, written
+    before any multi-GPU measurement so the first SCALE run shows whether the fabric behaves as
+    assumed.  Per step at N GPUs: the one-GPU step ``t1`` + the exchange's fixed cost (the measured
+    one-/two-shot call cost, profiles/comm_fixed_costs_r4.jsonl: flags, fences, no fabric hop) + the
+    fabric term: one-shot pulls every peer's whole 900 KB slab over that peer's link (all links in
+    parallel: n / link), two-shot pulls a 1/N shard from every peer twice (2 n / N per link), at
+    ``LINK_EFFICIENCY`` x 153.6 GB/s.  It ignores the overlap of the exchange with the finalize's own
+    reduction work (pessimistic) and any contention inside a GPU (optimistic)."""
+    bw = LINK_EFFICIENCY * XGMI_LINK_GBPS * 1e9  # bytes/s per link
+    out_ms, eff = {}, {}
+    for n in ns:
+        if n <= 1:
+            continue
+        if n >= twoshot_min_r:
+            extra_us = XGMI_TWOSHOT_CALL_US + 2.0 * (MNIST_GRAD_BYTES / n) / bw * 1e6
+        else:
+            extra_us = XGMI_CALL_US + MNIST_GRAD_BYTES / bw * 1e6
+        t = t1_ms + extra_us * 1e-3
+        out_ms[str(n)] = round(t, 5)
+        eff[str(n)] = round(t1_ms / t, 3)
+    return {"label": "modelled, not measured", "t1_ms": round(t1_ms, 5), "ms_per_step": out_ms,
+            "scaling_efficiency": eff,
+            "assumptions": {"link_GBps": XGMI_LINK_GBPS, "link_efficiency": LINK_EFFICIENCY,
+                            "oneshot_fixed_us": XGMI_CALL_US, "twoshot_fixed_us": XGMI_TWOSHOT_CALL_US,
+                            "grad_bytes": MNIST_GRAD_BYTES, "twoshot_from_n": twoshot_min_r}}
+
+
 def plan(grad_numel: int, world: int, local_world: Optional[int] = None, wire_dtype: str = "float32",
          bytes_per_pack: int = 0, algorithm: str = "rccl") -> BucketPlan:
     """Bucket plan for a flat gradient of ``grad_numel`` elements on ``world`` replicas."""

@@ -81,3 +81,26 @@ def test_abort_last():
     assert c.aborted and c.async_error() != 0
     with pytest.raises(RuntimeError, match="aborted"):
         c.all_reduce(t, 0)
+
+
+def test_clique_one_process_grouped_calls():
+    """The multi-device-per-process RCCL clique (ncclCommInitAll + ncclGroupStart/End of the
+    per-device calls, csrc/rccl_comm.cpp RcclClique) on the box's one device; a duplicate device is
+    refused with a clear error (RCCL cannot put two ranks on one GPU)."""
+    from tensorflow_distributed_learning_amd.ops import hip
+
+    C = hip()
+    cl = C.RcclClique([0])
+    assert cl.size == 1 and list(cl.devices) == [0]
+    t = torch.arange(8, dtype=torch.float32, device="cuda")
+    cl.all_reduce([t], 0)
+    cl.broadcast([t], 0)
+    torch.cuda.synchronize()
+    assert torch.equal(t, torch.arange(8, dtype=torch.float32, device="cuda"))
+    assert cl.async_error() == 0
+    with pytest.raises(Exception, match="distinct devices"):
+        C.RcclClique([0, 0])
+    with pytest.raises(Exception, match="one tensor per device"):
+        cl.all_reduce([t, t], 0)
+    cl.abort()
+    assert cl.aborted
