@@ -62,7 +62,16 @@ def main():
                     help="N > 1 without a launcher: one replica process per GPU (default, the scaling mode), "
                          "or ONE process driving all N devices (TF's single-process MirroredStrategy: one host "
                          "thread launching every device's captured graph; 'threads' is an alias)")
+    ap.add_argument("--engine", choices=["fused", "generic"], default="fused",
+                    help="fused: the hand-written fused MNIST step (the headline); generic: the autograd engine "
+                         "any model gets (TDL_DISABLE_FUSED=1) -- measures the cliff a model change meets")
+    ap.add_argument("--variant", choices=["reference", "same", "dropout"], default="reference",
+                    help="(generic engine) the reference CNN, with padding='same' convs, or with a Dropout layer")
     args = ap.parse_args()
+    if args.engine == "generic":
+        os.environ["TDL_DISABLE_FUSED"] = "1"
+    elif args.variant != "reference":
+        ap.error("--variant needs --engine generic (the fused engine runs the reference model only)")
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
 
@@ -106,16 +115,35 @@ def main():
     options.experimental_distribute.auto_shard_policy = tdl.data.AutoShardPolicy.OFF
     train = train.with_options(options)
 
+    def build():
+        if args.variant == "reference":
+            return build_mnist_cnn()
+        L = tdl.keras.layers
+        pad = "same" if args.variant == "same" else "valid"
+        layers = [L.Conv2D(32, 3, activation="relu", padding=pad, input_shape=(28, 28, 1)), L.MaxPooling2D(),
+                  L.Conv2D(64, 3, activation="relu", padding=pad), L.MaxPooling2D(), L.Flatten()]
+        if args.variant == "dropout":
+            layers.append(L.Dropout(0.25))
+        return tdl.keras.Sequential(layers + [L.Dense(128, activation="relu"), L.Dense(10)])
+
     with strategy.scope():
-        model = build_mnist_cnn()
+        model = build()
         model.compile(loss=tdl.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
                       optimizer=tdl.keras.optimizers.SGD(learning_rate=0.001),
                       metrics=[tdl.keras.metrics.SparseCategoricalAccuracy()],
                       steps_per_execution=spe)
     trainer = model._get_trainer()
-    handler = trainer.prepare(train)
-    if trainer.kind != "fused" or handler is None:
+    handler = trainer.prepare(train) if hasattr(trainer, "prepare") else None
+    if args.engine == "fused" and (trainer.kind != "fused" or handler is None):
         raise SystemExit(f"bench: fused MI355X engine not selected ({getattr(model, '_fused_reason', '?')})")
+    if handler is None:
+        if hasattr(trainer, "host_handler"):
+            handler = trainer.host_handler(train)
+        else:
+            from tensorflow_distributed_learning_amd.engine.trainer import HostDataHandler
+
+            handler = HostDataHandler(train, strategy)
+        handler.new_iterator()
     comm = strategy.extended.communicator
     dev = strategy.extended.device
 
@@ -125,13 +153,17 @@ def main():
         else:
             torch.cuda.synchronize(dev)
 
-    trainer.warm_graphs(K)
+    fused = trainer.kind == "fused"
+    if fused:
+        trainer.warm_graphs(K)
     if W:
-        trainer.warm_graphs(W)
+        if fused:
+            trainer.warm_graphs(W)
         trainer.run_train(handler, W)
     # input prefetch (depth one execution, as tf.data prefetch): the first timed execution's batch
     # indices are assembled and uploaded before the clock starts; later ones overlap the GPU
-    trainer.prefetch(handler, K)
+    if fused:
+        trainer.prefetch(handler, K)
     sync_all()
     comm.barrier()
     sync_all()
@@ -182,7 +214,7 @@ def main():
     # and the recorded one-GPU number otherwise -- the driver's SCALE run checks it
     predicted = bucketing.predict_mnist_scaling(
         dt / K * 1e3 if R == 1 and args.per_replica_batch == 64 else bucketing.MNIST_T1_MS_RECORDED,
-        twoshot_min_r=int(os.environ.get("TDL_FX_TWOSHOT_MIN_R", "3")))
+        twoshot_min_r=int(os.environ.get("TDL_FX_TWOSHOT_MIN_R", "3"))) if fused else None
     if rank == 0:
         print(json.dumps({
             "metric": "images/sec (whole node) MNIST CNN global_batch=64*N",
@@ -200,6 +232,7 @@ def main():
             "config": {"model": "tf_dist_example.py MNIST CNN (Conv32-Pool-Conv64-Pool-Dense128-Dense10, 225,034 params)",
                        "global_batch": B, "seq_len": None, "image_shape": [28, 28, 1],
                        "parallelism": f"dp{R}", "engine": trainer.kind, "communicator": comm.name,
+                       "variant": args.variant,
                        "process_model": "single-process" if single else ("one process per GPU" if R > 1 else "single"),
                        # what actually ran: the communicator class (torch RCCL process group, the
                        # framework's own RCCL communicator, gloo + xGMI, local) and the HIP IPC mode
@@ -209,9 +242,11 @@ def main():
                        "kernels_per_step": 2 if all(getattr(t, "_steps", None) and all(
                            getattr(st, "fused_bwd", False) for st in t._steps.values())
                            for t in getattr(trainer, "subs", [trainer])) else None,
-                       "steps_per_execution": spe, "graph_captured": bool(trainer.capture),
+                       "steps_per_execution": spe,
+                       "graph_captured": bool(getattr(trainer, "capture", None) if fused else getattr(
+                           trainer, "_graphs", None)),
                        "input_prefetch_executions": 1,
-                       "allreduce_in_graph": bool(trainer.capture_comm and R > 1),
+                       "allreduce_in_graph": bool(getattr(trainer, "capture_comm", False) and R > 1),
                        "replicas_identical": identical,
                        "final_loss": round(logs["loss"], 4),
                        # per-rank timed-region spread (the MAX is reported), and why any faster path

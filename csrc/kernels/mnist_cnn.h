@@ -80,11 +80,17 @@ struct MnistArgs {
 //      profiles/mnist_stagger_ab_r5.txt)
 //   4  SGD fused into the finalize (one replica, or the xGMI exchange): the gradient slab G is not
 //      written (nothing reads it on those paths; 900 KB fewer dirty lines for the kernel-end write-back)
+//   8  XCD-aware workgroup -> (image, quarter) map: the 4 quarter workgroups of an image get block
+//      ids of one residue mod 8 (blocks are dealt round-robin over the 8 XCDs, so they share one
+//      XCD's L2 for their two hand-offs) instead of 4 consecutive ids (4 XCDs); speed only, the
+//      protocol does not depend on placement (needs b % 8 == 0).  Measured: fused span 18.85 ->
+//      18.38 us, K=20 2.48-2.49 -> 2.52 M img/s, K=1000 2.59-2.60 -> 2.62-2.63 M (adopted)
 constexpr int kMnistVariantPrio = 1;
 constexpr int kMnistVariantStagger = 2;
 constexpr int kMnistVariantNoG = 4;
+constexpr int kMnistVariantXcd = 8;
 
-constexpr int kDefaultMnistVariant = 0;
+constexpr int kDefaultMnistVariant = kMnistVariantXcd;  // (measured +1.3 %: profiles/mnist_xcd_map_r6.txt)
 
 constexpr int kMnistPart2Rows = 289;
 // fused_bwd layout of part2: [b][73 row quads][64 columns][4 rows] (quad 72 = the bias row + 3 zero

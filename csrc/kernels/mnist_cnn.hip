@@ -997,7 +997,13 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   float* dCs = hws + kHeadW;               // fused_bwd: the dC2 grid (kDcF x kDcF cells)
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int i = lane & 15, g = lane >> 4;
-  const int bi = blockIdx.x >> 2, cq = blockIdx.x & 3;
+  int bi = blockIdx.x >> 2, cq = blockIdx.x & 3;
+  if ((a.variant & kMnistVariantXcd) && (a.b & 7) == 0) {
+    // block B -> XCD class B % 8, slot B / 8: each class holds b / 8 whole images (4 slots each)
+    const int x = blockIdx.x & 7, sl = blockIdx.x >> 3;
+    bi = x * (a.b >> 3) + (sl >> 2);
+    cq = sl & 3;
+  }
   // waves w and w + 4 share a SIMD; the younger half (4-7) loses the VALU issue arbitration in every
   // phase and reaches each barrier last (MI355X_MICROARCH.md, two waves per SIMD, item 4)
   if ((a.variant & kMnistVariantPrio) && __builtin_amdgcn_readfirstlane(wave) >= 4) __builtin_amdgcn_s_setprio(1);

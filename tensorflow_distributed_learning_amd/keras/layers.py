@@ -268,16 +268,21 @@ class Dense(Layer):
                 return self.activation(_dense.dense_bf16(x, w, b, (gw, gb), anchor=self.kernel.value))
             b = self.bias.value if self.bias is not None else None
             return self.activation(_dense.dense_bf16(x, self.kernel.cast(x.dtype), b))
-        if _conv_f32.dense_supported(x) and self.kernel.value.dtype == torch.float32:
-            # f32 on the GPU: the f32-MFMA GEMM of csrc/kernels/gemm_f32.hip (no hipBLASLt)
+        low = x.is_cuda and x.dtype == torch.bfloat16 and self.kernel.value.dtype == torch.float32
+        if (_conv_f32.dense_supported(x) or low) and self.kernel.value.dtype == torch.float32:
+            # f32 on the GPU: the f32-MFMA GEMM of csrc/kernels/gemm_f32.hip (no hipBLASLt); also a bf16
+            # input whose shape the bf16 GEMM does not tile (a 10-class head under mixed_bfloat16):
+            # f32 math on the f32 master weights, bf16 out (the layer's compute dtype)
+            xf = x.float() if low else x
             gw = self.kernel.grad_target()
             gb = self.bias.grad_target() if self.bias is not None else None
             if gw is not None and gw.is_contiguous() and (self.bias is None or gb is not None):
                 b = self.bias.value.detach() if self.bias is not None else None
-                return self.activation(_conv_f32.dense(x, self.kernel.value.detach(), b, (gw, gb),
-                                                       anchor=self.kernel.value))
-            b = self.bias.value if self.bias is not None else None
-            return self.activation(_conv_f32.dense(x, self.kernel.value, b))
+                y = _conv_f32.dense(xf, self.kernel.value.detach(), b, (gw, gb), anchor=self.kernel.value)
+            else:
+                b = self.bias.value if self.bias is not None else None
+                y = _conv_f32.dense(xf, self.kernel.value, b)
+            return self.activation(y.to(torch.bfloat16) if low else y)
         y = torch.matmul(x, self.kernel.cast(x.dtype))
         if self.bias is not None:
             y = y + self.bias.value.to(y.dtype)
