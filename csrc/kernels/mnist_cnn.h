@@ -89,6 +89,8 @@ constexpr int kMnistVariantPrio = 1;
 constexpr int kMnistVariantStagger = 2;
 constexpr int kMnistVariantNoG = 4;
 constexpr int kMnistVariantXcd = 8;
+//   (16, round 6: 5 of conv1's W3 prefetch loads moved into conv2 -- 0.9 % slower at K=1000 and
+//   K=20, removed; profiles/mnist_w3_late_rejected_r6.txt)
 
 constexpr int kDefaultMnistVariant = kMnistVariantXcd;  // (measured +1.3 %: profiles/mnist_xcd_map_r6.txt)
 

@@ -1286,6 +1286,7 @@ __global__ __launch_bounds__(512) void k_fwd_conv(MnistArgs a) {
   // ---- dP2 = (dH W3^T) * 1[P2 > 0] for this quarter's 400 features, from the W3 slice still in
   // registers (no K5 launch, no second read of W3), dH from this workgroup's own head (LDS) ----
   lds_barrier();
+  if (a.fused_bwd) stamp(a.stamps, 7);  // (fused: slot 7 = the dP2 phase's start, after the dH barrier)
   const f4 dh = ld4(sdh + n4);
   float v[25];
   {

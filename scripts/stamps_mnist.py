@@ -13,7 +13,7 @@ from tensorflow_distributed_learning_amd.models import mnist_cnn as M  # noqa: E
 
 KERNELS = {
     "fwd_conv": (8, 8, {0: "start", 1: "stage-issued", 2: "stage-barrier", 3: "conv1-done", 4: "barrier2",
-                        5: "conv2-mfma", 6: "dense1-partial", 7: "dP2-done"}, 256),
+                        5: "conv2-mfma", 6: "dense1-partial", 7: "dP2-done|fused: dP2-start"}, 256),
     "conv_bwd": (6, 8, {0: "start", 1: "stage-issued", 2: "stage-barrier", 3: "wgrad-done", 6: "dgrad-mfma",
                         4: "dgrad-epi", 5: "final-barrier"}, 256),
 }
