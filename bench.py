@@ -160,6 +160,8 @@ def main():
         if fused:
             trainer.warm_graphs(W)
         trainer.run_train(handler, W)
+    if not fused and hasattr(trainer, "warm_graphs"):
+        trainer.warm_graphs(K)  # generic engine: its execution graphs, captured once a step has run eagerly
     # input prefetch (depth one execution, as tf.data prefetch): the first timed execution's batch
     # indices are assembled and uploaded before the clock starts; later ones overlap the GPU
     if fused:

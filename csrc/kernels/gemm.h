@@ -24,6 +24,11 @@ void gap_bwd_bf16(const void* dy, void* dx, int N, int HW, int C, hipStream_t s)
 // Sparse softmax cross-entropy on f32 logits [N][K] with int64 labels: loss[n] = logsumexp(z[n]) -
 // z[n][label] (0 for a label outside [0, K)); backward dz = (softmax(z) - onehot) * g[n].
 void softmax_xent_fwd(const float* z, const long long* labels, int N, int K, float* loss, float* lse, hipStream_t s);
+// Fused loss head of the generic engine: loss_out[0] = sum of the rows' sparse softmax cross-entropy / gn,
+// dz = (softmax - onehot) / gn, and the loss / accuracy metric accumulators (f64, any may be null)
+// advanced by (sum of losses, N) / (correct top-1, N); one workgroup, rows summed in a fixed order.
+void xent_head(const float* z, const long long* labels, int N, int K, double gn, float* loss_out, float* dz,
+               double* lt_total, double* lt_count, double* acc_total, double* acc_count, hipStream_t s);
 void softmax_xent_bwd(const float* z, const long long* labels, int N, int K, const float* g, float* dz,
                       hipStream_t s);
 

@@ -310,7 +310,76 @@ __global__ __launch_bounds__(256) void k_softmax_xent(const float* __restrict__ 
   for (int k = lane; k < K; k += 64) dr[k] = (__expf(zr[k] - lse) - (k == y ? 1.f : 0.f)) * gr;
 }
 
+// Fused loss head (see gemm.h xent_head): 16 waves; wave w takes rows w, w + 16, ..; lane 0 of each
+// wave accumulates its rows' loss / correct flags in row order, thread 0 sums the waves in order.
+__global__ __launch_bounds__(1024) void k_xent_head(const float* __restrict__ z, const long long* __restrict__ lab,
+                                                    int N, int K, double gn, float* __restrict__ loss_out,
+                                                    float* __restrict__ dz, double* lt_total, double* lt_count,
+                                                    double* acc_total, double* acc_count) {
+  __shared__ double s_loss[16], s_cor[16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const float inv_gn = (float)(1.0 / gn);
+  double my_loss = 0.0, my_cor = 0.0;
+  for (int row = w; row < N; row += 16) {
+    const float* zr = z + (long long)row * K;
+    float mx = -INFINITY;
+    int am = K;
+    for (int k = lane; k < K; k += 64) {
+      const float v = zr[k];
+      if (v > mx) {
+        mx = v;
+        am = k;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {  // max, first index on ties (tf.argmax)
+      const float om = __shfl_xor(mx, o);
+      const int oa = __shfl_xor(am, o);
+      if (om > mx || (om == mx && oa < am)) {
+        mx = om;
+        am = oa;
+      }
+    }
+    float se = 0.f;
+    for (int k = lane; k < K; k += 64) se += __expf(zr[k] - mx);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) se += __shfl_xor(se, o);
+    const float lse = mx + __logf(se);
+    const long long y = lab[row];
+    const bool valid = y >= 0 && y < K;
+    float* dr = dz + (long long)row * K;
+    for (int k = lane; k < K; k += 64) dr[k] = (__expf(zr[k] - lse) - (k == y ? 1.f : 0.f)) * inv_gn;
+    if (lane == 0) {
+      my_loss += (double)(valid ? lse - zr[y] : 0.f);
+      my_cor += (valid && am == (int)y) ? 1.0 : 0.0;
+    }
+  }
+  if (lane == 0) {
+    s_loss[w] = my_loss;
+    s_cor[w] = my_cor;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tl = 0.0, tc = 0.0;
+    for (int i = 0; i < 16; ++i) {
+      tl += s_loss[i];
+      tc += s_cor[i];
+    }
+    loss_out[0] = (float)(tl / gn);
+    if (lt_total != nullptr) *lt_total += tl;
+    if (lt_count != nullptr) *lt_count += (double)N;
+    if (acc_total != nullptr) *acc_total += tc;
+    if (acc_count != nullptr) *acc_count += (double)N;
+  }
+}
+
 }  // namespace
+
+void xent_head(const float* z, const long long* labels, int N, int K, double gn, float* loss_out, float* dz,
+               double* lt_total, double* lt_count, double* acc_total, double* acc_count, hipStream_t s) {
+  hipLaunchKernelGGL(k_xent_head, dim3(1), dim3(1024), 0, s, z, labels, N, K, gn, loss_out, dz, lt_total, lt_count,
+                     acc_total, acc_count);
+}
 
 void softmax_xent_fwd(const float* z, const long long* labels, int N, int K, float* loss, float* lse, hipStream_t s) {
   hipLaunchKernelGGL(k_softmax_xent, dim3((N + 3) / 4), dim3(256), 0, s, z, labels, N, K, loss, lse, nullptr,

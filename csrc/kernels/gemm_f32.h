@@ -42,6 +42,13 @@ struct F32GemmArgs {
   int accumulate;  // out += result
   int vec_a, vec_b;  // 16-B operand loads (set by the host when layouts and alignment allow)
   F32ConvGeom g;
+  // Fusions of the layer around the GEMM (the generic engine's f32 Conv2D / Dense with a ReLU):
+  int act = 0;                    // epilogue: 0 = none, 1 = ReLU after the bias (forward)
+  const float* amask = nullptr;   // A operand *= (amask[same element] > 0): ReLU backward of the
+  const float* bmask = nullptr;   // layer's output; B likewise (masks share the operand's layout)
+  float* dbias = nullptr;         // bias gradient: a row of ones appended to A (ones_m = M - 1,
+  int ones_m = -1, ones_n = -1;   // kF32Gemm) or a column of ones appended to B (ones_n = N - 1,
+                                  // kF32ConvWgrad); that output row / column goes to dbias
 };
 
 constexpr int kF32Tile = 64;

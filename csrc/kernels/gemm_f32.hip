@@ -30,6 +30,15 @@ struct Ctr {
     mid = q % nmid;
     hi = q / nmid;
   }
+  __device__ void step1(int nmid, int nlo) {  // += 1: compares only (no division)
+    if (++lo == nlo) {
+      lo = 0;
+      if (++mid == nmid) {
+        mid = 0;
+        ++hi;
+      }
+    }
+  }
   __device__ void step(int d, int nmid, int nlo) {
     lo += d;
     if (lo >= nlo) {
@@ -46,13 +55,28 @@ struct Ctr {
 };
 
 __device__ __forceinline__ void out_store(const F32GemmArgs& a, int m, int n, float v) {
+  if (m == a.ones_m || n == a.ones_n) {  // the bias-gradient row / column
+    float* d = a.dbias + (m == a.ones_m ? n : m);
+    if (a.accumulate) v += *d;
+    *d = v;
+    return;
+  }
   if (a.bias != nullptr) v += a.bias[n];
   const int64_t i = a.trans_out ? (int64_t)n * a.ldo + m : (int64_t)m * a.ldo + n;
   if (a.accumulate) v += a.out[i];
+  if (a.act == 1) v = fmaxf(v, 0.f);
   a.out[i] = v;
 }
 
-template <int MODE>
+template <bool MA, bool MB>
+struct Slice {
+  float a[4], b[4];
+  float ma[MA ? 4 : 1], mb[MB ? 4 : 1];
+  unsigned va, vb;  // loaded value valid (else 0)
+  unsigned oa, ob;  // the appended row / column of ones (value 1, unmasked)
+};
+
+template <int MODE, bool MA, bool MB, bool VA, bool VB>
 __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
   __shared__ float As[16 * kLd];
   __shared__ float Bs[16 * kLd];
@@ -100,28 +124,66 @@ __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
   if constexpr (MODE == kF32ConvWgrad) kb.set(kbeg + kl, g.oh, g.ow);
 
   const bool s1 = g.sh == 1 && g.sw == 1;
-  float ra[4], rb[4];
-  auto load = [&](int k0) {
-    const int kk = k0 + kqa;  // A: reduction index of ra[0]
-    if constexpr (MODE == kF32Gemm) {
-      if (a.vec_a && arow && kk < kend) {
-        const f4 v = ld4(a.a + (int64_t)am * a.sam + kk);
+  using S = Slice<MA, MB>;
+
+  // A element e (valid or not) into slot i; a 16-B quad at slot 0 when vec
+  auto lda1 = [&](S& r, int i, bool ok, int64_t e) {
+    const int64_t q = ok ? e : 0;
+    r.a[i] = a.a[q];
+    if constexpr (MA) r.ma[i] = a.amask[q];
+    r.va |= ok ? 1u << i : 0u;
+  };
+  auto lda4 = [&](S& r, bool ok, int64_t e) {
+    const int64_t q = ok ? e : 0;
+    const f4 v = ld4(a.a + q);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) ra[i] = v[i];
+    for (int i = 0; i < 4; ++i) r.a[i] = v[i];
+    if constexpr (MA) {
+      const f4 mv = ld4(a.amask + q);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r.ma[i] = mv[i];
+    }
+    r.va = ok ? 15u : 0u;
+  };
+  auto ldb1 = [&](S& r, int i, bool ok, int64_t e) {
+    const int64_t q = ok ? e : 0;
+    r.b[i] = a.b[q];
+    if constexpr (MB) r.mb[i] = a.bmask[q];
+    r.vb |= ok ? 1u << i : 0u;
+  };
+  auto ldb4 = [&](S& r, bool ok, int64_t e) {
+    const int64_t q = ok ? e : 0;
+    const f4 v = ld4(a.b + q);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r.b[i] = v[i];
+    if constexpr (MB) {
+      const f4 mv = ld4(a.bmask + q);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r.mb[i] = mv[i];
+    }
+    r.vb = ok ? 15u : 0u;
+  };
+
+  auto load = [&](int k0, S& r) {
+    r.va = r.vb = r.oa = r.ob = 0u;
+    const int kk = k0 + kqa;  // A: reduction index of slot 0
+    if constexpr (MODE == kF32Gemm) {
+      const bool ones = am == a.ones_m;  // the appended row of ones (bias gradient)
+      if constexpr (VA) {
+        lda4(r, !ones && arow && kk < kend, (int64_t)am * a.sam + kk);
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          ra[i] = (arow && kk + i < kend) ? a.a[(int64_t)am * a.sam + (int64_t)(kk + i) * a.sak] : 0.f;
+          lda1(r, i, !ones && arow && kk + i < kend, (int64_t)am * a.sam + (int64_t)(kk + i) * a.sak);
       }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r.oa |= (ones && kk + i < kend) ? 1u << i : 0u;
     } else if constexpr (MODE == kF32ConvFwd || MODE == kF32ConvDgrad) {
       const int nlo = MODE == kF32ConvFwd ? g.c : g.k;
       Ctr c = ka;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        float v = 0.f;
-        if (a.vec_a && i > 0) {
-          v = ra[i];  // (filled by the vector load below)
-        } else if (arow && kk + i < kend) {
+        if (!VA || i == 0) {  // a 16-B quad at slot 0, or one element per slot
           int iy, ix;
           bool ok;
           if constexpr (MODE == kF32ConvFwd) {
@@ -134,30 +196,19 @@ __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
             ix = s1 ? tx : tx / g.sw;
             ok = ty >= 0 && tx >= 0 && (s1 || (iy * g.sh == ty && ix * g.sw == tx)) && iy < g.oh && ix < g.ow;
           }
-          if (ok) {
-            const int64_t base = MODE == kF32ConvFwd ? (((int64_t)an * g.h + iy) * g.w + ix) * g.c
-                                                     : (((int64_t)an * g.oh + iy) * g.ow + ix) * g.k;
-            if (a.vec_a) {
-              const f4 q = ld4(a.a + base + c.lo);
-              v = q[0];
-              ra[1] = q[1];
-              ra[2] = q[2];
-              ra[3] = q[3];
-            } else {
-              v = a.a[base + c.lo];
-            }
-          } else if (a.vec_a) {
-            ra[1] = ra[2] = ra[3] = 0.f;
-          }
-        } else if (a.vec_a) {
-          ra[1] = ra[2] = ra[3] = 0.f;
+          ok = ok && arow && kk + i < kend;
+          const int64_t base = MODE == kF32ConvFwd ? (((int64_t)an * g.h + iy) * g.w + ix) * g.c
+                                                   : (((int64_t)an * g.oh + iy) * g.ow + ix) * g.k;
+          if constexpr (VA)
+            lda4(r, ok, base + c.lo);
+          else
+            lda1(r, i, ok, base + c.lo);
+          if (!VA && i < 3) c.step1(g.s, nlo);
         }
-        ra[i] = v;
-        if (!a.vec_a && i < 3) c.step(1, g.s, nlo);
       }
     } else {  // wgrad: A(m = out channel, j) = dy[j][m]
 #pragma unroll
-      for (int i = 0; i < 4; ++i) ra[i] = (arow && kk + i < kend) ? a.a[(int64_t)(kk + i) * g.k + am] : 0.f;
+      for (int i = 0; i < 4; ++i) lda1(r, i, arow && kk + i < kend, (int64_t)(kk + i) * g.k + am);
     }
 
     const int kr = k0 + kl;  // B: reduction index of this thread's row
@@ -165,40 +216,27 @@ __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
     if constexpr (MODE == kF32ConvWgrad) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        float v = 0.f;
-        if (a.vec_b && i > 0) {
-          v = rb[i];
-        } else if (brow && bn + i < a.N) {
+        const int n = bn + i;
+        const bool ones = n == a.ones_n;  // the appended column of ones (bias gradient)
+        r.ob |= (ones && brow) ? 1u << i : 0u;
+        if (!VB || i == 0) {  // a 16-B quad at slot 0 (the ones column starts a quad), or one element per slot
           const int iy = kb.mid * g.sh - g.pt + wr[i] * g.dh, ix = kb.lo * g.sw - g.pl + ws_[i] * g.dw;
-          if (iy >= 0 && iy < g.h && ix >= 0 && ix < g.w) {
-            const int64_t base = (((int64_t)kb.hi * g.h + iy) * g.w + ix) * g.c + wc[i];
-            if (a.vec_b) {
-              const f4 q = ld4(a.b + base);
-              v = q[0];
-              rb[1] = q[1];
-              rb[2] = q[2];
-              rb[3] = q[3];
-            } else {
-              v = a.b[base];
-            }
-          } else if (a.vec_b) {
-            rb[1] = rb[2] = rb[3] = 0.f;
-          }
-        } else if (a.vec_b) {
-          rb[1] = rb[2] = rb[3] = 0.f;
+          const bool ok = !ones && brow && n < a.N && iy >= 0 && iy < g.h && ix >= 0 && ix < g.w;
+          const int64_t e = (((int64_t)kb.hi * g.h + iy) * g.w + ix) * g.c + wc[i];
+          if constexpr (VB)
+            ldb4(r, ok, e);
+          else
+            ldb1(r, i, ok, e);
         }
-        rb[i] = v;
       }
     } else {
       const int64_t sbk = MODE == kF32Gemm ? a.sbk : (int64_t)a.N;
       const int64_t sbn = MODE == kF32Gemm ? a.sbn : 1;
-      if (a.vec_b && brow && bn < a.N) {
-        const f4 v = ld4(a.b + (int64_t)kr * sbk + bn);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) rb[i] = v[i];
+      if constexpr (VB) {
+        ldb4(r, brow && bn < a.N, (int64_t)kr * sbk + bn);
       } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) rb[i] = (brow && bn + i < a.N) ? a.b[(int64_t)kr * sbk + (int64_t)(bn + i) * sbn] : 0.f;
+        for (int i = 0; i < 4; ++i) ldb1(r, i, brow && bn + i < a.N, (int64_t)kr * sbk + (int64_t)(bn + i) * sbn);
       }
     }
   };
@@ -211,29 +249,65 @@ __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
 
   const int wm = (wave & 1) * 32, wn = (wave >> 1) * 32;
   const int lr = lane & 15, lk = lane >> 4;
-  load(kbeg);
-  for (int k0 = kbeg; k0 < kend; k0 += 16) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) As[(kqa + i) * kLd + ml] = ra[i];
-    st4(&Bs[kl * kLd + nqb], f4{rb[0], rb[1], rb[2], rb[3]});
-    __syncthreads();
-    if (k0 + 16 < kend) {
-      if constexpr (MODE == kF32ConvFwd) ka.step(16, g.s, g.c);
-      if constexpr (MODE == kF32ConvDgrad) ka.step(16, g.s, g.k);
-      if constexpr (MODE == kF32ConvWgrad) kb.step(16, g.oh, g.ow);
-      load(k0 + 16);
+  // Register ring of kDepth slices: slice k + kDepth is loaded while slice k is multiplied, so a
+  // long reduction pays the global-load latency once per kDepth slices, not once per slice (the
+  // small-M / long-K shapes of the generic engine are latency-bound: few workgroups, many slices).
+  constexpr int kDepth = 4;
+  S ring[kDepth];
+  int kload = kbeg;  // reduction index of the next slice to load (the counters track the last one)
+  // (no branches around the loads: slices past kend load clamped addresses and become zeros, so
+  // the loop body is straight-line and the waits before each LDS write are exact vmcnt counts)
+  auto issue = [&](S& r) {
+    if (kload < kend) {  // (uniform; past the end the registers keep stale values, never stored)
+      if (kload != kbeg) {
+        if constexpr (MODE == kF32ConvFwd) ka.step(16, g.s, g.c);
+        if constexpr (MODE == kF32ConvDgrad) ka.step(16, g.s, g.k);
+        if constexpr (MODE == kF32ConvWgrad) kb.step(16, g.oh, g.ow);
+      }
+      load(kload, r);
     }
+    kload += 16;
+  };
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const int kr = (4 * ks + lk) * kLd;
-      const float a0 = As[kr + wm + lr], a1 = As[kr + wm + 16 + lr];
-      const float b0 = Bs[kr + wn + lr], b1 = Bs[kr + wn + 16 + lr];
-      acc[0][0] = mfma16x16x4(a0, b0, acc[0][0]);
-      acc[0][1] = mfma16x16x4(a0, b1, acc[0][1]);
-      acc[1][0] = mfma16x16x4(a1, b0, acc[1][0]);
-      acc[1][1] = mfma16x16x4(a1, b1, acc[1][1]);
+  for (int d = 0; d < kDepth; ++d) issue(ring[d]);
+  for (int k0 = kbeg; k0 < kend; k0 += 16 * kDepth) {
+#pragma unroll
+    for (int d = 0; d < kDepth; ++d) {
+      // (the LDS / MFMA work of slices past kend is skipped by a uniform branch; the loads are not
+      // (clamped, invalid), so no load sits in a branch and every wait stays an exact count)
+      const bool live = k0 + 16 * d < kend;
+      S& r = ring[d];
+      if (live) {
+        float av[4], bv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          av[i] = (r.va >> i & 1u) ? r.a[i] : 0.f;
+          bv[i] = (r.vb >> i & 1u) ? r.b[i] : 0.f;
+          if constexpr (MA) av[i] = r.ma[i] > 0.f ? av[i] : 0.f;
+          if constexpr (MB) bv[i] = r.mb[i] > 0.f ? bv[i] : 0.f;
+          av[i] = (r.oa >> i & 1u) ? 1.f : av[i];
+          bv[i] = (r.ob >> i & 1u) ? 1.f : bv[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) As[(kqa + i) * kLd + ml] = av[i];
+        st4(&Bs[kl * kLd + nqb], f4{bv[0], bv[1], bv[2], bv[3]});
+        __syncthreads();
+      }
+      issue(r);  // slice k0 + 16 (d + kDepth) into the registers just stored
+      if (live) {
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const int kr = (4 * ks + lk) * kLd;
+          const float a0 = As[kr + wm + lr], a1 = As[kr + wm + 16 + lr];
+          const float b0 = Bs[kr + wn + lr], b1 = Bs[kr + wn + 16 + lr];
+          acc[0][0] = mfma16x16x4(a0, b0, acc[0][0]);
+          acc[0][1] = mfma16x16x4(a0, b1, acc[0][1]);
+          acc[1][0] = mfma16x16x4(a1, b0, acc[1][0]);
+          acc[1][1] = mfma16x16x4(a1, b1, acc[1][1]);
+        }
+        __syncthreads();
+      }
     }
-    __syncthreads();
   }
 
   // D[(lane >> 4) * 4 + r][lane & 15] of each 16x16 block
@@ -253,13 +327,11 @@ __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
 }
 
 __device__ __forceinline__ void out_index(const F32GemmArgs& a, int64_t e, int& m, int& n) {
-  if (a.trans_out) {
-    n = (int)(e / a.M);
-    m = (int)(e - (int64_t)n * a.M);
-  } else {
-    m = (int)(e / a.N);
-    n = (int)(e - (int64_t)m * a.N);
-  }
+  // (selects, not branches writing through the references: the compiler spilled those to scratch)
+  const int64_t inner = a.trans_out ? a.M : a.N;
+  const int q = (int)(e / inner), r = (int)(e - (int64_t)q * inner);
+  m = a.trans_out ? r : q;
+  n = a.trans_out ? q : r;
 }
 
 // Split-reduction epilogue: the slices summed in a fixed order, then bias / accumulate / store.
@@ -301,16 +373,37 @@ __global__ __launch_bounds__(256) void k_gemm_f32_reduce_wave(F32GemmArgs a) {
   if (lane == 0) out_store(a, m, n, v);
 }
 
+// the operand-vectorisation instantiation of a (mode, mask) kernel
+template <int MODE, bool MA, bool MB>
+void launch_v(const F32GemmArgs& a, dim3 grid, hipStream_t s) {
+  if (a.vec_a && a.vec_b) hipLaunchKernelGGL((k_gemm_f32<MODE, MA, MB, true, true>), grid, dim3(256), 0, s, a);
+  else if (a.vec_a) hipLaunchKernelGGL((k_gemm_f32<MODE, MA, MB, true, false>), grid, dim3(256), 0, s, a);
+  else if (a.vec_b) hipLaunchKernelGGL((k_gemm_f32<MODE, MA, MB, false, true>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((k_gemm_f32<MODE, MA, MB, false, false>), grid, dim3(256), 0, s, a);
+}
+
 }  // namespace
 
 void f32_gemm_launch(int mode, const F32GemmArgs& a, hipStream_t s) {
   if (a.M <= 0 || a.N <= 0) return;
   const dim3 grid((a.M + kF32Tile - 1) / kF32Tile, (a.N + kF32Tile - 1) / kF32Tile, a.splits);
+  const bool ma = a.amask != nullptr, mb = a.bmask != nullptr;
   switch (mode) {
-    case kF32Gemm: hipLaunchKernelGGL(k_gemm_f32<kF32Gemm>, grid, dim3(256), 0, s, a); break;
-    case kF32ConvFwd: hipLaunchKernelGGL(k_gemm_f32<kF32ConvFwd>, grid, dim3(256), 0, s, a); break;
-    case kF32ConvDgrad: hipLaunchKernelGGL(k_gemm_f32<kF32ConvDgrad>, grid, dim3(256), 0, s, a); break;
-    default: hipLaunchKernelGGL(k_gemm_f32<kF32ConvWgrad>, grid, dim3(256), 0, s, a); break;
+    case kF32Gemm:
+      if (ma && mb) launch_v<kF32Gemm, true, true>(a, grid, s);
+      else if (ma) launch_v<kF32Gemm, true, false>(a, grid, s);
+      else if (mb) launch_v<kF32Gemm, false, true>(a, grid, s);
+      else launch_v<kF32Gemm, false, false>(a, grid, s);
+      break;
+    case kF32ConvFwd: launch_v<kF32ConvFwd, false, false>(a, grid, s); break;
+    case kF32ConvDgrad:
+      if (ma) launch_v<kF32ConvDgrad, true, false>(a, grid, s);
+      else launch_v<kF32ConvDgrad, false, false>(a, grid, s);
+      break;
+    default:
+      if (ma) launch_v<kF32ConvWgrad, true, false>(a, grid, s);
+      else launch_v<kF32ConvWgrad, false, false>(a, grid, s);
+      break;
   }
   if (a.splits > 1) {
     const int64_t mn = (int64_t)a.M * a.N;

@@ -674,9 +674,30 @@ at::Tensor f32_out(c10::optional<at::Tensor>& out, at::IntArrayRef shape, const 
   return fresh(shape, o);
 }
 
-// C = op(A) op(B) (+ bias) in f32; ta = 0: a is [M][K], 1: [K][M]; tb = 0: b is [N][K], 1: [K][N]
+// ReLU mask of an operand (the layer's output, same layout as the operand): nullptr when absent
+const float* f32_mask(const c10::optional<at::Tensor>& mask, const at::Tensor& like, const char* what) {
+  if (!mask.has_value() || !mask->defined()) return nullptr;
+  f32_check(*mask, what);
+  TORCH_CHECK(mask->numel() == like.numel(), what, " must have the operand's shape");
+  return mask->data_ptr<float>();
+}
+bool mask_al16(const c10::optional<at::Tensor>& mask) {
+  return !mask.has_value() || !mask->defined() || al16(*mask);
+}
+// bias gradient target [n] (written, or += when accumulating)
+float* f32_dbias(c10::optional<at::Tensor>& dbias, int64_t n) {
+  if (!dbias.has_value() || !dbias->defined()) return nullptr;
+  f32_check(*dbias, "f32 gemm: dbias");
+  TORCH_CHECK(dbias->numel() == n, "f32 gemm: dbias must have ", n, " elements");
+  return dbias->data_ptr<float>();
+}
+
+// C = op(A) op(B) (+ bias) in f32; ta = 0: a is [M][K], 1: [K][M]; tb = 0: b is [N][K], 1: [K][N].
+// act = 1: ReLU epilogue.  amask / bmask: operand * (mask > 0) (ReLU backward).  dbias: a row of ones
+// appended to A, its output row (the column sums of op(B): a bias gradient) written to dbias.
 at::Tensor gemm_f32(at::Tensor a, int64_t ta, at::Tensor b, int64_t tb, c10::optional<at::Tensor> bias,
-                    c10::optional<at::Tensor> out, bool accumulate) {
+                    c10::optional<at::Tensor> out, bool accumulate, int64_t act, c10::optional<at::Tensor> amask,
+                    c10::optional<at::Tensor> bmask, c10::optional<at::Tensor> dbias) {
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "gemm_f32: 2-D operands");
   f32_check(a, "gemm_f32: a");
   f32_check(b, "gemm_f32: b");
@@ -698,8 +719,16 @@ at::Tensor gemm_f32(at::Tensor a, int64_t ta, at::Tensor b, int64_t tb, c10::opt
   g.Kred = (int)K;
   g.ldo = N;
   g.accumulate = accumulate && out.has_value() && out->defined();
-  g.vec_a = g.sak == 1 && g.sam % 4 == 0 && K % 4 == 0 && al16(a);
-  g.vec_b = g.sbn == 1 && g.sbk % 4 == 0 && N % 4 == 0 && al16(b);
+  g.act = (int)act;
+  g.amask = f32_mask(amask, a, "gemm_f32: amask");
+  g.bmask = f32_mask(bmask, b, "gemm_f32: bmask");
+  g.vec_a = g.sak == 1 && g.sam % 4 == 0 && K % 4 == 0 && al16(a) && mask_al16(amask);
+  g.vec_b = g.sbn == 1 && g.sbk % 4 == 0 && N % 4 == 0 && al16(b) && mask_al16(bmask);
+  g.dbias = f32_dbias(dbias, N);
+  if (g.dbias != nullptr) {
+    TORCH_CHECK(act == 0, "gemm_f32: dbias with an activation epilogue");
+    g.ones_m = g.M++;  // the appended row of ones
+  }
   f32_run(tdl::kF32Gemm, g, a.options());
   return c;
 }
@@ -728,7 +757,7 @@ tdl::F32ConvGeom f32_geom(const at::Tensor& x_like, int64_t k, int64_t r, int64_
 
 // y[N][OH][OW][K] = conv(x NHWC, w HWIO) (+ bias); padding (pt, pl) top / left, the rest implied by OH / OW
 at::Tensor conv_f32_fwd(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> bias, int64_t oh, int64_t ow, int64_t sh,
-                        int64_t sw, int64_t pt, int64_t pl, int64_t dh, int64_t dw) {
+                        int64_t sw, int64_t pt, int64_t pl, int64_t dh, int64_t dw, int64_t act) {
   f32_check(x, "conv_f32_fwd: x");
   f32_check(w, "conv_f32_fwd: w");
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && w.size(2) == x.size(3), "conv_f32_fwd: x NHWC, w [R][S][C][K]");
@@ -746,13 +775,14 @@ at::Tensor conv_f32_fwd(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> bi
   g.ldo = K;
   g.vec_a = x.size(3) % 4 == 0 && al16(x);
   g.vec_b = K % 4 == 0 && al16(w);
+  g.act = (int)act;
   f32_run(tdl::kF32ConvFwd, g, x.options());
   return y;
 }
 
 // dx[N][H][W][C] of a conv with dy [N][OH][OW][K] and wt = w as [R][S][K][C]
 at::Tensor conv_f32_dgrad(at::Tensor dy, at::Tensor wt, int64_t h, int64_t wd, int64_t sh, int64_t sw, int64_t pt,
-                          int64_t pl, int64_t dh, int64_t dw) {
+                          int64_t pl, int64_t dh, int64_t dw, c10::optional<at::Tensor> dy_mask) {
   f32_check(dy, "conv_f32_dgrad: dy");
   f32_check(wt, "conv_f32_dgrad: wt");
   TORCH_CHECK(dy.dim() == 4 && wt.dim() == 4 && wt.size(2) == dy.size(3), "conv_f32_dgrad: dy NHWC, wt [R][S][K][C]");
@@ -767,7 +797,8 @@ at::Tensor conv_f32_dgrad(at::Tensor dy, at::Tensor wt, int64_t h, int64_t wd, i
   g.N = (int)C;
   g.Kred = (int)(wt.size(0) * wt.size(1) * K);
   g.ldo = C;
-  g.vec_a = K % 4 == 0 && al16(dy);
+  g.amask = f32_mask(dy_mask, dy, "conv_f32_dgrad: dy_mask");
+  g.vec_a = K % 4 == 0 && al16(dy) && mask_al16(dy_mask);
   g.vec_b = C % 4 == 0 && al16(wt);
   f32_run(tdl::kF32ConvDgrad, g, dy.options());
   return dx;
@@ -775,7 +806,8 @@ at::Tensor conv_f32_dgrad(at::Tensor dy, at::Tensor wt, int64_t h, int64_t wd, i
 
 // dW HWIO [R][S][C][K] of a conv with x NHWC and dy [N][OH][OW][K] (into / += out when given)
 at::Tensor conv_f32_wgrad(at::Tensor x, at::Tensor dy, int64_t r, int64_t s, int64_t sh, int64_t sw, int64_t pt,
-                          int64_t pl, int64_t dh, int64_t dw, c10::optional<at::Tensor> out, bool accumulate) {
+                          int64_t pl, int64_t dh, int64_t dw, c10::optional<at::Tensor> out, bool accumulate,
+                          c10::optional<at::Tensor> dy_mask, c10::optional<at::Tensor> dbias) {
   f32_check(x, "conv_f32_wgrad: x");
   f32_check(dy, "conv_f32_wgrad: dy");
   TORCH_CHECK(x.dim() == 4 && dy.dim() == 4 && x.size(0) == dy.size(0), "conv_f32_wgrad: x, dy NHWC");
@@ -794,6 +826,9 @@ at::Tensor conv_f32_wgrad(at::Tensor x, at::Tensor dy, int64_t r, int64_t s, int
   g.trans_out = 1;
   g.accumulate = accumulate && out.has_value() && out->defined();
   g.vec_b = C % 4 == 0 && al16(x);
+  g.amask = f32_mask(dy_mask, dy, "conv_f32_wgrad: dy_mask");
+  g.dbias = f32_dbias(dbias, K);
+  if (g.dbias != nullptr) g.ones_n = g.N++;  // the appended column of ones: sum over pixels of dy
   f32_run(tdl::kF32ConvWgrad, g, x.options());
   return dW;
 }
@@ -825,6 +860,30 @@ std::vector<at::Tensor> xent_fwd(at::Tensor z, at::Tensor labels) {
   return {loss, lse};
 }
 
+double* f64_scalar(const c10::optional<at::Tensor>& t, const char* what) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kDouble && t->numel() == 1, what, ": f64 GPU scalar expected");
+  return t->data_ptr<double>();
+}
+
+// the generic engine's fused loss head: (loss [] = sum / gn, dz [N][K] = (softmax - onehot) / gn), metric
+// accumulators advanced in place
+std::vector<at::Tensor> xent_head(at::Tensor z, at::Tensor labels, double gn, c10::optional<at::Tensor> lt_total,
+                                  c10::optional<at::Tensor> lt_count, c10::optional<at::Tensor> acc_total,
+                                  c10::optional<at::Tensor> acc_count) {
+  TORCH_CHECK(z.is_cuda() && z.is_contiguous() && z.scalar_type() == at::kFloat && z.dim() == 2, "xent_head: f32 [N][K] logits");
+  TORCH_CHECK(labels.is_cuda() && labels.is_contiguous() && labels.scalar_type() == at::kLong &&
+                  labels.numel() == z.size(0), "xent_head: int64 [N] labels");
+  TORCH_CHECK(gn > 0, "xent_head: global batch must be positive");
+  auto loss = at::empty({}, z.options());
+  auto dz = fresh(z.sizes(), z.options());
+  tdl::xent_head(z.data_ptr<float>(), reinterpret_cast<const long long*>(labels.data_ptr<int64_t>()), (int)z.size(0),
+                 (int)z.size(1), gn, loss.data_ptr<float>(), dz.data_ptr<float>(), f64_scalar(lt_total, "lt_total"),
+                 f64_scalar(lt_count, "lt_count"), f64_scalar(acc_total, "acc_total"), f64_scalar(acc_count, "acc_count"),
+                 cur_stream());
+  return {loss, dz};
+}
+
 at::Tensor xent_bwd(at::Tensor z, at::Tensor labels, at::Tensor g) {
   TORCH_CHECK(z.is_cuda() && z.is_contiguous() && z.scalar_type() == at::kFloat && z.dim() == 2, "xent: f32 [N][K] logits");
   TORCH_CHECK(labels.is_contiguous() && labels.scalar_type() == at::kLong && labels.numel() == z.size(0), "xent: labels");
@@ -839,25 +898,35 @@ at::Tensor xent_bwd(at::Tensor z, at::Tensor labels, at::Tensor g) {
 void register_ops(pybind11::module& m) {
   m.def("xent_fwd", &xent_fwd, "sparse softmax cross-entropy forward: (loss, logsumexp)");
   m.def("xent_bwd", &xent_bwd, "sparse softmax cross-entropy backward: (softmax - onehot) * g");
+  m.def("xent_head", &xent_head, "fused loss head: mean-reduced sparse softmax cross-entropy, its dlogits and "
+        "the loss / accuracy metric accumulators", pybind11::arg("z"), pybind11::arg("labels"), pybind11::arg("gn"),
+        pybind11::arg("lt_total") = pybind11::none(), pybind11::arg("lt_count") = pybind11::none(),
+        pybind11::arg("acc_total") = pybind11::none(), pybind11::arg("acc_count") = pybind11::none());
   m.def("gemm_bf16", &gemm_bf16, "bf16 MFMA GEMM with either storage per operand (Dense fwd / dgrad / wgrad)",
         pybind11::arg("a"), pybind11::arg("ta"), pybind11::arg("b"), pybind11::arg("tb"),
         pybind11::arg("bias") = pybind11::none(), pybind11::arg("out") = pybind11::none(),
         pybind11::arg("accumulate") = false, pybind11::arg("alpha") = 1.0);
-  m.def("gemm_f32", &gemm_f32, "f32 MFMA GEMM (v_mfma_f32_16x16x4_f32) with either storage per operand",
+  m.def("gemm_f32", &gemm_f32, "f32 MFMA GEMM (v_mfma_f32_16x16x4_f32) with either storage per operand; "
+        "ReLU epilogue, ReLU-masked operands, bias gradient as an appended row of ones",
         pybind11::arg("a"), pybind11::arg("ta"), pybind11::arg("b"), pybind11::arg("tb"),
         pybind11::arg("bias") = pybind11::none(), pybind11::arg("out") = pybind11::none(),
-        pybind11::arg("accumulate") = false);
-  m.def("conv_f32_fwd", &conv_f32_fwd, "NHWC f32 implicit-GEMM convolution forward, any geometry",
+        pybind11::arg("accumulate") = false, pybind11::arg("act") = 0, pybind11::arg("amask") = pybind11::none(),
+        pybind11::arg("bmask") = pybind11::none(), pybind11::arg("dbias") = pybind11::none());
+  m.def("conv_f32_fwd", &conv_f32_fwd, "NHWC f32 implicit-GEMM convolution forward, any geometry (act 1: + ReLU)",
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("bias"), pybind11::arg("oh"), pybind11::arg("ow"),
         pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("pt"), pybind11::arg("pl"), pybind11::arg("dh") = 1,
-        pybind11::arg("dw") = 1);
-  m.def("conv_f32_dgrad", &conv_f32_dgrad, "NHWC f32 convolution input gradient, any geometry (wt: [R][S][K][C])",
+        pybind11::arg("dw") = 1, pybind11::arg("act") = 0);
+  m.def("conv_f32_dgrad", &conv_f32_dgrad, "NHWC f32 convolution input gradient, any geometry (wt: [R][S][K][C]); "
+        "dy_mask: dy * (mask > 0)",
         pybind11::arg("dy"), pybind11::arg("wt"), pybind11::arg("h"), pybind11::arg("w"), pybind11::arg("sh"),
-        pybind11::arg("sw"), pybind11::arg("pt"), pybind11::arg("pl"), pybind11::arg("dh") = 1, pybind11::arg("dw") = 1);
-  m.def("conv_f32_wgrad", &conv_f32_wgrad, "NHWC f32 convolution weight gradient (HWIO), deterministic split-K",
+        pybind11::arg("sw"), pybind11::arg("pt"), pybind11::arg("pl"), pybind11::arg("dh") = 1, pybind11::arg("dw") = 1,
+        pybind11::arg("dy_mask") = pybind11::none());
+  m.def("conv_f32_wgrad", &conv_f32_wgrad, "NHWC f32 convolution weight gradient (HWIO), deterministic split-K; "
+        "dy_mask: dy * (mask > 0); dbias: the bias gradient from an appended column of ones",
         pybind11::arg("x"), pybind11::arg("dy"), pybind11::arg("r"), pybind11::arg("s"), pybind11::arg("sh"),
         pybind11::arg("sw"), pybind11::arg("pt"), pybind11::arg("pl"), pybind11::arg("dh") = 1, pybind11::arg("dw") = 1,
-        pybind11::arg("out") = pybind11::none(), pybind11::arg("accumulate") = false);
+        pybind11::arg("out") = pybind11::none(), pybind11::arg("accumulate") = false,
+        pybind11::arg("dy_mask") = pybind11::none(), pybind11::arg("dbias") = pybind11::none());
   m.def("gap_fwd", &gap_fwd, "NHWC bf16 global average pooling");
   m.def("gap_bwd", &gap_bwd, "NHWC bf16 global average pooling backward");
   m.def("slab_cast_bf16", &slab_cast_bf16, "f32 -> bf16 copy of a whole weight slab (one launch)");

@@ -18,6 +18,7 @@ import math
 import os
 from typing import Dict, List, Optional, Tuple
 
+import numpy as np
 import torch
 
 from ..data import dataset as D
@@ -324,6 +325,13 @@ class GenericTrainer:
             ctx = torch.autocast(self.device.type, enabled=False)
         with ctx:
             y_pred = model(x, training=True)
+        fused = self._fused_head(y, y_pred, sw)
+        if fused is not None:
+            loss = fused(global_n)
+            reg = model._regularization_loss()
+            if reg is not None:
+                loss = loss + reg / self.strategy.num_replicas_in_sync
+            return loss, None, y_pred
         per_ex = self.loss.per_example(y, y_pred.float() if y_pred.dtype != torch.float32 else y_pred)
         if sw is not None:
             per_ex = per_ex * sw.to(per_ex.dtype)
@@ -334,7 +342,34 @@ class GenericTrainer:
             loss = loss + reg / self.strategy.num_replicas_in_sync
         return loss, per_ex, y_pred
 
-    def train_step(self, batch, global_n: int, sync_lr: bool = True):
+    def _fused_head(self, y, y_pred, sw):
+        """The one-kernel loss head (ops/dense.py xent_head) when the step's loss and metrics are what it
+        computes: SparseCategoricalCrossentropy(from_logits=True) on f32 2-D logits, no sample weights,
+        metrics none or SparseCategoricalAccuracy.  Returns ``f(global_n) -> loss`` (the metric
+        accumulators are advanced by the kernel), or None."""
+        from ..keras import losses as _losses
+        from ..keras import metrics as _metrics
+        from ..ops import dense as _dense
+
+        if (sw is not None or y is None or os.environ.get("TDL_FUSED_HEAD", "1") != "1" or
+                not isinstance(self.loss, _losses.SparseCategoricalCrossentropy) or not self.loss.from_logits or
+                self.loss.ignore_class is not None or y_pred.dtype != torch.float32 or y_pred.dim() != 2 or
+                y.dim() != 1 or not _dense.xent_head_supported(y_pred, y.long())):
+            return None
+        if len(self.metrics) > 1 or (self.metrics and type(self.metrics[0]) is not _metrics.SparseCategoricalAccuracy):
+            return None
+        accs = []
+        for m in [self.loss_tracker] + list(self.metrics):
+            m._to(y_pred.device)
+            accs += [m.total._value, m.count._value]
+        while len(accs) < 4:
+            accs.append(None)
+        labels = y.long()
+        return lambda gn: _dense.xent_head(y_pred, labels, gn, accs[:2], accs[2:])
+
+    def train_step(self, batch, global_n: int, sync_lr: bool = True, t_add: int = 0):
+        """One whole step.  ``t_add``: the step's offset inside a multi-step execution graph whose
+        first step count is the optimizer's device ``t_dev`` (Adam's bias correction)."""
         x, y, sw = _split_xy(_to_device(batch, self.device))
         from ..utils import fault
 
@@ -408,15 +443,18 @@ class GenericTrainer:
                 else:
                     self.comm.all_reduce(G, "sum")
         with torch.no_grad(), trace_range("tdl.optimizer"):
-            self.optimizer.apply_flat(self.W, G, sync_lr=sync_lr)
+            self.optimizer.apply_flat(self.W, G, sync_lr=sync_lr, t_add=t_add)
             if _ck.enabled():
                 _ck.record("slab_W", self.W)
-            self.loss_tracker.update_state(per_ex.detach())
-            yp = y_pred.detach()
-            for m in self.metrics:
-                m.update_state(y, yp, sw)
+            if per_ex is not None:  # (the fused loss head advanced the metric accumulators itself)
+                self.loss_tracker.update_state(per_ex.detach())
+                yp = y_pred.detach()
+                for m in self.metrics:
+                    m.update_state(y, yp, sw)
 
-    def run_train(self, handler: HostDataHandler, steps: int) -> int:
+    def run_train(self, handler, steps: int) -> int:
+        if not isinstance(handler, HostDataHandler) and hasattr(handler, "take"):
+            return self._run_device(handler, steps)
         done = 0
         for _ in range(steps):
             try:
@@ -489,6 +527,156 @@ class GenericTrainer:
             self.optimizer.iterations = it0  # capture records, it does not run a step
         torch.cuda.current_stream(dev).wait_stream(s)
         return static, graph
+
+    # ------------------------------------------------------------------ device-resident executions
+    def prepare(self, dataset):
+        """Device-resident input for ANY model (the fused engine's data path, data/device.py): an
+        in-memory ``[map].cache().shuffle().batch().repeat()`` pipeline of (features, labels) is
+        uploaded to HBM once, and each execution of ``steps_per_execution`` steps is ONE captured
+        hipGraph that gathers its batches from HBM by the execution's index vector (one async H2D
+        copy per execution) and runs K whole steps: forward, backward, all-reduce, optimizer and
+        metrics (TF's ``steps_per_execution``: K steps per ``tf.function`` call).  None: host pipeline.
+        TDL_GENERIC_DEVICE_DATA=0 keeps the host pipeline."""
+        if self.device.type != "cuda" or os.environ.get("TDL_GENERIC_DEVICE_DATA", "1") != "1":
+            return None
+        from ..data import device as DD
+        from . import fused as F
+
+        lp = DD.lower(dataset)
+        if lp is None or not isinstance(lp.columns, (tuple, list)) or len(lp.columns) != 2:
+            return None
+        x, y = lp.columns
+        if not (isinstance(x, torch.Tensor) and isinstance(y, torch.Tensor)) or not x.is_floating_point():
+            return None
+        R = self.comm.world_size
+        if lp.batch_size % R or not self._graphable():  # (_graphable is collective at R > 1: every rank is here)
+            return None
+        key = (x.data_ptr(), tuple(x.shape), y.data_ptr(), tuple(y.shape), x._version, y._version)
+        if getattr(self, "_dev_key", None) != key:
+            self._X = x.to(self.device).contiguous()
+            self._Y = y.to(self.device).contiguous()
+            self._dev_key = key
+        policy = input_lib.effective_policy(dataset) if R > 1 else None
+        seed = input_lib.shared_seed(self.strategy) if policy is not None and policy.name in ("DATA", "FILE") else None
+        return F.DeviceHandler(lp, seed, self.comm.rank, R)
+
+    def _dev_upload(self, idx) -> None:
+        """The execution's sample ids into the device index buffer (stream-ordered after the previous
+        execution's graph, which reads the same buffer), through a ring of pinned staging buffers."""
+        n = int(idx.size)
+        if getattr(self, "_dev_idx", None) is None or self._dev_idx.numel() < n:
+            self._dev_idx = torch.zeros(max(n, 1024), dtype=torch.int32, device=self.device)
+            self._graphs = {k: v for k, v in self._graphs.items() if k[0] != "dev"}  # they read the old buffer
+            self._dev_stage = [None] * 4
+            self._dev_ev = [None] * 4
+            self._dev_slot = 0
+        s = self._dev_slot
+        self._dev_slot = (s + 1) % len(self._dev_stage)
+        if self._dev_stage[s] is None or self._dev_stage[s].numel() < n:
+            self._dev_stage[s] = torch.empty(self._dev_idx.numel(), dtype=torch.int32, pin_memory=True)
+        elif self._dev_ev[s] is not None:
+            self._dev_ev[s].synchronize()  # the copy out of this staging buffer has run
+        self._dev_stage[s][:n].numpy()[:] = idx
+        self._dev_idx[:n].copy_(self._dev_stage[s][:n], non_blocking=True)
+        if os.environ.get("TDL_DEV_SYNC_UPLOAD", "0") == "1":
+            torch.cuda.current_stream(self.device).synchronize()
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._dev_ev[s] = ev
+
+    def _dev_step(self, k: int, b: int, global_n: int, sync_lr: bool):
+        ii = self._dev_idx[k * b:(k + 1) * b]
+        self.train_step((self._X.index_select(0, ii), self._Y.index_select(0, ii)), global_n, sync_lr=sync_lr,
+                        t_add=k)
+
+    def warm_graphs(self, steps: int, b: Optional[int] = None):
+        """Capture (without running) the execution graphs ``run_train(steps)`` will replay, once a
+        step of this batch size has run eagerly (bench.py: ahead of the timed region)."""
+        b = b if b is not None else getattr(self, "_dev_b", None)
+        if b is None or b not in getattr(self, "_dev_warm", ()) or self._graph_ok is False:
+            return
+        K = max(1, self.model._steps_per_execution)
+        sizes = ({K} if steps >= K else set()) | ({steps % K} if steps % K else set())
+        if getattr(self, "_dev_idx", None) is None or self._dev_idx.numel() < max(sizes) * b:
+            self._dev_upload(np.zeros(max(sizes) * b, dtype=np.int32))
+        for k in sizes:
+            if ("dev", k, b) not in self._graphs:
+                self._dev_capture(k, b)
+
+    def _run_device(self, handler, steps: int) -> int:
+        import gc
+
+        gc.freeze()  # long-lived state out of the cyclic GC's generations (engine/fused.py run_train)
+        done, b, opt = 0, handler.b, self.optimizer
+        self._dev_b = b
+        if not hasattr(self, "_dev_warm"):
+            self._dev_warm = set()
+        spe = max(1, self.model._steps_per_execution)
+        while done < steps:
+            idx = handler.take(min(spe, steps - done))
+            if idx is None:
+                one = handler.next_ragged()  # an epoch's partial batch: one eager step of its size
+                if one is None:
+                    break
+                ids, n, gb = one
+                if n == 0:
+                    raise RuntimeError("generic device path: a replica got no samples of a partial batch")
+                self._dev_upload(ids)
+                opt._sync_lr()
+                self._dev_step(0, n, gb, sync_lr=False)
+                done += 1
+                continue
+            K = idx.size // b
+            if os.environ.get("TDL_DEV_TRACE") == "1":
+                self._dev_trace = getattr(self, "_dev_trace", []) + [np.array(idx)]
+            self._dev_upload(idx)
+            opt._sync_lr()
+            graph = self._graphs.get(("dev", K, b))
+            if (graph is None and b in self._dev_warm and self._graph_ok is not False and
+                    os.environ.get("TDL_GENERIC_DEVICE_EAGER", "0") != "1"):
+                graph = self._dev_capture(K, b)
+            if graph is None:
+                # the first execution at this batch size runs eagerly (allocator warm-up, autotuning
+                # decisions), or every one does when a layer cannot be captured
+                t0 = opt.iterations
+                for k in range(K):
+                    self._dev_step(k, b, b * self.comm.world_size, sync_lr=False)
+                opt.iterations = t0 + K
+                self._dev_warm.add(b)
+            else:
+                graph.replay()
+                opt.iterations += K
+            done += K
+        return done
+
+    def _dev_capture(self, K: int, b: int):
+        dev = self.device
+        torch.cuda.synchronize(dev)
+        graph = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        it0 = self.optimizer.iterations
+        try:
+            pool = None
+            if os.environ.get("TDL_DEV_SHARED_POOL", "0") == "1":
+                if getattr(self, "_dev_pool", None) is None:
+                    self._dev_pool = torch.cuda.graph_pool_handle()
+                pool = self._dev_pool
+            with torch.cuda.graph(graph, stream=s, pool=pool):
+                for k in range(K):
+                    self._dev_step(k, b, b * self.comm.world_size, sync_lr=False)
+        except Exception as e:  # noqa: BLE001 - a layer with host-side logic: stay eager
+            import warnings
+
+            warnings.warn(f"execution graph capture failed, training eagerly: {type(e).__name__}: {e}")
+            torch.cuda.synchronize(dev)
+            self._graph_ok = False
+            return None
+        finally:
+            self.optimizer.iterations = it0  # capture records, it does not run a step
+        torch.cuda.current_stream(dev).wait_stream(s)
+        self._graphs[("dev", K, b)] = graph
+        return graph
 
     @torch.no_grad()
     def test_step(self, batch):

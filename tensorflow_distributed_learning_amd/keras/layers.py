@@ -276,13 +276,15 @@ class Dense(Layer):
             xf = x.float() if low else x
             gw = self.kernel.grad_target()
             gb = self.bias.grad_target() if self.bias is not None else None
+            act = _fused_act(self.activation)  # ReLU inside the GEMMs (forward epilogue, backward masks)
             if gw is not None and gw.is_contiguous() and (self.bias is None or gb is not None):
                 b = self.bias.value.detach() if self.bias is not None else None
-                y = _conv_f32.dense(xf, self.kernel.value.detach(), b, (gw, gb), anchor=self.kernel.value)
+                y = _conv_f32.dense(xf, self.kernel.value.detach(), b, (gw, gb), anchor=self.kernel.value, act=act)
             else:
                 b = self.bias.value if self.bias is not None else None
-                y = _conv_f32.dense(xf, self.kernel.value, b)
-            return self.activation(y.to(torch.bfloat16) if low else y)
+                y = _conv_f32.dense(xf, self.kernel.value, b, act=act)
+            y = y.to(torch.bfloat16) if low else y
+            return y if act else self.activation(y)
         y = torch.matmul(x, self.kernel.cast(x.dtype))
         if self.bias is not None:
             y = y + self.bias.value.to(y.dtype)
@@ -295,6 +297,13 @@ class Dense(Layer):
         return dict(super().get_config(), units=self.units, activation=_act.serialize(self.activation),
                     use_bias=self.use_bias, kernel_initializer=_init.serialize(self.kernel_initializer),
                     bias_initializer=_init.serialize(self.bias_initializer))
+
+
+def _fused_act(fn) -> int:
+    """1 when the layer's activation is the plain ReLU the f32 GEMM kernels fuse (gemm_f32.hip), else 0."""
+    import os
+
+    return 1 if fn is _act.relu and os.environ.get("TDL_FUSE_ACT", "1") == "1" else 0
 
 
 def _autocast_input(x):
@@ -424,12 +433,19 @@ class Conv2D(Layer):
                 pw = _same_pads(x.shape[2], self.kernel_size[1], self.strides[1], self.dilation_rate[1])
                 pads = (ph[0], ph[1], pw[0], pw[1])
             gt = self.kernel.grad_target()
+            gb = None
             if gt is not None and gt.is_contiguous():
                 wv, anchor = self.kernel.value.detach(), self.kernel.value
+                if b is not None:
+                    gb = self.bias.grad_target()
+                    if gb is not None:  # the bias gradient from the weight-gradient kernel, into the slab
+                        b = self.bias.value.detach().to(x.dtype)
             else:
                 gt, wv, anchor = None, self.kernel.cast(x.dtype), None
-            y = _conv_f32.conv2d(x, wv, b, self.strides, pads, self.dilation_rate, grad_out=gt, anchor=anchor)
-            return self.activation(y)
+            act = _fused_act(self.activation)  # ReLU inside the GEMMs (forward epilogue, backward masks)
+            y = _conv_f32.conv2d(x, wv, b, self.strides, pads, self.dilation_rate, grad_out=gt, anchor=anchor, act=act,
+                                 gb_out=gb)
+            return y if act else self.activation(y)
         if x.is_cuda:  # no hand-written kernel covers this conv: library path, counted (ops/conv.py)
             _conv._lib("conv2d", f"{str(x.dtype).replace('torch.', '')} C={x.shape[-1]} K={w.shape[0]} "
                        f"{self.kernel_size[0]}x{self.kernel_size[1]}/{self.strides[0]} {self.padding}")

@@ -110,8 +110,9 @@ class Optimizer:
             n = torch.linalg.vector_norm(G)
             G.mul_(torch.clamp(norm / (n + 1e-12), max=1.0))
 
-    def apply_flat(self, W: torch.Tensor, G: torch.Tensor, sync_lr: bool = True):
-        """w <- update(w, g) over the whole slab (gradients already all-reduced)."""
+    def apply_flat(self, W: torch.Tensor, G: torch.Tensor, sync_lr: bool = True, t_add: int = 0):
+        """w <- update(w, g) over the whole slab (gradients already all-reduced).  ``t_add``: this
+        step's offset from ``t_dev`` inside a multi-step execution (only Adam reads a step count)."""
         if self._n != W.numel() or self._device != W.device:
             self.build(W.numel(), W.device)
         if sync_lr:
@@ -293,13 +294,13 @@ class Adam(Optimizer):
                        int(t_add), self.beta_1, self.beta_2, self.epsilon, float(self.weight_decay or 0.0))
         return True
 
-    def apply_flat(self, W, G, sync_lr: bool = True):
+    def apply_flat(self, W, G, sync_lr: bool = True, t_add: int = 0):
         if self._n != W.numel() or self._device != W.device:
             self.build(W.numel(), W.device)
         if sync_lr:
             self._sync_lr()
         if (self.clipvalue is None and not (self.global_clipnorm or self.clipnorm)
-                and self.device_update(W, G)):  # decay + update in one kernel
+                and self.device_update(W, G, t_add)):  # decay + update in one kernel
             self.iterations += 1
             return
         super().apply_flat(W, G, sync_lr=False)

@@ -33,62 +33,83 @@ def out_size(i, k, s, d, p0, p1):
     return (i + p0 + p1 - (k - 1) * d - 1) // s + 1
 
 
-def fwd(x, w_hwio, bias, stride, pads, dil=(1, 1)) -> torch.Tensor:
-    """f32 ``y = conv(x, w) + bias``; ``pads = (top, bottom, left, right)``."""
+def fwd(x, w_hwio, bias, stride, pads, dil=(1, 1), act=0) -> torch.Tensor:
+    """f32 ``y = conv(x, w) + bias`` (``act=1``: ReLU in the epilogue); ``pads = (top, bottom, left, right)``."""
     R, S = w_hwio.shape[0], w_hwio.shape[1]
     oh = out_size(x.shape[1], R, stride[0], dil[0], pads[0], pads[1])
     ow = out_size(x.shape[2], S, stride[1], dil[1], pads[2], pads[3])
     b = _c32(bias) if bias is not None else None
-    return hip().conv_f32_fwd(_c32(x), _c32(w_hwio), b, oh, ow, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1])
+    return hip().conv_f32_fwd(_c32(x), _c32(w_hwio), b, oh, ow, stride[0], stride[1], pads[0], pads[2], dil[0], dil[1],
+                              act=int(act))
 
 
-def dgrad(dy, w_hwio, hw, stride, pads, dil=(1, 1)) -> torch.Tensor:
-    """f32 input gradient of :func:`fwd` for an input of spatial size ``hw``."""
+def dgrad(dy, w_hwio, hw, stride, pads, dil=(1, 1), dy_mask=None) -> torch.Tensor:
+    """f32 input gradient of :func:`fwd` for an input of spatial size ``hw`` (``dy_mask``: the ReLU
+    output whose mask applies to ``dy``)."""
     wt = _c32(w_hwio).permute(0, 1, 3, 2).contiguous()  # [R][S][K][C]
-    return hip().conv_f32_dgrad(_c32(dy), wt, hw[0], hw[1], stride[0], stride[1], pads[0], pads[2], dil[0], dil[1])
+    return hip().conv_f32_dgrad(_c32(dy), wt, hw[0], hw[1], stride[0], stride[1], pads[0], pads[2], dil[0], dil[1],
+                                dy_mask=dy_mask)
 
 
-def wgrad(x, dy, rs, stride, pads, dil=(1, 1), out=None, accumulate=False) -> torch.Tensor:
-    """f32 HWIO weight gradient of :func:`fwd` (added into the f32 ``out`` when ``accumulate``)."""
+def wgrad(x, dy, rs, stride, pads, dil=(1, 1), out=None, accumulate=False, dy_mask=None, dbias=None) -> torch.Tensor:
+    """f32 HWIO weight gradient of :func:`fwd` (added into the f32 ``out`` when ``accumulate``); with
+    ``dbias`` the bias gradient comes from the same kernel (a column of ones appended to the gathered
+    input: no separate reduction)."""
     return hip().conv_f32_wgrad(_c32(x), _c32(dy), rs[0], rs[1], stride[0], stride[1], pads[0], pads[2], dil[0],
-                                dil[1], out=out, accumulate=accumulate)
+                                dil[1], out=out, accumulate=accumulate, dy_mask=dy_mask, dbias=dbias)
 
 
 class _ConvF32(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, stride, pads, dil, grad_out, anchor=None):
-        y = fwd(x, w, b, stride, pads, dil)
-        ctx.save_for_backward(x, w)
+    def forward(ctx, x, w, b, stride, pads, dil, grad_out, anchor=None, act=0, gb_out=None):
+        y = fwd(x, w, b, stride, pads, dil, act)
+        ctx.save_for_backward(x, w, y if act else None)
         ctx.geo = (stride, pads, dil)
         ctx.has_b = b is not None
-        ctx.grad_out = grad_out
+        ctx.grad_out, ctx.gb_out = grad_out, gb_out
         ctx.dtypes = (x.dtype, w.dtype)
         return y.to(x.dtype)
 
     @staticmethod
     def backward(ctx, dy):
-        x, w = ctx.saved_tensors
+        x, w, y = ctx.saved_tensors
         stride, pads, dil = ctx.geo
+        dy = _c32(dy)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = dgrad(dy, w, (x.shape[1], x.shape[2]), stride, pads, dil).to(ctx.dtypes[0])
+            dx = dgrad(dy, w, (x.shape[1], x.shape[2]), stride, pads, dil, dy_mask=y).to(ctx.dtypes[0])
         rs = (w.shape[0], w.shape[1])
+        want_db = ctx.has_b and (ctx.gb_out is not None or ctx.needs_input_grad[2])
         if ctx.grad_out is not None:
-            wgrad(x, dy, rs, stride, pads, dil, out=ctx.grad_out, accumulate=True)
+            # slab targets: dW (and db, from the same kernel) added in place
+            dbt = ctx.gb_out if ctx.gb_out is not None else (
+                torch.zeros(w.shape[-1], dtype=torch.float32, device=dy.device) if want_db else None)
+            wgrad(x, dy, rs, stride, pads, dil, out=ctx.grad_out, accumulate=True, dy_mask=y, dbias=dbt)
+            if ctx.gb_out is None and want_db:
+                db = dbt
         elif ctx.needs_input_grad[1]:
-            dw = wgrad(x, dy, rs, stride, pads, dil).to(ctx.dtypes[1])
-        if ctx.has_b and ctx.needs_input_grad[2]:
-            db = dy.float().sum((0, 1, 2))
-        return dx, dw, db, None, None, None, None, None
+            dbt = torch.empty(w.shape[-1], dtype=torch.float32, device=dy.device) if want_db else None
+            dw = wgrad(x, dy, rs, stride, pads, dil, dy_mask=y, dbias=dbt).to(ctx.dtypes[1])
+            db = dbt
+        elif want_db:
+            g = dy.float() if y is None else dy.float() * (y > 0)
+            if ctx.gb_out is not None:
+                ctx.gb_out.add_(g.sum((0, 1, 2)))
+            else:
+                db = g.sum((0, 1, 2))
+        return dx, dw, db, None, None, None, None, None, None, None
 
 
-def conv2d(x, w_hwio, bias=None, stride=(1, 1), pads=(0, 0, 0, 0), dil=(1, 1), grad_out=None, anchor=None):
+def conv2d(x, w_hwio, bias=None, stride=(1, 1), pads=(0, 0, 0, 0), dil=(1, 1), grad_out=None, anchor=None, act=0,
+           gb_out=None):
     """``conv(x NHWC, w HWIO) + bias`` with zero padding ``pads = (top, bottom, left, right)``, computed
-    in f32 (bf16 / f16 operands are widened), returned in x's dtype.  ``grad_out``: an f32 HWIO view the
-    weight gradient is ADDED into (``w`` then needs no autograd; ``anchor`` -- the variable's leaf --
-    keeps the backward alive when nothing else needs a gradient, as in ops/conv.py)."""
+    in f32 (bf16 / f16 operands are widened), returned in x's dtype.  ``act=1``: ReLU fused into the
+    epilogue and, in the backward, into the operand loads of the input- and weight-gradient kernels
+    (the mask comes from the saved output).  ``grad_out`` / ``gb_out``: f32 slab views the weight /
+    bias gradients are ADDED into (``w`` / ``bias`` then need no autograd; ``anchor`` -- the variable's
+    leaf -- keeps the backward alive when nothing else needs a gradient, as in ops/conv.py)."""
     return _ConvF32.apply(x, w_hwio, bias, tuple(int(s) for s in stride), tuple(int(p) for p in pads),
-                          tuple(int(d) for d in dil), grad_out, anchor)
+                          tuple(int(d) for d in dil), grad_out, anchor, int(act), gb_out)
 
 
 # ------------------------------------------------------------------------------------------ Dense
@@ -98,12 +119,12 @@ def dense_supported(x: torch.Tensor) -> bool:
 
 class _DenseF32(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, targets, anchor=None):
+    def forward(ctx, x, w, b, targets, anchor=None, act=0):
         C = hip()
         x2 = _c32(x.reshape(-1, x.shape[-1]))
         wc = _c32(w)
-        y = C.gemm_f32(x2, 0, wc, 1, bias=_c32(b) if b is not None else None)
-        ctx.save_for_backward(x2, wc)
+        y = C.gemm_f32(x2, 0, wc, 1, bias=_c32(b) if b is not None else None, act=int(act))
+        ctx.save_for_backward(x2, wc, y if act else None)
         ctx.has_b = b is not None
         ctx.targets = targets
         ctx.xshape = x.shape
@@ -112,25 +133,35 @@ class _DenseF32(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         C = hip()
-        x, w = ctx.saved_tensors
+        x, w, y = ctx.saved_tensors
         dy = _c32(dy.reshape(-1, dy.shape[-1]))
-        dx = C.gemm_f32(dy, 0, w, 0).reshape(ctx.xshape) if ctx.needs_input_grad[0] else None
+        dx = C.gemm_f32(dy, 0, w, 0, amask=y).reshape(ctx.xshape) if ctx.needs_input_grad[0] else None
         gw_t, gb_t = ctx.targets if ctx.targets is not None else (None, None)
         dw = db = None
+        want_db = ctx.has_b and (gb_t is not None or ctx.needs_input_grad[2])
         if gw_t is not None:
-            C.gemm_f32(x, 1, dy, 1, out=gw_t, accumulate=True)
+            # dW (+ db as an appended row of ones) added straight into the slab views
+            dbt = gb_t if gb_t is not None else (
+                torch.zeros(w.shape[1], dtype=torch.float32, device=dy.device) if want_db else None)
+            C.gemm_f32(x, 1, dy, 1, out=gw_t, accumulate=True, bmask=y, dbias=dbt)
+            if gb_t is None and want_db:
+                db = dbt
         elif ctx.needs_input_grad[1]:
-            dw = C.gemm_f32(x, 1, dy, 1)
-        if ctx.has_b:
-            s = dy.sum(0)
+            dbt = torch.empty(w.shape[1], dtype=torch.float32, device=dy.device) if want_db else None
+            dw = C.gemm_f32(x, 1, dy, 1, bmask=y, dbias=dbt)
+            db = dbt
+        elif want_db:
+            s = (dy if y is None else dy * (y > 0)).sum(0)
             if gb_t is not None:
                 gb_t.add_(s)
-            elif ctx.needs_input_grad[2]:
+            else:
                 db = s
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
 
 
-def dense(x, w, b=None, targets=None, anchor=None):
+def dense(x, w, b=None, targets=None, anchor=None, act=0):
     """f32 ``x [..., in] @ w [in, out] (+ b)`` on the f32-MFMA GEMM; ``targets = (dW, db)`` f32 slab views
-    the gradients are added into (as ops/dense.py ``dense_bf16``)."""
-    return _DenseF32.apply(x, w, b, targets, anchor)
+    the gradients are added into (as ops/dense.py ``dense_bf16``); ``act=1``: ReLU fused (epilogue
+    forward; operand masks of the input- and weight-gradient GEMMs backward, the bias gradient as a
+    row of ones in the weight-gradient GEMM)."""
+    return _DenseF32.apply(x, w, b, targets, anchor, int(act))

@@ -111,3 +111,30 @@ def xent_supported(z: torch.Tensor, labels: torch.Tensor) -> bool:
 def softmax_xent(z: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
     """Per-example sparse softmax cross-entropy of f32 logits ``z [N, K]`` and int64 ``labels [N]``."""
     return _SoftmaxXent.apply(z, labels)
+
+
+class _XentHead(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z, labels, gn, accs):
+        loss, dz = hip().xent_head(z.contiguous(), labels.contiguous(), float(gn), *accs)
+        ctx.save_for_backward(dz)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (dz,) = ctx.saved_tensors
+        return dz * g, None, None, None
+
+
+def xent_head_supported(z: torch.Tensor, labels: torch.Tensor) -> bool:
+    """The fused head covers per-replica batches up to 8192 rows of up to 4096 classes (one workgroup)."""
+    return xent_supported(z, labels) and z.shape[0] <= 8192 and z.shape[1] <= 4096
+
+
+def xent_head(z: torch.Tensor, labels: torch.Tensor, global_n: int, loss_acc=(None, None), acc_acc=(None, None)):
+    """The generic engine's loss head in ONE kernel (csrc/kernels/gemm.hip k_xent_head): the mean-reduced
+    sparse softmax cross-entropy ``sum(per-example loss) / global_n`` (tf.nn.compute_average_loss), its
+    logit gradient (saved for the backward), and the loss-tracker / SparseCategoricalAccuracy f64
+    accumulators ``(total, count)`` advanced in place -- instead of ~15 PyTorch reduction / elementwise
+    kernels per step (tf_dist_example.py:49-52)."""
+    return _XentHead.apply(z, labels, float(global_n), tuple(loss_acc) + tuple(acc_acc))

@@ -183,3 +183,90 @@ def test_dense_f32_large_gemm_with_ragged_edges():
     bias = torch.randn(4100, generator=g).cuda()
     y = CF.dense(a, b, bias)
     _close(y, a.double() @ b.double() + bias.double())
+
+
+# ---------------------------------------------------------------------------------------------
+# Fusions used by the generic engine: ReLU in the forward epilogue, the ReLU mask in the backward
+# kernels' operand loads, and the bias gradient from the weight-gradient kernel (a column / row of
+# ones), against float64 autograd of relu(conv + b) / relu(x @ w + b).
+
+@pytest.mark.parametrize("case", CASES[:6], ids=[f"c{i}" for i in range(6)])
+@pytest.mark.parametrize("targets", [False, True], ids=["autograd", "slab"])
+def test_conv_f32_fused_relu_and_bias_grad(case, targets):
+    N, H, W, C, K, R, S, stride, pads, dil = case
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(N, H, W, C, generator=g)
+    w = torch.randn(R, S, C, K, generator=g) / (R * S * C) ** 0.5
+    b = torch.randn(K, generator=g) * 0.3
+    yr, xd, wd, bd = _ref(x, w, b, stride, pads, dil)
+    yr = torch.relu(yr)
+    dy = torch.randn(yr.shape, generator=g)
+    (yr * dy.double()).sum().backward()
+    xc = x.cuda().requires_grad_(True)
+    if targets:
+        gw = torch.full(w.shape, 0.5, device="cuda")  # the kernels ADD into slab views
+        gb = torch.full((K,), 0.25, device="cuda")
+        wl = w.cuda().requires_grad_(True)
+        y = CF.conv2d(xc, w.cuda(), b.cuda(), stride, pads, dil, grad_out=gw, anchor=wl, act=1, gb_out=gb)
+        y.backward(dy.cuda())
+        _close(gw - 0.5, wd.grad)
+        _close(gb - 0.25, bd.grad)
+    else:
+        wc, bc = w.cuda().requires_grad_(True), b.cuda().requires_grad_(True)
+        y = CF.conv2d(xc, wc, bc, stride, pads, dil, act=1)
+        y.backward(dy.cuda())
+        _close(wc.grad, wd.grad)
+        _close(bc.grad, bd.grad)
+    _close(y, yr)
+    _close(xc.grad, xd.grad)
+
+
+@pytest.mark.parametrize("shape", [(64, 1600, 128), (37, 70, 33), (8, 5, 3)])
+@pytest.mark.parametrize("targets", [False, True], ids=["autograd", "slab"])
+def test_dense_f32_fused_relu_and_bias_grad(shape, targets):
+    M, I, O = shape
+    g = torch.Generator().manual_seed(3)
+    x, w, b = torch.randn(M, I, generator=g), torch.randn(I, O, generator=g) / I ** 0.5, torch.randn(O, generator=g)
+    xd, wd, bd = (t.double().requires_grad_(True) for t in (x, w, b))
+    yr = torch.relu(xd @ wd + bd)
+    dy = torch.randn(M, O, generator=g)
+    (yr * dy.double()).sum().backward()
+    xc = x.cuda().requires_grad_(True)
+    if targets:
+        gw, gb = torch.zeros(I, O, device="cuda"), torch.zeros(O, device="cuda")
+        y = CF.dense(xc, w.cuda(), b.cuda(), (gw, gb), anchor=w.cuda().requires_grad_(True), act=1)
+        y.backward(dy.cuda())
+        _close(gw, wd.grad)
+        _close(gb, bd.grad)
+    else:
+        wc, bc = w.cuda().requires_grad_(True), b.cuda().requires_grad_(True)
+        y = CF.dense(xc, wc, bc, act=1)
+        y.backward(dy.cuda())
+        _close(wc.grad, wd.grad)
+        _close(bc.grad, bd.grad)
+    _close(y, yr)
+    _close(xc.grad, xd.grad)
+
+
+@pytest.mark.parametrize("NK", [(64, 10), (300, 1000), (7, 3)])
+def test_xent_head_loss_grad_and_metrics(NK):
+    from tensorflow_distributed_learning_amd.ops import dense as D
+
+    N, K = NK
+    g = torch.Generator().manual_seed(4)
+    z = torch.randn(N, K, generator=g) * 3
+    y = torch.randint(0, K, (N,), generator=g)
+    gn = 2 * N  # e.g. two replicas
+    zd = z.double().requires_grad_(True)
+    ref = F.cross_entropy(zd, y, reduction="sum") / gn
+    ref.backward()
+    accs = [torch.full((), v, dtype=torch.float64, device="cuda") for v in (1.5, 3.0, 2.0, 3.0)]
+    zc = z.cuda().requires_grad_(True)
+    loss = D.xent_head(zc, y.cuda(), gn, accs[:2], accs[2:])
+    (loss * 0.5).backward()
+    _close(loss, ref, 1e-6)
+    _close(zc.grad, zd.grad * 0.5, 1e-6)
+    per = F.cross_entropy(zd.detach(), y, reduction="none")
+    np.testing.assert_allclose(float(accs[0]), 1.5 + float(per.sum()), rtol=1e-6)
+    assert float(accs[1]) == 3.0 + N and float(accs[3]) == 3.0 + N
+    assert float(accs[2]) == 2.0 + float((z.argmax(1) == y).sum())
