@@ -366,10 +366,13 @@ __global__ __launch_bounds__(1024) void k_xent_head(const float* __restrict__ z,
       tc += s_cor[i];
     }
     loss_out[0] = (float)(tl / gn);
-    if (lt_total != nullptr) *lt_total += tl;
-    if (lt_count != nullptr) *lt_count += (double)N;
-    if (acc_total != nullptr) *acc_total += tc;
-    if (acc_count != nullptr) *acc_count += (double)N;
+    // the four read-modify-writes' loads issued together (one memory round trip, not four)
+    const double l0 = lt_total != nullptr ? *lt_total : 0.0, l1 = lt_count != nullptr ? *lt_count : 0.0;
+    const double a0 = acc_total != nullptr ? *acc_total : 0.0, a1 = acc_count != nullptr ? *acc_count : 0.0;
+    if (lt_total != nullptr) *lt_total = l0 + tl;
+    if (lt_count != nullptr) *lt_count = l1 + (double)N;
+    if (acc_total != nullptr) *acc_total = a0 + tc;
+    if (acc_count != nullptr) *acc_count = a1 + (double)N;
   }
 }
 

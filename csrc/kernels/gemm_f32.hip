@@ -346,14 +346,22 @@ __global__ __launch_bounds__(256) void k_gemm_f32_reduce(F32GemmArgs a) {
   const float* src = a.ws + (int64_t)m * a.N + n;
   float v = 0.f;
   int z = 0;
-  for (; z + 8 <= a.splits; z += 8) {
-    float p[8];
+  for (; z + 16 <= a.splits; z += 16) {  // 16 independent partial loads in flight per round
+    float p[16];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) p[u] = src[(z + u) * mn];
+    for (int u = 0; u < 16; ++u) p[u] = src[(z + u) * mn];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v += p[u];
+    for (int u = 0; u < 16; ++u) v += p[u];
   }
-  for (; z < a.splits; ++z) v += src[z * mn];
+  {
+    float p[16];  // the remainder, also in one round (clamped loads, zero past the end)
+#pragma unroll
+    for (int u = 0; u < 16; ++u) p[u] = src[(int64_t)min(z + u, a.splits - 1) * mn];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) p[u] = z + u < a.splits ? p[u] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v += p[u];
+  }
   out_store(a, m, n, v);
 }
 

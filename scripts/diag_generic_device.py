@@ -1,5 +1,13 @@
 """Diagnostic: a generic-engine device execution graph replayed after an epoch boundary vs the same
-three steps run eagerly / through a fresh capture, from the same weights and indices."""
+three steps run eagerly / through a fresh capture, from the same weights and indices, per variable.
+
+Round 6 finding (kept as the regression check): with the conv bias gradient taken by PyTorch's
+``dy.sum((0, 1, 2))`` -- a multi-block reduction with a global-memory semaphore buffer zeroed by a
+captured memset node -- a captured multi-step graph replayed after eager work on the device (the
+epoch-end metric read / reset) produced garbage for that one reduction (9 of 16 channels 0) while a
+fresh capture of the same steps was exact.  The bias gradients now come from the weight-gradient
+kernel itself (gemm_f32.hip, a column / row of ones), so no such reduction remains in the step.
+TDL_GENERIC_DEVICE_EAGER=1 runs the device path without capture for comparison."""
 import os
 import sys
 

@@ -578,8 +578,6 @@ class GenericTrainer:
             self._dev_ev[s].synchronize()  # the copy out of this staging buffer has run
         self._dev_stage[s][:n].numpy()[:] = idx
         self._dev_idx[:n].copy_(self._dev_stage[s][:n], non_blocking=True)
-        if os.environ.get("TDL_DEV_SYNC_UPLOAD", "0") == "1":
-            torch.cuda.current_stream(self.device).synchronize()
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.device))
         self._dev_ev[s] = ev
@@ -627,8 +625,6 @@ class GenericTrainer:
                 done += 1
                 continue
             K = idx.size // b
-            if os.environ.get("TDL_DEV_TRACE") == "1":
-                self._dev_trace = getattr(self, "_dev_trace", []) + [np.array(idx)]
             self._dev_upload(idx)
             opt._sync_lr()
             graph = self._graphs.get(("dev", K, b))
@@ -657,12 +653,7 @@ class GenericTrainer:
         s.wait_stream(torch.cuda.current_stream(dev))
         it0 = self.optimizer.iterations
         try:
-            pool = None
-            if os.environ.get("TDL_DEV_SHARED_POOL", "0") == "1":
-                if getattr(self, "_dev_pool", None) is None:
-                    self._dev_pool = torch.cuda.graph_pool_handle()
-                pool = self._dev_pool
-            with torch.cuda.graph(graph, stream=s, pool=pool):
+            with torch.cuda.graph(graph, stream=s):
                 for k in range(K):
                     self._dev_step(k, b, b * self.comm.world_size, sync_lr=False)
         except Exception as e:  # noqa: BLE001 - a layer with host-side logic: stay eager
