@@ -49,6 +49,8 @@ struct F32GemmArgs {
   float* dbias = nullptr;         // bias gradient: a row of ones appended to A (ones_m = M - 1,
   int ones_m = -1, ones_n = -1;   // kF32Gemm) or a column of ones appended to B (ones_n = N - 1,
                                   // kF32ConvWgrad); that output row / column goes to dbias
+  int b_hwio = 0;                 // kF32ConvDgrad: b is the forward kernel w HWIO [R][S][C][K] itself
+                                  // (B(k = (r, s, kk), n = c) read transposed: no transpose pass)
 };
 
 constexpr int kF32Tile = 64;

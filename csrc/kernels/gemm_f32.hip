@@ -229,6 +229,11 @@ __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
             ldb1(r, i, ok, e);
         }
       }
+    } else if (MODE == kF32ConvDgrad && a.b_hwio) {  // w HWIO: B(kr = rs * K + kk, n = c) = w[rs][c][kk]
+      const int rs = kr / g.k, kk2 = kr - rs * g.k;
+      const int64_t row = (int64_t)rs * a.N * g.k + kk2;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ldb1(r, i, brow && bn + i < a.N, row + (int64_t)(bn + i) * g.k);
     } else {
       const int64_t sbk = MODE == kF32Gemm ? a.sbk : (int64_t)a.N;
       const int64_t sbn = MODE == kF32Gemm ? a.sbn : 1;
@@ -415,7 +420,7 @@ void f32_gemm_launch(int mode, const F32GemmArgs& a, hipStream_t s) {
   }
   if (a.splits > 1) {
     const int64_t mn = (int64_t)a.M * a.N;
-    if (a.splits >= 32 && mn <= 16384)
+    if (a.splits >= 16)  // one wave per output: every partial of an output in one load round
       hipLaunchKernelGGL(k_gemm_f32_reduce_wave, dim3((unsigned)((mn + 3) / 4)), dim3(256), 0, s, a);
     else
       hipLaunchKernelGGL(k_gemm_f32_reduce, dim3((unsigned)((mn + 255) / 256)), dim3(256), 0, s, a);

@@ -782,11 +782,13 @@ at::Tensor conv_f32_fwd(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> bi
 
 // dx[N][H][W][C] of a conv with dy [N][OH][OW][K] and wt = w as [R][S][K][C]
 at::Tensor conv_f32_dgrad(at::Tensor dy, at::Tensor wt, int64_t h, int64_t wd, int64_t sh, int64_t sw, int64_t pt,
-                          int64_t pl, int64_t dh, int64_t dw, c10::optional<at::Tensor> dy_mask) {
+                          int64_t pl, int64_t dh, int64_t dw, c10::optional<at::Tensor> dy_mask, bool w_hwio) {
   f32_check(dy, "conv_f32_dgrad: dy");
   f32_check(wt, "conv_f32_dgrad: wt");
-  TORCH_CHECK(dy.dim() == 4 && wt.dim() == 4 && wt.size(2) == dy.size(3), "conv_f32_dgrad: dy NHWC, wt [R][S][K][C]");
-  const int64_t C = wt.size(3), K = dy.size(3);
+  // wt: [R][S][K][C], or (w_hwio) the forward kernel [R][S][C][K] read transposed in the kernel
+  TORCH_CHECK(dy.dim() == 4 && wt.dim() == 4 && wt.size(w_hwio ? 3 : 2) == dy.size(3),
+              "conv_f32_dgrad: dy NHWC, wt [R][S][K][C] (or w [R][S][C][K] with w_hwio)");
+  const int64_t C = wt.size(w_hwio ? 2 : 3), K = dy.size(3);
   auto dx = fresh({dy.size(0), h, wd, C}, dy.options());
   tdl::F32GemmArgs g{};
   g.g = f32_geom(dx, K, wt.size(0), wt.size(1), dy.size(1), dy.size(2), sh, sw, pt, pl, dh, dw);
@@ -799,7 +801,8 @@ at::Tensor conv_f32_dgrad(at::Tensor dy, at::Tensor wt, int64_t h, int64_t wd, i
   g.ldo = C;
   g.amask = f32_mask(dy_mask, dy, "conv_f32_dgrad: dy_mask");
   g.vec_a = K % 4 == 0 && al16(dy) && mask_al16(dy_mask);
-  g.vec_b = C % 4 == 0 && al16(wt);
+  g.vec_b = !w_hwio && C % 4 == 0 && al16(wt);
+  g.b_hwio = w_hwio ? 1 : 0;
   f32_run(tdl::kF32ConvDgrad, g, dy.options());
   return dx;
 }
@@ -920,7 +923,7 @@ void register_ops(pybind11::module& m) {
         "dy_mask: dy * (mask > 0)",
         pybind11::arg("dy"), pybind11::arg("wt"), pybind11::arg("h"), pybind11::arg("w"), pybind11::arg("sh"),
         pybind11::arg("sw"), pybind11::arg("pt"), pybind11::arg("pl"), pybind11::arg("dh") = 1, pybind11::arg("dw") = 1,
-        pybind11::arg("dy_mask") = pybind11::none());
+        pybind11::arg("dy_mask") = pybind11::none(), pybind11::arg("w_hwio") = false);
   m.def("conv_f32_wgrad", &conv_f32_wgrad, "NHWC f32 convolution weight gradient (HWIO), deterministic split-K; "
         "dy_mask: dy * (mask > 0); dbias: the bias gradient from an appended column of ones",
         pybind11::arg("x"), pybind11::arg("dy"), pybind11::arg("r"), pybind11::arg("s"), pybind11::arg("sh"),

@@ -342,6 +342,14 @@ class GenericTrainer:
             loss = loss + reg / self.strategy.num_replicas_in_sync
         return loss, per_ex, y_pred
 
+    def _seed(self) -> torch.Tensor:
+        """The backward seed d(loss)/d(loss) = 1, allocated once (autograd would fill a new one every
+        step; the fused loss head recognises this one and skips its scaling kernel)."""
+        s = getattr(self, "_seed_t", None)
+        if s is None:
+            s = self._seed_t = torch.ones((), dtype=torch.float32, device=self.device)
+        return s
+
     def _fused_head(self, y, y_pred, sw):
         """The one-kernel loss head (ops/dense.py xent_head) when the step's loss and metrics are what it
         computes: SparseCategoricalCrossentropy(from_logits=True) on f32 2-D logits, no sample weights,
@@ -365,7 +373,7 @@ class GenericTrainer:
         while len(accs) < 4:
             accs.append(None)
         labels = y.long()
-        return lambda gn: _dense.xent_head(y_pred, labels, gn, accs[:2], accs[2:])
+        return lambda gn: _dense.xent_head(y_pred, labels, gn, accs[:2], accs[2:], seed=self._seed())
 
     def train_step(self, batch, global_n: int, sync_lr: bool = True, t_add: int = 0):
         """One whole step.  ``t_add``: the step's offset inside a multi-step execution graph whose
@@ -411,7 +419,7 @@ class GenericTrainer:
         _conv.side_stream_window(self.device.type == "cuda")
         try:
             with trace_range("tdl.backward"):
-                loss.backward()
+                loss.backward(self._seed())
         finally:
             _conv.side_stream_window(False)
             _conv.join_side()  # every slab weight gradient queued on the side stream is in G

@@ -13,6 +13,8 @@ Reference: the Keras layers / loss of ``tf_dist_example.py:41-50`` (and keras.ap
 """
 from __future__ import annotations
 
+from typing import Optional
+
 import torch
 
 from . import hip
@@ -115,15 +117,18 @@ def softmax_xent(z: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
 
 class _XentHead(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, z, labels, gn, accs):
+    def forward(ctx, z, labels, gn, accs, seed):
         loss, dz = hip().xent_head(z.contiguous(), labels.contiguous(), float(gn), *accs)
         ctx.save_for_backward(dz)
+        ctx.seed_ptr = seed.data_ptr() if seed is not None else None
         return loss
 
     @staticmethod
     def backward(ctx, g):
         (dz,) = ctx.saved_tensors
-        return dz * g, None, None, None
+        if ctx.seed_ptr is not None and g.data_ptr() == ctx.seed_ptr:
+            return dz, None, None, None, None  # the trainer's own backward seed (1.0): no scaling kernel
+        return dz * g, None, None, None, None
 
 
 def xent_head_supported(z: torch.Tensor, labels: torch.Tensor) -> bool:
@@ -131,10 +136,11 @@ def xent_head_supported(z: torch.Tensor, labels: torch.Tensor) -> bool:
     return xent_supported(z, labels) and z.shape[0] <= 8192 and z.shape[1] <= 4096
 
 
-def xent_head(z: torch.Tensor, labels: torch.Tensor, global_n: int, loss_acc=(None, None), acc_acc=(None, None)):
+def xent_head(z: torch.Tensor, labels: torch.Tensor, global_n: int, loss_acc=(None, None), acc_acc=(None, None),
+              seed: Optional[torch.Tensor] = None):
     """The generic engine's loss head in ONE kernel (csrc/kernels/gemm.hip k_xent_head): the mean-reduced
     sparse softmax cross-entropy ``sum(per-example loss) / global_n`` (tf.nn.compute_average_loss), its
     logit gradient (saved for the backward), and the loss-tracker / SparseCategoricalAccuracy f64
     accumulators ``(total, count)`` advanced in place -- instead of ~15 PyTorch reduction / elementwise
     kernels per step (tf_dist_example.py:49-52)."""
-    return _XentHead.apply(z, labels, float(global_n), tuple(loss_acc) + tuple(acc_acc))
+    return _XentHead.apply(z, labels, float(global_n), tuple(loss_acc) + tuple(acc_acc), seed)

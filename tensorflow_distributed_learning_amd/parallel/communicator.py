@@ -468,6 +468,9 @@ class NativeRcclCommunicator(TorchCommunicator):
             s.wait_stream(torch.cuda.current_stream(dev))
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=s):
+                # (a kernel in front of the collective: at world 1 RCCL's in-place all-reduce records
+                # no node, and an empty graph proves nothing about replay)
+                t.mul_(1.0)
                 self.rccl.all_reduce(t, 0)
             torch.cuda.synchronize(dev)
         except Exception:  # noqa: BLE001 - capture unsupported: eager collectives
