@@ -46,9 +46,14 @@ def fwd(x, w_hwio, bias, stride, pads, dil=(1, 1), act=0) -> torch.Tensor:
 def dgrad(dy, w_hwio, hw, stride, pads, dil=(1, 1), dy_mask=None) -> torch.Tensor:
     """f32 input gradient of :func:`fwd` for an input of spatial size ``hw`` (``dy_mask``: the ReLU
     output whose mask applies to ``dy``)."""
-    # the kernel reads w HWIO transposed (w_hwio): no [R][S][K][C] copy per step
-    return hip().conv_f32_dgrad(_c32(dy), _c32(w_hwio), hw[0], hw[1], stride[0], stride[1], pads[0], pads[2], dil[0],
-                                dil[1], dy_mask=dy_mask, w_hwio=True)
+    if w_hwio.numel() <= (1 << 16):
+        # small kernels (the generic engine's layers): read w HWIO transposed in the kernel (w_hwio), no
+        # [R][S][K][C] copy kernel per step; large ones keep the copy for 16-B operand loads
+        return hip().conv_f32_dgrad(_c32(dy), _c32(w_hwio), hw[0], hw[1], stride[0], stride[1], pads[0], pads[2],
+                                    dil[0], dil[1], dy_mask=dy_mask, w_hwio=True)
+    wt = _c32(w_hwio).permute(0, 1, 3, 2).contiguous()  # [R][S][K][C]
+    return hip().conv_f32_dgrad(_c32(dy), wt, hw[0], hw[1], stride[0], stride[1], pads[0], pads[2], dil[0], dil[1],
+                                dy_mask=dy_mask)
 
 
 def wgrad(x, dy, rs, stride, pads, dil=(1, 1), out=None, accumulate=False, dy_mask=None, dbias=None) -> torch.Tensor:
