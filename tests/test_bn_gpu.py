@@ -414,7 +414,10 @@ def test_bn_apply_deferred_into_1x1_conv_trains_like_unfused(mask_stats):
     wu, lu, du, nu = run(False)
     assert df and not du
     if mask_stats:
-        assert nf >= 3 and nu >= 3  # both fuse the BN backward reduction into the 1x1 conv's dgrad
+        # both fuse the BN backward reduction into the 1x1 conv's dgrad (counted per host-side call: with
+        # the generic engine's device executions the first step runs eagerly, the second is captured,
+        # the third replays the graph without Python)
+        assert nf >= 2 and nu >= 2
     np.testing.assert_allclose(lf, lu, rtol=1e-2)
     for a, b in zip(wf, wu):
         scale = max(float(np.abs(b).max()), 1e-3)
