@@ -6,6 +6,8 @@
 namespace tdl {
 
 // out[r, :] = src[idx[r], :] * scale   (row gather of a device-resident dataset; f32 rows)
+void gather_xy(const float* src, const void* lab, const int* idx, float* out, void* out_lab, int64_t rows,
+               int64_t row_elems, int lab_bytes, hipStream_t s);
 void gather_rows_f32(const float* src, const int* idx, float* out, int64_t rows, int64_t row_elems, float scale,
                      hipStream_t s);
 // out[r, :] = float(src[idx[r], :]) * scale   (uint8 images -> f32, the reference's map(scale))

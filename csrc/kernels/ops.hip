@@ -40,6 +40,35 @@ __global__ __launch_bounds__(256) void k_gather_i32(const int* __restrict__ src,
   if (r < rows) out[r] = src[idx[r]];
 }
 
+// a batch of (f32 feature row, label) pairs of a device-resident dataset in ONE launch (the generic
+// engine's device input path): workgroup r copies row idx[r] and its thread 0 the label (4 or 8 bytes)
+__global__ __launch_bounds__(256) void k_gather_xy(const float* __restrict__ src, const void* __restrict__ lab,
+                                                   const int* __restrict__ idx, float* __restrict__ out,
+                                                   void* __restrict__ out_lab, int64_t row_elems, int lab_bytes) {
+  const int64_t r = blockIdx.x;
+  const int64_t i = idx[r];
+  const float* s = src + i * row_elems;
+  float* o = out + r * row_elems;
+  if ((row_elems & 3) == 0) {
+    for (int64_t e = threadIdx.x * 4; e < row_elems; e += 1024) st4(o + e, ld4(s + e));
+  } else {
+    for (int64_t e = threadIdx.x; e < row_elems; e += 256) o[e] = s[e];
+  }
+  if (threadIdx.x == 0) {
+    if (lab_bytes == 8)
+      static_cast<long long*>(out_lab)[r] = static_cast<const long long*>(lab)[i];
+    else
+      static_cast<int*>(out_lab)[r] = static_cast<const int*>(lab)[i];
+  }
+}
+
+void gather_xy(const float* src, const void* lab, const int* idx, float* out, void* out_lab, int64_t rows,
+               int64_t row_elems, int lab_bytes, hipStream_t s) {
+  if (rows == 0) return;
+  hipLaunchKernelGGL(k_gather_xy, dim3((unsigned)rows), dim3(256), 0, s, src, lab, idx, out, out_lab, row_elems,
+                     lab_bytes);
+}
+
 void gather_rows_f32(const float* src, const int* idx, float* out, int64_t rows, int64_t row_elems, float scale,
                      hipStream_t s) {
   if (rows == 0) return;

@@ -30,6 +30,26 @@ at::Tensor fresh(at::IntArrayRef shape, const at::TensorOptions& o, int level = 
   return (fp && poison() >= level) ? at::full(shape, std::numeric_limits<float>::quiet_NaN(), o) : at::empty(shape, o);
 }
 
+// (x [n, ...] f32, y [n]) = (X[idx], Y[idx]) in one launch; Y int64 or int32
+std::vector<at::Tensor> gather_xy(at::Tensor X, at::Tensor Y, at::Tensor idx) {
+  TORCH_CHECK(X.is_cuda() && Y.is_cuda() && idx.is_cuda(), "gather_xy: GPU tensors expected");
+  TORCH_CHECK(X.is_contiguous() && Y.is_contiguous() && idx.is_contiguous(), "gather_xy: contiguous tensors expected");
+  TORCH_CHECK(X.scalar_type() == at::kFloat && X.dim() >= 1, "gather_xy: X must be f32 [N, ...]");
+  TORCH_CHECK((Y.scalar_type() == at::kLong || Y.scalar_type() == at::kInt) && Y.dim() == 1 && Y.size(0) == X.size(0),
+              "gather_xy: Y must be int64 / int32 [N]");
+  TORCH_CHECK(idx.scalar_type() == at::kInt && idx.dim() == 1, "gather_xy: idx must be int32 [n]");
+  const int64_t rows = idx.numel();
+  auto shape = X.sizes().vec();
+  shape[0] = rows;
+  auto x = at::empty(shape, X.options());
+  auto y = at::empty({rows}, Y.options());
+  const int64_t row_elems = X.size(0) > 0 ? X.numel() / X.size(0) : 0;
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(X.data_ptr()) % 16 == 0, "gather_xy: X must be 16-byte aligned");
+  tdl::gather_xy(X.data_ptr<float>(), Y.data_ptr(), idx.data_ptr<int>(), x.data_ptr<float>(), y.data_ptr(), rows,
+                 row_elems, (int)Y.element_size(), cur_stream());
+  return {x, y};
+}
+
 at::Tensor gather_rows(at::Tensor src, at::Tensor idx, double scale) {
   TORCH_CHECK(src.is_cuda() && idx.is_cuda(), "gather_rows: GPU tensors expected");
   TORCH_CHECK(src.is_contiguous() && idx.is_contiguous(), "gather_rows: contiguous tensors expected");
@@ -983,6 +1003,7 @@ void register_ops(pybind11::module& m) {
   m.def("conv_dgrad", &conv_dgrad, "NHWC bf16 implicit-GEMM stride-1 convolution input gradient (MFMA)",
         pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("h"), pybind11::arg("wd"), pybind11::arg("pt"),
         pybind11::arg("pl"), pybind11::arg("residual") = pybind11::none());
+  m.def("gather_xy", &gather_xy, "a batch of (feature row, label) pairs of a device-resident dataset, one launch");
   m.def("gather_rows", &gather_rows, "row gather (+u8->f32 scale) of a device-resident dataset");
   m.def("gather_labels", &gather_labels);
   m.def("bn_forward_train", &bn_forward_train, "NHWC batch-norm training forward (+relu)", pybind11::arg("x"),

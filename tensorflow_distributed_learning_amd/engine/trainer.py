@@ -461,7 +461,9 @@ class GenericTrainer:
                     m.update_state(y, yp, sw)
 
     def run_train(self, handler, steps: int) -> int:
-        if not isinstance(handler, HostDataHandler) and hasattr(handler, "take"):
+        from .fused import DeviceHandler
+
+        if isinstance(handler, DeviceHandler):  # (prepare(): device-resident input, execution graphs)
             return self._run_device(handler, steps)
         done = 0
         for _ in range(steps):
@@ -564,6 +566,11 @@ class GenericTrainer:
             self._X = x.to(self.device).contiguous()
             self._Y = y.to(self.device).contiguous()
             self._dev_key = key
+        from ..ops import hip
+
+        self._gather_xy = (self._X.dtype == torch.float32 and self._Y.dim() == 1 and
+                           self._Y.dtype in (torch.int64, torch.int32) and hasattr(hip(), "gather_xy") and
+                           self._X.data_ptr() % 16 == 0)
         policy = input_lib.effective_policy(dataset) if R > 1 else None
         seed = input_lib.shared_seed(self.strategy) if policy is not None and policy.name in ("DATA", "FILE") else None
         return F.DeviceHandler(lp, seed, self.comm.rank, R)
@@ -592,8 +599,13 @@ class GenericTrainer:
 
     def _dev_step(self, k: int, b: int, global_n: int, sync_lr: bool):
         ii = self._dev_idx[k * b:(k + 1) * b]
-        self.train_step((self._X.index_select(0, ii), self._Y.index_select(0, ii)), global_n, sync_lr=sync_lr,
-                        t_add=k)
+        if self._gather_xy:  # features and labels of the batch in one hand-written kernel
+            from ..ops import hip
+
+            x, y = hip().gather_xy(self._X, self._Y, ii)
+        else:
+            x, y = self._X.index_select(0, ii), self._Y.index_select(0, ii)
+        self.train_step((x, y), global_n, sync_lr=sync_lr, t_add=k)
 
     def warm_graphs(self, steps: int, b: Optional[int] = None):
         """Capture (without running) the execution graphs ``run_train(steps)`` will replay, once a
