@@ -55,15 +55,17 @@ struct F32GemmArgs {
 
 constexpr int kF32Tile = 64;
 
-// Reduction split for a (mode-independent) M x N x Kred problem: enough workgroups to fill 256 CUs.
-inline void f32_gemm_plan(F32GemmArgs& a) {
+// Reduction split for a (mode-independent) M x N x Kred problem: enough workgroups to fill 256 CUs,
+// each with at least `kmin` reduction elements (the kernel keeps 4 slices of 16 in flight, so a
+// split of <= 64 is one memory round trip; 128 -- two -- until round 6), at most `cap` splits.
+inline void f32_gemm_plan(F32GemmArgs& a, int kmin = 64, int cap = 1024) {
   const int64_t tiles = (int64_t)((a.M + kF32Tile - 1) / kF32Tile) * ((a.N + kF32Tile - 1) / kF32Tile);
   int splits = 1;
   if (tiles < 512 && a.Kred > 256) {
     const int64_t want = (1024 + tiles - 1) / tiles;
-    const int64_t most = (a.Kred + 127) / 128;
+    const int64_t most = (a.Kred + kmin - 1) / kmin;
     splits = (int)(want < most ? want : most);
-    if (splits > 256) splits = 256;
+    if (splits > cap) splits = cap;
     if (splits < 1) splits = 1;
   }
   int chunk = (a.Kred + splits - 1) / splits;

@@ -2,6 +2,7 @@
 #include <torch/extension.h>
 
 #include <cstdlib>
+#include <cstdio>
 #include <limits>
 #include <c10/hip/HIPStream.h>
 
@@ -668,7 +669,13 @@ bool al16(const at::Tensor& t) { return reinterpret_cast<uintptr_t>(t.data_ptr()
 
 void f32_run(int mode, tdl::F32GemmArgs& a, const at::TensorOptions& o) {
   TORCH_CHECK(a.Kred > 0, "f32 gemm: empty reduction");
-  tdl::f32_gemm_plan(a);
+  // TDL_F32_SPLIT="kmin,cap" (A/B of the split plan; default 64,1024)
+  static const std::pair<int, int> plan = [] {
+    int kmin = 64, cap = 1024;
+    if (const char* e = std::getenv("TDL_F32_SPLIT")) std::sscanf(e, "%d,%d", &kmin, &cap);
+    return std::make_pair(kmin < 16 ? 16 : kmin, cap < 1 ? 1 : cap);
+  }();
+  tdl::f32_gemm_plan(a, plan.first, plan.second);
   at::Tensor ws;
   if (a.splits > 1) {
     ws = at::empty({(int64_t)a.splits * a.M * a.N}, o);
