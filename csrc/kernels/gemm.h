@@ -27,8 +27,10 @@ void softmax_xent_fwd(const float* z, const long long* labels, int N, int K, flo
 // Fused loss head of the generic engine: loss_out[0] = sum of the rows' sparse softmax cross-entropy / gn,
 // dz = (softmax - onehot) / gn, and the loss / accuracy metric accumulators (f64, any may be null)
 // advanced by (sum of losses, N) / (correct top-1, N); one workgroup, rows summed in a fixed order.
+// rows_ws: null for a one-workgroup head (small N*K), else [2N] f32 scratch of the two-kernel form
 void xent_head(const float* z, const long long* labels, int N, int K, double gn, float* loss_out, float* dz,
-               double* lt_total, double* lt_count, double* acc_total, double* acc_count, hipStream_t s);
+               double* lt_total, double* lt_count, double* acc_total, double* acc_count, float* rows_ws,
+               hipStream_t s);
 void softmax_xent_bwd(const float* z, const long long* labels, int N, int K, const float* g, float* dz,
                       hipStream_t s);
 

@@ -376,12 +376,94 @@ __global__ __launch_bounds__(1024) void k_xent_head(const float* __restrict__ z,
   }
 }
 
+// Large heads (ResNet-50: 256 rows x 1000 classes): one wave per row over many workgroups writes the row's
+// loss / correct flag and dlogits, then k_xent_finish (one workgroup) sums the rows in a fixed order.
+__global__ __launch_bounds__(256) void k_xent_rows(const float* __restrict__ z, const long long* __restrict__ lab,
+                                                   int N, int K, double gn, float* __restrict__ dz,
+                                                   float* __restrict__ row_loss, float* __restrict__ row_cor) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= N) return;
+  const float inv_gn = (float)(1.0 / gn);
+  const float* zr = z + (long long)row * K;
+  float mx = -INFINITY;
+  int am = K;
+  for (int k = lane; k < K; k += 64) {
+    const float v = zr[k];
+    if (v > mx) {
+      mx = v;
+      am = k;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(mx, o);
+    const int oa = __shfl_xor(am, o);
+    if (om > mx || (om == mx && oa < am)) {
+      mx = om;
+      am = oa;
+    }
+  }
+  float se = 0.f;
+  for (int k = lane; k < K; k += 64) se += __expf(zr[k] - mx);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) se += __shfl_xor(se, o);
+  const float lse = mx + __logf(se);
+  const long long y = lab[row];
+  const bool valid = y >= 0 && y < K;
+  float* dr = dz + (long long)row * K;
+  for (int k = lane; k < K; k += 64) dr[k] = (__expf(zr[k] - lse) - (k == y ? 1.f : 0.f)) * inv_gn;
+  if (lane == 0) {
+    row_loss[row] = valid ? lse - zr[y] : 0.f;
+    row_cor[row] = (valid && am == (int)y) ? 1.f : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_xent_finish(const float* __restrict__ row_loss, const float* __restrict__ row_cor,
+                                                      int N, double gn, float* __restrict__ loss_out, double* lt_total,
+                                                      double* lt_count, double* acc_total, double* acc_count) {
+  __shared__ double s_l[1024], s_c[1024];
+  const int t = threadIdx.x;
+  double l = 0.0, c = 0.0;
+  for (int r = t; r < N; r += 1024) {  // (each thread its rows in order, then a fixed tree)
+    l += (double)row_loss[r];
+    c += (double)row_cor[r];
+  }
+  s_l[t] = l;
+  s_c[t] = c;
+  __syncthreads();
+  for (int w = 512; w > 0; w >>= 1) {
+    if (t < w) {
+      s_l[t] += s_l[t + w];
+      s_c[t] += s_c[t + w];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    const double tl = s_l[0], tc = s_c[0];
+    loss_out[0] = (float)(tl / gn);
+    const double l0 = lt_total != nullptr ? *lt_total : 0.0, l1 = lt_count != nullptr ? *lt_count : 0.0;
+    const double a0 = acc_total != nullptr ? *acc_total : 0.0, a1 = acc_count != nullptr ? *acc_count : 0.0;
+    if (lt_total != nullptr) *lt_total = l0 + tl;
+    if (lt_count != nullptr) *lt_count = l1 + (double)N;
+    if (acc_total != nullptr) *acc_total = a0 + tc;
+    if (acc_count != nullptr) *acc_count = a1 + (double)N;
+  }
+}
+
 }  // namespace
 
 void xent_head(const float* z, const long long* labels, int N, int K, double gn, float* loss_out, float* dz,
-               double* lt_total, double* lt_count, double* acc_total, double* acc_count, hipStream_t s) {
-  hipLaunchKernelGGL(k_xent_head, dim3(1), dim3(1024), 0, s, z, labels, N, K, gn, loss_out, dz, lt_total, lt_count,
-                     acc_total, acc_count);
+               double* lt_total, double* lt_count, double* acc_total, double* acc_count, float* rows_ws,
+               hipStream_t s) {
+  if (rows_ws == nullptr) {  // small head: everything in one workgroup
+    hipLaunchKernelGGL(k_xent_head, dim3(1), dim3(1024), 0, s, z, labels, N, K, gn, loss_out, dz, lt_total, lt_count,
+                       acc_total, acc_count);
+    return;
+  }
+  hipLaunchKernelGGL(k_xent_rows, dim3((N + 3) / 4), dim3(256), 0, s, z, labels, N, K, gn, dz, rows_ws, rows_ws + N);
+  hipLaunchKernelGGL(k_xent_finish, dim3(1), dim3(1024), 0, s, rows_ws, rows_ws + N, N, gn, loss_out, lt_total,
+                     lt_count, acc_total, acc_count);
 }
 
 void softmax_xent_fwd(const float* z, const long long* labels, int N, int K, float* loss, float* lse, hipStream_t s) {

@@ -907,10 +907,13 @@ std::vector<at::Tensor> xent_head(at::Tensor z, at::Tensor labels, double gn, c1
   TORCH_CHECK(gn > 0, "xent_head: global batch must be positive");
   auto loss = at::empty({}, z.options());
   auto dz = fresh(z.sizes(), z.options());
+  // one workgroup up to 64K logits (the reference CNN's 64 x 10), else per-row waves + a finishing sum
+  at::Tensor ws;
+  if (z.numel() > 65536) ws = at::empty({2 * z.size(0)}, z.options());
   tdl::xent_head(z.data_ptr<float>(), reinterpret_cast<const long long*>(labels.data_ptr<int64_t>()), (int)z.size(0),
                  (int)z.size(1), gn, loss.data_ptr<float>(), dz.data_ptr<float>(), f64_scalar(lt_total, "lt_total"),
                  f64_scalar(lt_count, "lt_count"), f64_scalar(acc_total, "acc_total"), f64_scalar(acc_count, "acc_count"),
-                 cur_stream());
+                 ws.defined() ? ws.data_ptr<float>() : nullptr, cur_stream());
   return {loss, dz};
 }
 

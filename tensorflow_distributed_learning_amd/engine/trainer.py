@@ -361,8 +361,12 @@ class GenericTrainer:
 
         if (sw is not None or y is None or os.environ.get("TDL_FUSED_HEAD", "1") != "1" or
                 not isinstance(self.loss, _losses.SparseCategoricalCrossentropy) or not self.loss.from_logits or
-                self.loss.ignore_class is not None or y_pred.dtype != torch.float32 or y_pred.dim() != 2 or
-                y.dim() != 1 or not _dense.xent_head_supported(y_pred, y.long())):
+                self.loss.ignore_class is not None or y_pred.dim() != 2 or y.dim() != 1 or
+                y_pred.dtype not in (torch.float32, torch.bfloat16, torch.float16)):
+            return None
+        # (mixed precision: the loss is computed on f32 logits, as the unfused path's y_pred.float())
+        y_pred = y_pred.float() if y_pred.dtype != torch.float32 else y_pred
+        if not _dense.xent_head_supported(y_pred, y.long()):
             return None
         if len(self.metrics) > 1 or (self.metrics and type(self.metrics[0]) is not _metrics.SparseCategoricalAccuracy):
             return None

@@ -43,7 +43,8 @@ with strategy.scope():
     h = L.GlobalAveragePooling2D()(h)
     m = tdl.keras.Model(inp, L.Dense(10)(h))
     m.compile(loss=tdl.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
-              optimizer=tdl.keras.optimizers.SGD(learning_rate=0.05, momentum=0.9), bucket_bytes=200_000)
+              optimizer=tdl.keras.optimizers.SGD(learning_rate=0.05, momentum=0.9), bucket_bytes=200_000,
+              steps_per_execution=int(os.environ.get("TDL_TEST_SPE", "1")))
 hist = m.fit(ds, epochs=2, steps_per_epoch=5, verbose=0)
 tr = m._trainer
 w = np.concatenate([v.ravel() for v in m.get_weights()]).astype(np.float64)
@@ -59,10 +60,10 @@ json.dump({"choices": sorted([str(k), v] for k, v in CV.choices().items()), "los
 """
 
 
-def _run(tmp_path, args, conv="hip"):
+def _run(tmp_path, args, conv="hip", spe=1):
     s = tmp_path / "job.py"
     s.write_text(textwrap.dedent(BODY))
-    env = dict(os.environ, PYTHONPATH=ROOT, TDL_SHARE_GPU="1", TDL_CONV=conv)
+    env = dict(os.environ, PYTHONPATH=ROOT, TDL_SHARE_GPU="1", TDL_CONV=conv, TDL_TEST_SPE=str(spe))
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "TF_CONFIG"):
         env.pop(k, None)
     r = subprocess.run([sys.executable, "-m", "tensorflow_distributed_learning_amd.launch"] + args + [str(s), str(tmp_path)],
@@ -93,6 +94,13 @@ def _check(tmp_path, R, single):
 def test_generic_bucketed_xgmi_replicas(tmp_path, R, single):
     _run(tmp_path, ["--nproc-per-node", str(R)])
     _check(tmp_path, R, single)
+
+
+def test_generic_device_execution_graphs_two_replicas(tmp_path, single):
+    """steps_per_execution=3 over the device-resident input: each execution is ONE captured graph
+    of 3 steps whose bucket exchanges are launched from the backward hooks inside it."""
+    _run(tmp_path, ["--nproc-per-node", "2"], spe=3)
+    _check(tmp_path, 2, single)
 
 
 def test_generic_config5_layout_two_workers_two_replicas(tmp_path, single):
