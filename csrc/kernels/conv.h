@@ -98,6 +98,7 @@ void conv_force_tile(int tile);
 // it measured faster (>= 32 k-tiles, >= one workgroup per CU), 3 = the ring kernel wherever its
 // 256-row tiles give >= one workgroup per CU (tests, sweeps)
 void conv_force_impl(int impl);
+void conv_force_halo(int on);  // 1: the halo kernel for stride-1 multi-tap convs where its window fits
 void conv_force_mfma(int mf);  // dma1 main loop MFMA form: 32 (32x32x16, default) or 16 (16x16x32)
 // A/B hook: main loop of the implicit-GEMM kernel: 0 single LDS stage (4 waves per SIMD), 1 / 2
 // register prefetch depth (default 2, single stage for 1-2 k-tile reductions), 3 depth 2 always

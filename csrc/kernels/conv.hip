@@ -18,7 +18,11 @@
 // blockIdx -> tile mapping is XCD-aware: the 8 XCDs take workgroups round-robin, so the bijective
 // remap below hands each XCD a contiguous run of logical tiles (the column tiles of a row block
 // are adjacent), and the row block's activations are read into one L2 instead of eight.
+#include <algorithm>
+#include <array>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 
 #include "kernels/conv.h"
 #include "kernels/common.h"
@@ -830,6 +834,166 @@ __global__ __launch_bounds__(64 * WGM * WGN, MINW) void k_conv_glds(Igemm a) {
         a, acc32, lds, tm, tn, wm * WTM, wn * WTN);
 }
 
+// ---- halo (input-reuse) main loop: stride-1 KH x KW convolutions ----
+// The im2col loaders above fetch every input pixel once per filter tap (9x for a 3x3), which makes the
+// 3x3 shapes L2 -> LDS bound (28x28 3x3: ~12.8 TB/s chip-wide into LDS at 0.8 PF/s; the LDS-DMA
+// gather ceiling is ~70 GB/s per CU, MI355X_MICROARCH.md 'gather into LDS').  Here a BM-row output
+// tile loads its input window ONCE per 64-channel chunk and every tap reads shifted rows of it:
+// with the input viewed as zero-padded to Hp = OH + KH - 1 by Wp = OW + KW - 1 (padding is virtual:
+// out-of-image slots are LDS-DMA range-check zeros), output pixel (n, oh, ow) of tap (kh, kw) reads
+// padded pixel pidx(n, oh, ow) + kh * Wp + kw, pidx = (n * Hp + oh) * Wp + ow.  A tile of consecutive
+// output rows therefore needs ONE contiguous run of padded pixels, [pidx(m0), pidx(m_last) + (KH-1) Wp
+// + KW - 1] -- its "slots" (128 B = 64 channels each, 16-B chunks XOR-swizzled by slot) -- plus the
+// BN x 64 weight tile of the current tap.  Per 64-channel chunk a 256 x 128 tile then moves ~64 KB of
+// input + 9 x 16 KB of weights instead of 9 x (32 + 16) KB.  Single LDS stage for the weights, 8 waves
+// (4 x 2 of 64 x WTN on v_mfma_f32_32x32x16_bf16), two workgroups per CU; rows are still the linear
+// (n, oh, ow) order, so the conv_epilogue variants (BN statistics, residual, BN-group backward) apply
+// unchanged.  The same kernel runs the stride-1 input gradient (dy as the image, mirrored taps).
+template <int BM, int BN, int WGM, int WGN, int NSLOT, int EK>
+__global__ __launch_bounds__(64 * WGM * WGN, 4) void k_conv_halo(Igemm a, int Hp, int Wp) {
+  constexpr int NW = WGM * WGN, NT = 64 * NW;
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  constexpr int MI32 = WTM / 32, NJ32 = WTN / 32;
+  constexpr int A_ELEMS = NSLOT * LDS_ROW, B_ELEMS = BN * LDS_ROW;
+  constexpr int LDS_E = (A_ELEMS + B_ELEMS) > BM * (BN + 8) ? (A_ELEMS + B_ELEMS) : BM * (BN + 8);
+  constexpr int A_LD = NSLOT / (8 * NW);  // 8-slot LDS-DMA wave-instructions per wave, input window
+  constexpr int B_LD = BN / (8 * NW);     // ..., weight tile
+  static_assert(NSLOT % (8 * NW) == 0 && BN % (8 * NW) == 0 && MI32 >= 1 && NJ32 >= 1 && WTM % 32 == 0 &&
+                    WTN % 32 == 0,
+                "halo geometry");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_E];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int ntn = a.K / BN;
+  const int tn = wg % ntn, tm = wg / ntn;
+
+  const int HWp = Hp * Wp;
+  auto pidx = [&](int m) {
+    const int ow = m % a.OW, t = m / a.OW, oh = t % a.OH, n = t / a.OH;
+    return (n * Hp + oh) * Wp + ow;
+  };
+  const int m0 = tm * BM, mlast = min(m0 + BM, a.M) - 1;
+  const int pbase = pidx(m0);
+  const int nslot = pidx(mlast) + (a.KH - 1) * Wp + a.KW - pbase;  // <= NSLOT (host-checked)
+
+  const auto x_rsrc = buf_rsrc(a.x, (unsigned)((long long)a.N * a.H * a.W * a.C * 2));
+  const auto w_rsrc = buf_rsrc(a.w, (unsigned)((long long)a.KH * a.KW * a.C * a.K * 2));
+  // input window: lane L of wave-instruction i fills slot 8 (i NW + wave) + L / 8, position L % 8, i.e.
+  // fetches chunk (L % 8) ^ swz(slot) of that padded pixel (zeros outside the image / past the window)
+  int a_vo[A_LD];
+#pragma unroll
+  for (int i = 0; i < A_LD; ++i) {
+    const int s = (i * NW + wave) * 8 + (lane >> 3);
+    const int chunk = (lane & 7) ^ swz(s);
+    const int P = pbase + s;
+    const int n = P / HWp, rem = P - n * HWp, ph = rem / Wp, pw = rem - ph * Wp;
+    const int ih = ph - a.PT, iw = pw - a.PL;
+    const bool ok = s < nslot && n < a.N && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+    a_vo[i] = ok ? (int)(((((long long)n * a.H + ih) * a.W + iw) * a.C + chunk * 8) * 2) : (int)0x80000000;
+  }
+  int b_vo[B_LD];
+#pragma unroll
+  for (int i = 0; i < B_LD; ++i) {
+    const int row = (i * NW + wave) * 8 + (lane >> 3);
+    const int chunk = (lane & 7) ^ swz(row);
+    b_vo[i] = (int)(((long long)(tn * BN + row) * a.w_col + chunk * 8) * 2);
+  }
+  // this lane's fragment rows (32x32x16: row l & 31 of each 32-row block) as window slots of tap (0, 0);
+  // rows past M read a valid slot (their results are never stored)
+  const int frow32 = lane & 31, kq = lane >> 5;
+  int sb[MI32];
+#pragma unroll
+  for (int i = 0; i < MI32; ++i) sb[i] = pidx(min(m0 + wm * WTM + i * 32 + frow32, mlast)) - pbase;
+
+  f16v acc32[MI32][NJ32];
+#pragma unroll
+  for (int i = 0; i < MI32; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ32; ++j)
+#pragma unroll
+      for (int z = 0; z < 16; ++z) acc32[i][j][z] = 0.f;
+
+  uint16_t* const la = lds;
+  uint16_t* const lb = lds + A_ELEMS;
+  const int ctiles = a.C / BK, taps = a.KH * a.KW;
+  for (int c = 0; c < ctiles; ++c) {
+    int kh = 0, kw = 0;
+    for (int tap = 0; tap < taps; ++tap) {
+      if (c | tap) __syncthreads();  // every wave done reading the previous weight tile (and window)
+      if (tap == 0) {
+#pragma unroll
+        for (int i = 0; i < A_LD; ++i)
+          if ((i * NW + wave) * 8 < nslot)  // (wave-uniform)
+            lds_dma16(x_rsrc, la + (i * NW + wave) * 8 * LDS_ROW, a_vo[i], c * BK * 2);
+      }
+      const int wkh = a.flip ? a.KH - 1 - kh : kh, wkw = a.flip ? a.KW - 1 - kw : kw;
+      const int soff_b = (int)((wkh * a.w_kh + wkw * a.w_kw + c * BK) * 2);
+#pragma unroll
+      for (int i = 0; i < B_LD; ++i) lds_dma16(w_rsrc, lb + (i * NW + wave) * 8 * LDS_ROW, b_vo[i], soff_b);
+      wait_vmcnt_barrier<0>();
+      const int toff = kh * Wp + kw;
+#pragma unroll
+      for (int st = 0; st < BK / 16; ++st) {
+        bf16x8 fa[MI32], fb[NJ32];
+#pragma unroll
+        for (int i = 0; i < MI32; ++i) {
+          const int sl = sb[i] + toff;
+          fa[i] = *reinterpret_cast<const bf16x8*>(la + sl * LDS_ROW + (((2 * st + kq) ^ swz(sl)) * 8));
+        }
+#pragma unroll
+        for (int j = 0; j < NJ32; ++j) {
+          const int row = wn * WTN + j * 32 + frow32;
+          fb[j] = *reinterpret_cast<const bf16x8*>(lb + row * LDS_ROW + (((2 * st + kq) ^ swz(row)) * 8));
+        }
+#pragma unroll
+        for (int i = 0; i < MI32; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ32; ++j)
+            acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j], fa[i], acc32[i][j], 0, 0, 0);
+      }
+      if (++kw == a.KW) {
+        kw = 0;
+        ++kh;
+      }
+    }
+  }
+  __syncthreads();  // every wave done reading the window: the epilogue reuses the LDS
+  conv_epilogue<BM, BN, NT, EK, WTM, WTN, LDS_E, 2, 32>(a, acc32, lds, tm, tn, wm * WTM, wn * WTN);
+}
+
+constexpr int kHaloBM = 256, kHaloSlots = 512;
+
+// padded geometry of the halo kernel and the longest window over its row tiles (host; cached per shape)
+int halo_window(const Igemm& a, int& Hp, int& Wp) {
+  Hp = a.OH + a.KH - 1;
+  Wp = a.OW + a.KW - 1;
+  static std::mutex mu;
+  static std::map<std::array<int, 6>, int> cache;
+  const std::array<int, 6> key{a.N, a.OH, a.OW, a.KH, a.KW, a.M};
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
+  auto pidx = [&](long long m) {
+    const long long ow = m % a.OW, t = m / a.OW, oh = t % a.OH, n = t / a.OH;
+    return (n * Hp + oh) * Wp + ow;
+  };
+  long long worst = 0;
+  for (long long m0 = 0; m0 < a.M; m0 += kHaloBM) {
+    const long long ml = std::min<long long>(m0 + kHaloBM, a.M) - 1;
+    worst = std::max(worst, pidx(ml) + (long long)(a.KH - 1) * Wp + a.KW - pidx(m0));
+  }
+  const int w = (int)std::min<long long>(worst, 1 << 30);
+  std::lock_guard<std::mutex> g(mu);
+  cache[key] = w;
+  return w;
+}
+
 int g_depth = 2;  // main-loop variant; conv_force_depth for A/B sweeps
 bool g_single = true;  // default: the single-stage, 4-waves-per-SIMD variant for every reduction length
 
@@ -877,9 +1041,10 @@ int g_mf = [] {
 int g_impl = [] {  // (TDL_CONV_IMPL: the conv_force_impl A/B hook from the environment)
   const char* e = std::getenv("TDL_CONV_IMPL");
   const int v = e != nullptr ? std::atoi(e) : 2;
-  return (v == 1 || (v >= 3 && v <= 6)) ? v : 2;
+  return (v == 1 || (v >= 3 && v <= 7)) ? v : 2;
 }();  // 1: v1 only; 2: the LDS-DMA ring kernel where it measured faster; 3: wherever it fits;
-                 // 4 / 5: the single-stage LDS-DMA kernel (dma1) at 4 / 3 waves per SIMD wherever v1 runs
+                 // 4 / 5: the single-stage LDS-DMA kernel (dma1) at 4 / 3 waves per SIMD wherever v1 runs;
+                 // 7: the halo kernel wherever it fits, else the default selection
 
 template <int BM, int BN, int WGM, int WGN, int STAGES = 3, int MINW = 1, int MF = 16>
 void launch_v2(const Igemm& a, hipStream_t s) {
@@ -918,6 +1083,32 @@ bool use_dma1(const Igemm& a) {
   return g_impl == 2 && g_single && ktiles >= 9 && a.K % 128 == 0 && (a.KH * a.KW > 1 || a.scatter);
 }
 
+// halo kernel (k_conv_halo) for stride-1 multi-tap convolutions whose longest input window fits
+// kHaloSlots: forced by impl 7, by default where the per-shape A/B favoured it (TDL_CONV_HALO=0/1
+// overrides)
+int g_halo = [] {
+  const char* e = std::getenv("TDL_CONV_HALO");
+  return e != nullptr ? std::atoi(e) : 0;
+}();
+
+bool use_halo(const Igemm& a, int& Hp, int& Wp) {
+  if (g_forced_tile != 0 || !(g_impl == 7 || (g_impl == 2 && g_halo != 0))) return false;
+  if (a.SH != 1 || a.SW != 1 || a.scatter || a.in_ss || a.KH * a.KW < 2 || a.K % 64 != 0 || a.C % BK != 0)
+    return false;
+  return halo_window(a, Hp, Wp) <= kHaloSlots;
+}
+
+template <int BN>
+void launch_halo(const Igemm& a, int Hp, int Wp, hipStream_t s) {
+  const dim3 grid((a.M + kHaloBM - 1) / kHaloBM * (a.K / BN)), block(512);
+  if (a.bn_part && a.bn_ss)
+    hipLaunchKernelGGL((k_conv_halo<kHaloBM, BN, 4, 2, kHaloSlots, 3>), grid, block, 0, s, a, Hp, Wp);
+  else if (a.bn_part)
+    hipLaunchKernelGGL((k_conv_halo<kHaloBM, BN, 4, 2, kHaloSlots, 1>), grid, block, 0, s, a, Hp, Wp);
+  else
+    hipLaunchKernelGGL((k_conv_halo<kHaloBM, BN, 4, 2, kHaloSlots, 0>), grid, block, 0, s, a, Hp, Wp);
+}
+
 // Tile choice, from the sweep over the ResNet-50 b=256 convolutions (profiles/conv_tile_sweep_r1.jsonl):
 // 128 x 128 wins every shape with K % 128 == 0, including the 7x7 ones whose grid is under two
 // workgroups per CU (the 64-column tile's extra LDS traffic per MFMA costs more than the idle CUs);
@@ -931,6 +1122,13 @@ void launch(const Igemm& a, hipStream_t s) {
       hipLaunchKernelGGL((k_conv_igemm<128, 64, 0, 0, true>), dim3((a.M + 127) / 128 * (a.K / 64)), dim3(256), 0, s, a);
     }
     return;
+  }
+  {
+    int Hp, Wp;
+    if (use_halo(a, Hp, Wp)) {
+      if (a.K % 128 == 0) return launch_halo<128>(a, Hp, Wp, s);
+      return launch_halo<64>(a, Hp, Wp, s);
+    }
   }
   if (use_v2(a.M, a.K, a.KH * a.KW * (a.C / BK), a.KH * a.KW)) {
     if (a.K % 128 == 0) return launch_v2<256, 128, 4, 2>(a, s);
@@ -955,7 +1153,8 @@ void launch(const Igemm& a, hipStream_t s) {
 }  // namespace
 
 void conv_force_tile(int tile) { g_forced_tile = tile; }
-void conv_force_impl(int impl) { g_impl = (impl == 1 || (impl >= 3 && impl <= 6)) ? impl : 2; }
+void conv_force_impl(int impl) { g_impl = (impl == 1 || (impl >= 3 && impl <= 7)) ? impl : 2; }
+void conv_force_halo(int on) { g_halo = on; }
 void conv_force_mfma(int mf) { g_mf = mf == 16 ? 16 : 32; }
 void conv_force_depth(int depth) {
   // 0: single stage everywhere, 1 / 2: register prefetch depth 1 / the default selection (single
@@ -982,14 +1181,40 @@ bool conv_bf16_supported(const ConvGeom& g) {
          (long long)g.KH * g.KW * g.C * g.K < two_gib_elems;
 }
 
+static Igemm fwd_args(const ConvGeom& g, const void* x, const void* w_ohwi, void* y) {
+  return Igemm{static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w_ohwi), static_cast<uint16_t*>(y),
+               g.N, g.H, g.W, g.C, g.OH, g.OW, g.K, g.KH, g.KW, g.SH, g.SW, g.PT, g.PL, 0,
+               (long long)g.KH * g.KW * g.C, (long long)g.KW * g.C, (long long)g.C, g.N * g.OH * g.OW, 0, 0, 0,
+               nullptr, nullptr};
+}
+
+// image = dy [N][OH][OW][K] (reduction channels K), output = dx [N][H][W][C] (columns C), stride 1,
+// mirrored taps with padding KH-1-PT / KW-1-PL
+static Igemm dgrad_args(const ConvGeom& g, const void* dy, const void* w_hwio, void* dx) {
+  return Igemm{static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w_hwio), static_cast<uint16_t*>(dx),
+               g.N, g.OH, g.OW, g.K, g.H, g.W, g.C, g.KH, g.KW, 1, 1, g.KH - 1 - g.PT, g.KW - 1 - g.PL, 1,
+               (long long)g.K, (long long)g.KW * g.C * g.K, (long long)g.C * g.K, g.N * g.H * g.W, 0, 0, 0,
+               nullptr, nullptr};
+}
+
 // the row tile launch() picks (the BN partial-sum rows of an epilogue are per row tile)
 int conv_fwd_row_tile(const ConvGeom& g, bool in_bn) {
   if (in_bn) return 128;
+  {
+    int Hp, Wp;
+    const Igemm a = fwd_args(g, nullptr, nullptr, nullptr);
+    if (use_halo(a, Hp, Wp)) return kHaloBM;
+  }
   if (use_v2(g.N * g.OH * g.OW, g.K, g.KH * g.KW * (g.C / BK), g.KH * g.KW)) return 256;
   return (g_forced_tile == 3 && g.K % 128 == 0) ? 256 : 128;
 }
 
 int conv_dgrad_row_tile(const ConvGeom& g) {
+  {
+    int Hp, Wp;
+    const Igemm a = dgrad_args(g, nullptr, nullptr, nullptr);
+    if (use_halo(a, Hp, Wp)) return kHaloBM;
+  }
   if (use_v2(g.N * g.H * g.W, g.C, g.KH * g.KW * (g.K / BK), g.KH * g.KW)) return 256;
   return (g_forced_tile == 3 && g.C % 128 == 0) ? 256 : 128;
 }
@@ -1001,10 +1226,8 @@ int conv_dgrad_s2_row_tile(const ConvGeom& g) {
 
 void conv_fwd_bf16(const void* x, const void* w_ohwi, void* y, const ConvGeom& g, hipStream_t s, float* stats,
                    const float* in_ss) {
-  Igemm a{static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w_ohwi), static_cast<uint16_t*>(y),
-          g.N, g.H, g.W, g.C, g.OH, g.OW, g.K, g.KH, g.KW, g.SH, g.SW, g.PT, g.PL, 0,
-          (long long)g.KH * g.KW * g.C, (long long)g.KW * g.C, (long long)g.C, g.N * g.OH * g.OW, 0, 0, 0, nullptr,
-          stats};
+  Igemm a = fwd_args(g, x, w_ohwi, y);
+  a.stats = stats;
   a.in_ss = in_ss;
   launch(a, s);
 }
@@ -1014,11 +1237,14 @@ void conv_dgrad_bf16(const void* dy, const void* w_hwio, void* dx, const ConvGeo
                      float* bn_part2, const float* bn_ss) {
   // image = dy [N][OH][OW][K] (reduction channels K), output = dx [N][H][W][C] (columns C), stride 1,
   // mirrored taps with padding KH-1-PT / KW-1-PL
-  Igemm a{static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(w_hwio), static_cast<uint16_t*>(dx),
-          g.N, g.OH, g.OW, g.K, g.H, g.W, g.C, g.KH, g.KW, 1, 1, g.KH - 1 - g.PT, g.KW - 1 - g.PL, 1,
-          (long long)g.K, (long long)g.KW * g.C * g.K, (long long)g.C * g.K, g.N * g.H * g.W, 0, 0, 0,
-          static_cast<const uint16_t*>(residual), nullptr, static_cast<const uint16_t*>(bn_y),
-          static_cast<const uint16_t*>(bn_x), bn_part, static_cast<const uint16_t*>(bn_x2), bn_part2, bn_ss};
+  Igemm a = dgrad_args(g, dy, w_hwio, dx);
+  a.res = static_cast<const uint16_t*>(residual);
+  a.bn_y = static_cast<const uint16_t*>(bn_y);
+  a.bn_x = static_cast<const uint16_t*>(bn_x);
+  a.bn_part = bn_part;
+  a.bn_x2 = static_cast<const uint16_t*>(bn_x2);
+  a.bn_part2 = bn_part2;
+  a.bn_ss = bn_ss;
   launch(a, s);
 }
 
