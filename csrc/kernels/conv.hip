@@ -850,7 +850,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, MINW) void k_conv_glds(Igemm a) {
 // (n, oh, ow) order, so the conv_epilogue variants (BN statistics, residual, BN-group backward) apply
 // unchanged.  The same kernel runs the stride-1 input gradient (dy as the image, mirrored taps).
 template <int BM, int BN, int WGM, int WGN, int NSLOT, int EK>
-__global__ __launch_bounds__(64 * WGM * WGN, 4) void k_conv_halo(Igemm a, int Hp, int Wp) {
+__global__ __launch_bounds__(64 * WGM * WGN, 4) void k_conv_halo(Igemm a, int Hp, int Wp, int diag) {
   constexpr int NW = WGM * WGN, NT = 64 * NW;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   constexpr int MI32 = WTM / 32, NJ32 = WTN / 32;
@@ -924,7 +924,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, 4) void k_conv_halo(Igemm a, int Hp
     int kh = 0, kw = 0;
     for (int tap = 0; tap < taps; ++tap) {
       if (c | tap) __syncthreads();  // every wave done reading the previous weight tile (and window)
-      if (tap == 0) {
+      const bool ld = !(diag & 1) || (c == 0 && tap == 0);  // diag 1: loads of the first step only
+      if (tap == 0 && ld) {
 #pragma unroll
         for (int i = 0; i < A_LD; ++i)
           if ((i * NW + wave) * 8 < nslot)  // (wave-uniform)
@@ -933,11 +934,12 @@ __global__ __launch_bounds__(64 * WGM * WGN, 4) void k_conv_halo(Igemm a, int Hp
       const int wkh = a.flip ? a.KH - 1 - kh : kh, wkw = a.flip ? a.KW - 1 - kw : kw;
       const int soff_b = (int)((wkh * a.w_kh + wkw * a.w_kw + c * BK) * 2);
 #pragma unroll
-      for (int i = 0; i < B_LD; ++i) lds_dma16(w_rsrc, lb + (i * NW + wave) * 8 * LDS_ROW, b_vo[i], soff_b);
+      for (int i = 0; i < B_LD; ++i)
+        if (ld) lds_dma16(w_rsrc, lb + (i * NW + wave) * 8 * LDS_ROW, b_vo[i], soff_b);
       wait_vmcnt_barrier<0>();
       const int toff = kh * Wp + kw;
 #pragma unroll
-      for (int st = 0; st < BK / 16; ++st) {
+      for (int st = 0; st < ((diag & 2) ? 0 : BK / 16); ++st) {  // diag 2: no MFMA work
         bf16x8 fa[MI32], fb[NJ32];
 #pragma unroll
         for (int i = 0; i < MI32; ++i) {
@@ -1084,15 +1086,32 @@ bool use_dma1(const Igemm& a) {
 }
 
 // halo kernel (k_conv_halo) for stride-1 multi-tap convolutions whose longest input window fits
-// kHaloSlots: forced by impl 7, by default where the per-shape A/B favoured it (TDL_CONV_HALO=0/1
-// overrides)
+// kHaloSlots: forced by impl 7 or g_halo 1; by default (g_halo 2) only where the per-shape A/B
+// favoured it (profiles/conv_halo_r6.txt, b=256 Keras ResNet-50 3x3 shapes, three boxes):
+//   14x14x256 3x3  fwd 72.6 -> 67.1 us, dgrad 71.4 -> 67.2 (the 256-row tile spans 1.3 images)
+//   56x56x64 (+-3 %, noise), 28x28x128 (+3-10 % slower), 7x7x512 (+10-14 % slower): default kernels
+// Both kernels sit at the ~0.85-0.9 PF/s ceiling of a one-barrier-per-k-tile loop: with the loads
+// removed (TDL_CONV_HALO_DIAG=1) the halo kernel still needs 58-88 us, so the im2col re-reads were not
+// the limiter; a two-window / two-stage ring at one workgroup per CU measured 30-50 % slower.
+// TDL_CONV_HALO=0/1/2 overrides.
 int g_halo = [] {
   const char* e = std::getenv("TDL_CONV_HALO");
+  return e != nullptr ? std::atoi(e) : 2;
+}();
+
+bool halo_default_shape(const Igemm& a) {
+  const int hw = a.OH * a.OW;
+  return a.KH == 3 && a.KW == 3 && hw > 128 && hw <= 256 && a.C >= 256 && a.K >= 256;
+}
+
+int g_halo_diag = [] {  // timing diagnostics (wrong results): 1 compute only, 2 loads only
+  const char* e = std::getenv("TDL_CONV_HALO_DIAG");
   return e != nullptr ? std::atoi(e) : 0;
 }();
 
 bool use_halo(const Igemm& a, int& Hp, int& Wp) {
   if (g_forced_tile != 0 || !(g_impl == 7 || (g_impl == 2 && g_halo != 0))) return false;
+  if (g_impl != 7 && g_halo == 2 && !halo_default_shape(a)) return false;
   if (a.SH != 1 || a.SW != 1 || a.scatter || a.in_ss || a.KH * a.KW < 2 || a.K % 64 != 0 || a.C % BK != 0)
     return false;
   return halo_window(a, Hp, Wp) <= kHaloSlots;
@@ -1102,11 +1121,11 @@ template <int BN>
 void launch_halo(const Igemm& a, int Hp, int Wp, hipStream_t s) {
   const dim3 grid((a.M + kHaloBM - 1) / kHaloBM * (a.K / BN)), block(512);
   if (a.bn_part && a.bn_ss)
-    hipLaunchKernelGGL((k_conv_halo<kHaloBM, BN, 4, 2, kHaloSlots, 3>), grid, block, 0, s, a, Hp, Wp);
+    hipLaunchKernelGGL((k_conv_halo<kHaloBM, BN, 4, 2, kHaloSlots, 3>), grid, block, 0, s, a, Hp, Wp, g_halo_diag);
   else if (a.bn_part)
-    hipLaunchKernelGGL((k_conv_halo<kHaloBM, BN, 4, 2, kHaloSlots, 1>), grid, block, 0, s, a, Hp, Wp);
+    hipLaunchKernelGGL((k_conv_halo<kHaloBM, BN, 4, 2, kHaloSlots, 1>), grid, block, 0, s, a, Hp, Wp, g_halo_diag);
   else
-    hipLaunchKernelGGL((k_conv_halo<kHaloBM, BN, 4, 2, kHaloSlots, 0>), grid, block, 0, s, a, Hp, Wp);
+    hipLaunchKernelGGL((k_conv_halo<kHaloBM, BN, 4, 2, kHaloSlots, 0>), grid, block, 0, s, a, Hp, Wp, g_halo_diag);
 }
 
 // Tile choice, from the sweep over the ResNet-50 b=256 convolutions (profiles/conv_tile_sweep_r1.jsonl):
@@ -1126,8 +1145,8 @@ void launch(const Igemm& a, hipStream_t s) {
   {
     int Hp, Wp;
     if (use_halo(a, Hp, Wp)) {
-      if (a.K % 128 == 0) return launch_halo<128>(a, Hp, Wp, s);
-      return launch_halo<64>(a, Hp, Wp, s);
+      if (a.K % 128 == 0 && g_halo != 3) return launch_halo<128>(a, Hp, Wp, s);
+      return launch_halo<64>(a, Hp, Wp, s);  // (g_halo 3: 64-column tiles everywhere, an A/B arm)
     }
   }
   if (use_v2(a.M, a.K, a.KH * a.KW * (a.C / BK), a.KH * a.KW)) {

@@ -12,6 +12,7 @@ sys.path.insert(0, ".")
 from tensorflow_distributed_learning_amd.ops import hip  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+HALO_ARM = int(sys.argv[2]) if len(sys.argv) > 2 else 1  # conv_force_halo value of the halo arm
 # (H, W, C, K, calls per ResNet-50 step)
 SHAPES = [(56, 56, 64, 64, 3), (28, 28, 128, 128, 4), (14, 14, 256, 256, 6), (7, 7, 512, 512, 3)]
 
@@ -48,7 +49,7 @@ def main():
         for d, fn in fns.items():
             C.conv_force_halo(0)
             y0 = fn()
-            C.conv_force_halo(1)
+            C.conv_force_halo(HALO_ARM)
             y1 = fn()
             if d == "fwd":
                 ref = F.conv2d(x.float().permute(0, 3, 1, 2), k.float().permute(3, 2, 0, 1), None, 1, 1).permute(0, 2, 3, 1)
@@ -57,10 +58,10 @@ def main():
                                          ).permute(0, 2, 3, 1)
             ts = {"default": [], "halo": []}
             for _ in range(3):
-                for arm, on in (("default", 0), ("halo", 1)):
+                for arm, on in (("default", 0), ("halo", HALO_ARM)):
                     C.conv_force_halo(on)
                     ts[arm].append(t(fn))
-            C.conv_force_halo(0)
+            C.conv_force_halo(2)
             med = {a: sorted(v)[1] for a, v in ts.items()}
             for a in tot:
                 tot[a] += med[a] * calls

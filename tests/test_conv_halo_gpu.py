@@ -17,7 +17,7 @@ def C():
 
     c = hip()
     yield c
-    c.conv_force_halo(0)
+    c.conv_force_halo(2)
     c.conv_force_impl(2)
 
 
@@ -26,7 +26,7 @@ def _both(C, fn):
     a = fn()
     C.conv_force_halo(1)
     b = fn()
-    C.conv_force_halo(0)
+    C.conv_force_halo(2)
     return a, b
 
 
@@ -108,12 +108,26 @@ def test_halo_selection_reports_256_row_tiles(C):
     """The BN partial buffers of a halo launch have one row per 256 output rows."""
     x = torch.randn(4, 28, 28, 128, device="cuda").bfloat16()
     w = (torch.randn(128, 3, 3, 128, device="cuda") * 0.03).bfloat16()
-    _, s0 = C.conv_fwd_stats(x, w, 28, 28, 1, 1, 1, 1)
+    _, s0 = C.conv_fwd_stats(x, w, 28, 28, 1, 1, 1, 1)  # (not a default halo shape)
     C.conv_force_halo(1)
     try:
         _, s1 = C.conv_fwd_stats(x, w, 28, 28, 1, 1, 1, 1)
     finally:
-        C.conv_force_halo(0)
+        C.conv_force_halo(2)
     M = 4 * 28 * 28
     assert s1.shape[0] < s0.shape[0]
     assert s1.shape[0] >= (M + 255) // 256
+
+
+def test_halo_default_takes_only_the_14x14_class(C):
+    """Default selection (TDL_CONV_HALO unset): the halo kernel for 3x3 convs on 14x14-class maps with
+    >= 256 channels (256-row partial-sum tiles), the other kernels elsewhere (128-row tiles)."""
+    M = 2 * 14 * 14
+    x = torch.randn(2, 14, 14, 256, device="cuda").bfloat16()
+    w = (torch.randn(256, 3, 3, 256, device="cuda") * 0.02).bfloat16()
+    _, s = C.conv_fwd_stats(x, w, 14, 14, 1, 1, 1, 1)
+    assert s.shape[0] <= (M + 255) // 256 + 1  # 256-row tiles (+ scratch rows)
+    x2 = torch.randn(2, 28, 28, 128, device="cuda").bfloat16()
+    w2 = (torch.randn(128, 3, 3, 128, device="cuda") * 0.03).bfloat16()
+    _, s2 = C.conv_fwd_stats(x2, w2, 28, 28, 1, 1, 1, 1)
+    assert s2.shape[0] >= (2 * 28 * 28 + 127) // 128
