@@ -316,6 +316,59 @@ __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
   }
 
   // D[(lane >> 4) * 4 + r][lane & 15] of each 16x16 block
+  if (a.splits > 1) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm + 16 * i + 4 * lk + r, n = n0 + wn + 16 * j + lr;
+          if (m < a.M && n < a.N) a.ws[((int64_t)blockIdx.z * a.M + m) * a.N + n] = acc[i][j][r];
+        }
+    return;
+  }
+  // out_store's operands (bias, the accumulated output or bias gradient) for all 16 outputs of the
+  // lane loaded first, then the stores: one memory round trip instead of one per output (each
+  // load-add-store of out_store waited for its load with vmcnt(0)); same arithmetic order as out_store
+  float bv[2][2][4], ov[2][2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm + 16 * i + 4 * lk + r, n = n0 + wn + 16 * j + lr;
+        bv[i][j][r] = ov[i][j][r] = 0.f;
+      }
+  // (each batch behind ONE uniform branch, clamped addresses inside it: no per-element branch, so the
+  // compiler waits once for the batch -- a vmcnt(0) per element would also wait for the stores)
+  if (a.bias != nullptr) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = n0 + wn + 16 * j + lr;
+        const float t = a.bias[n < a.N ? n : 0];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[i][j][r] = t;
+      }
+  }
+  if (a.accumulate) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm + 16 * i + 4 * lk + r, n = n0 + wn + 16 * j + lr;
+          const bool ok = m < a.M && n < a.N;
+          const bool ones = m == a.ones_m || n == a.ones_n;
+          const int64_t o = ones ? (int64_t)(m == a.ones_m ? n : m)
+                                 : (a.trans_out ? (int64_t)n * a.ldo + m : (int64_t)m * a.ldo + n);
+          ov[i][j][r] = (ones ? a.dbias : a.out)[ok ? o : 0];
+        }
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -324,10 +377,16 @@ __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wm + 16 * i + 4 * lk + r, n = n0 + wn + 16 * j + lr;
         if (m >= a.M || n >= a.N) continue;
-        if (a.splits > 1)
-          a.ws[((int64_t)blockIdx.z * a.M + m) * a.N + n] = acc[i][j][r];
-        else
-          out_store(a, m, n, acc[i][j][r]);
+        float v = acc[i][j][r];
+        if (m == a.ones_m || n == a.ones_n) {  // the bias-gradient row / column
+          if (a.accumulate) v += ov[i][j][r];
+          a.dbias[m == a.ones_m ? n : m] = v;
+          continue;
+        }
+        if (a.bias != nullptr) v += bv[i][j][r];
+        if (a.accumulate) v += ov[i][j][r];
+        if (a.act == 1) v = fmaxf(v, 0.f);
+        a.out[a.trans_out ? (int64_t)n * a.ldo + m : (int64_t)m * a.ldo + n] = v;
       }
 }
 
