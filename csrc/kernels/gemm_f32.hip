@@ -86,8 +86,13 @@ __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
   const int kend = min(a.Kred, kbeg + a.kchunk);
   const F32ConvGeom& g = a.g;
 
-  // A: row ml, reduction quad kqa; B: reduction row kl, column quad nqb
-  const int ml = lane, kqa = wave * 4;
+  // A: row ml, reduction quad kqa; B: reduction row kl, column quad nqb.  With 16-B quads (VA: the
+  // reduction is contiguous in memory, e.g. the channels of an NHWC pixel) four adjacent lanes read the
+  // 64 contiguous bytes of one row's slice, so a wave-instruction touches 16 rows instead of 64 (a 16-B
+  // piece of 64 different 256-B pixel rows: 4x the cache lines per useful byte); the element-wise
+  // loaders keep a row per lane (then consecutive lanes read consecutive rows, e.g. a transposed A).
+  // (the quad-major As writes are 4-way bank-conflicted; the MFMA reads, 8x as many, stay conflict-free)
+  const int ml = VA ? t >> 2 : lane, kqa = VA ? (t & 3) * 4 : wave * 4;
   const int kl = t >> 4, nqb = (t & 15) * 4;
   const int am = m0 + ml, bn = n0 + nqb;
   const bool arow = am < a.M;
