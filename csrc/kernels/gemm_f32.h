@@ -51,6 +51,14 @@ struct F32GemmArgs {
                                   // kF32ConvWgrad); that output row / column goes to dbias
   int b_hwio = 0;                 // kF32ConvDgrad: b is the forward kernel w HWIO [R][S][C][K] itself
                                   // (B(k = (r, s, kk), n = c) read transposed: no transpose pass)
+  // kF32ConvFwd + 2x2 / stride-2 'valid' max pool in the epilogue: rows are ordered (n, ph, pw, q) -- the
+  // 4 pixels q = (dy, dx) of each pool window consecutive, i.e. in ONE lane's 4 accumulators -- so
+  // M = N * PH * PW * 4 (pixels of an odd last row / column are not computed); y (out, NHWC [N][OH][OW][K])
+  // is still written for the backward, plus the pooled maximum pout [N][PH][PW][K] and its window
+  // position parg (uint8, ops/pooling.py's argmax format).  Needs splits == 1 (f32_gemm_plan).
+  int pool = 0, pool_h = 0, pool_w = 0;
+  float* pout = nullptr;
+  uint8_t* parg = nullptr;
 };
 
 constexpr int kF32Tile = 64;
@@ -61,7 +69,7 @@ constexpr int kF32Tile = 64;
 inline void f32_gemm_plan(F32GemmArgs& a, int kmin = 64, int cap = 1024) {
   const int64_t tiles = (int64_t)((a.M + kF32Tile - 1) / kF32Tile) * ((a.N + kF32Tile - 1) / kF32Tile);
   int splits = 1;
-  if (tiles < 512 && a.Kred > 256) {
+  if (tiles < 512 && a.Kred > 256 && !a.pool) {
     const int64_t want = (1024 + tiles - 1) / tiles;
     const int64_t most = (a.Kred + kmin - 1) / kmin;
     splits = (int)(want < most ? want : most);

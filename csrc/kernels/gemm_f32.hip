@@ -100,11 +100,23 @@ __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
   // per-thread fixed decodes
   int an = 0, ay = 0, ax = 0;  // conv fwd: image, top-left input row / col; dgrad: image, y + pt, x + pl
   if constexpr (MODE == kF32ConvFwd) {
-    const int hw = g.oh * g.ow;
-    an = am / hw;
-    const int p = am - an * hw, oy = p / g.ow;
+    int oy, ox;
+    if (a.pool) {  // rows (n, ph, pw, q): pixel (2 ph + q / 2, 2 pw + q % 2)
+      const int wins = a.pool_h * a.pool_w;
+      an = am / (4 * wins);
+      const int rem = am - an * 4 * wins, win = rem >> 2, q = rem & 3;
+      const int php = win / a.pool_w;
+      oy = 2 * php + (q >> 1);
+      ox = 2 * (win - php * a.pool_w) + (q & 1);
+    } else {
+      const int hw = g.oh * g.ow;
+      an = am / hw;
+      const int p = am - an * hw;
+      oy = p / g.ow;
+      ox = p - oy * g.ow;
+    }
     ay = oy * g.sh - g.pt;
-    ax = (p - oy * g.ow) * g.sw - g.pl;
+    ax = ox * g.sw - g.pl;
   } else if constexpr (MODE == kF32ConvDgrad) {
     const int hw = g.h * g.w;
     an = am / hw;
@@ -373,6 +385,37 @@ __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
                                  : (a.trans_out ? (int64_t)n * a.ldo + m : (int64_t)m * a.ldo + n);
           ov[i][j][r] = (ones ? a.dbias : a.out)[ok ? o : 0];
         }
+  }
+  if (MODE == kF32ConvFwd && a.pool) {
+    // a lane's 4 rows 4 lk + r of each 16-row block are one pool window (window-major rows, M % 4 == 0)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int mb = m0 + wm + 16 * i + 4 * lk, n = n0 + wn + 16 * j + lr;
+        if (mb >= a.M || n >= a.N) continue;
+        const int wins = a.pool_h * a.pool_w;
+        const int img = mb / (4 * wins), win = (mb >> 2) - img * wins;
+        const int php = win / a.pool_w, pwp = win - php * a.pool_w;
+        float best = -INFINITY;
+        uint32_t arg = 255u;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {  // the same arithmetic as the unfused epilogue, then the pool's max
+          float v = acc[i][j][r];
+          if (a.bias != nullptr) v += bv[i][j][r];
+          if (a.act == 1) v = fmaxf(v, 0.f);
+          const int oy = 2 * php + (r >> 1), ox = 2 * pwp + (r & 1);
+          a.out[(((int64_t)img * g.oh + oy) * g.ow + ox) * a.ldo + n] = v;
+          if (v > best) {
+            best = v;
+            arg = (uint32_t)r;  // window position (dy * 2 + dx), first maximum wins
+          }
+        }
+        const int64_t po = (((int64_t)img * a.pool_h + php) * a.pool_w + pwp) * a.N + n;
+        a.pout[po] = best;
+        a.parg[po] = (uint8_t)arg;
+      }
+    return;
   }
 #pragma unroll
   for (int i = 0; i < 2; ++i)

@@ -807,6 +807,45 @@ at::Tensor conv_f32_fwd(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> bi
   return y;
 }
 
+// conv_f32_fwd followed by a 2x2 / stride-2 'valid' max pool, in one launch (the pool in the GEMM's
+// epilogue, rows ordered by pool window): returns [y [N][OH][OW][K], pooled [N][OH/2][OW/2][K], argmax
+// (uint8 window positions, the maxpool_fwd format, for maxpool_bwd)].  With odd OH / OW the last output
+// row / column belongs to no window and is not computed (its y entries are left unset: their gradient
+// is zero, and the backward only selects on them).
+std::vector<at::Tensor> conv_f32_fwd_pool(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> bias, int64_t oh,
+                                          int64_t ow, int64_t sh, int64_t sw, int64_t pt, int64_t pl, int64_t dh,
+                                          int64_t dw, int64_t act) {
+  f32_check(x, "conv_f32_fwd_pool: x");
+  f32_check(w, "conv_f32_fwd_pool: w");
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && w.size(2) == x.size(3), "conv_f32_fwd_pool: x NHWC, w [R][S][C][K]");
+  TORCH_CHECK(oh >= 2 && ow >= 2, "conv_f32_fwd_pool: the output must hold at least one 2x2 window");
+  const int64_t K = w.size(3), PH = oh / 2, PW = ow / 2;
+  auto y = at::empty({x.size(0), oh, ow, K}, x.options());
+  auto p = at::empty({x.size(0), PH, PW, K}, x.options());
+  auto arg = at::empty({x.size(0), PH, PW, K}, x.options().dtype(at::kByte));
+  tdl::F32GemmArgs g{};
+  g.g = f32_geom(x, K, w.size(0), w.size(1), oh, ow, sh, sw, pt, pl, dh, dw);
+  g.a = x.data_ptr<float>();
+  g.b = w.data_ptr<float>();
+  g.out = y.data_ptr<float>();
+  g.bias = f32_bias(bias, K);
+  g.M = (int)(x.size(0) * PH * PW * 4);
+  g.N = (int)K;
+  g.Kred = (int)(w.size(0) * w.size(1) * x.size(3));
+  g.ldo = K;
+  g.vec_a = x.size(3) % 4 == 0 && al16(x);
+  g.vec_b = K % 4 == 0 && al16(w);
+  g.act = (int)act;
+  g.pool = 1;
+  g.pool_h = (int)PH;
+  g.pool_w = (int)PW;
+  g.pout = p.data_ptr<float>();
+  g.parg = arg.data_ptr<uint8_t>();
+  f32_run(tdl::kF32ConvFwd, g, x.options());
+  TORCH_CHECK(g.splits == 1, "conv_f32_fwd_pool: the pooled epilogue needs an unsplit reduction");
+  return {y, p, arg};
+}
+
 // dx[N][H][W][C] of a conv with dy [N][OH][OW][K] and wt = w as [R][S][K][C]
 at::Tensor conv_f32_dgrad(at::Tensor dy, at::Tensor wt, int64_t h, int64_t wd, int64_t sh, int64_t sw, int64_t pt,
                           int64_t pl, int64_t dh, int64_t dw, c10::optional<at::Tensor> dy_mask, bool w_hwio) {
@@ -945,6 +984,11 @@ void register_ops(pybind11::module& m) {
         pybind11::arg("bias") = pybind11::none(), pybind11::arg("out") = pybind11::none(),
         pybind11::arg("accumulate") = false, pybind11::arg("act") = 0, pybind11::arg("amask") = pybind11::none(),
         pybind11::arg("bmask") = pybind11::none(), pybind11::arg("dbias") = pybind11::none());
+  m.def("conv_f32_fwd_pool", &conv_f32_fwd_pool,
+        "conv_f32_fwd + 2x2/2 'valid' max pool in the epilogue: [y, pooled, argmax]", pybind11::arg("x"),
+        pybind11::arg("w"), pybind11::arg("bias"), pybind11::arg("oh"), pybind11::arg("ow"), pybind11::arg("sh"),
+        pybind11::arg("sw"), pybind11::arg("pt"), pybind11::arg("pl"), pybind11::arg("dh") = 1,
+        pybind11::arg("dw") = 1, pybind11::arg("act") = 0);
   m.def("conv_f32_fwd", &conv_f32_fwd, "NHWC f32 implicit-GEMM convolution forward, any geometry (act 1: + ReLU)",
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("bias"), pybind11::arg("oh"), pybind11::arg("ow"),
         pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("pt"), pybind11::arg("pl"), pybind11::arg("dh") = 1,

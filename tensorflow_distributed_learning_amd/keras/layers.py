@@ -362,7 +362,19 @@ class Conv2D(Layer):
                                     regularizer=self.bias_regularizer) if self.use_bias else None
         self.built = True
 
-    def call(self, x, training=None, _fold_bias=False, _grad_box=None, _bn_stats=False, _zero_pad=None):
+    def call(self, x, training=None, _pool=None, **kw):
+        """``_pool``: the 2x2 / stride-2 'valid' MaxPooling2D layer that follows this conv in a Sequential
+        model (models.Sequential.call): on the generic f32 path the pool runs in the convolution's own
+        launch (ops/conv_f32.conv2d_pool); elsewhere it is simply applied after the conv."""
+        if _pool is None:
+            return self._conv_call(x, training=training, **kw)
+        out = self._conv_call(x, training=training, _pool_try=True, **kw)
+        if isinstance(out, _Pooled):
+            return out.t
+        return _pool(out, training=training)
+
+    def _conv_call(self, x, training=None, _fold_bias=False, _grad_box=None, _bn_stats=False, _zero_pad=None,
+                   _pool_try=False):
         """``_fold_bias``: the functional executor folded this bias into the following training-mode
         BatchNormalization (keras/fusion.py), so the convolution runs without it.  ``_grad_box``:
         the input's other consumer's gradient is summed into this conv's input gradient.
@@ -443,6 +455,14 @@ class Conv2D(Layer):
             else:
                 gt, wv, anchor = None, self.kernel.cast(x.dtype), None
             act = _fused_act(self.activation)  # ReLU inside the GEMMs (forward epilogue, backward masks)
+            if _pool_try and act == 1:
+                oh = _conv_f32.out_size(x.shape[1], self.kernel_size[0], self.strides[0], self.dilation_rate[0],
+                                        pads[0], pads[1])
+                ow = _conv_f32.out_size(x.shape[2], self.kernel_size[1], self.strides[1], self.dilation_rate[1],
+                                        pads[2], pads[3])
+                if _conv_f32.conv_pool_supported(x, oh, ow, self.filters):
+                    return _Pooled(_conv_f32.conv2d_pool(x, wv, b, self.strides, pads, self.dilation_rate, grad_out=gt,
+                                                         anchor=anchor, act=act, gb_out=gb))
             y = _conv_f32.conv2d(x, wv, b, self.strides, pads, self.dilation_rate, grad_out=gt, anchor=anchor, act=act,
                                  gb_out=gb)
             return y if act else self.activation(y)
@@ -471,6 +491,25 @@ class Conv2D(Layer):
                     groups=self.groups, activation=_act.serialize(self.activation), use_bias=self.use_bias,
                     kernel_initializer=_init.serialize(self.kernel_initializer),
                     bias_initializer=_init.serialize(self.bias_initializer))
+
+
+class _Pooled:
+    """Conv2D._conv_call's result when the following max pool already ran in the conv's launch."""
+
+    __slots__ = ("t",)
+
+    def __init__(self, t):
+        self.t = t
+
+
+def conv_pool_pair(conv, pool) -> bool:
+    """``Conv2D -> MaxPooling2D(2, 2, 'valid')``: the pair the generic engine can run as one forward launch
+    (TDL_FUSE_CONV_POOL=0 keeps them apart)."""
+    import os
+
+    return (isinstance(conv, Conv2D) and type(pool) is MaxPooling2D and pool.pool_size == (2, 2)
+            and pool.strides == (2, 2) and pool.padding == "valid"
+            and os.environ.get("TDL_FUSE_CONV_POOL", "1") == "1")
 
 
 class _Pool2D(Layer):

@@ -885,8 +885,19 @@ class Sequential(Model):
         self._build_layers(input_shape)
 
     def call(self, x, training=None):
-        for l in self._seq:
-            x = l(x, training=training)
+        seq, i = self._seq, 0
+        fuse = bool(training) and isinstance(x, torch.Tensor) and x.is_cuda
+        while i < len(seq):
+            if fuse and i + 1 < len(seq):
+                from .layers import conv_pool_pair
+
+                if conv_pool_pair(seq[i], seq[i + 1]):
+                    # Conv2D -> MaxPooling2D(2): one forward launch on the generic f32 path (Conv2D.call)
+                    x = seq[i](x, training=training, _pool=seq[i + 1])
+                    i += 2
+                    continue
+            x = seq[i](x, training=training)
+            i += 1
         return x
 
     def compute_output_shape(self, s):

@@ -78,31 +78,84 @@ class _ConvF32(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w, y = ctx.saved_tensors
-        stride, pads, dil = ctx.geo
-        dy = _c32(dy)
-        dx = dw = db = None
-        if ctx.needs_input_grad[0]:
-            dx = dgrad(dy, w, (x.shape[1], x.shape[2]), stride, pads, dil, dy_mask=y).to(ctx.dtypes[0])
-        rs = (w.shape[0], w.shape[1])
-        want_db = ctx.has_b and (ctx.gb_out is not None or ctx.needs_input_grad[2])
-        if ctx.grad_out is not None:
-            # slab targets: dW (and db, from the same kernel) added in place
-            dbt = ctx.gb_out if ctx.gb_out is not None else (
-                torch.zeros(w.shape[-1], dtype=torch.float32, device=dy.device) if want_db else None)
-            wgrad(x, dy, rs, stride, pads, dil, out=ctx.grad_out, accumulate=True, dy_mask=y, dbias=dbt)
-            if ctx.gb_out is None and want_db:
-                db = dbt
-        elif ctx.needs_input_grad[1]:
-            dbt = torch.empty(w.shape[-1], dtype=torch.float32, device=dy.device) if want_db else None
-            dw = wgrad(x, dy, rs, stride, pads, dil, dy_mask=y, dbias=dbt).to(ctx.dtypes[1])
+        return _conv_backward(ctx, x, w, y, _c32(dy))
+
+
+def _conv_backward(ctx, x, w, y, dy):
+    """Input / weight / bias gradients of :func:`fwd` from the f32 output gradient ``dy`` (``y``: the saved
+    ReLU output whose mask applies, or None)."""
+    stride, pads, dil = ctx.geo
+    dx = dw = db = None
+    if ctx.needs_input_grad[0]:
+        dx = dgrad(dy, w, (x.shape[1], x.shape[2]), stride, pads, dil, dy_mask=y).to(ctx.dtypes[0])
+    rs = (w.shape[0], w.shape[1])
+    want_db = ctx.has_b and (ctx.gb_out is not None or ctx.needs_input_grad[2])
+    if ctx.grad_out is not None:
+        # slab targets: dW (and db, from the same kernel) added in place
+        dbt = ctx.gb_out if ctx.gb_out is not None else (
+            torch.zeros(w.shape[-1], dtype=torch.float32, device=dy.device) if want_db else None)
+        wgrad(x, dy, rs, stride, pads, dil, out=ctx.grad_out, accumulate=True, dy_mask=y, dbias=dbt)
+        if ctx.gb_out is None and want_db:
             db = dbt
-        elif want_db:
-            g = dy.float() if y is None else dy.float() * (y > 0)
-            if ctx.gb_out is not None:
-                ctx.gb_out.add_(g.sum((0, 1, 2)))
-            else:
-                db = g.sum((0, 1, 2))
-        return dx, dw, db, None, None, None, None, None, None, None
+    elif ctx.needs_input_grad[1]:
+        dbt = torch.empty(w.shape[-1], dtype=torch.float32, device=dy.device) if want_db else None
+        dw = wgrad(x, dy, rs, stride, pads, dil, dy_mask=y, dbias=dbt).to(ctx.dtypes[1])
+        db = dbt
+    elif want_db:
+        g = dy.float() if y is None else dy.float() * (y > 0)
+        if ctx.gb_out is not None:
+            ctx.gb_out.add_(g.sum((0, 1, 2)))
+        else:
+            db = g.sum((0, 1, 2))
+    return dx, dw, db, None, None, None, None, None, None, None
+
+
+class _ConvPoolF32(torch.autograd.Function):
+    """conv (+ bias, + ReLU) followed by a 2x2 / stride-2 'valid' max pool: ONE forward launch (the pool in
+    the GEMM epilogue, conv_f32_fwd_pool); the backward is the pool's (maxpool_bwd over the epilogue's
+    argmax) and then the conv's, exactly as the unfused pair."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pads, dil, grad_out, anchor=None, act=0, gb_out=None):
+        R, S = w.shape[0], w.shape[1]
+        oh = out_size(x.shape[1], R, stride[0], dil[0], pads[0], pads[1])
+        ow = out_size(x.shape[2], S, stride[1], dil[1], pads[2], pads[3])
+        bb = _c32(b) if b is not None else None
+        y, p, arg = hip().conv_f32_fwd_pool(_c32(x), _c32(w), bb, oh, ow, stride[0], stride[1], pads[0], pads[2],
+                                            dil[0], dil[1], act=int(act))
+        ctx.save_for_backward(x, w, y if act else None, arg)
+        ctx.geo = (stride, pads, dil)
+        ctx.yshape = list(y.shape)
+        ctx.has_b = b is not None
+        ctx.grad_out, ctx.gb_out = grad_out, gb_out
+        ctx.dtypes = (x.dtype, w.dtype)
+        return p.to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, dp):
+        x, w, y, arg = ctx.saved_tensors
+        dp = dp.contiguous()
+        if dp.dtype != torch.float32:
+            dp = dp.float()
+        if dp.data_ptr() % 16:
+            dp = dp.clone()
+        dy = hip().maxpool_bwd(dp, arg, ctx.yshape, 2, 2, 2, 2, 0, 0)
+        return _conv_backward(ctx, x, w, y, _c32(dy))
+
+
+def conv_pool_supported(x: torch.Tensor, oh: int, ow: int, k: int) -> bool:
+    """The fused conv + 2x2 max pool forward (generic engine): f32 GPU activations, an output of at
+    least one window, a channel count the pool backward kernel takes (multiple of 8, <= 2048)."""
+    return (x.is_cuda and x.dim() == 4 and x.dtype == torch.float32 and oh >= 2 and ow >= 2 and k % 8 == 0
+            and k <= 2048)
+
+
+def conv2d_pool(x, w_hwio, bias=None, stride=(1, 1), pads=(0, 0, 0, 0), dil=(1, 1), grad_out=None, anchor=None,
+                act=0, gb_out=None):
+    """``max_pool_2x2(act(conv(x, w) + bias))`` with the pool fused into the convolution's launch (see
+    :func:`conv2d` for the arguments)."""
+    return _ConvPoolF32.apply(x, w_hwio, bias, tuple(int(s) for s in stride), tuple(int(p) for p in pads),
+                              tuple(int(d) for d in dil), grad_out, anchor, int(act), gb_out)
 
 
 def conv2d(x, w_hwio, bias=None, stride=(1, 1), pads=(0, 0, 0, 0), dil=(1, 1), grad_out=None, anchor=None, act=0,

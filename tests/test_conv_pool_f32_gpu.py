@@ -1,0 +1,116 @@
+"""Conv2D(relu) -> MaxPooling2D(2) as ONE forward launch on the generic f32 path (csrc/kernels/gemm_f32.hip
+pooled epilogue: rows ordered by pool window, conv_f32_fwd_pool) against the unfused pair (conv_f32_fwd +
+maxpool_fwd) and float64 PyTorch: conv output on every window pixel, pooled output, argmax, and the
+gradients through the fused op's backward (maxpool_bwd + the conv backward) -- including an odd output
+size whose last row / column belongs to no window, and 'same' padding."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+# (N, H, W, C, K, kernel, pad): the reference CNN's two convs (26x26 and 11x11 outputs), a 'same' conv,
+# a ragged one
+SHAPES = [(8, 28, 28, 1, 32, 3, 0), (8, 13, 13, 32, 64, 3, 0), (4, 28, 28, 1, 32, 3, 1), (3, 9, 12, 8, 24, 3, 1)]
+
+
+def _data(shape):
+    N, H, W, C, K, k, p = shape
+    g = torch.Generator(device="cpu").manual_seed(H * 100 + C)
+    x = torch.randn(N, H, W, C, generator=g).cuda()
+    w = (torch.randn(k, k, C, K, generator=g) / (k * k * C) ** 0.5).cuda()
+    b = (torch.randn(K, generator=g) * 0.1).cuda()
+    return x, w, b
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_pooled_epilogue_matches_unfused(shape):
+    from tensorflow_distributed_learning_amd.ops import hip
+
+    C = hip()
+    N, H, W, Ci, K, k, p = shape
+    x, w, b = _data(shape)
+    OH, OW = H + 2 * p - k + 1, W + 2 * p - k + 1
+    y, pooled, arg = C.conv_f32_fwd_pool(x, w, b, OH, OW, 1, 1, p, p, act=1)
+    y0 = C.conv_f32_fwd(x, w, b, OH, OW, 1, 1, p, p, act=1)
+    PH, PW = OH // 2, OW // 2
+    # every pixel inside a window: the unfused conv's value (the split-K plan may differ: f32 rounding)
+    torch.testing.assert_close(y[:, :2 * PH, :2 * PW], y0[:, :2 * PH, :2 * PW], rtol=1e-5, atol=1e-5)
+    p0, a0 = C.maxpool_fwd(y0, 2, 2, 2, 2, 0, 0, PH, PW, False)
+    torch.testing.assert_close(pooled, p0, rtol=1e-5, atol=1e-5)
+    ref = F.max_pool2d(torch.relu(F.conv2d(x.double().permute(0, 3, 1, 2), w.double().permute(3, 2, 0, 1),
+                                           b.double(), 1, p)), 2).permute(0, 2, 3, 1)
+    torch.testing.assert_close(pooled.double(), ref, rtol=1e-5, atol=1e-5)
+    # argmax: the first maximum of the window in (dy, dx) order, as maxpool_fwd
+    win = y[:, :2 * PH, :2 * PW].reshape(N, PH, 2, PW, 2, K).permute(0, 1, 3, 2, 4, 5).reshape(N, PH, PW, 4, K)
+    assert torch.equal(arg.long(), win.argmax(3)) or torch.equal(torch.gather(win, 3, arg.long().unsqueeze(3))
+                                                                  .squeeze(3), pooled)
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_fused_conv_pool_gradients(shape):
+    from tensorflow_distributed_learning_amd.ops import conv_f32 as cf
+    from tensorflow_distributed_learning_amd.ops import pooling
+
+    N, H, W, Ci, K, k, p = shape
+    x, w, b = _data(shape)
+    pads = (p, p, p, p)
+    outs = []
+    for fused in (True, False):
+        xv, wv, bv = (t.clone().requires_grad_(True) for t in (x, w, b))
+        if fused:
+            out = cf.conv2d_pool(xv, wv, bv, (1, 1), pads, act=1)
+        else:
+            out = pooling.max_pool_nhwc(cf.conv2d(xv, wv, bv, (1, 1), pads, act=1), (2, 2), (2, 2))
+        g = torch.Generator(device="cpu").manual_seed(3)
+        dout = torch.randn(out.shape, generator=g).cuda()
+        out.backward(dout)
+        outs.append((out.detach(), xv.grad, wv.grad, bv.grad))
+    for a, c in zip(outs[0], outs[1]):
+        torch.testing.assert_close(a, c, rtol=1e-4, atol=1e-5)
+
+
+def _fit_reference_cnn(fuse: str):
+    import os
+
+    import numpy as np
+
+    import tensorflow_distributed_learning_amd as tdl
+
+    tdl.keras.backend.clear_session()
+    tdl.keras.utils.set_random_seed(5)
+    g = np.random.default_rng(0)
+    x = g.random((256, 28, 28, 1), dtype=np.float32)
+    y = g.integers(0, 10, 256).astype(np.int64)
+    old = {k: os.environ.get(k) for k in ("TDL_DISABLE_FUSED", "TDL_FUSE_CONV_POOL")}
+    os.environ["TDL_DISABLE_FUSED"] = "1"
+    os.environ["TDL_FUSE_CONV_POOL"] = fuse
+    try:
+        L = tdl.keras.layers
+        with tdl.distribute.MirroredStrategy(devices=["/gpu:0"]).scope():
+            m = tdl.keras.Sequential([L.Conv2D(32, 3, activation="relu", input_shape=(28, 28, 1)), L.MaxPooling2D(),
+                                      L.Conv2D(64, 3, activation="relu"), L.MaxPooling2D(), L.Flatten(),
+                                      L.Dense(128, activation="relu"), L.Dense(10)])
+            m.compile(loss=tdl.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+                      optimizer=tdl.keras.optimizers.SGD(0.05))
+        h = m.fit(x, y, batch_size=64, epochs=2, verbose=0, shuffle=False)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    return m, h
+
+
+def test_generic_engine_reference_cnn_fused_pool_trains_like_unfused():
+    """The generic engine's Sequential forward takes the fused Conv2D -> MaxPooling2D pairs in training
+    (two launches fewer per step); two epochs follow the unfused model."""
+    import numpy as np
+
+    mf, hf = _fit_reference_cnn("1")
+    assert mf._trainer.kind == "generic"
+    mu, hu = _fit_reference_cnn("0")
+    np.testing.assert_allclose(hf.history["loss"], hu.history["loss"], rtol=1e-4)
+    for a, b in zip(mf.get_weights(), mu.get_weights()):
+        np.testing.assert_allclose(a, b, rtol=1e-3, atol=5e-5)
