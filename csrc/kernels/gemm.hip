@@ -320,7 +320,56 @@ __global__ __launch_bounds__(1024) void k_xent_head(const float* __restrict__ z,
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float inv_gn = (float)(1.0 / gn);
   double my_loss = 0.0, my_cor = 0.0;
-  for (int row = w; row < N; row += 16) {
+  if (K <= 64) {
+    // small heads (the reference CNN's 10 classes): a row is one load per lane, and each wave issues
+    // the loads of its next 4 rows (logits and labels) before any math, so the rows do not pay one
+    // dependent memory round trip each (the label load, then the logit at the label); z[y] comes from
+    // lane y.  Same arithmetic and row order as the general loop below.
+    for (int base = w; base < N; base += 64) {
+      float v[4];
+      long long yy[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = base + 16 * i;
+        const bool ok = row < N;
+        v[i] = (ok && lane < K) ? z[(long long)row * K + lane] : -INFINITY;
+        yy[i] = ok ? lab[row] : -1;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = base + 16 * i;
+        if (row >= N) break;  // (wave-uniform)
+        float mx = -INFINITY;
+        int am = K;
+        if (lane < K && v[i] > mx) {
+          mx = v[i];
+          am = lane;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {  // max, first index on ties (tf.argmax)
+          const float om = __shfl_xor(mx, o);
+          const int oa = __shfl_xor(am, o);
+          if (om > mx || (om == mx && oa < am)) {
+            mx = om;
+            am = oa;
+          }
+        }
+        float se = lane < K ? __expf(v[i] - mx) : 0.f;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) se += __shfl_xor(se, o);
+        const float lse = mx + __logf(se);
+        const long long y = yy[i];
+        const bool valid = y >= 0 && y < K;
+        const float zy = __shfl(v[i], valid ? (int)y : 0);
+        if (lane < K) dz[(long long)row * K + lane] = (__expf(v[i] - lse) - (lane == y ? 1.f : 0.f)) * inv_gn;
+        if (lane == 0) {
+          my_loss += (double)(valid ? lse - zy : 0.f);
+          my_cor += (valid && am == (int)y) ? 1.0 : 0.0;
+        }
+      }
+    }
+  }
+  for (int row = K <= 64 ? N : w; row < N; row += 16) {
     const float* zr = z + (long long)row * K;
     float mx = -INFINITY;
     int am = K;

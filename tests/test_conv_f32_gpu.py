@@ -248,7 +248,7 @@ def test_dense_f32_fused_relu_and_bias_grad(shape, targets):
     _close(xc.grad, xd.grad)
 
 
-@pytest.mark.parametrize("NK", [(64, 10), (300, 1000), (7, 3)])
+@pytest.mark.parametrize("NK", [(64, 10), (300, 1000), (7, 3), (130, 64), (65, 10), (33, 65)])
 def test_xent_head_loss_grad_and_metrics(NK):
     from tensorflow_distributed_learning_amd.ops import dense as D
 
