@@ -59,6 +59,12 @@ struct F32GemmArgs {
   int pool = 0, pool_h = 0, pool_w = 0;
   float* pout = nullptr;
   uint8_t* parg = nullptr;
+  // kF32ConvDgrad / kF32ConvWgrad with the output gradient given POOLED (the backward of that fused
+  // forward): a = the pool's output gradient [N][PH][PW][K], amask = the pooled maximum, pin_arg = its
+  // window positions; the conv-output gradient the loader forms is, at pixel (oy, ox) of the g.oh x g.ow
+  // grid, pooled gradient * [argmax == this pixel] * [maximum > 0] (pixels outside every window: 0)
+  // -- the max-pool backward and the ReLU mask without their own pass.  Uses pool_h / pool_w.
+  const uint8_t* pin_arg = nullptr;
 };
 
 constexpr int kF32Tile = 64;

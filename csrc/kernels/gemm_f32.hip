@@ -74,9 +74,10 @@ struct Slice {
   float ma[MA ? 4 : 1], mb[MB ? 4 : 1];
   unsigned va, vb;  // loaded value valid (else 0)
   unsigned oa, ob;  // the appended row / column of ones (value 1, unmasked)
+  unsigned pa, pp;  // PIN: the 4 elements' argmax bytes and their own window positions (byte i each)
 };
 
-template <int MODE, bool MA, bool MB, bool VA, bool VB>
+template <int MODE, bool MA, bool MB, bool VA, bool VB, bool PIN = false>
 __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
   __shared__ float As[16 * kLd];
   __shared__ float Bs[16 * kLd];
@@ -139,6 +140,7 @@ __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
   if constexpr (MODE == kF32ConvFwd) ka.set(kbeg + kqa, g.s, g.c);
   if constexpr (MODE == kF32ConvDgrad) ka.set(kbeg + kqa, g.s, g.k);
   if constexpr (MODE == kF32ConvWgrad) kb.set(kbeg + kl, g.oh, g.ow);
+  if constexpr (MODE == kF32ConvWgrad && PIN) ka.set(kbeg + kqa, g.oh, g.ow);  // (img, oy, ox) of the A quad
 
   const bool s1 = g.sh == 1 && g.sw == 1;
   using S = Slice<MA, MB>;
@@ -183,6 +185,7 @@ __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
 
   auto load = [&](int k0, S& r) {
     r.va = r.vb = r.oa = r.ob = 0u;
+    r.pa = r.pp = 0u;
     const int kk = k0 + kqa;  // A: reduction index of slot 0
     if constexpr (MODE == kF32Gemm) {
       const bool ones = am == a.ones_m;  // the appended row of ones (bias gradient)
@@ -214,14 +217,37 @@ __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
             ok = ty >= 0 && tx >= 0 && (s1 || (iy * g.sh == ty && ix * g.sw == tx)) && iy < g.oh && ix < g.ow;
           }
           ok = ok && arow && kk + i < kend;
-          const int64_t base = MODE == kF32ConvFwd ? (((int64_t)an * g.h + iy) * g.w + ix) * g.c
-                                                   : (((int64_t)an * g.oh + iy) * g.ow + ix) * g.k;
+          int64_t base = MODE == kF32ConvFwd ? (((int64_t)an * g.h + iy) * g.w + ix) * g.c
+                                             : (((int64_t)an * g.oh + iy) * g.ow + ix) * g.k;
+          if constexpr (PIN && MODE == kF32ConvDgrad) {  // the pool window of dy pixel (iy, ix)
+            ok = ok && iy < 2 * a.pool_h && ix < 2 * a.pool_w;
+            base = (((int64_t)an * a.pool_h + (iy >> 1)) * a.pool_w + (ix >> 1)) * g.k;
+            const unsigned pos = (unsigned)(((iy & 1) << 1) | (ix & 1));
+            if constexpr (VA) {
+              r.pa = *reinterpret_cast<const unsigned*>(a.pin_arg + (ok ? base + c.lo : 0));
+              r.pp = pos * 0x01010101u;
+            } else {
+              r.pa |= (unsigned)a.pin_arg[ok ? base + c.lo : 0] << (8 * i);
+              r.pp |= pos << (8 * i);
+            }
+          }
           if constexpr (VA)
             lda4(r, ok, base + c.lo);
           else
             lda1(r, i, ok, base + c.lo);
           if (!VA && i < 3) c.step1(g.s, nlo);
         }
+      }
+    } else if constexpr (PIN) {  // wgrad, pooled dy: pixel j = kk + i -> its window, argmax check
+      Ctr c = ka;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (i) c.step1(g.oh, g.ow);
+        const bool ok = arow && kk + i < kend && c.mid < 2 * a.pool_h && c.lo < 2 * a.pool_w;
+        const int64_t e = (((int64_t)c.hi * a.pool_h + (c.mid >> 1)) * a.pool_w + (c.lo >> 1)) * g.k + am;
+        lda1(r, i, ok, e);
+        r.pa |= (unsigned)a.pin_arg[ok ? e : 0] << (8 * i);
+        r.pp |= (unsigned)(((c.mid & 1) << 1) | (c.lo & 1)) << (8 * i);
       }
     } else {  // wgrad: A(m = out channel, j) = dy[j][m]
 #pragma unroll
@@ -285,6 +311,7 @@ __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
         if constexpr (MODE == kF32ConvFwd) ka.step(16, g.s, g.c);
         if constexpr (MODE == kF32ConvDgrad) ka.step(16, g.s, g.k);
         if constexpr (MODE == kF32ConvWgrad) kb.step(16, g.oh, g.ow);
+        if constexpr (MODE == kF32ConvWgrad && PIN) ka.step(16, g.oh, g.ow);
       }
       load(kload, r);
     }
@@ -306,6 +333,7 @@ __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
           av[i] = (r.va >> i & 1u) ? r.a[i] : 0.f;
           bv[i] = (r.vb >> i & 1u) ? r.b[i] : 0.f;
           if constexpr (MA) av[i] = r.ma[i] > 0.f ? av[i] : 0.f;
+          if constexpr (PIN) av[i] = ((r.pa >> (8 * i)) & 0xffu) == ((r.pp >> (8 * i)) & 0xffu) ? av[i] : 0.f;
           if constexpr (MB) bv[i] = r.mb[i] > 0.f ? bv[i] : 0.f;
           av[i] = (r.oa >> i & 1u) ? 1.f : av[i];
           bv[i] = (r.ob >> i & 1u) ? 1.f : bv[i];
@@ -494,12 +522,12 @@ __global__ __launch_bounds__(256) void k_gemm_f32_reduce_wave(F32GemmArgs a) {
 }
 
 // the operand-vectorisation instantiation of a (mode, mask) kernel
-template <int MODE, bool MA, bool MB>
+template <int MODE, bool MA, bool MB, bool PIN = false>
 void launch_v(const F32GemmArgs& a, dim3 grid, hipStream_t s) {
-  if (a.vec_a && a.vec_b) hipLaunchKernelGGL((k_gemm_f32<MODE, MA, MB, true, true>), grid, dim3(256), 0, s, a);
-  else if (a.vec_a) hipLaunchKernelGGL((k_gemm_f32<MODE, MA, MB, true, false>), grid, dim3(256), 0, s, a);
-  else if (a.vec_b) hipLaunchKernelGGL((k_gemm_f32<MODE, MA, MB, false, true>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((k_gemm_f32<MODE, MA, MB, false, false>), grid, dim3(256), 0, s, a);
+  if (a.vec_a && a.vec_b) hipLaunchKernelGGL((k_gemm_f32<MODE, MA, MB, true, true, PIN>), grid, dim3(256), 0, s, a);
+  else if (a.vec_a) hipLaunchKernelGGL((k_gemm_f32<MODE, MA, MB, true, false, PIN>), grid, dim3(256), 0, s, a);
+  else if (a.vec_b) hipLaunchKernelGGL((k_gemm_f32<MODE, MA, MB, false, true, PIN>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((k_gemm_f32<MODE, MA, MB, false, false, PIN>), grid, dim3(256), 0, s, a);
 }
 
 }  // namespace
@@ -517,11 +545,13 @@ void f32_gemm_launch(int mode, const F32GemmArgs& a, hipStream_t s) {
       break;
     case kF32ConvFwd: launch_v<kF32ConvFwd, false, false>(a, grid, s); break;
     case kF32ConvDgrad:
-      if (ma) launch_v<kF32ConvDgrad, true, false>(a, grid, s);
+      if (a.pin_arg != nullptr) launch_v<kF32ConvDgrad, true, false, true>(a, grid, s);  // (amask = the maximum)
+      else if (ma) launch_v<kF32ConvDgrad, true, false>(a, grid, s);
       else launch_v<kF32ConvDgrad, false, false>(a, grid, s);
       break;
     default:
-      if (ma) launch_v<kF32ConvWgrad, true, false>(a, grid, s);
+      if (a.pin_arg != nullptr) launch_v<kF32ConvWgrad, true, false, true>(a, grid, s);
+      else if (ma) launch_v<kF32ConvWgrad, true, false>(a, grid, s);
       else launch_v<kF32ConvWgrad, false, false>(a, grid, s);
       break;
   }

@@ -847,8 +847,24 @@ std::vector<at::Tensor> conv_f32_fwd_pool(at::Tensor x, at::Tensor w, c10::optio
 }
 
 // dx[N][H][W][C] of a conv with dy [N][OH][OW][K] and wt = w as [R][S][K][C]
+// pooled output gradient (pin_arg given: the backward of conv_f32_fwd_pool): dy = the pool's output gradient
+// [N][PH][PW][K], dy_mask = the pooled maximum, pin_arg = its argmax, (out_h, out_w) = the conv's output size
+static void f32_pin(tdl::F32GemmArgs& g, const at::Tensor& dy, const c10::optional<at::Tensor>& pin_arg,
+                    const c10::optional<at::Tensor>& dy_mask, int64_t out_h, int64_t out_w, const char* what) {
+  if (!pin_arg.has_value() || !pin_arg->defined()) return;
+  TORCH_CHECK(pin_arg->is_cuda() && pin_arg->scalar_type() == at::kByte && pin_arg->is_contiguous() &&
+                  pin_arg->sizes() == dy.sizes(), what, ": pin_arg must be a contiguous uint8 tensor shaped like dy");
+  TORCH_CHECK(dy_mask.has_value() && dy_mask->defined(), what, ": pin_arg needs dy_mask (the pooled maximum)");
+  TORCH_CHECK(out_h >= 2 * dy.size(1) && out_w >= 2 * dy.size(2) && out_h <= 2 * dy.size(1) + 1 &&
+                  out_w <= 2 * dy.size(2) + 1, what, ": (out_h, out_w) must be the pooled conv's output size");
+  g.pin_arg = pin_arg->data_ptr<uint8_t>();
+  g.pool_h = (int)dy.size(1);
+  g.pool_w = (int)dy.size(2);
+}
+
 at::Tensor conv_f32_dgrad(at::Tensor dy, at::Tensor wt, int64_t h, int64_t wd, int64_t sh, int64_t sw, int64_t pt,
-                          int64_t pl, int64_t dh, int64_t dw, c10::optional<at::Tensor> dy_mask, bool w_hwio) {
+                          int64_t pl, int64_t dh, int64_t dw, c10::optional<at::Tensor> dy_mask, bool w_hwio,
+                          c10::optional<at::Tensor> pin_arg, int64_t out_h, int64_t out_w) {
   f32_check(dy, "conv_f32_dgrad: dy");
   f32_check(wt, "conv_f32_dgrad: wt");
   // wt: [R][S][K][C], or (w_hwio) the forward kernel [R][S][C][K] read transposed in the kernel
@@ -857,7 +873,10 @@ at::Tensor conv_f32_dgrad(at::Tensor dy, at::Tensor wt, int64_t h, int64_t wd, i
   const int64_t C = wt.size(w_hwio ? 2 : 3), K = dy.size(3);
   auto dx = fresh({dy.size(0), h, wd, C}, dy.options());
   tdl::F32GemmArgs g{};
-  g.g = f32_geom(dx, K, wt.size(0), wt.size(1), dy.size(1), dy.size(2), sh, sw, pt, pl, dh, dw);
+  const bool pin = pin_arg.has_value() && pin_arg->defined();
+  g.g = f32_geom(dx, K, wt.size(0), wt.size(1), pin ? out_h : dy.size(1), pin ? out_w : dy.size(2), sh, sw, pt, pl,
+                 dh, dw);
+  f32_pin(g, dy, pin_arg, dy_mask, out_h, out_w, "conv_f32_dgrad");
   g.a = dy.data_ptr<float>();
   g.b = wt.data_ptr<float>();
   g.out = dx.data_ptr<float>();
@@ -876,21 +895,25 @@ at::Tensor conv_f32_dgrad(at::Tensor dy, at::Tensor wt, int64_t h, int64_t wd, i
 // dW HWIO [R][S][C][K] of a conv with x NHWC and dy [N][OH][OW][K] (into / += out when given)
 at::Tensor conv_f32_wgrad(at::Tensor x, at::Tensor dy, int64_t r, int64_t s, int64_t sh, int64_t sw, int64_t pt,
                           int64_t pl, int64_t dh, int64_t dw, c10::optional<at::Tensor> out, bool accumulate,
-                          c10::optional<at::Tensor> dy_mask, c10::optional<at::Tensor> dbias) {
+                          c10::optional<at::Tensor> dy_mask, c10::optional<at::Tensor> dbias,
+                          c10::optional<at::Tensor> pin_arg, int64_t out_h, int64_t out_w) {
   f32_check(x, "conv_f32_wgrad: x");
   f32_check(dy, "conv_f32_wgrad: dy");
   TORCH_CHECK(x.dim() == 4 && dy.dim() == 4 && x.size(0) == dy.size(0), "conv_f32_wgrad: x, dy NHWC");
   const int64_t C = x.size(3), K = dy.size(3);
   auto dW = f32_out(out, {r, s, C, K}, x.options());
   tdl::F32GemmArgs g{};
-  g.g = f32_geom(x, K, r, s, dy.size(1), dy.size(2), sh, sw, pt, pl, dh, dw);
+  const bool pin = pin_arg.has_value() && pin_arg->defined();
+  const int64_t oh = pin ? out_h : dy.size(1), ow = pin ? out_w : dy.size(2);
+  g.g = f32_geom(x, K, r, s, oh, ow, sh, sw, pt, pl, dh, dw);
+  f32_pin(g, dy, pin_arg, dy_mask, out_h, out_w, "conv_f32_wgrad");
   g.a = dy.data_ptr<float>();
   g.b = x.data_ptr<float>();
   g.out = dW.data_ptr<float>();
   g.M = (int)K;
   g.N = (int)(r * s * C);
-  TORCH_CHECK(dy.numel() / K < (int64_t)1 << 31, "conv_f32_wgrad: reduction too long");
-  g.Kred = (int)(dy.size(0) * dy.size(1) * dy.size(2));
+  TORCH_CHECK(dy.size(0) * oh * ow < (int64_t)1 << 31, "conv_f32_wgrad: reduction too long");
+  g.Kred = (int)(dy.size(0) * oh * ow);
   g.ldo = K;
   g.trans_out = 1;
   g.accumulate = accumulate && out.has_value() && out->defined();
@@ -997,13 +1020,15 @@ void register_ops(pybind11::module& m) {
         "dy_mask: dy * (mask > 0)",
         pybind11::arg("dy"), pybind11::arg("wt"), pybind11::arg("h"), pybind11::arg("w"), pybind11::arg("sh"),
         pybind11::arg("sw"), pybind11::arg("pt"), pybind11::arg("pl"), pybind11::arg("dh") = 1, pybind11::arg("dw") = 1,
-        pybind11::arg("dy_mask") = pybind11::none(), pybind11::arg("w_hwio") = false);
+        pybind11::arg("dy_mask") = pybind11::none(), pybind11::arg("w_hwio") = false,
+        pybind11::arg("pin_arg") = pybind11::none(), pybind11::arg("out_h") = 0, pybind11::arg("out_w") = 0);
   m.def("conv_f32_wgrad", &conv_f32_wgrad, "NHWC f32 convolution weight gradient (HWIO), deterministic split-K; "
         "dy_mask: dy * (mask > 0); dbias: the bias gradient from an appended column of ones",
         pybind11::arg("x"), pybind11::arg("dy"), pybind11::arg("r"), pybind11::arg("s"), pybind11::arg("sh"),
         pybind11::arg("sw"), pybind11::arg("pt"), pybind11::arg("pl"), pybind11::arg("dh") = 1, pybind11::arg("dw") = 1,
         pybind11::arg("out") = pybind11::none(), pybind11::arg("accumulate") = false,
-        pybind11::arg("dy_mask") = pybind11::none(), pybind11::arg("dbias") = pybind11::none());
+        pybind11::arg("dy_mask") = pybind11::none(), pybind11::arg("dbias") = pybind11::none(),
+        pybind11::arg("pin_arg") = pybind11::none(), pybind11::arg("out_h") = 0, pybind11::arg("out_w") = 0);
   m.def("gap_fwd", &gap_fwd, "NHWC bf16 global average pooling");
   m.def("gap_bwd", &gap_bwd, "NHWC bf16 global average pooling backward");
   m.def("slab_cast_bf16", &slab_cast_bf16, "f32 -> bf16 copy of a whole weight slab (one launch)");

@@ -43,25 +43,30 @@ def fwd(x, w_hwio, bias, stride, pads, dil=(1, 1), act=0) -> torch.Tensor:
                               act=int(act))
 
 
-def dgrad(dy, w_hwio, hw, stride, pads, dil=(1, 1), dy_mask=None) -> torch.Tensor:
+def dgrad(dy, w_hwio, hw, stride, pads, dil=(1, 1), dy_mask=None, pin=None) -> torch.Tensor:
     """f32 input gradient of :func:`fwd` for an input of spatial size ``hw`` (``dy_mask``: the ReLU
-    output whose mask applies to ``dy``)."""
+    output whose mask applies to ``dy``).  ``pin = (argmax, out_h, out_w)``: ``dy`` is the gradient of a
+    2x2 max pool over the conv's ReLU output and ``dy_mask`` the pooled maximum (conv2d_pool's backward:
+    the loader routes and masks it, no max-pool backward pass)."""
+    kw = dict(pin_arg=pin[0], out_h=pin[1], out_w=pin[2]) if pin is not None else {}
     if w_hwio.numel() <= (1 << 16):
         # small kernels (the generic engine's layers): read w HWIO transposed in the kernel (w_hwio), no
         # [R][S][K][C] copy kernel per step; large ones keep the copy for 16-B operand loads
         return hip().conv_f32_dgrad(_c32(dy), _c32(w_hwio), hw[0], hw[1], stride[0], stride[1], pads[0], pads[2],
-                                    dil[0], dil[1], dy_mask=dy_mask, w_hwio=True)
+                                    dil[0], dil[1], dy_mask=dy_mask, w_hwio=True, **kw)
     wt = _c32(w_hwio).permute(0, 1, 3, 2).contiguous()  # [R][S][K][C]
     return hip().conv_f32_dgrad(_c32(dy), wt, hw[0], hw[1], stride[0], stride[1], pads[0], pads[2], dil[0], dil[1],
-                                dy_mask=dy_mask)
+                                dy_mask=dy_mask, **kw)
 
 
-def wgrad(x, dy, rs, stride, pads, dil=(1, 1), out=None, accumulate=False, dy_mask=None, dbias=None) -> torch.Tensor:
+def wgrad(x, dy, rs, stride, pads, dil=(1, 1), out=None, accumulate=False, dy_mask=None, dbias=None,
+          pin=None) -> torch.Tensor:
     """f32 HWIO weight gradient of :func:`fwd` (added into the f32 ``out`` when ``accumulate``); with
     ``dbias`` the bias gradient comes from the same kernel (a column of ones appended to the gathered
-    input: no separate reduction)."""
+    input: no separate reduction).  ``pin``: as for :func:`dgrad`."""
+    kw = dict(pin_arg=pin[0], out_h=pin[1], out_w=pin[2]) if pin is not None else {}
     return hip().conv_f32_wgrad(_c32(x), _c32(dy), rs[0], rs[1], stride[0], stride[1], pads[0], pads[2], dil[0],
-                                dil[1], out=out, accumulate=accumulate, dy_mask=dy_mask, dbias=dbias)
+                                dil[1], out=out, accumulate=accumulate, dy_mask=dy_mask, dbias=dbias, **kw)
 
 
 class _ConvF32(torch.autograd.Function):
@@ -81,27 +86,31 @@ class _ConvF32(torch.autograd.Function):
         return _conv_backward(ctx, x, w, y, _c32(dy))
 
 
-def _conv_backward(ctx, x, w, y, dy):
+def _conv_backward(ctx, x, w, y, dy, pin=None, unpool=None):
     """Input / weight / bias gradients of :func:`fwd` from the f32 output gradient ``dy`` (``y``: the saved
-    ReLU output whose mask applies, or None)."""
+    ReLU output whose mask applies, or None).  ``pin``: ``dy`` / ``y`` are the pooled gradient / maximum
+    of conv2d_pool (see :func:`dgrad`); ``unpool()`` then gives the plain conv-output gradient and ReLU
+    output for the one path the kernels do not cover (a bias gradient without a weight gradient)."""
     stride, pads, dil = ctx.geo
     dx = dw = db = None
     if ctx.needs_input_grad[0]:
-        dx = dgrad(dy, w, (x.shape[1], x.shape[2]), stride, pads, dil, dy_mask=y).to(ctx.dtypes[0])
+        dx = dgrad(dy, w, (x.shape[1], x.shape[2]), stride, pads, dil, dy_mask=y, pin=pin).to(ctx.dtypes[0])
     rs = (w.shape[0], w.shape[1])
     want_db = ctx.has_b and (ctx.gb_out is not None or ctx.needs_input_grad[2])
     if ctx.grad_out is not None:
         # slab targets: dW (and db, from the same kernel) added in place
         dbt = ctx.gb_out if ctx.gb_out is not None else (
             torch.zeros(w.shape[-1], dtype=torch.float32, device=dy.device) if want_db else None)
-        wgrad(x, dy, rs, stride, pads, dil, out=ctx.grad_out, accumulate=True, dy_mask=y, dbias=dbt)
+        wgrad(x, dy, rs, stride, pads, dil, out=ctx.grad_out, accumulate=True, dy_mask=y, dbias=dbt, pin=pin)
         if ctx.gb_out is None and want_db:
             db = dbt
     elif ctx.needs_input_grad[1]:
         dbt = torch.empty(w.shape[-1], dtype=torch.float32, device=dy.device) if want_db else None
-        dw = wgrad(x, dy, rs, stride, pads, dil, dy_mask=y, dbias=dbt).to(ctx.dtypes[1])
+        dw = wgrad(x, dy, rs, stride, pads, dil, dy_mask=y, dbias=dbt, pin=pin).to(ctx.dtypes[1])
         db = dbt
     elif want_db:
+        if pin is not None:
+            dy, y = unpool()
         g = dy.float() if y is None else dy.float() * (y > 0)
         if ctx.gb_out is not None:
             ctx.gb_out.add_(g.sum((0, 1, 2)))
@@ -123,7 +132,7 @@ class _ConvPoolF32(torch.autograd.Function):
         bb = _c32(b) if b is not None else None
         y, p, arg = hip().conv_f32_fwd_pool(_c32(x), _c32(w), bb, oh, ow, stride[0], stride[1], pads[0], pads[2],
                                             dil[0], dil[1], act=int(act))
-        ctx.save_for_backward(x, w, y if act else None, arg)
+        ctx.save_for_backward(x, w, y if act else None, arg, p if act else None)
         ctx.geo = (stride, pads, dil)
         ctx.yshape = list(y.shape)
         ctx.has_b = b is not None
@@ -133,14 +142,23 @@ class _ConvPoolF32(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dp):
-        x, w, y, arg = ctx.saved_tensors
-        dp = dp.contiguous()
-        if dp.dtype != torch.float32:
-            dp = dp.float()
-        if dp.data_ptr() % 16:
-            dp = dp.clone()
-        dy = hip().maxpool_bwd(dp, arg, ctx.yshape, 2, 2, 2, 2, 0, 0)
-        return _conv_backward(ctx, x, w, y, _c32(dy))
+        import os
+
+        x, w, y, arg, p = ctx.saved_tensors
+        dp = _c32(dp)
+
+        def unpool():
+            return _c32(hip().maxpool_bwd(dp, arg, ctx.yshape, 2, 2, 2, 2, 0, 0)), y
+
+        if y is not None and os.environ.get("TDL_FUSE_CONV_POOL_BWD", "0") == "1":
+            # the input / weight gradient kernels read the POOLED gradient and route it through the argmax
+            # (and the ReLU mask: maximum > 0) in their operand loaders: no max-pool backward pass.  Off by
+            # default: the per-element window decode and argmax loads cost the weight-gradient kernels
+            # ~4-5 us each, more than the two pool-backward launches they replace (+1.7 % per step,
+            # profiles/generic_engine_r6.txt)
+            return _conv_backward(ctx, x, w, p, dp, pin=(arg, ctx.yshape[1], ctx.yshape[2]), unpool=unpool)
+        dy, _ = unpool()
+        return _conv_backward(ctx, x, w, y, dy)
 
 
 def conv_pool_supported(x: torch.Tensor, oh: int, ow: int, k: int) -> bool:

@@ -114,3 +114,24 @@ def test_generic_engine_reference_cnn_fused_pool_trains_like_unfused():
     np.testing.assert_allclose(hf.history["loss"], hu.history["loss"], rtol=1e-4)
     for a, b in zip(mf.get_weights(), mu.get_weights()):
         np.testing.assert_allclose(a, b, rtol=1e-3, atol=5e-5)
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_pooled_gradient_loaders_match_maxpool_backward_bitwise(shape, monkeypatch):
+    """The fused op's backward reads the POOLED gradient in the input / weight gradient kernels' operand
+    loaders (argmax routing + ReLU mask); it matches the max-pool backward pass followed by the plain
+    kernels (TDL_FUSE_CONV_POOL_BWD=0) bit for bit, bias gradient included."""
+    from tensorflow_distributed_learning_amd.ops import conv_f32 as cf
+
+    x, w, b = _data(shape)
+    p = shape[6]
+    res = []
+    for env in ("1", "0"):
+        monkeypatch.setenv("TDL_FUSE_CONV_POOL_BWD", env)
+        xv, wv, bv = (t.clone().requires_grad_(True) for t in (x, w, b))
+        out = cf.conv2d_pool(xv, wv, bv, (1, 1), (p, p, p, p), act=1)
+        g = torch.Generator(device="cpu").manual_seed(11)
+        out.backward(torch.randn(out.shape, generator=g).cuda())
+        res.append((xv.grad, wv.grad, bv.grad))
+    for a, c in zip(res[0], res[1]):
+        assert torch.equal(a, c)
