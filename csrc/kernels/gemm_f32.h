@@ -55,10 +55,13 @@ struct F32GemmArgs {
   // 4 pixels q = (dy, dx) of each pool window consecutive, i.e. in ONE lane's 4 accumulators -- so
   // M = N * PH * PW * 4 (pixels of an odd last row / column are not computed); y (out, NHWC [N][OH][OW][K])
   // is still written for the backward, plus the pooled maximum pout [N][PH][PW][K] and its window
-  // position parg (uint8, ops/pooling.py's argmax format).  Needs splits == 1 (f32_gemm_plan).
+  // position parg (uint8, ops/pooling.py's argmax format).  Split reductions (< 16 slices) end in
+  // k_gemm_f32_reduce_pool, which applies the same epilogue.
   int pool = 0, pool_h = 0, pool_w = 0;
   float* pout = nullptr;
   uint8_t* parg = nullptr;
+  int plan_m = 0;  // > 0: the split plan of an M = plan_m problem (the pooled conv takes the unfused conv's
+                   // reduction split, so its partial sums -- and outputs -- are bit-identical to it)
   // kF32ConvDgrad / kF32ConvWgrad with the output gradient given POOLED (the backward of that fused
   // forward): a = the pool's output gradient [N][PH][PW][K], amask = the pooled maximum, pin_arg = its
   // window positions; the conv-output gradient the loader forms is, at pixel (oy, ox) of the g.oh x g.ow
@@ -73,9 +76,10 @@ constexpr int kF32Tile = 64;
 // each with at least `kmin` reduction elements (the kernel keeps 4 slices of 16 in flight, so a
 // split of <= 64 is one memory round trip; 128 -- two -- until round 6), at most `cap` splits.
 inline void f32_gemm_plan(F32GemmArgs& a, int kmin = 64, int cap = 1024) {
-  const int64_t tiles = (int64_t)((a.M + kF32Tile - 1) / kF32Tile) * ((a.N + kF32Tile - 1) / kF32Tile);
+  const int64_t pm = a.plan_m > 0 ? a.plan_m : a.M;
+  const int64_t tiles = (int64_t)((pm + kF32Tile - 1) / kF32Tile) * ((a.N + kF32Tile - 1) / kF32Tile);
   int splits = 1;
-  if (tiles < 512 && a.Kred > 256 && !a.pool) {
+  if (tiles < 512 && a.Kred > 256) {
     const int64_t want = (1024 + tiles - 1) / tiles;
     const int64_t most = (a.Kred + kmin - 1) / kmin;
     splits = (int)(want < most ? want : most);
@@ -88,6 +92,10 @@ inline void f32_gemm_plan(F32GemmArgs& a, int kmin = 64, int cap = 1024) {
   a.kchunk = chunk;
   a.splits = (a.Kred + chunk - 1) / chunk;
   if (a.splits < 1) a.splits = 1;
+  if (a.pool && a.splits >= 16) {  // (the pooled reduction replicates the < 16-slice reduce only)
+    a.kchunk = (a.Kred + 15) / 16 * 16;
+    a.splits = 1;
+  }
 }
 
 void f32_gemm_launch(int mode, const F32GemmArgs& a, hipStream_t s);

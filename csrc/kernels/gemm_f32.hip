@@ -505,6 +505,57 @@ __global__ __launch_bounds__(256) void k_gemm_f32_reduce(F32GemmArgs a) {
   out_store(a, m, n, v);
 }
 
+// Split-reduction of the pooled conv (F32GemmArgs::pool, < 16 slices): one thread per (pool window,
+// column) sums each of the window's 4 rows exactly as k_gemm_f32_reduce sums an output (slices in
+// order, rounds of 16 with zero-filled remainders: the same bits as the unfused conv's reduction), then
+// the pooled epilogue of k_gemm_f32 (bias, ReLU, y, maximum, argmax).
+__global__ __launch_bounds__(256) void k_gemm_f32_reduce_pool(F32GemmArgs a) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t wins = (int64_t)(a.M >> 2) * a.N;
+  if (e >= wins) return;
+  const int win = (int)(e / a.N), n = (int)(e - (int64_t)win * a.N);
+  const int64_t mn = (int64_t)a.M * a.N;
+  const int wpi = a.pool_h * a.pool_w;
+  const int img = win / wpi, wi = win - img * wpi;
+  const int php = wi / a.pool_w, pwp = wi - php * a.pool_w;
+  const float bias = a.bias != nullptr ? a.bias[n] : 0.f;
+  float best = -INFINITY;
+  uint32_t arg = 255u;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float* src = a.ws + (int64_t)(4 * win + r) * a.N + n;
+    float v = 0.f;
+    int z = 0;
+    for (; z + 16 <= a.splits; z += 16) {
+      float p[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) p[u] = src[(z + u) * mn];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v += p[u];
+    }
+    {
+      float p[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) p[u] = src[(int64_t)min(z + u, a.splits - 1) * mn];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) p[u] = z + u < a.splits ? p[u] : 0.f;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v += p[u];
+    }
+    if (a.bias != nullptr) v += bias;
+    if (a.act == 1) v = fmaxf(v, 0.f);
+    const int oy = 2 * php + (r >> 1), ox = 2 * pwp + (r & 1);
+    a.out[(((int64_t)img * a.g.oh + oy) * a.g.ow + ox) * a.ldo + n] = v;
+    if (v > best) {
+      best = v;
+      arg = (uint32_t)r;
+    }
+  }
+  const int64_t po = (((int64_t)img * a.pool_h + php) * a.pool_w + pwp) * a.N + n;
+  a.pout[po] = best;
+  a.parg[po] = (uint8_t)arg;
+}
+
 // Many slices over few outputs (a small weight gradient over a long reduction): one wave per output,
 // lane l sums slices l, l + 64, .. in order, then a fixed xor butterfly over the wave (deterministic).
 __global__ __launch_bounds__(256) void k_gemm_f32_reduce_wave(F32GemmArgs a) {
@@ -555,7 +606,10 @@ void f32_gemm_launch(int mode, const F32GemmArgs& a, hipStream_t s) {
       else launch_v<kF32ConvWgrad, false, false>(a, grid, s);
       break;
   }
-  if (a.splits > 1) {
+  if (a.splits > 1 && a.pool) {
+    const int64_t wins = (int64_t)(a.M >> 2) * a.N;
+    hipLaunchKernelGGL(k_gemm_f32_reduce_pool, dim3((unsigned)((wins + 255) / 256)), dim3(256), 0, s, a);
+  } else if (a.splits > 1) {
     const int64_t mn = (int64_t)a.M * a.N;
     if (a.splits >= 16)  // one wave per output: every partial of an output in one load round
       hipLaunchKernelGGL(k_gemm_f32_reduce_wave, dim3((unsigned)((mn + 3) / 4)), dim3(256), 0, s, a);

@@ -172,9 +172,7 @@ def test_reference_cnn_any_optimizer_on_fused_kernels(name, make_opt):
     # (RMSprop's first steps are g / sqrt((1 - rho) g^2) = +-lr / sqrt(1 - rho), amplified by momentum)
     lr = float(mf.optimizer.current_lr())
     step = {"rmsprop-momentum": lr / np.sqrt(1 - 0.9) / (1 - 0.5)}.get(name, lr)
-    # (RMSprop + momentum flips the most: 1.6 % of one tensor's weights once the generic engine's conv2 forward
-    # runs unsplit inside the fused conv + pool launch, i.e. with a different f32 summation order)
-    frac = 3e-2 if name == "rmsprop-momentum" else 1e-3
+    frac = 1e-2 if name == "rmsprop-momentum" else 1e-3
     for a, b in zip(mf.get_weights(), mg.get_weights()):
         off = ~np.isclose(a, b, rtol=5e-3, atol=5e-4)
         assert off.mean() < frac, (name, off.mean())
