@@ -72,6 +72,7 @@ class Plan:
         self.pool_pad: Dict[int, tuple] = {}  # id(max-pool / stem conv node) -> (padding input, padding)
         self.conv_box: Dict[int, int] = {}   # id(conv node) -> id(input tensor) of its GradBox
         self.taps: Dict[int, set] = {}       # id(node or group last node) -> ids of inputs read through a tap
+        self.conv_pool: Dict[int, object] = {}  # id(conv node) -> the 2x2 MaxPooling2D node it runs (Conv2D._pool)
 
     def __len__(self):
         return len(self.groups)
@@ -171,6 +172,20 @@ def plan(nodes: List[L.Node], outputs) -> Plan:
                     g.defer = c
     if os.environ.get("TDL_FUSE_GRAD_SUM", "1") == "1":
         _plan_grad_sums(p, nodes, consumers, outs)
+    # Conv2D -> MaxPooling2D(2, 2, 'valid') whose conv output has no other reader and which no other plan
+    # touches: the pool runs inside the conv's call (one launch on the generic f32 path, Conv2D._pool)
+    in_groups = {id(g.bn_node) for g in p.groups.values()} | {id(g.last) for g in p.groups.values()}
+    for n in nodes:
+        if id(n) in p.skip or id(n) in p.conv_nobias or id(n) in p.conv_box or id(n) in p.pool_pad or \
+                id(n) in p.taps or id(n) in in_groups:
+            continue
+        out_t = _single_tensor(n.outputs)
+        c = only_consumer(out_t) if out_t is not None and isinstance(n.layer, L.Conv2D) else None
+        if c is None or not L.conv_pool_pair(n.layer, c.layer) or c.inputs is not out_t or id(c) in p.skip or \
+                id(c) in p.pool_pad or id(c) in p.taps or id(c) in in_groups:
+            continue
+        p.conv_pool[id(n)] = c
+        p.skip.add(id(c))
     return p
 
 

@@ -143,7 +143,7 @@ class Model(Layer):
         fp = None
         if training and isinstance(xs[0], torch.Tensor) and (xs[0].is_cuda or _FUSE_CPU[0]):
             fp = self._fusion()  # keras/fusion.py: conv-bias/BN/ReLU/Add groups (training, GPU)
-            if not fp.groups and not fp.pool_pad and not fp.conv_box:
+            if not fp.groups and not fp.pool_pad and not fp.conv_box and not fp.conv_pool:
                 fp = None
         boxes = {}  # id(tensor) -> GradBox of its two consumers' backward contributions
         self.__dict__["_grad_boxes"] = boxes
@@ -176,6 +176,9 @@ class Model(Layer):
                 if pp is not None:  # fused ZeroPadding2D: read the padding layer's input
                     src = pp[0]
                     kw["_zero_pad"] = pp[1]
+                cpn = fp.conv_pool.get(id(n))
+                if cpn is not None:  # Conv2D -> MaxPooling2D(2): the pool runs inside the conv's call
+                    kw["_pool"] = cpn.layer
             if fp is not None and (id(n) in fp.conv_box or id(n) in fp.taps):
                 from ..ops.conv import GradBox, grad_tap
 
@@ -196,6 +199,8 @@ class Model(Layer):
                     vals[id(t)] = o
             else:
                 vals[id(n.outputs)] = out
+            if fp is not None and id(n) in fp.conv_pool:  # (the conv's own output is read by the pool only)
+                vals[id(fp.conv_pool[id(n)].outputs)] = out
         return _map(lambda t: vals[id(t)], self._outputs)
 
     # ------------------------------------------------------------------ build / call

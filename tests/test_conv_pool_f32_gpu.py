@@ -71,7 +71,7 @@ def test_fused_conv_pool_gradients(shape):
         assert torch.equal(a, c)
 
 
-def _fit_reference_cnn(fuse: str):
+def _fit_reference_cnn(fuse: str, functional: bool = False):
     import os
 
     import numpy as np
@@ -89,9 +89,15 @@ def _fit_reference_cnn(fuse: str):
     try:
         L = tdl.keras.layers
         with tdl.distribute.MirroredStrategy(devices=["/gpu:0"]).scope():
-            m = tdl.keras.Sequential([L.Conv2D(32, 3, activation="relu", input_shape=(28, 28, 1)), L.MaxPooling2D(),
-                                      L.Conv2D(64, 3, activation="relu"), L.MaxPooling2D(), L.Flatten(),
-                                      L.Dense(128, activation="relu"), L.Dense(10)])
+            if functional:  # the functional executor's fusion plan (keras/fusion.py conv_pool)
+                inp = L.Input(shape=(28, 28, 1))
+                h = L.MaxPooling2D()(L.Conv2D(32, 3, activation="relu")(inp))
+                h = L.MaxPooling2D()(L.Conv2D(64, 3, activation="relu")(h))
+                m = tdl.keras.Model(inp, L.Dense(10)(L.Dense(128, activation="relu")(L.Flatten()(h))))
+            else:
+                m = tdl.keras.Sequential([L.Conv2D(32, 3, activation="relu", input_shape=(28, 28, 1)),
+                                          L.MaxPooling2D(), L.Conv2D(64, 3, activation="relu"), L.MaxPooling2D(),
+                                          L.Flatten(), L.Dense(128, activation="relu"), L.Dense(10)])
             m.compile(loss=tdl.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
                       optimizer=tdl.keras.optimizers.SGD(0.05))
         h = m.fit(x, y, batch_size=64, epochs=2, verbose=0, shuffle=False)
@@ -104,14 +110,16 @@ def _fit_reference_cnn(fuse: str):
     return m, h
 
 
-def test_generic_engine_reference_cnn_fused_pool_trains_like_unfused():
-    """The generic engine's Sequential forward takes the fused Conv2D -> MaxPooling2D pairs in training
-    (two launches fewer per step); two epochs match the unfused model bit for bit."""
+@pytest.mark.parametrize("functional", [False, True], ids=["sequential", "functional"])
+def test_generic_engine_reference_cnn_fused_pool_trains_like_unfused(functional):
+    """The generic engine's Sequential forward (and the functional executor's fusion plan) takes the fused
+    Conv2D -> MaxPooling2D pairs in training (two launches fewer per step); two epochs match the unfused
+    model bit for bit."""
     import numpy as np
 
-    mf, hf = _fit_reference_cnn("1")
+    mf, hf = _fit_reference_cnn("1", functional)
     assert mf._trainer.kind == "generic"
-    mu, hu = _fit_reference_cnn("0")
+    mu, hu = _fit_reference_cnn("0", functional)
     assert hf.history["loss"] == hu.history["loss"]
     for a, b in zip(mf.get_weights(), mu.get_weights()):
         assert np.array_equal(a, b)

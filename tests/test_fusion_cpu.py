@@ -37,6 +37,7 @@ def test_plan_shapes_resnet50():
     m = tdl.keras.applications.ResNet50(weights=None, classes=10, classifier_activation=None, input_shape=(32, 32, 3))
     p = fusion.plan(m._nodes, m._outputs)
     assert len(p.groups) == 53 and len(p.conv_nobias) == 53
+    assert not p.conv_pool  # (every conv feeds a BN; the stem's pool is 3x3)
     assert sum(g.residual is not None for g in p.groups.values()) == 16
     assert sum(g.relu and g.residual is None for g in p.groups.values()) == 33
     # the 4 conv blocks: the block-output group also reduces its projection-shortcut BN's backward
@@ -123,3 +124,31 @@ def test_zero_pad_max_pool_fusion_matches():
     finally:
         models._FUSE_CPU[0] = False
     torch.testing.assert_close(y1, y0)
+
+
+def _functional_reference_cnn():
+    k = tdl.keras
+    L = k.layers
+    inp = L.Input(shape=(28, 28, 1))
+    h = L.MaxPooling2D()(L.Conv2D(32, 3, activation="relu")(inp))
+    h = L.MaxPooling2D()(L.Conv2D(64, 3, activation="relu")(h))
+    h = L.Dense(128, activation="relu")(L.Flatten()(h))
+    return k.Model(inp, L.Dense(10)(h))
+
+
+def test_plan_runs_conv_maxpool_pairs_as_one_call(monkeypatch):
+    """Conv2D -> MaxPooling2D(2, 2, 'valid') with no other reader of the conv output: the pool node is
+    skipped and runs inside the conv's call (Conv2D._pool); TDL_FUSE_CONV_POOL=0 keeps them apart; a
+    conv output with a second reader is never fused."""
+    m = _functional_reference_cnn()
+    p = fusion.plan(m._nodes, m._outputs)
+    assert len(p.conv_pool) == 2
+    assert all(type(pn.layer).__name__ == "MaxPooling2D" and id(pn) in p.skip for pn in p.conv_pool.values())
+    monkeypatch.setenv("TDL_FUSE_CONV_POOL", "0")
+    assert not fusion.plan(m._nodes, m._outputs).conv_pool
+    monkeypatch.delenv("TDL_FUSE_CONV_POOL")
+    L = tdl.keras.layers
+    inp = L.Input(shape=(12, 12, 4))
+    c = L.Conv2D(8, 3, activation="relu")(inp)
+    two = tdl.keras.Model(inp, [L.MaxPooling2D()(c), L.Flatten()(c)])
+    assert not fusion.plan(two._nodes, two._outputs).conv_pool
