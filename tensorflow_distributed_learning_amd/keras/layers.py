@@ -507,7 +507,7 @@ def conv_pool_pair(conv, pool) -> bool:
     (TDL_FUSE_CONV_POOL=0 keeps them apart)."""
     import os
 
-    return (isinstance(conv, Conv2D) and type(pool) is MaxPooling2D and pool.pool_size == (2, 2)
+    return (type(conv) is Conv2D and type(pool) is MaxPooling2D and pool.pool_size == (2, 2)
             and pool.strides == (2, 2) and pool.padding == "valid"
             and os.environ.get("TDL_FUSE_CONV_POOL", "1") == "1")
 
