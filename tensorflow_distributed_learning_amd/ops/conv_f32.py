@@ -49,7 +49,9 @@ def dgrad(dy, w_hwio, hw, stride, pads, dil=(1, 1), dy_mask=None, pin=None) -> t
     2x2 max pool over the conv's ReLU output and ``dy_mask`` the pooled maximum (conv2d_pool's backward:
     the loader routes and masks it, no max-pool backward pass)."""
     kw = dict(pin_arg=pin[0], out_h=pin[1], out_w=pin[2]) if pin is not None else {}
-    if w_hwio.numel() <= (1 << 16):
+    import os
+
+    if w_hwio.numel() <= int(os.environ.get("TDL_F32_DGRAD_HWIO_MAX", 1 << 16)):
         # small kernels (the generic engine's layers): read w HWIO transposed in the kernel (w_hwio), no
         # [R][S][K][C] copy kernel per step; large ones keep the copy for 16-B operand loads
         return hip().conv_f32_dgrad(_c32(dy), _c32(w_hwio), hw[0], hw[1], stride[0], stride[1], pads[0], pads[2],
