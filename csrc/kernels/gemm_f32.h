@@ -68,6 +68,10 @@ struct F32GemmArgs {
   // grid, pooled gradient * [argmax == this pixel] * [maximum > 0] (pixels outside every window: 0)
   // -- the max-pool backward and the ReLU mask without their own pass.  Uses pool_h / pool_w.
   const uint8_t* pin_arg = nullptr;
+  // element counts of a / b (and of amask / bmask, shaped alike): when both are set and < 2^29 the kernel
+  // reads its operands through buffer resources with 32-bit offsets (out-of-range offsets read 0), so
+  // the loaders need no 64-bit address math and no clamped-address selects (0: the generic form)
+  int64_t na = 0, nb = 0;
 };
 
 constexpr int kF32Tile = 64;

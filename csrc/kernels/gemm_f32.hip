@@ -13,6 +13,9 @@
 //
 // The convolution index decodes run on mixed-radix counters advanced by 16 per slice (a division
 // only on wrap-around), not per-element integer divisions.
+#include <cstdlib>
+#include <type_traits>
+
 #include "common.h"
 #include "gemm_f32.h"
 
@@ -77,8 +80,9 @@ struct Slice {
   unsigned pa, pp;  // PIN: the 4 elements' argmax bytes and their own window positions (byte i each)
 };
 
-template <int MODE, bool MA, bool MB, bool VA, bool VB, bool PIN = false>
+template <int MODE, bool MA, bool MB, bool VA, bool VB, bool PIN = false, bool BUF = false>
 __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
+  using I = std::conditional_t<BUF, int, int64_t>;  // operand element index (32-bit with buffer loads)
   __shared__ float As[16 * kLd];
   __shared__ float Bs[16 * kLd];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -145,38 +149,69 @@ __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
   const bool s1 = g.sh == 1 && g.sw == 1;
   using S = Slice<MA, MB>;
 
-  // A element e (valid or not) into slot i; a 16-B quad at slot 0 when vec
-  auto lda1 = [&](S& r, int i, bool ok, int64_t e) {
-    const int64_t q = ok ? e : 0;
-    r.a[i] = a.a[q];
-    if constexpr (MA) r.ma[i] = a.amask[q];
+  // A element e (valid or not) into slot i; a 16-B quad at slot 0 when vec.  BUF: buffer loads at 32-bit
+  // byte offsets, an invalid element reads offset 0x80000000 (out of range: 0); else a clamped address
+  // (built unconditionally: scalar work only, dead without BUF)
+  const auto ra = buf_rsrc(a.a, (unsigned)(a.na * 4)), rb = buf_rsrc(a.b, (unsigned)(a.nb * 4));
+  const auto ram = buf_rsrc(MA ? a.amask : a.a, (unsigned)(a.na * 4));
+  const auto rbm = buf_rsrc(MB ? a.bmask : a.b, (unsigned)(a.nb * 4));
+  auto lda1 = [&](S& r, int i, bool ok, I e) {
+    if constexpr (BUF) {
+      const int vo = ok ? (int)e * 4 : (int)0x80000000;
+      r.a[i] = ld1_buf(ra, vo, 0);
+      if constexpr (MA) r.ma[i] = ld1_buf(ram, vo, 0);
+    } else {
+      const I q = ok ? e : 0;
+      r.a[i] = a.a[q];
+      if constexpr (MA) r.ma[i] = a.amask[q];
+    }
     r.va |= ok ? 1u << i : 0u;
   };
-  auto lda4 = [&](S& r, bool ok, int64_t e) {
-    const int64_t q = ok ? e : 0;
-    const f4 v = ld4(a.a + q);
+  auto lda4 = [&](S& r, bool ok, I e) {
+    f4 v, mv;
+    if constexpr (BUF) {
+      const int vo = ok ? (int)e * 4 : (int)0x80000000;
+      v = ld4_buf(ra, vo, 0);
+      if constexpr (MA) mv = ld4_buf(ram, vo, 0);
+    } else {
+      const I q = ok ? e : 0;
+      v = ld4(a.a + q);
+      if constexpr (MA) mv = ld4(a.amask + q);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) r.a[i] = v[i];
     if constexpr (MA) {
-      const f4 mv = ld4(a.amask + q);
 #pragma unroll
       for (int i = 0; i < 4; ++i) r.ma[i] = mv[i];
     }
     r.va = ok ? 15u : 0u;
   };
-  auto ldb1 = [&](S& r, int i, bool ok, int64_t e) {
-    const int64_t q = ok ? e : 0;
-    r.b[i] = a.b[q];
-    if constexpr (MB) r.mb[i] = a.bmask[q];
+  auto ldb1 = [&](S& r, int i, bool ok, I e) {
+    if constexpr (BUF) {
+      const int vo = ok ? (int)e * 4 : (int)0x80000000;
+      r.b[i] = ld1_buf(rb, vo, 0);
+      if constexpr (MB) r.mb[i] = ld1_buf(rbm, vo, 0);
+    } else {
+      const I q = ok ? e : 0;
+      r.b[i] = a.b[q];
+      if constexpr (MB) r.mb[i] = a.bmask[q];
+    }
     r.vb |= ok ? 1u << i : 0u;
   };
-  auto ldb4 = [&](S& r, bool ok, int64_t e) {
-    const int64_t q = ok ? e : 0;
-    const f4 v = ld4(a.b + q);
+  auto ldb4 = [&](S& r, bool ok, I e) {
+    f4 v, mv;
+    if constexpr (BUF) {
+      const int vo = ok ? (int)e * 4 : (int)0x80000000;
+      v = ld4_buf(rb, vo, 0);
+      if constexpr (MB) mv = ld4_buf(rbm, vo, 0);
+    } else {
+      const I q = ok ? e : 0;
+      v = ld4(a.b + q);
+      if constexpr (MB) mv = ld4(a.bmask + q);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) r.b[i] = v[i];
     if constexpr (MB) {
-      const f4 mv = ld4(a.bmask + q);
 #pragma unroll
       for (int i = 0; i < 4; ++i) r.mb[i] = mv[i];
     }
@@ -190,11 +225,11 @@ __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
     if constexpr (MODE == kF32Gemm) {
       const bool ones = am == a.ones_m;  // the appended row of ones (bias gradient)
       if constexpr (VA) {
-        lda4(r, !ones && arow && kk < kend, (int64_t)am * a.sam + kk);
+        lda4(r, !ones && arow && kk < kend, (I)am * (I)a.sam + kk);
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          lda1(r, i, !ones && arow && kk + i < kend, (int64_t)am * a.sam + (int64_t)(kk + i) * a.sak);
+          lda1(r, i, !ones && arow && kk + i < kend, (I)am * (I)a.sam + (I)(kk + i) * (I)a.sak);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) r.oa |= (ones && kk + i < kend) ? 1u << i : 0u;
@@ -217,11 +252,11 @@ __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
             ok = ty >= 0 && tx >= 0 && (s1 || (iy * g.sh == ty && ix * g.sw == tx)) && iy < g.oh && ix < g.ow;
           }
           ok = ok && arow && kk + i < kend;
-          int64_t base = MODE == kF32ConvFwd ? (((int64_t)an * g.h + iy) * g.w + ix) * g.c
-                                             : (((int64_t)an * g.oh + iy) * g.ow + ix) * g.k;
+          I base = MODE == kF32ConvFwd ? (((I)an * g.h + iy) * g.w + ix) * g.c
+                                             : (((I)an * g.oh + iy) * g.ow + ix) * g.k;
           if constexpr (PIN && MODE == kF32ConvDgrad) {  // the pool window of dy pixel (iy, ix)
             ok = ok && iy < 2 * a.pool_h && ix < 2 * a.pool_w;
-            base = (((int64_t)an * a.pool_h + (iy >> 1)) * a.pool_w + (ix >> 1)) * g.k;
+            base = (((I)an * a.pool_h + (iy >> 1)) * a.pool_w + (ix >> 1)) * g.k;
             const unsigned pos = (unsigned)(((iy & 1) << 1) | (ix & 1));
             if constexpr (VA) {
               r.pa = *reinterpret_cast<const unsigned*>(a.pin_arg + (ok ? base + c.lo : 0));
@@ -244,14 +279,14 @@ __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
       for (int i = 0; i < 4; ++i) {
         if (i) c.step1(g.oh, g.ow);
         const bool ok = arow && kk + i < kend && c.mid < 2 * a.pool_h && c.lo < 2 * a.pool_w;
-        const int64_t e = (((int64_t)c.hi * a.pool_h + (c.mid >> 1)) * a.pool_w + (c.lo >> 1)) * g.k + am;
+        const I e = (((I)c.hi * a.pool_h + (c.mid >> 1)) * a.pool_w + (c.lo >> 1)) * g.k + am;
         lda1(r, i, ok, e);
         r.pa |= (unsigned)a.pin_arg[ok ? e : 0] << (8 * i);
         r.pp |= (unsigned)(((c.mid & 1) << 1) | (c.lo & 1)) << (8 * i);
       }
     } else {  // wgrad: A(m = out channel, j) = dy[j][m]
 #pragma unroll
-      for (int i = 0; i < 4; ++i) lda1(r, i, arow && kk + i < kend, (int64_t)(kk + i) * g.k + am);
+      for (int i = 0; i < 4; ++i) lda1(r, i, arow && kk + i < kend, (I)(kk + i) * g.k + am);
     }
 
     const int kr = k0 + kl;  // B: reduction index of this thread's row
@@ -265,7 +300,7 @@ __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
         if (!VB || i == 0) {  // a 16-B quad at slot 0 (the ones column starts a quad), or one element per slot
           const int iy = kb.mid * g.sh - g.pt + wr[i] * g.dh, ix = kb.lo * g.sw - g.pl + ws_[i] * g.dw;
           const bool ok = !ones && brow && n < a.N && iy >= 0 && iy < g.h && ix >= 0 && ix < g.w;
-          const int64_t e = (((int64_t)kb.hi * g.h + iy) * g.w + ix) * g.c + wc[i];
+          const I e = (((I)kb.hi * g.h + iy) * g.w + ix) * g.c + wc[i];
           if constexpr (VB)
             ldb4(r, ok, e);
           else
@@ -274,17 +309,17 @@ __global__ __launch_bounds__(256) void k_gemm_f32(F32GemmArgs a) {
       }
     } else if (MODE == kF32ConvDgrad && a.b_hwio) {  // w HWIO: B(kr = rs * K + kk, n = c) = w[rs][c][kk]
       const int rs = kr / g.k, kk2 = kr - rs * g.k;
-      const int64_t row = (int64_t)rs * a.N * g.k + kk2;
+      const I row = (I)rs * a.N * g.k + kk2;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) ldb1(r, i, brow && bn + i < a.N, row + (int64_t)(bn + i) * g.k);
+      for (int i = 0; i < 4; ++i) ldb1(r, i, brow && bn + i < a.N, row + (I)(bn + i) * g.k);
     } else {
-      const int64_t sbk = MODE == kF32Gemm ? a.sbk : (int64_t)a.N;
-      const int64_t sbn = MODE == kF32Gemm ? a.sbn : 1;
+      const I sbk = MODE == kF32Gemm ? (I)a.sbk : (I)a.N;
+      const I sbn = MODE == kF32Gemm ? (I)a.sbn : 1;
       if constexpr (VB) {
-        ldb4(r, brow && bn < a.N, (int64_t)kr * sbk + bn);
+        ldb4(r, brow && bn < a.N, (I)kr * sbk + bn);
       } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) ldb1(r, i, brow && bn + i < a.N, (int64_t)kr * sbk + (int64_t)(bn + i) * sbn);
+        for (int i = 0; i < 4; ++i) ldb1(r, i, brow && bn + i < a.N, (I)kr * sbk + (I)(bn + i) * sbn);
       }
     }
   };
@@ -573,12 +608,28 @@ __global__ __launch_bounds__(256) void k_gemm_f32_reduce_wave(F32GemmArgs a) {
 }
 
 // the operand-vectorisation instantiation of a (mode, mask) kernel
+template <int MODE, bool MA, bool MB, bool PIN, bool BUF>
+void launch_vb(const F32GemmArgs& a, dim3 grid, hipStream_t s) {
+  if (a.vec_a && a.vec_b) hipLaunchKernelGGL((k_gemm_f32<MODE, MA, MB, true, true, PIN, BUF>), grid, dim3(256), 0, s, a);
+  else if (a.vec_a) hipLaunchKernelGGL((k_gemm_f32<MODE, MA, MB, true, false, PIN, BUF>), grid, dim3(256), 0, s, a);
+  else if (a.vec_b) hipLaunchKernelGGL((k_gemm_f32<MODE, MA, MB, false, true, PIN, BUF>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((k_gemm_f32<MODE, MA, MB, false, false, PIN, BUF>), grid, dim3(256), 0, s, a);
+}
+
+// buffer-resource operand loads when both operands (and their masks) fit 32-bit byte offsets
+// (TDL_F32_BUF=0 keeps the 64-bit address form everywhere: A/B hook)
+bool f32_buf_ok(const F32GemmArgs& a) {
+  static const bool on = [] {
+    const char* e = std::getenv("TDL_F32_BUF");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return on && a.na > 0 && a.nb > 0 && a.na < (int64_t(1) << 29) && a.nb < (int64_t(1) << 29);
+}
+
 template <int MODE, bool MA, bool MB, bool PIN = false>
 void launch_v(const F32GemmArgs& a, dim3 grid, hipStream_t s) {
-  if (a.vec_a && a.vec_b) hipLaunchKernelGGL((k_gemm_f32<MODE, MA, MB, true, true, PIN>), grid, dim3(256), 0, s, a);
-  else if (a.vec_a) hipLaunchKernelGGL((k_gemm_f32<MODE, MA, MB, true, false, PIN>), grid, dim3(256), 0, s, a);
-  else if (a.vec_b) hipLaunchKernelGGL((k_gemm_f32<MODE, MA, MB, false, true, PIN>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((k_gemm_f32<MODE, MA, MB, false, false, PIN>), grid, dim3(256), 0, s, a);
+  if (f32_buf_ok(a) && !PIN) launch_vb<MODE, MA, MB, PIN, true>(a, grid, s);
+  else launch_vb<MODE, MA, MB, PIN, false>(a, grid, s);
 }
 
 }  // namespace

@@ -735,6 +735,8 @@ at::Tensor gemm_f32(at::Tensor a, int64_t ta, at::Tensor b, int64_t tb, c10::opt
   tdl::F32GemmArgs g{};
   g.a = a.data_ptr<float>();
   g.b = b.data_ptr<float>();
+  g.na = a.numel();
+  g.nb = b.numel();
   g.out = c.data_ptr<float>();
   g.bias = f32_bias(bias, N);
   g.sam = ta ? 1 : a.stride(0);
@@ -794,6 +796,8 @@ at::Tensor conv_f32_fwd(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> bi
   g.g = f32_geom(x, K, w.size(0), w.size(1), oh, ow, sh, sw, pt, pl, dh, dw);
   g.a = x.data_ptr<float>();
   g.b = w.data_ptr<float>();
+  g.na = x.numel();
+  g.nb = w.numel();
   g.out = y.data_ptr<float>();
   g.bias = f32_bias(bias, K);
   g.M = (int)(x.size(0) * oh * ow);
@@ -827,6 +831,8 @@ std::vector<at::Tensor> conv_f32_fwd_pool(at::Tensor x, at::Tensor w, c10::optio
   g.g = f32_geom(x, K, w.size(0), w.size(1), oh, ow, sh, sw, pt, pl, dh, dw);
   g.a = x.data_ptr<float>();
   g.b = w.data_ptr<float>();
+  g.na = x.numel();
+  g.nb = w.numel();
   g.out = y.data_ptr<float>();
   g.bias = f32_bias(bias, K);
   g.M = (int)(x.size(0) * PH * PW * 4);
@@ -879,6 +885,8 @@ at::Tensor conv_f32_dgrad(at::Tensor dy, at::Tensor wt, int64_t h, int64_t wd, i
   f32_pin(g, dy, pin_arg, dy_mask, out_h, out_w, "conv_f32_dgrad");
   g.a = dy.data_ptr<float>();
   g.b = wt.data_ptr<float>();
+  g.na = dy.numel();
+  g.nb = wt.numel();
   g.out = dx.data_ptr<float>();
   g.M = (int)(dy.size(0) * h * wd);
   g.N = (int)C;
@@ -909,6 +917,8 @@ at::Tensor conv_f32_wgrad(at::Tensor x, at::Tensor dy, int64_t r, int64_t s, int
   f32_pin(g, dy, pin_arg, dy_mask, out_h, out_w, "conv_f32_wgrad");
   g.a = dy.data_ptr<float>();
   g.b = x.data_ptr<float>();
+  g.na = dy.numel();
+  g.nb = x.numel();
   g.out = dW.data_ptr<float>();
   g.M = (int)K;
   g.N = (int)(r * s * C);
