@@ -263,22 +263,22 @@ class MnistStep {
   tdl::MnistArgs a_;
 };
 
-void sgd(at::Tensor w, at::Tensor g, at::Tensor lr) {
+void sgd(at::Tensor w, at::Tensor g, at::Tensor lr, bool zero_grad) {
   check_cuda_f32(w, "w");
   check_cuda_f32(g, "g");
   check_cuda_f32(lr, "lr");
   TORCH_CHECK(w.numel() == g.numel());
-  tdl::sgd_apply(w.data_ptr<float>(), g.data_ptr<float>(), lr.data_ptr<float>(), w.numel(), cur_stream());
+  tdl::sgd_apply(w.data_ptr<float>(), g.data_ptr<float>(), lr.data_ptr<float>(), w.numel(), cur_stream(), zero_grad);
 }
 
-void sgd_momentum(at::Tensor w, at::Tensor g, at::Tensor v, at::Tensor lr, double m, bool nesterov) {
+void sgd_momentum(at::Tensor w, at::Tensor g, at::Tensor v, at::Tensor lr, double m, bool nesterov, bool zero_grad) {
   check_cuda_f32(w, "w");
   check_cuda_f32(g, "g");
   check_cuda_f32(v, "v");
   check_cuda_f32(lr, "lr");
   TORCH_CHECK(w.numel() == g.numel() && v.numel() == w.numel());
   tdl::sgd_momentum_apply(w.data_ptr<float>(), g.data_ptr<float>(), v.data_ptr<float>(), lr.data_ptr<float>(),
-                          (float)m, nesterov, w.numel(), cur_stream());
+                          (float)m, nesterov, w.numel(), cur_stream(), zero_grad);
 }
 
 // Flat-slab Adam / AdamW (+AMSGrad): state m, v (vhat), device lr and execution-start step t0
@@ -357,8 +357,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("error", &MnistStep::error, pybind11::arg("reset") = false)
       .def("buffers", &MnistStep::buffers)
       .def("set_stamps", &MnistStep::set_stamps);
-  m.def("sgd", &sgd);
-  m.def("sgd_momentum", &sgd_momentum);
+  m.def("sgd", &sgd, "w -= lr * g over a flat slab (zero_grad: g := 0 afterwards)", pybind11::arg("w"),
+        pybind11::arg("g"), pybind11::arg("lr"), pybind11::arg("zero_grad") = false);
+  m.def("sgd_momentum", &sgd_momentum, "Keras momentum SGD over a flat slab (zero_grad: g := 0 afterwards)",
+        pybind11::arg("w"), pybind11::arg("g"), pybind11::arg("v"), pybind11::arg("lr"), pybind11::arg("m"),
+        pybind11::arg("nesterov"), pybind11::arg("zero_grad") = false);
   m.def("adam", &adam, pybind11::arg("w"), pybind11::arg("g"), pybind11::arg("m"), pybind11::arg("v"),
         pybind11::arg("vhat"), pybind11::arg("lr"), pybind11::arg("t0"), pybind11::arg("t_add"), pybind11::arg("b1"),
         pybind11::arg("b2"), pybind11::arg("eps"), pybind11::arg("wd") = 0.0);

@@ -135,9 +135,10 @@ void mnist_finalize(const MnistArgs& a, bool apply_sgd, bool with_dense, hipStre
 void mnist_finalize_x(const MnistArgs& a, bool apply_sgd, hipStream_t s);
 
 // Plain SGD over a flat slab: w -= lr * g  (lr read from device memory).
-void sgd_apply(float* w, const float* g, const float* lr, int64_t n, hipStream_t s);
+// zero_g: g is zeroed after its use (the next step accumulates into it without a fill launch)
+void sgd_apply(float* w, const float* g, const float* lr, int64_t n, hipStream_t s, bool zero_g = false);
 // Momentum SGD (Keras semantics): v = m*v - lr*g ; w += v  (nesterov: w += m*v - lr*g)
 void sgd_momentum_apply(float* w, const float* g, float* v, const float* lr, float momentum,
-                        bool nesterov, int64_t n, hipStream_t s);
+                        bool nesterov, int64_t n, hipStream_t s, bool zero_g = false);
 
 }  // namespace tdl

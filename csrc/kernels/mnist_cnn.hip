@@ -1662,8 +1662,11 @@ __device__ __forceinline__ void finalize_x_body(const MnistArgs& a, int apply_sg
 // --------------------------------------------------------------------------------------------
 // Optimizer kernels over flat slabs.
 // --------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_sgd(float* __restrict__ w, const float* __restrict__ g,
-                                             const float* __restrict__ lrp, int64_t n) {
+// gz (optional, = g): the gradient is zeroed after its use, so the next step's backward can accumulate
+// into it without a separate fill launch (engine/trainer.py)
+// (g is not __restrict__: gz aliases it)
+__global__ __launch_bounds__(256) void k_sgd(float* __restrict__ w, const float* g, const float* __restrict__ lrp,
+                                             int64_t n, float* gz) {
   const float lr = *lrp;
   const int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   if (i4 + 3 < n) {
@@ -1671,14 +1674,18 @@ __global__ __launch_bounds__(256) void k_sgd(float* __restrict__ w, const float*
     const f4 gv = ld4(g + i4);
     wv -= lr * gv;
     st4(w + i4, wv);
+    if (gz != nullptr) st4(gz + i4, zero4());
   } else {
-    for (int64_t j = i4; j < n; ++j) w[j] -= lr * g[j];
+    for (int64_t j = i4; j < n; ++j) {
+      w[j] -= lr * g[j];
+      if (gz != nullptr) gz[j] = 0.f;
+    }
   }
 }
 
-__global__ __launch_bounds__(256) void k_sgd_momentum(float* __restrict__ w, const float* __restrict__ g,
+__global__ __launch_bounds__(256) void k_sgd_momentum(float* __restrict__ w, const float* g,
                                                       float* __restrict__ v, const float* __restrict__ lrp,
-                                                      float m, int nesterov, int64_t n) {
+                                                      float m, int nesterov, int64_t n, float* gz) {
   const float lr = *lrp;
   const int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   if (i4 + 3 < n) {
@@ -1688,11 +1695,14 @@ __global__ __launch_bounds__(256) void k_sgd_momentum(float* __restrict__ w, con
     wv += nesterov ? (m * vv - lr * gv) : vv;
     st4(w + i4, wv);
     st4(v + i4, vv);
+    if (gz != nullptr) st4(gz + i4, zero4());
   } else {
     for (int64_t j = i4; j < n; ++j) {
-      const float vj = m * v[j] - lr * g[j];
+      const float gj = g[j];
+      const float vj = m * v[j] - lr * gj;
       v[j] = vj;
-      w[j] += nesterov ? (m * vj - lr * g[j]) : vj;
+      w[j] += nesterov ? (m * vj - lr * gj) : vj;
+      if (gz != nullptr) gz[j] = 0.f;
     }
   }
 }
@@ -1753,15 +1763,16 @@ void mnist_finalize_x(const MnistArgs& a, bool apply_sgd, hipStream_t s) {
     default: go(std::integral_constant<int, 1>{}); break;
   }
 }
-void sgd_apply(float* w, const float* g, const float* lr, int64_t n, hipStream_t s) {
+void sgd_apply(float* w, const float* g, const float* lr, int64_t n, hipStream_t s, bool zero_g) {
   const int64_t nt = (n + 3) / 4;
-  hipLaunchKernelGGL(k_sgd, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, w, g, lr, n);
+  hipLaunchKernelGGL(k_sgd, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, w, g, lr, n,
+                     zero_g ? const_cast<float*>(g) : nullptr);
 }
 void sgd_momentum_apply(float* w, const float* g, float* v, const float* lr, float momentum, bool nesterov,
-                        int64_t n, hipStream_t s) {
+                        int64_t n, hipStream_t s, bool zero_g) {
   const int64_t nt = (n + 3) / 4;
   hipLaunchKernelGGL(k_sgd_momentum, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, w, g, v, lr, momentum,
-                     nesterov ? 1 : 0, n);
+                     nesterov ? 1 : 0, n, zero_g ? const_cast<float*>(g) : nullptr);
 }
 
 }  // namespace tdl

@@ -389,7 +389,10 @@ class GenericTrainer:
         self._skip_comm = self.comm.world_size > 1 and fault.maybe_skip_collective(self.comm.rank,
                                                                                    int(self.optimizer.iterations))
         G = self.G
-        G.zero_()
+        if getattr(self, "_g_clean", None) == G.data_ptr():  # the previous step's optimizer kernel zeroed G
+            self._g_clean = None
+        else:
+            G.zero_()
         if self._buckets is not None:
             self._counts = list(self._pending)
             self._works = []
@@ -455,7 +458,15 @@ class GenericTrainer:
                 else:
                     self.comm.all_reduce(G, "sum")
         with torch.no_grad(), trace_range("tdl.optimizer"):
-            self.optimizer.apply_flat(self.W, G, sync_lr=sync_lr, t_add=t_add)
+            opt = self.optimizer
+            opt._zero_grad_after, opt._zeroed_grad = G.is_cuda, False
+            try:
+                opt.apply_flat(self.W, G, sync_lr=sync_lr, t_add=t_add)
+            finally:
+                opt._zero_grad_after = False
+            # (only an optimizer kernel that zeroed G after reading it marks this slab clean)
+            self._g_clean = G.data_ptr() if opt._zeroed_grad else None
+            opt._zeroed_grad = False
             if _ck.enabled():
                 _ck.record("slab_W", self.W)
             if per_ex is not None:  # (the fused loss head advanced the metric accumulators itself)

@@ -241,10 +241,13 @@ class SGD(Optimizer):
         from .. import ops
 
         C = ops.hip()
+        # (the generic trainer's request: zero G after its use, so its next step needs no fill launch)
+        zero = bool(getattr(self, "_zero_grad_after", False))
         if self.momentum > 0:
-            C.sgd_momentum(W, G, self._slots["momentum"], self.lr_dev, self.momentum, self.nesterov)
+            C.sgd_momentum(W, G, self._slots["momentum"], self.lr_dev, self.momentum, self.nesterov, zero_grad=zero)
         else:
-            C.sgd(W, G, self.lr_dev)
+            C.sgd(W, G, self.lr_dev, zero_grad=zero)
+        self._zeroed_grad = zero
         return True
 
     def _update(self, W, G):
