@@ -23,5 +23,6 @@ void maxpool_backward(const void* dy, const uint8_t* arg, void* dx, bool bf16, c
 int maxpool_backward_blocks(const PoolGeom& g);
 // A/B hook: the generic window loops (default) or the unrolled kernels for 3x3 stride-2 pooling
 void maxpool_force_generic(bool generic);
+void maxpool_w2(bool on);  // 2x2 stride-2 backward in scatter form (default on)
 
 }  // namespace tdl

@@ -5,6 +5,8 @@
 //           max pool) or zero (a fused ZeroPadding2D in front, the ResNet stem).
 // backward: gather form — each input element sums dy over the <= ceil(k/s)^2 windows whose
 //           argmax points at it: no atomics, deterministic, one pass over dx.
+#include <cstdlib>
+
 #include "common.h"
 #include "pool.h"
 
@@ -266,6 +268,68 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd(const void* __restrict__ dy
   }
 }
 
+// 2x2 stride-2 windows without padding (every input element in at most one window): scatter form, one
+// thread per (window, channel group) writes the window's four input pixels (dy at the argmax, zero
+// elsewhere) and, on the last window of an odd row / column, the zeros of the uncovered edge pixels.
+// 32-bit index math (total < 2^31, checked on the host); a quarter of the generic form's threads and no
+// per-input-pixel window search.  Same values as the gather form: 0 + dy at the argmax, 0 elsewhere.
+template <bool BF>
+__global__ __launch_bounds__(256) void k_maxpool_bwd_w2(const void* __restrict__ dy, const uint8_t* __restrict__ arg,
+                                                        void* __restrict__ dx, PoolGeom g) {
+  const int G = g.C >> 3;
+  const int total = g.N * g.OH * g.OW * G;
+  const bool edge_w = g.W > 2 * g.OW, edge_h = g.H > 2 * g.OH;
+  for (int t = blockIdx.x * 256 + threadIdx.x; t < total; t += gridDim.x * 256) {
+    const int cg = t % G;
+    int r = t / G;
+    const int ow = r % g.OW;
+    r /= g.OW;
+    const int oh = r % g.OH;
+    const int n = r / g.OH;
+    const int o = t * 8;  // ((n * OH + oh) * OW + ow) * C + cg * 8
+    const uint2 a = *reinterpret_cast<const uint2*>(arg + o);
+    float d[8];
+    ld8<BF>(dy, o, d);
+    const int x0 = ((n * g.H + 2 * oh) * g.W + 2 * ow) * g.C + cg * 8;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t aj = ((j < 4 ? a.x : a.y) >> (8 * (j & 3))) & 0xffu;
+        v[j] = aj == (uint32_t)q ? 0.f + d[j] : 0.f;
+      }
+      st8<BF>(dx, x0 + ((q >> 1) * g.W + (q & 1)) * g.C, v);
+    }
+    const bool lw = edge_w && ow == g.OW - 1, lh = edge_h && oh == g.OH - 1;
+    if (lw || lh) {
+      float z[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) z[j] = 0.f;
+      if (lw) {
+        st8<BF>(dx, x0 + 2 * g.C, z);
+        st8<BF>(dx, x0 + (g.W + 2) * g.C, z);
+      }
+      if (lh) {
+        st8<BF>(dx, x0 + 2 * g.W * g.C, z);
+        st8<BF>(dx, x0 + (2 * g.W + 1) * g.C, z);
+      }
+      if (lw && lh) st8<BF>(dx, x0 + (2 * g.W + 2) * g.C, z);
+    }
+  }
+}
+
+// TDL_POOL_W2=0 / maxpool_w2(false): the gather form for these windows too (A/B hook)
+bool g_pool_w2 = [] {
+  const char* e = std::getenv("TDL_POOL_W2");
+  return e == nullptr || std::atoi(e) != 0;
+}();
+
+bool w2(const PoolGeom& g) {
+  return g_pool_w2 && g.kh == 2 && g.kw == 2 && g.sh == 2 && g.sw == 2 && g.pt == 0 && g.pl == 0 &&
+         g.OH == g.H / 2 && g.OW == g.W / 2 && (int64_t)g.N * g.H * g.W * g.C < (int64_t(1) << 31);
+}
+
 int grid_for(int64_t n) { return (int)std::min<int64_t>((n + 255) / 256, 256 * 32); }
 
 // maxpool_force_generic (A/B hook).  Default: the generic loops -- the unrolled 3x3 stride-2 kernels
@@ -278,6 +342,8 @@ bool k3s2(const PoolGeom& g) { return g_pool_k3s2 && g.kh == 3 && g.kw == 3 && g
 }  // namespace
 
 void maxpool_force_generic(bool generic) { g_pool_k3s2 = !generic; }
+
+void maxpool_w2(bool on) { g_pool_w2 = on; }
 
 void maxpool_forward(const void* x, void* y, uint8_t* arg, bool bf16, const PoolGeom& g, hipStream_t s,
                      const float* bn_ss) {
@@ -313,6 +379,14 @@ void maxpool_backward(const void* dy, const uint8_t* arg, void* dx, bool bf16, c
       hipLaunchKernelGGL((k_maxpool_bwd<true, false, true>), gr, b, 0, s, dy, arg, dx, g, bn_x, bn_ss, part);
     else
       hipLaunchKernelGGL((k_maxpool_bwd<false, false, true>), gr, b, 0, s, dy, arg, dx, g, bn_x, bn_ss, part);
+    return;
+  }
+  if (w2(g)) {
+    const dim3 gw(grid_for((int64_t)g.N * g.OH * g.OW * (g.C / 8)));
+    if (bf16)
+      hipLaunchKernelGGL((k_maxpool_bwd_w2<true>), gw, b, 0, s, dy, arg, dx, g);
+    else
+      hipLaunchKernelGGL((k_maxpool_bwd_w2<false>), gw, b, 0, s, dy, arg, dx, g);
     return;
   }
   if (k3s2(g)) {

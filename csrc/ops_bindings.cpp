@@ -1077,6 +1077,8 @@ void register_ops(pybind11::module& m) {
         "weight-gradient A/B hook: single LDS stage at 3 waves/SIMD (True) or double-buffered (False, default)");
   m.def("maxpool_force_generic", &tdl::maxpool_force_generic,
         "max-pool A/B hook: generic window loops (True, default) or the unrolled 3x3 stride-2 kernels (False)");
+  m.def("maxpool_w2", &tdl::maxpool_w2,
+        "max-pool backward A/B hook: 2x2 stride-2 unpadded windows in scatter form (True, default) or the gather form");
   m.def("conv_force_depth", &tdl::conv_force_depth, "conv main-loop A/B hook: 0 single stage, 1/2 prefetch depth, 3 depth 2 without the short-reduction single-stage variant");
   m.def("stem_fwd", &stem_fwd, "small-channel stride-2 conv (ResNet stem): (y, packed x[, BN part])",
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("pt"), pybind11::arg("pb"), pybind11::arg("pl"),

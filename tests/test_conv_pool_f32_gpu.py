@@ -144,3 +144,33 @@ def test_pooled_gradient_loaders_match_maxpool_backward_bitwise(shape, monkeypat
         res.append((xv.grad, wv.grad, bv.grad))
     for a, c in zip(res[0], res[1]):
         assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("shape", [(8, 26, 26, 32), (8, 11, 11, 64), (3, 9, 12, 24), (2, 7, 7, 16)])
+@pytest.mark.parametrize("bf16", [False, True], ids=["f32", "bf16"])
+def test_maxpool_2x2_backward_scatter_form(shape, bf16):
+    """The 2x2 stride-2 max-pool backward in scatter form (csrc/kernels/pool.hip k_maxpool_bwd_w2: one thread
+    per window writes its four pixels, the last window of an odd row / column also the edge zeros) equals the
+    gather form bit for bit -- every pixel written, odd sizes included -- and PyTorch's max-pool gradient."""
+    from tensorflow_distributed_learning_amd.ops import hip
+
+    C = hip()
+    N, H, W, K = shape
+    g = torch.Generator(device="cpu").manual_seed(H * 7 + K)
+    x = torch.randn(N, H, W, K, generator=g).cuda()
+    if bf16:
+        x = x.bfloat16()
+    PH, PW = H // 2, W // 2
+    y, arg = C.maxpool_fwd(x, 2, 2, 2, 2, 0, 0, PH, PW, False)
+    dy = torch.randn(y.shape, generator=g).cuda().to(x.dtype)
+    res = []
+    try:
+        for on in (True, False):
+            C.maxpool_w2(on)
+            res.append(C.maxpool_bwd(dy, arg, list(x.shape), 2, 2, 2, 2, 0, 0))
+    finally:
+        C.maxpool_w2(True)
+    assert torch.equal(res[0], res[1])
+    xr = x.float().permute(0, 3, 1, 2).clone().requires_grad_(True)
+    F.max_pool2d(xr, 2).backward(dy.float().permute(0, 3, 1, 2))
+    assert torch.equal(res[0].float(), xr.grad.permute(0, 2, 3, 1))
