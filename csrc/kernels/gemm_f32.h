@@ -103,5 +103,7 @@ inline void f32_gemm_plan(F32GemmArgs& a, int kmin = 64, int cap = 1024) {
 }
 
 void f32_gemm_launch(int mode, const F32GemmArgs& a, hipStream_t s);
+// many-slice reductions over >= 8192 outputs: 16 outputs per wave (default) or one (A/B hook)
+void f32_reduce16(bool on);
 
 }  // namespace tdl

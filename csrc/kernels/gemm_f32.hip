@@ -607,6 +607,62 @@ __global__ __launch_bounds__(256) void k_gemm_f32_reduce_wave(F32GemmArgs a) {
   if (lane == 0) out_store(a, m, n, v);
 }
 
+// Many slices over many outputs: a wave sums 16 consecutive partial-slab entries (64 contiguous bytes of
+// each slice, four 16-B loads per lane, instead of a 4-B load per output and slice spread over 64 cache
+// lines).  Per output the arithmetic of k_gemm_f32_reduce_wave: lane l sums slices l, l + 64, .. in
+// order, then the same xor butterfly (whose result is the same on every lane) -- bit-identical.
+template <bool V4>
+__global__ __launch_bounds__(256) void k_gemm_f32_reduce_wave16(F32GemmArgs a) {
+  const int64_t mn = (int64_t)a.M * a.N;
+  const int64_t f0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
+  const int lane = threadIdx.x & 63;
+  if (f0 >= mn) return;
+  const int nv = (int)(mn - f0 < 16 ? mn - f0 : 16);
+  const float* src = a.ws + f0;
+  float acc[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll 2
+  for (int z = lane; z < a.splits; z += 64) {
+    const float* q = src + (int64_t)z * mn;
+    float p[16];
+    if (V4 && nv == 16) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f4 u = reinterpret_cast<const f4*>(q)[i];
+        p[4 * i] = u.x;
+        p[4 * i + 1] = u.y;
+        p[4 * i + 2] = u.z;
+        p[4 * i + 3] = u.w;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) p[i] = i < nv ? q[i] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] += p[i];
+  }
+  float v = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const float s = wave_sum(acc[i]);
+    v = lane == i ? s : v;
+  }
+  if (lane < nv) {
+    const int64_t f = f0 + lane;
+    const int m = (int)(f / a.N), n = (int)(f - (int64_t)m * a.N);
+    out_store(a, m, n, v);
+  }
+}
+
+// TDL_F32_REDUCE16=0: every many-slice reduction one wave per output (A/B hook)
+bool g_reduce16 = [] {
+  const char* e = std::getenv("TDL_F32_REDUCE16");
+  return e == nullptr || std::atoi(e) != 0;
+}();
+
+bool reduce16_on() { return g_reduce16; }
+
 // the operand-vectorisation instantiation of a (mode, mask) kernel
 template <int MODE, bool MA, bool MB, bool PIN, bool BUF>
 void launch_vb(const F32GemmArgs& a, dim3 grid, hipStream_t s) {
@@ -633,6 +689,8 @@ void launch_v(const F32GemmArgs& a, dim3 grid, hipStream_t s) {
 }
 
 }  // namespace
+
+void f32_reduce16(bool on) { g_reduce16 = on; }
 
 void f32_gemm_launch(int mode, const F32GemmArgs& a, hipStream_t s) {
   if (a.M <= 0 || a.N <= 0) return;
@@ -662,7 +720,13 @@ void f32_gemm_launch(int mode, const F32GemmArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_gemm_f32_reduce_pool, dim3((unsigned)((wins + 255) / 256)), dim3(256), 0, s, a);
   } else if (a.splits > 1) {
     const int64_t mn = (int64_t)a.M * a.N;
-    if (a.splits >= 16)  // one wave per output: every partial of an output in one load round
+    if (a.splits >= 16 && mn >= 512 * 16 && reduce16_on()) {  // >= 512 waves of 16 outputs
+      const dim3 gr((unsigned)((mn + 63) / 64));
+      if (mn % 4 == 0)
+        hipLaunchKernelGGL(k_gemm_f32_reduce_wave16<true>, gr, dim3(256), 0, s, a);
+      else
+        hipLaunchKernelGGL(k_gemm_f32_reduce_wave16<false>, gr, dim3(256), 0, s, a);
+    } else if (a.splits >= 16)  // one wave per output: every partial of an output in one load round
       hipLaunchKernelGGL(k_gemm_f32_reduce_wave, dim3((unsigned)((mn + 3) / 4)), dim3(256), 0, s, a);
     else
       hipLaunchKernelGGL(k_gemm_f32_reduce, dim3((unsigned)((mn + 255) / 256)), dim3(256), 0, s, a);

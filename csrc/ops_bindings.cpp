@@ -1070,6 +1070,8 @@ void register_ops(pybind11::module& m) {
   m.def("conv_force_impl", &tdl::conv_force_impl,
         "conv main loop A/B hook: 1 v1 register staged, 2 default selection, 3 LDS-DMA ring, 4/5 dma1 at 4/3 waves "
         "per SIMD on 16x16x32 MFMAs, 6 dma1 on 32x32x16 MFMAs everywhere");
+  m.def("f32_reduce16", &tdl::f32_reduce16,
+        "f32 split-K reduce A/B hook: 16 outputs per wave over many slices (True, default) or one output per wave");
   m.def("conv_force_halo", &tdl::conv_force_halo, "halo (input-reuse) main loop for stride-1 multi-tap convs: 1 on, 0 off");
   m.def("conv_force_mfma", &tdl::conv_force_mfma, "dma1 MFMA form: 32 (32x32x16, default) or 16 (16x16x32)");
   m.def("conv_wgrad3x3_set_rows", &tdl::conv_wgrad3x3_set_rows, "3x3 row-kernel wgrad: output rows per slice (0 = auto)");

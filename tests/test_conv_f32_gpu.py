@@ -270,3 +270,32 @@ def test_xent_head_loss_grad_and_metrics(NK):
     np.testing.assert_allclose(float(accs[0]), 1.5 + float(per.sum()), rtol=1e-6)
     assert float(accs[1]) == 3.0 + N and float(accs[3]) == 3.0 + N
     assert float(accs[2]) == 2.0 + float((z.argmax(1) == y).sum())
+
+
+@pytest.mark.parametrize("shape", [(64, 13, 13, 32, 64), (64, 26, 26, 33, 35)], ids=["cnn_conv2", "ragged"])
+def test_split_k_reduce_16_outputs_per_wave_is_bit_identical(shape):
+    """Many-slice split-K reductions over >= 8192 outputs sum 16 consecutive partial-slab entries per wave
+    (k_gemm_f32_reduce_wave16, 16-B loads; scalar loads when M * N is not a multiple of 4): the weight and
+    bias gradients equal the one-output-per-wave reduce bit for bit, and float64."""
+    from tensorflow_distributed_learning_amd.ops import hip
+
+    N, H, W, C, K = shape
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(N, H, W, C, generator=g)
+    w = torch.randn(3, 3, C, K, generator=g) / (9 * C) ** 0.5
+    b = torch.randn(K, generator=g)
+    yr, xd, wd, bd = _ref(x, w, b, (1, 1), (0, 0, 0, 0), (1, 1))
+    dy = torch.randn(yr.shape, generator=g)
+    yr.backward(dy.double())
+    grads = []
+    try:
+        for on in (True, False):
+            hip().f32_reduce16(on)
+            xc, wc, bc = (t.cuda().requires_grad_(True) for t in (x, w, b))
+            CF.conv2d(xc, wc, bc, (1, 1), (0, 0, 0, 0)).backward(dy.cuda())
+            grads.append((wc.grad, bc.grad))
+    finally:
+        hip().f32_reduce16(True)
+    assert torch.equal(grads[0][0], grads[1][0]) and torch.equal(grads[0][1], grads[1][1])
+    _close(grads[0][0], wd.grad)
+    _close(grads[0][1], bd.grad)
