@@ -544,6 +544,7 @@ __global__ __launch_bounds__(256) void k_gemm_f32_reduce(F32GemmArgs a) {
 // column) sums each of the window's 4 rows exactly as k_gemm_f32_reduce sums an output (slices in
 // order, rounds of 16 with zero-filled remainders: the same bits as the unfused conv's reduction), then
 // the pooled epilogue of k_gemm_f32 (bias, ReLU, y, maximum, argmax).
+template <bool HOIST>
 __global__ __launch_bounds__(256) void k_gemm_f32_reduce_pool(F32GemmArgs a) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t wins = (int64_t)(a.M >> 2) * a.N;
@@ -556,6 +557,35 @@ __global__ __launch_bounds__(256) void k_gemm_f32_reduce_pool(F32GemmArgs a) {
   const float bias = a.bias != nullptr ? a.bias[n] : 0.f;
   float best = -INFINITY;
   uint32_t arg = 255u;
+  if (HOIST && a.splits < 16) {
+    // the 4 rows' partials all loaded before any store (the stores to out may alias the slab for the
+    // compiler, which then kept each row's loads behind the previous row's store: 4 serial round trips)
+    float p[4][16];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float* src = a.ws + (int64_t)(4 * win + r) * a.N + n;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) p[r][u] = src[(int64_t)min(u, a.splits - 1) * mn];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v = 0.f;  // = k_gemm_f32_reduce's remainder round: slices in order, zeros past the end
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v += u < a.splits ? p[r][u] : 0.f;
+      if (a.bias != nullptr) v += bias;
+      if (a.act == 1) v = fmaxf(v, 0.f);
+      const int oy = 2 * php + (r >> 1), ox = 2 * pwp + (r & 1);
+      a.out[(((int64_t)img * a.g.oh + oy) * a.g.ow + ox) * a.ldo + n] = v;
+      if (v > best) {
+        best = v;
+        arg = (uint32_t)r;
+      }
+    }
+    const int64_t po = (((int64_t)img * a.pool_h + php) * a.pool_w + pwp) * a.N + n;
+    a.pout[po] = best;
+    a.parg[po] = (uint8_t)arg;
+    return;
+  }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const float* src = a.ws + (int64_t)(4 * win + r) * a.N + n;
@@ -717,7 +747,14 @@ void f32_gemm_launch(int mode, const F32GemmArgs& a, hipStream_t s) {
   }
   if (a.splits > 1 && a.pool) {
     const int64_t wins = (int64_t)(a.M >> 2) * a.N;
-    hipLaunchKernelGGL(k_gemm_f32_reduce_pool, dim3((unsigned)((wins + 255) / 256)), dim3(256), 0, s, a);
+    static const bool hoist = [] {  // TDL_F32_POOLRED_HOIST=0: row by row (A/B hook)
+      const char* e = std::getenv("TDL_F32_POOLRED_HOIST");
+      return e == nullptr || std::atoi(e) != 0;
+    }();
+    if (hoist)
+      hipLaunchKernelGGL(k_gemm_f32_reduce_pool<true>, dim3((unsigned)((wins + 255) / 256)), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL(k_gemm_f32_reduce_pool<false>, dim3((unsigned)((wins + 255) / 256)), dim3(256), 0, s, a);
   } else if (a.splits > 1) {
     const int64_t mn = (int64_t)a.M * a.N;
     if (a.splits >= 16 && mn >= 512 * 16 && reduce16_on()) {  // >= 512 waves of 16 outputs
