@@ -18,6 +18,7 @@
 #include "kernels/gemm.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace tdl {
 namespace {
@@ -312,6 +313,7 @@ __global__ __launch_bounds__(256) void k_softmax_xent(const float* __restrict__ 
 
 // Fused loss head (see gemm.h xent_head): 16 waves; wave w takes rows w, w + 16, ..; lane 0 of each
 // wave accumulates its rows' loss / correct flags in row order, thread 0 sums the waves in order.
+template <bool PRE>
 __global__ __launch_bounds__(1024) void k_xent_head(const float* __restrict__ z, const long long* __restrict__ lab,
                                                     int N, int K, double gn, float* __restrict__ loss_out,
                                                     float* __restrict__ dz, double* lt_total, double* lt_count,
@@ -320,6 +322,15 @@ __global__ __launch_bounds__(1024) void k_xent_head(const float* __restrict__ z,
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float inv_gn = (float)(1.0 / gn);
   double my_loss = 0.0, my_cor = 0.0;
+  // the metric accumulators' old values, loaded by thread 0 before the rows (only this kernel writes them,
+  // in stream order): their round trip overlaps the rows' instead of following the block reduction
+  double l0 = 0.0, l1 = 0.0, a0 = 0.0, a1 = 0.0;
+  if (PRE && threadIdx.x == 0) {
+    l0 = lt_total != nullptr ? *lt_total : 0.0;
+    l1 = lt_count != nullptr ? *lt_count : 0.0;
+    a0 = acc_total != nullptr ? *acc_total : 0.0;
+    a1 = acc_count != nullptr ? *acc_count : 0.0;
+  }
   if (K <= 64) {
     // small heads (the reference CNN's 10 classes): a row is one load per lane, and each wave issues
     // the loads of its next 4 rows (logits and labels) before any math, so the rows do not pay one
@@ -415,9 +426,12 @@ __global__ __launch_bounds__(1024) void k_xent_head(const float* __restrict__ z,
       tc += s_cor[i];
     }
     loss_out[0] = (float)(tl / gn);
-    // the four read-modify-writes' loads issued together (one memory round trip, not four)
-    const double l0 = lt_total != nullptr ? *lt_total : 0.0, l1 = lt_count != nullptr ? *lt_count : 0.0;
-    const double a0 = acc_total != nullptr ? *acc_total : 0.0, a1 = acc_count != nullptr ? *acc_count : 0.0;
+    if (!PRE) {  // (TDL_XENT_PREFETCH=0: loaded here, A/B hook)
+      l0 = lt_total != nullptr ? *lt_total : 0.0;
+      l1 = lt_count != nullptr ? *lt_count : 0.0;
+      a0 = acc_total != nullptr ? *acc_total : 0.0;
+      a1 = acc_count != nullptr ? *acc_count : 0.0;
+    }
     if (lt_total != nullptr) *lt_total = l0 + tl;
     if (lt_count != nullptr) *lt_count = l1 + (double)N;
     if (acc_total != nullptr) *acc_total = a0 + tc;
@@ -506,8 +520,16 @@ void xent_head(const float* z, const long long* labels, int N, int K, double gn,
                double* lt_total, double* lt_count, double* acc_total, double* acc_count, float* rows_ws,
                hipStream_t s) {
   if (rows_ws == nullptr) {  // small head: everything in one workgroup
-    hipLaunchKernelGGL(k_xent_head, dim3(1), dim3(1024), 0, s, z, labels, N, K, gn, loss_out, dz, lt_total, lt_count,
-                       acc_total, acc_count);
+    static const bool pre = [] {
+      const char* e = std::getenv("TDL_XENT_PREFETCH");
+      return e == nullptr || std::atoi(e) != 0;
+    }();
+    if (pre)
+      hipLaunchKernelGGL(k_xent_head<true>, dim3(1), dim3(1024), 0, s, z, labels, N, K, gn, loss_out, dz, lt_total,
+                         lt_count, acc_total, acc_count);
+    else
+      hipLaunchKernelGGL(k_xent_head<false>, dim3(1), dim3(1024), 0, s, z, labels, N, K, gn, loss_out, dz, lt_total,
+                         lt_count, acc_total, acc_count);
     return;
   }
   hipLaunchKernelGGL(k_xent_rows, dim3((N + 3) / 4), dim3(256), 0, s, z, labels, N, K, gn, dz, rows_ws, rows_ws + N);
