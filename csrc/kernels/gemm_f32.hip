@@ -511,7 +511,9 @@ __device__ __forceinline__ void out_index(const F32GemmArgs& a, int64_t e, int& 
 
 // Split-reduction epilogue: the slices summed in a fixed order, then bias / accumulate / store.
 // Outputs are walked in storage order (coalesced stores, strided partial reads when transposed).
-// Few slices: one thread per output, 8 independent partial loads in flight.
+// Few slices: one thread per output, 16 independent partial loads in flight.  R < 16: at most R slices
+// (no full round), only R loads issued; the sum still adds all 16 terms (zeros past the end): same bits.
+template <int R>
 __global__ __launch_bounds__(256) void k_gemm_f32_reduce(F32GemmArgs a) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t mn = (int64_t)a.M * a.N;
@@ -531,9 +533,9 @@ __global__ __launch_bounds__(256) void k_gemm_f32_reduce(F32GemmArgs a) {
   {
     float p[16];  // the remainder, also in one round (clamped loads, zero past the end)
 #pragma unroll
-    for (int u = 0; u < 16; ++u) p[u] = src[(int64_t)min(z + u, a.splits - 1) * mn];
+    for (int u = 0; u < R; ++u) p[u] = src[(int64_t)min(z + u, a.splits - 1) * mn];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) p[u] = z + u < a.splits ? p[u] : 0.f;
+    for (int u = 0; u < 16; ++u) p[u] = u < R && z + u < a.splits ? p[u] : 0.f;
 #pragma unroll
     for (int u = 0; u < 16; ++u) v += p[u];
   }
@@ -765,8 +767,19 @@ void f32_gemm_launch(int mode, const F32GemmArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(k_gemm_f32_reduce_wave16<false>, gr, dim3(256), 0, s, a);
     } else if (a.splits >= 16)  // one wave per output: every partial of an output in one load round
       hipLaunchKernelGGL(k_gemm_f32_reduce_wave, dim3((unsigned)((mn + 3) / 4)), dim3(256), 0, s, a);
-    else
-      hipLaunchKernelGGL(k_gemm_f32_reduce, dim3((unsigned)((mn + 255) / 256)), dim3(256), 0, s, a);
+    else {
+      static const bool narrow = [] {  // TDL_F32_REDUCE_NARROW=0: 16 loads whatever the slice count (A/B hook)
+        const char* e = std::getenv("TDL_F32_REDUCE_NARROW");
+        return e == nullptr || std::atoi(e) != 0;
+      }();
+      const dim3 gr((unsigned)((mn + 255) / 256));
+      if (narrow && a.splits <= 4)
+        hipLaunchKernelGGL(k_gemm_f32_reduce<4>, gr, dim3(256), 0, s, a);
+      else if (narrow && a.splits <= 8)
+        hipLaunchKernelGGL(k_gemm_f32_reduce<8>, gr, dim3(256), 0, s, a);
+      else
+        hipLaunchKernelGGL(k_gemm_f32_reduce<16>, gr, dim3(256), 0, s, a);
+    }
   }
 }
 
