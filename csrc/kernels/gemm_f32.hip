@@ -546,7 +546,7 @@ __global__ __launch_bounds__(256) void k_gemm_f32_reduce(F32GemmArgs a) {
 // column) sums each of the window's 4 rows exactly as k_gemm_f32_reduce sums an output (slices in
 // order, rounds of 16 with zero-filled remainders: the same bits as the unfused conv's reduction), then
 // the pooled epilogue of k_gemm_f32 (bias, ReLU, y, maximum, argmax).
-template <bool HOIST>
+template <bool HOIST, int R = 16>
 __global__ __launch_bounds__(256) void k_gemm_f32_reduce_pool(F32GemmArgs a) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t wins = (int64_t)(a.M >> 2) * a.N;
@@ -567,13 +567,13 @@ __global__ __launch_bounds__(256) void k_gemm_f32_reduce_pool(F32GemmArgs a) {
     for (int r = 0; r < 4; ++r) {
       const float* src = a.ws + (int64_t)(4 * win + r) * a.N + n;
 #pragma unroll
-      for (int u = 0; u < 16; ++u) p[r][u] = src[(int64_t)min(u, a.splits - 1) * mn];
+      for (int u = 0; u < R; ++u) p[r][u] = src[(int64_t)min(u, a.splits - 1) * mn];  // (R >= splits)
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float v = 0.f;  // = k_gemm_f32_reduce's remainder round: slices in order, zeros past the end
 #pragma unroll
-      for (int u = 0; u < 16; ++u) v += u < a.splits ? p[r][u] : 0.f;
+      for (int u = 0; u < 16; ++u) v += u < R && u < a.splits ? p[r][u] : 0.f;
       if (a.bias != nullptr) v += bias;
       if (a.act == 1) v = fmaxf(v, 0.f);
       const int oy = 2 * php + (r >> 1), ox = 2 * pwp + (r & 1);
@@ -695,6 +695,15 @@ bool g_reduce16 = [] {
 
 bool reduce16_on() { return g_reduce16; }
 
+// TDL_F32_REDUCE_NARROW=0: the few-slice reduces issue 16 loads whatever the slice count (A/B hook)
+bool reduce_narrow() {
+  static const bool on = [] {
+    const char* e = std::getenv("TDL_F32_REDUCE_NARROW");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return on;
+}
+
 // the operand-vectorisation instantiation of a (mode, mask) kernel
 template <int MODE, bool MA, bool MB, bool PIN, bool BUF>
 void launch_vb(const F32GemmArgs& a, dim3 grid, hipStream_t s) {
@@ -753,7 +762,12 @@ void f32_gemm_launch(int mode, const F32GemmArgs& a, hipStream_t s) {
       const char* e = std::getenv("TDL_F32_POOLRED_HOIST");
       return e == nullptr || std::atoi(e) != 0;
     }();
-    if (hoist)
+    const bool narrow = reduce_narrow();
+    if (hoist && narrow && a.splits <= 4)  // (only the loads the slices need: the 16-term sums unchanged)
+      hipLaunchKernelGGL((k_gemm_f32_reduce_pool<true, 4>), dim3((unsigned)((wins + 255) / 256)), dim3(256), 0, s, a);
+    else if (hoist && narrow && a.splits <= 8)
+      hipLaunchKernelGGL((k_gemm_f32_reduce_pool<true, 8>), dim3((unsigned)((wins + 255) / 256)), dim3(256), 0, s, a);
+    else if (hoist)
       hipLaunchKernelGGL(k_gemm_f32_reduce_pool<true>, dim3((unsigned)((wins + 255) / 256)), dim3(256), 0, s, a);
     else
       hipLaunchKernelGGL(k_gemm_f32_reduce_pool<false>, dim3((unsigned)((wins + 255) / 256)), dim3(256), 0, s, a);
@@ -768,10 +782,7 @@ void f32_gemm_launch(int mode, const F32GemmArgs& a, hipStream_t s) {
     } else if (a.splits >= 16)  // one wave per output: every partial of an output in one load round
       hipLaunchKernelGGL(k_gemm_f32_reduce_wave, dim3((unsigned)((mn + 3) / 4)), dim3(256), 0, s, a);
     else {
-      static const bool narrow = [] {  // TDL_F32_REDUCE_NARROW=0: 16 loads whatever the slice count (A/B hook)
-        const char* e = std::getenv("TDL_F32_REDUCE_NARROW");
-        return e == nullptr || std::atoi(e) != 0;
-      }();
+      const bool narrow = reduce_narrow();
       const dim3 gr((unsigned)((mn + 255) / 256));
       if (narrow && a.splits <= 4)
         hipLaunchKernelGGL(k_gemm_f32_reduce<4>, gr, dim3(256), 0, s, a);
