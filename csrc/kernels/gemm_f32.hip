@@ -639,28 +639,28 @@ __global__ __launch_bounds__(256) void k_gemm_f32_reduce_wave(F32GemmArgs a) {
   if (lane == 0) out_store(a, m, n, v);
 }
 
-// Many slices over many outputs: a wave sums 16 consecutive partial-slab entries (64 contiguous bytes of
-// each slice, four 16-B loads per lane, instead of a 4-B load per output and slice spread over 64 cache
-// lines).  Per output the arithmetic of k_gemm_f32_reduce_wave: lane l sums slices l, l + 64, .. in
+// Many slices over many outputs: a wave sums OUT (16, or 4 for a few hundred outputs) consecutive
+// partial-slab entries (OUT * 4 contiguous bytes of each slice as 16-B loads per lane, instead of a 4-B
+// load per output and slice spread over 64 cache lines).  Per output the arithmetic of k_gemm_f32_reduce_wave: lane l sums slices l, l + 64, .. in
 // order, then the same xor butterfly (whose result is the same on every lane) -- bit-identical.
-template <bool V4>
+template <int OUT, bool V4>
 __global__ __launch_bounds__(256) void k_gemm_f32_reduce_wave16(F32GemmArgs a) {
   const int64_t mn = (int64_t)a.M * a.N;
-  const int64_t f0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
+  const int64_t f0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * OUT;
   const int lane = threadIdx.x & 63;
   if (f0 >= mn) return;
-  const int nv = (int)(mn - f0 < 16 ? mn - f0 : 16);
+  const int nv = (int)(mn - f0 < OUT ? mn - f0 : OUT);
   const float* src = a.ws + f0;
-  float acc[16];
+  float acc[OUT];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  for (int i = 0; i < OUT; ++i) acc[i] = 0.f;
 #pragma unroll 2
   for (int z = lane; z < a.splits; z += 64) {
     const float* q = src + (int64_t)z * mn;
-    float p[16];
-    if (V4 && nv == 16) {
+    float p[OUT];
+    if (V4 && nv == OUT) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < OUT / 4; ++i) {
         const f4 u = reinterpret_cast<const f4*>(q)[i];
         p[4 * i] = u.x;
         p[4 * i + 1] = u.y;
@@ -669,14 +669,14 @@ __global__ __launch_bounds__(256) void k_gemm_f32_reduce_wave16(F32GemmArgs a) {
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) p[i] = i < nv ? q[i] : 0.f;
+      for (int i = 0; i < OUT; ++i) p[i] = i < nv ? q[i] : 0.f;
     }
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] += p[i];
+    for (int i = 0; i < OUT; ++i) acc[i] += p[i];
   }
   float v = 0.f;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
+  for (int i = 0; i < OUT; ++i) {
     const float s = wave_sum(acc[i]);
     v = lane == i ? s : v;
   }
@@ -776,9 +776,15 @@ void f32_gemm_launch(int mode, const F32GemmArgs& a, hipStream_t s) {
     if (a.splits >= 16 && mn >= 512 * 16 && reduce16_on()) {  // >= 512 waves of 16 outputs
       const dim3 gr((unsigned)((mn + 63) / 64));
       if (mn % 4 == 0)
-        hipLaunchKernelGGL(k_gemm_f32_reduce_wave16<true>, gr, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_gemm_f32_reduce_wave16<16, true>), gr, dim3(256), 0, s, a);
       else
-        hipLaunchKernelGGL(k_gemm_f32_reduce_wave16<false>, gr, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_gemm_f32_reduce_wave16<16, false>), gr, dim3(256), 0, s, a);
+    } else if (a.splits >= 16 && mn >= 64 * 4 && reduce16_on()) {  // >= 64 waves of 4 outputs
+      const dim3 gr((unsigned)((mn + 15) / 16));
+      if (mn % 4 == 0)
+        hipLaunchKernelGGL((k_gemm_f32_reduce_wave16<4, true>), gr, dim3(256), 0, s, a);
+      else
+        hipLaunchKernelGGL((k_gemm_f32_reduce_wave16<4, false>), gr, dim3(256), 0, s, a);
     } else if (a.splits >= 16)  // one wave per output: every partial of an output in one load round
       hipLaunchKernelGGL(k_gemm_f32_reduce_wave, dim3((unsigned)((mn + 3) / 4)), dim3(256), 0, s, a);
     else {

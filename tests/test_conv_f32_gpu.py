@@ -272,10 +272,11 @@ def test_xent_head_loss_grad_and_metrics(NK):
     assert float(accs[2]) == 2.0 + float((z.argmax(1) == y).sum())
 
 
-@pytest.mark.parametrize("shape", [(64, 13, 13, 32, 64), (64, 26, 26, 33, 35)], ids=["cnn_conv2", "ragged"])
+@pytest.mark.parametrize("shape", [(64, 13, 13, 32, 64), (64, 26, 26, 33, 35), (64, 28, 28, 1, 32), (64, 20, 20, 2, 15)],
+                         ids=["cnn_conv2", "ragged", "cnn_conv1_4_per_wave", "ragged_4_per_wave"])
 def test_split_k_reduce_16_outputs_per_wave_is_bit_identical(shape):
-    """Many-slice split-K reductions over >= 8192 outputs sum 16 consecutive partial-slab entries per wave
-    (k_gemm_f32_reduce_wave16, 16-B loads; scalar loads when M * N is not a multiple of 4): the weight and
+    """Many-slice split-K reductions sum 16 (>= 8192 outputs) or 4 (>= 256) consecutive partial-slab entries
+    per wave (k_gemm_f32_reduce_wave16, 16-B loads; scalar loads when M * N is not a multiple of 4): the weight and
     bias gradients equal the one-output-per-wave reduce bit for bit, and float64."""
     from tensorflow_distributed_learning_amd.ops import hip
 
